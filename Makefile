@@ -1,0 +1,46 @@
+# MI355X (gfx950) build of the drop-in libwhisper.so (C ABI of include/whisper.h + owk.h).
+#
+#   make            -> open-whisper-kit_amd/lib/libwhisper.so
+#   make oracle     -> oracle/_ref/libwhisper_ref.so (reference CPU path; test infrastructure)
+#
+# hipcc cross-compiles for gfx950 without a GPU. -ffp-contract=off keeps every
+# elementwise f32 op a single rounding like the reference's separate ggml ops
+# (fused multiply-adds are written explicitly where the reference fuses).
+HIPCC    ?= /opt/rocm/bin/hipcc
+ARCH     ?= gfx950
+JOBS     ?= 8
+PKG      := open-whisper-kit_amd
+SRC      := $(PKG)/csrc
+OBJDIR   := $(PKG)/build
+LIB      := $(PKG)/lib/libwhisper.so
+
+FLAGS    := -O3 -std=c++17 -fPIC -ffp-contract=off --offload-arch=$(ARCH) -Iinclude -I$(SRC) \
+            -DWHISPER_SHARED -DWHISPER_BUILD -Wall -Wno-unused-function -Wno-unused-variable
+
+HIP_SRCS := $(wildcard $(SRC)/*.hip)
+CPP_SRCS := $(wildcard $(SRC)/*.cpp)
+OBJS     := $(patsubst $(SRC)/%.hip,$(OBJDIR)/%.hip.o,$(HIP_SRCS)) \
+            $(patsubst $(SRC)/%.cpp,$(OBJDIR)/%.cpp.o,$(CPP_SRCS))
+HDRS     := $(wildcard $(SRC)/*.h) $(wildcard include/*.h)
+
+all: $(LIB)
+
+$(LIB): $(OBJS)
+	@mkdir -p $(dir $@)
+	$(HIPCC) -shared --offload-arch=$(ARCH) -o $@ $(OBJS) -Wl,--no-undefined -Wl,-soname,libwhisper.so
+
+$(OBJDIR)/%.hip.o: $(SRC)/%.hip $(HDRS)
+	@mkdir -p $(OBJDIR)
+	$(HIPCC) $(FLAGS) -c $< -o $@
+
+$(OBJDIR)/%.cpp.o: $(SRC)/%.cpp $(HDRS)
+	@mkdir -p $(OBJDIR)
+	$(HIPCC) $(FLAGS) -x hip -c $< -o $@
+
+oracle:
+	$(MAKE) -C oracle/ref -j$(JOBS)
+
+clean:
+	rm -rf $(OBJDIR) $(PKG)/lib
+
+.PHONY: all clean oracle

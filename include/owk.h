@@ -1,0 +1,61 @@
+/*
+ * owk.h -- MI355X engine extensions beyond the reference whisper.h ABI.
+ *
+ * The reference processes one clip per whisper_full() call (ref src/whisper.cpp:7778).
+ * The MI355X engine is batch-major: owk_full_batch() runs N independent clips
+ * through one stage-major pipeline (batched mel -> conv -> encoder -> cross-KV ->
+ * decoder steps), each clip with its own whisper_state holding results readable with
+ * the standard whisper_full_*_from_state() getters. Per-clip decoding semantics are
+ * exactly those of whisper_full_with_state (ref src/whisper.cpp:6827-7776).
+ */
+#ifndef OWK_H
+#define OWK_H
+
+#include "whisper.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* extra per-call options (all-zero = reference behaviour) */
+struct owk_full_ext {
+    /* fixed-work mode for throughput runs: mask <|endoftext|> on the device, equivalent
+     * to a logits_filter_callback doing logits[eot] = -INF (ref whisper.cpp:6254-6256) */
+    int suppress_eot;
+    int reserved[7];
+};
+
+/* run n_clips clips; states[i] receives clip i's segments. Returns 0 if every clip
+ * succeeded, else the first non-zero whisper_full error code. */
+WHISPER_API int owk_full_batch(struct whisper_context * ctx, struct whisper_state ** states,
+                               struct whisper_full_params params, const struct owk_full_ext * ext,
+                               const float * const * samples, const int * n_samples, int n_clips);
+
+/* per-kernel-class device timing with HIP events recorded on the engine stream */
+WHISPER_API void owk_prof_enable(struct whisper_context * ctx, int enable);
+WHISPER_API void owk_prof_reset(struct whisper_context * ctx);
+/* total device milliseconds and launch count of one kernel class since reset;
+ * returns 0 if the class is known */
+WHISPER_API int owk_prof_read(struct whisper_context * ctx, const char * kernel_class, double * total_ms, long * launches);
+/* algorithmic work (flops, bytes) the engine attributes to a kernel class since reset */
+WHISPER_API int owk_prof_work(struct whisper_context * ctx, const char * kernel_class, double * flops, double * bytes);
+/* comma-separated list of kernel classes seen since reset (owned by ctx) */
+WHISPER_API const char * owk_prof_classes(struct whisper_context * ctx);
+
+/* test hooks: intermediates of the last staged call on a state
+ * (mel [n_mel][n_len] f32; encoder output [n_audio_ctx][d] f32; cross K/V f16 bits) */
+WHISPER_API int owk_debug_mel(struct whisper_state * st, float * out, int cap);
+WHISPER_API int owk_debug_enc(struct whisper_context * ctx, struct whisper_state * st, int index, float * out, int cap);
+WHISPER_API int owk_debug_cross(struct whisper_context * ctx, struct whisper_state * st, int slot, int layer,
+                                uint16_t * k, uint16_t * v);
+WHISPER_API const uint16_t * owk_debug_gelu_table(void);
+
+/* library identity: 1 when the gfx950 HIP code object is present and a device is usable */
+WHISPER_API int owk_device_ok(int device);
+WHISPER_API const char * owk_build_info(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* OWK_H */

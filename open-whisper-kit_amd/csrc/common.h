@@ -1,0 +1,66 @@
+// Shared host/device definitions for the MI355X (gfx950) Whisper engine.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <stdexcept>
+#include <string>
+
+#define OWK_HIP_CHECK(expr)                                                                  \
+    do {                                                                                     \
+        hipError_t owk_err_ = (expr);                                                        \
+        if (owk_err_ != hipSuccess) {                                                        \
+            char owk_buf_[512];                                                              \
+            snprintf(owk_buf_, sizeof(owk_buf_), "HIP error %s at %s:%d: %s",                 \
+                     hipGetErrorString(owk_err_), __FILE__, __LINE__, #expr);                \
+            throw std::runtime_error(owk_buf_);                                              \
+        }                                                                                    \
+    } while (0)
+
+namespace owk {
+
+typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+typedef _Float16 half4 __attribute__((ext_vector_type(4)));
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+
+// host-side IEEE binary16 conversion (round-to-nearest-even), identical to the
+// F16C/_cvtss_sh path the reference uses for GGML_CPU_FP32_TO_FP16.
+static inline uint16_t f32_to_f16_host(float f) {
+    _Float16 h = (_Float16) f;
+    uint16_t u;
+    __builtin_memcpy(&u, &h, 2);
+    return u;
+}
+static inline float f16_to_f32_host(uint16_t u) {
+    _Float16 h;
+    __builtin_memcpy(&h, &u, 2);
+    return (float) h;
+}
+
+// RAII device allocation
+struct DevBuf {
+    void * ptr = nullptr;
+    size_t bytes = 0;
+    DevBuf() = default;
+    DevBuf(const DevBuf &) = delete;
+    DevBuf & operator=(const DevBuf &) = delete;
+    ~DevBuf() { release(); }
+    void release() {
+        if (ptr) (void) hipFree(ptr);
+        ptr = nullptr;
+        bytes = 0;
+    }
+    void alloc(size_t n) {
+        if (n <= bytes && ptr) return;
+        release();
+        if (n == 0) return;
+        OWK_HIP_CHECK(hipMalloc(&ptr, n));
+        bytes = n;
+    }
+    template <typename T> T * as() const { return (T *) ptr; }
+};
+
+} // namespace owk

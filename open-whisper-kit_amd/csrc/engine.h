@@ -1,0 +1,129 @@
+// Batch-major device engine: mel -> conv -> encoder -> cross-KV for many clips at once,
+// and batched decoder passes over rows drawn from any number of clips / decoders.
+#pragma once
+
+#include <map>
+#include <string>
+#include <vector>
+
+#include "kernels.h"
+#include "model.h"
+
+namespace owk {
+
+// per-kernel-class HIP-event timing + algorithmic work counters
+struct Prof {
+    bool on = false;
+    struct Rec {
+        int cls;
+        hipEvent_t a, b;
+        double flops, bytes;
+    };
+    std::vector<std::string> names;
+    std::vector<Rec> pending;
+    std::vector<hipEvent_t> pool;
+    struct Tot {
+        double ms = 0, flops = 0, bytes = 0;
+        long n = 0;
+    };
+    std::vector<Tot> tot;
+    std::string classes_csv;
+    int cls_id(const char * name);
+    hipEvent_t ev();
+    void flush();
+    void reset();
+    ~Prof();
+};
+
+struct ProfScope {
+    Prof * p;
+    hipStream_t s;
+    int cls = -1;
+    hipEvent_t a = nullptr;
+    double flops, bytes;
+    ProfScope(Prof * p_, hipStream_t s_, const char * name, double flops_ = 0, double bytes_ = 0);
+    ~ProfScope();
+};
+
+struct DecodeRow {
+    int slot;        // clip slot (cross-KV / self-KV / mel owner)
+    int token;
+    int pos;
+    int cell;        // self-KV cell receiving this token's K/V
+    int key_off;     // visible self-attention cells: key_list[key_off .. key_off+n_keys)
+    int n_keys;
+    int mode_self;   // 0 one_chunk (F16 acc), 1 tiled (F32 acc)
+    int mode_cross;
+    int logit_row;   // -1: no logits for this row
+};
+
+class Engine {
+public:
+    Engine(const Model * m, Prof * prof);
+    ~Engine();
+
+    const Model * m;
+    Prof * prof;
+    hipStream_t stream = nullptr;
+
+    int cap_slots = 0;   // clip slots with cross-KV storage
+    int kv_cells = 0;    // self-KV cells per slot
+
+    void reserve(int slots, int cells);
+
+    // ---- mel ----
+    // computes normalised log-mel for clips into slots[i]
+    void compute_mel(const std::vector<int> & slots, const std::vector<const float *> & pcm,
+                     const std::vector<int> & n_samples);
+    void set_mel(int slot, const float * host, int n_len, int n_mel);
+    int mel_len(int slot) const { return slot < (int) mel_len_.size() ? mel_len_[slot] : 0; }
+    void download_mel(int slot, float * host) const;
+
+    // ---- encoder + cross KV ----
+    void encode(const std::vector<int> & slots, const std::vector<int> & offsets);
+    // debug: f32 encoder output of the last encode (row-major [n*1500][d]) and cross KV
+    void download_enc(int index, float * host) const;
+    void download_cross(int slot, int layer, uint16_t * k_host, uint16_t * v_host) const;
+
+    // ---- decoder ----
+    // runs all rows through the decoder; raw logits for rows with logit_row >= 0 are
+    // left on the device in logits_dev() [n_logit_rows][n_vocab]
+    void decode(const std::vector<DecodeRow> & rows, const std::vector<int> & key_list, int n_logit_rows);
+    float * logits_dev() const { return logits_.as<float>(); }
+    void download_logits(int logit_row, float * host) const;
+    void upload_logits(int logit_row, const float * host);
+    // on-device whisper_process_logits + greedy pick
+    void process_logits(const std::vector<LogitJob> & jobs, const VocabInfo & vi, std::vector<TokenOut> & out,
+                        float * probs_host, float * logprobs_host);
+
+    // state->logits emulation for the no-speech probability (see k_logits.hip)
+    void logits_maxes(int n_logit_rows, std::vector<float> & out);
+    void row0_update(const std::vector<std::pair<int, int>> & map);  // (logit row or -1 = zeros, slot)
+    void nosp(const std::vector<std::pair<int, float>> & req, std::vector<float> & out);  // (slot, max)
+
+    void sync();
+
+private:
+    DevBuf row0_, lmax_, map_, nosp_idx_, nosp_max_, nosp_out_;
+    // slot storage
+    DevBuf cross_k_, cross_v_;   // [L][cap_slots][n_audio_ctx][d]
+    DevBuf self_k_, self_v_;     // [L][cap_slots][kv_cells][d]
+    std::vector<DevBuf *> mel_;  // per slot [n_mel][n_len]
+    std::vector<int> mel_len_;
+
+    // encoder workspace
+    DevBuf e_a1_, e_c1_, e_a2_, e_x_, e_xn_, e_q_, e_k_, e_vt_, e_ao_, e_h_, e_enc_, e_enc32_;
+    DevBuf e_win_, e_slotmap_;
+    int enc_rows_cap_ = 0;
+    int last_enc_n_ = 0;
+
+    // decoder workspace
+    DevBuf d_x_, d_xn_, d_q_, d_ao_, d_h_, d_tok_, d_pos_, d_rowoff_, d_rows_self_, d_rows_cross_, d_keys_,
+        d_lsel_, d_xl_;
+    DevBuf logits_, lg_jobs_, lg_out_, lg_probs_, lg_lp_, suppress_;
+    int dec_rows_cap_ = 0;
+
+    DevBuf mel_jobs_, pcm_tmp_;
+};
+
+} // namespace owk

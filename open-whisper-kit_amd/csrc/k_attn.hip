@@ -1,0 +1,301 @@
+// Attention kernels, gfx950.
+//
+// Encoder: flash attention on MFMA (f16 operands, f32 online softmax) reproducing the
+// reference's tiled CPU path (ggml-cpu/ops.cpp:8275-8546, taken for the encoder since
+// n_q >= 32 and n_kv = 1536 is a multiple of 16): F32 accumulators, and the 36 all-zero
+// padded keys of kv_pad (GGML_PAD(1500,256) rows never written, whisper.cpp:2055,
+// 2142-2159) folded in analytically at the end (score 0, value 0).
+//
+// Decoder: one wave per (query row, head) emulating the reference's per-key visit
+// order. In decode steps and short prefills the reference takes the "one_chunk" path
+// (ops.cpp:8140-8233) whose V accumulator is F16 and is rounded after every key;
+// that rounding is reproduced exactly (scores via f32 dot of f16 Q/K, expf, fma,
+// f32->f16 RNE per key). Long prefills (n_q >= 32) use the tiled F32 path.
+#include "kernels.h"
+
+namespace owk {
+
+typedef __attribute__((address_space(3))) void * lds_ptr_t;
+
+// ----------------------------------------------------------------------------------
+// Encoder flash attention.
+// Block = 4 waves = 64 queries of one (clip, head); KV tiles of 64 keys staged in LDS:
+//   K tile  [64 keys][64 dims] (row-major, from the [clip*T+t][d] K buffer)
+//   Vt tile [64 dims][64 keys] (from the transposed V written by the QKV epilogue)
+// S^T = K . Q^T is computed so each lane owns 16 scores of ONE query (lane&15): the
+// softmax needs only 2 cross-lane shuffles and P^T feeds the P.V MFMA as the B operand
+// straight from registers (key order inside a k-step permuted consistently on both
+// operands).
+// ----------------------------------------------------------------------------------
+constexpr int FA_KT = 64;                     // keys per tile
+constexpr int FA_TILE_BYTES = FA_KT * 64 * 2; // 8 KB (K tile or Vt tile)
+
+__global__ __launch_bounds__(256, 2) void k_attn_encoder(const _Float16 * __restrict__ q, const _Float16 * __restrict__ k,
+                                                         const _Float16 * __restrict__ vt, int T, int Tpad, int H,
+                                                         float scale, int n_zero_pad, _Float16 * __restrict__ out) {
+    __shared__ __attribute__((aligned(1024))) char smem[4 * FA_TILE_BYTES];  // 2 stages x (K, Vt)
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int qt = blockIdx.x, h = blockIdx.y, clip = blockIdx.z;
+    const int d = H * 64;
+    const int g = lane >> 4, l16 = lane & 15;
+
+    // Q fragments (B operand of S^T = K.Q^T): q = l16, dims 32*s + 8*g .. +8
+    const int qi = qt * 64 + wave * 16 + l16;
+    const int qc = min(qi, T - 1);
+    const _Float16 * qrow = q + ((size_t) clip * T + qc) * d + h * 64;
+    const half8 qf0 = *(const half8 *) (qrow + 8 * g);
+    const half8 qf1 = *(const half8 *) (qrow + 32 + 8 * g);
+
+    const _Float16 * kbase = k + (size_t) clip * T * d + h * 64;
+    const _Float16 * vbase = vt + ((size_t) clip * H + h) * 64 * Tpad;
+
+    auto stage = [&](int buf, int kt) {
+        char * sK = smem + buf * 2 * FA_TILE_BYTES;
+        char * sV = sK + FA_TILE_BYTES;
+        // 8 KB each = 8 groups of 8 rows x 128 B; 2 groups per wave per tensor
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int grp = wave * 2 + i;
+            const int row = grp * 8 + (lane >> 3);
+            const int c = (lane & 7) ^ ((row >> 1) & 7);
+            const int key = min(kt * FA_KT + row, T - 1);
+            __builtin_amdgcn_global_load_lds((const void *) (kbase + (size_t) key * d + c * 8),
+                                             (lds_ptr_t) (sK + grp * 1024), 16, 0, 0);
+            __builtin_amdgcn_global_load_lds((const void *) (vbase + (size_t) row * Tpad + kt * FA_KT + c * 8),
+                                             (lds_ptr_t) (sV + grp * 1024), 16, 0, 0);
+        }
+    };
+
+    floatx4 o[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) o[i] = floatx4{0.f, 0.f, 0.f, 0.f};
+    float m = -INFINITY;  // running max of this lane's query (uniform over the 4 lanes of a query)
+    float lsum = 0.0f;    // partial row sum over this lane's keys
+
+    const int ntiles = (T + FA_KT - 1) / FA_KT;
+    stage(0, 0);
+    __syncthreads();
+    for (int kt = 0; kt < ntiles; ++kt) {
+        const int cur = kt & 1;
+        if (kt + 1 < ntiles) stage(cur ^ 1, kt + 1);
+        const char * sK = smem + cur * 2 * FA_TILE_BYTES;
+        const char * sV = sK + FA_TILE_BYTES;
+
+        // S^T tiles: keys 16*t + 4*g + e, query l16
+        floatx4 sc[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const int row = t * 16 + l16;
+            const half8 a0 = *(const half8 *) (sK + row * 128 + (((0 + g) ^ ((row >> 1) & 7)) << 4));
+            const half8 a1 = *(const half8 *) (sK + row * 128 + (((4 + g) ^ ((row >> 1) & 7)) << 4));
+            floatx4 z = floatx4{0.f, 0.f, 0.f, 0.f};
+            z = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, qf0, z, 0, 0, 0);
+            z = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1, qf1, z, 0, 0, 0);
+            sc[t] = z;
+        }
+        float tmax = -INFINITY;
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int key = kt * FA_KT + t * 16 + 4 * g + e;
+                float v = sc[t][e] * scale;
+                if (key >= T) v = -INFINITY;
+                sc[t][e] = v;
+                tmax = fmaxf(tmax, v);
+            }
+        tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
+        tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+        const float mnew = fmaxf(m, tmax);
+        const float alpha = expf(m - mnew);  // m = -inf on the first tile -> 0
+        m = mnew;
+        float ps = 0.0f;
+        half8 pb[2];
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const float p = expf(sc[t][e] - mnew);
+                ps += p;
+                pb[t >> 1][(t & 1) * 4 + e] = (_Float16) p;
+            }
+        lsum = lsum * alpha + ps;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) o[i] *= alpha;
+
+        // O^T[dim][q] += V^T[dim][key] . P^T[key][q]; k-step ks covers keys 32*ks..+32 with
+        // element j<4 -> key 32ks + 4g + j, j>=4 -> key 32ks + 16 + 4g + (j-4)
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) {
+            const int row = dt * 16 + l16;  // dim
+            const char * vr = sV + row * 128;
+            const int sw = (row >> 1) & 7;
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks) {
+                const int b0 = ks * 64 + 8 * g;        // byte offset of key 32ks + 4g
+                const int b1 = ks * 64 + 32 + 8 * g;   // byte offset of key 32ks + 16 + 4g
+                const half4 lo = *(const half4 *) (vr + ((((b0 >> 4) ^ sw) << 4) | (b0 & 15)));
+                const half4 hi = *(const half4 *) (vr + ((((b1 >> 4) ^ sw) << 4) | (b1 & 15)));
+                half8 a;
+                a[0] = lo[0]; a[1] = lo[1]; a[2] = lo[2]; a[3] = lo[3];
+                a[4] = hi[0]; a[5] = hi[1]; a[6] = hi[2]; a[7] = hi[3];
+                o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, pb[ks], o[dt], 0, 0, 0);
+            }
+        }
+        __syncthreads();
+    }
+
+    // total row sum over the 4 lanes of each query, then the zero-padded keys
+    lsum += __shfl_xor(lsum, 16, 64);
+    lsum += __shfl_xor(lsum, 32, 64);
+    if (n_zero_pad > 0) {
+        const float mnew = fmaxf(m, 0.0f);
+        const float alpha = expf(m - mnew);
+        lsum = lsum * alpha + (float) n_zero_pad * expf(0.0f - mnew);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) o[i] *= alpha;
+    }
+    if (qi < T) {
+        const float inv = lsum == 0.0f ? 0.0f : 1.0f / lsum;
+        _Float16 * orow = out + ((size_t) clip * T + qi) * d + h * 64;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) {
+            half4 r;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) r[e] = (_Float16) (o[dt][e] * inv);
+            *(half4 *) (orow + dt * 16 + 4 * g) = r;
+        }
+    }
+}
+
+void attn_encoder(hipStream_t s, const _Float16 * q, const _Float16 * k, const _Float16 * vt, int n_clips, int T,
+                  int Tpad, int H, float scale, int n_zero_pad, _Float16 * out) {
+    if (Tpad < ((T + FA_KT - 1) / FA_KT) * FA_KT) throw std::runtime_error("attn_encoder: Tpad too small");
+    hipLaunchKernelGGL(k_attn_encoder, dim3((T + 63) / 64, H, n_clips), dim3(256), 0, s, q, k, vt, T, Tpad, H, scale,
+                       n_zero_pad, out);
+}
+
+// ----------------------------------------------------------------------------------
+// Decoder attention, reference-order emulation. Block = 4 waves = 4 heads of one row.
+// Phase 1 (parallel): scores s_i = dot(K_i, Q) * scale for all listed keys -> LDS.
+// Phase 2 (sequential over keys, lanes = the 64 head dims):
+//   one_chunk: if s > M { M = s; ms = exp(Mold-M); acc = f16(acc*ms); vs = 1 }
+//              else    { vs = exp(s-M) };  acc = f16(fma(v, vs, acc)); S = S*ms + vs
+//   tiled:     tiles of 16 keys, F32 accumulator (ops.cpp:8417-8510)
+// ----------------------------------------------------------------------------------
+constexpr int DA_MAX_KEYS = 2048;
+
+__global__ __launch_bounds__(256) void k_attn_decoder(const _Float16 * __restrict__ q, int ldq,
+                                                      const _Float16 * __restrict__ kb, const _Float16 * __restrict__ vb,
+                                                      int ld_kv, const AttnRow * __restrict__ rows,
+                                                      const int * __restrict__ key_idx, int H, float scale,
+                                                      _Float16 * __restrict__ out, int ldo) {
+    __shared__ float sc[4][DA_MAX_KEYS];
+    __shared__ _Float16 qs[4][64];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const AttnRow job = rows[blockIdx.y];
+    const int h = blockIdx.x * 4 + wave;
+    if (h >= H) return;
+    const int n = job.n_keys;
+    const int * list = job.key_list >= 0 ? key_idx + job.key_list : nullptr;
+    const _Float16 * kh = kb + job.kv_base + h * 64;
+    const _Float16 * vh = vb + job.kv_base + h * 64;
+
+    qs[wave][lane] = q[(size_t) job.q_row * ldq + h * 64 + lane];
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+
+    // phase 1: scores
+    for (int i = lane; i < n; i += 64) {
+        const int cell = list ? list[i] : i;
+        const half8 * kr = (const half8 *) (kh + (size_t) cell * ld_kv);
+        float acc = 0.0f;
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+            const half8 kv = kr[c];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) acc = fmaf((float) kv[e], (float) qs[wave][c * 8 + e], acc);
+        }
+        sc[wave][i] = acc * scale;
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+
+    float result;
+    if (job.mode == 0) {
+        float M = -INFINITY, S = 0.0f, acc = 0.0f;  // acc always holds an f16-representable value
+        int i = 0;
+        // prefetch V for the first key
+        for (; i < n; ++i) {
+            const int cell = list ? list[i] : i;
+            const float v = (float) vh[(size_t) cell * ld_kv + lane];
+            const float s = sc[wave][i];
+            float ms = 1.0f, vs = 1.0f;
+            if (s > M) {
+                const float Mold = M;
+                M = s;
+                ms = expf(Mold - M);
+                acc = (float) (_Float16) (acc * ms);
+            } else {
+                vs = expf(s - M);
+            }
+            acc = (float) (_Float16) fmaf(v, vs, acc);
+            S = fmaf(S, ms, vs);
+        }
+        for (int j = 0; j < job.n_zero_pad; ++j) {  // all-zero keys: s = 0, v = 0
+            float ms = 1.0f, vs = 1.0f;
+            if (0.0f > M) {
+                const float Mold = M;
+                M = 0.0f;
+                ms = expf(Mold - M);
+                acc = (float) (_Float16) (acc * ms);
+            } else {
+                vs = expf(0.0f - M);
+            }
+            S = fmaf(S, ms, vs);
+        }
+        const float S_inv = S == 0.0f ? 0.0f : 1.0f / S;
+        result = acc * S_inv;
+    } else {
+        float M = -INFINITY, S = 0.0f, acc = 0.0f;
+        const int total = n + job.n_zero_pad;
+        for (int t0 = 0; t0 < total; t0 += 16) {
+            const int t1 = min(t0 + 16, total);
+            float tmax = -INFINITY;
+            for (int i = t0; i < t1; ++i) tmax = fmaxf(tmax, i < n ? sc[wave][i] : 0.0f);
+            if (tmax == -INFINITY) continue;
+            const float Mnew = fmaxf(M, tmax);
+            if (Mnew > M) {
+                const float ms = expf(M - Mnew);
+                acc *= ms;
+                S *= ms;
+            }
+            M = Mnew;
+            float ts = 0.0f;
+            for (int i = t0; i < t1; ++i) {
+                const float s = i < n ? sc[wave][i] : 0.0f;
+                const float p = expf(s - Mnew);
+                ts += p;
+                if (i < n) {
+                    const int cell = list ? list[i] : i;
+                    acc = fmaf((float) vh[(size_t) cell * ld_kv + lane], p, acc);
+                }
+            }
+            S += ts;
+        }
+        const float S_inv = S == 0.0f ? 0.0f : 1.0f / S;
+        result = acc * S_inv;
+    }
+    out[(size_t) job.q_row * ldo + h * 64 + lane] = (_Float16) result;
+}
+
+void attn_decoder(hipStream_t s, const _Float16 * q, int ldq, const _Float16 * kbase, const _Float16 * vbase, int ld_kv,
+                  const AttnRow * rows_dev, int n_rows, const int * key_idx, int H, float scale, int max_keys,
+                  _Float16 * out, int ldo) {
+    if (n_rows <= 0) return;
+    if (max_keys > DA_MAX_KEYS) throw std::runtime_error("attn_decoder: too many keys");
+    hipLaunchKernelGGL(k_attn_decoder, dim3((H + 3) / 4, n_rows), dim3(256), 0, s, q, ldq, kbase, vbase, ld_kv, rows_dev,
+                       key_idx, H, scale, out, ldo);
+}
+
+} // namespace owk

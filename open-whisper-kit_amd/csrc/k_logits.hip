@@ -1,0 +1,255 @@
+// Logit filtering, log-softmax and token selection on the device, gfx950.
+//
+// One block per decoder row re-implements whisper_process_logits (ref
+// src/whisper.cpp:6177-6445) and the greedy branch of whisper_sample_token
+// (6460-6517) so a decode step returns ~32 bytes per sequence instead of the
+// reference's 200 KB logits download and O(n_vocab) host loop per decoder.
+// Masks are applied in the reference's order; log-sum-exp sums run in double.
+#include "kernels.h"
+
+namespace owk {
+
+constexpr int LG_THREADS = 1024;
+constexpr int LG_WAVES = LG_THREADS / 64;
+
+enum : int {
+    LF_INITIAL = 1, LF_LAST_TS = 2, LF_PENULT_TS = 4, LF_HAS_TS = 8, LF_SUPPRESS_BLANK = 16,
+    LF_NO_TS = 32, LF_TDRZ = 64, LF_SUPPRESS_EOT = 128, LF_NEED_NOSP = 256, LF_MAX_INIT_TS = 512,
+};
+
+__device__ __forceinline__ float block_max(float v, float * red) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+    const int w = threadIdx.x >> 6;
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) red[w] = v;
+    __syncthreads();
+    float r = red[0];
+    for (int i = 1; i < LG_WAVES; ++i) r = fmaxf(r, red[i]);
+    return r;
+}
+
+__device__ __forceinline__ double block_sum(double v, double * red) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    const int w = threadIdx.x >> 6;
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) red[w] = v;
+    __syncthreads();
+    double r = 0.0;
+    for (int i = 0; i < LG_WAVES; ++i) r += red[i];
+    return r;
+}
+
+// (value, index) max with the smallest index winning ties ("first max", whisper.cpp:6496-6502)
+__device__ __forceinline__ void block_argmax(float & v, int & idx, float * redv, int * redi) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const float ov = __shfl_xor(v, o, 64);
+        const int oi = __shfl_xor(idx, o, 64);
+        if (ov > v || (ov == v && oi < idx)) { v = ov; idx = oi; }
+    }
+    const int w = threadIdx.x >> 6;
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) { redv[w] = v; redi[w] = idx; }
+    __syncthreads();
+    v = redv[0]; idx = redi[0];
+    for (int i = 1; i < LG_WAVES; ++i)
+        if (redv[i] > v || (redv[i] == v && redi[i] < idx)) { v = redv[i]; idx = redi[i]; }
+}
+
+__device__ __forceinline__ bool masked(int i, int f, int ts_min, const VocabInfo & vi) {
+    if ((f & LF_SUPPRESS_BLANK) && (f & LF_INITIAL) && (i == vi.eot || i == vi.space)) return true;
+    if (i == vi.not_) return true;
+    if ((f & LF_NO_TS) && i >= vi.beg) return true;
+    if (i == vi.sot || i == vi.nosp) return true;
+    if (!(f & LF_TDRZ) && i == vi.solm) return true;
+    if (i == vi.translate || i == vi.transcribe || i == vi.prev) return true;
+    if (i >= vi.lang_begin && i < vi.lang_begin + vi.n_lang) return true;
+    if ((f & LF_SUPPRESS_EOT) && i == vi.eot) return true;
+    if (f & LF_LAST_TS) {
+        if (f & LF_PENULT_TS) { if (i >= vi.beg) return true; }
+        else if (i < vi.eot) return true;
+    }
+    if ((f & LF_INITIAL) && (f & LF_MAX_INIT_TS) && i >= vi.beg + vi.tid0_max + 1) return true;
+    if ((f & LF_HAS_TS) && i >= vi.beg && i < vi.beg + ts_min) return true;
+    return false;
+}
+
+__global__ __launch_bounds__(LG_THREADS) void k_process_logits(float * __restrict__ logits, int n_vocab,
+                                                              const LogitJob * __restrict__ jobs, VocabInfo vi,
+                                                              TokenOut * __restrict__ outv, float * __restrict__ lp_out,
+                                                              float * __restrict__ pr_out) {
+    __shared__ float redf[LG_WAVES];
+    __shared__ double redd[LG_WAVES];
+    __shared__ int redi[LG_WAVES];
+    __shared__ int apply_ts_rule;
+    const LogitJob job = jobs[blockIdx.x];
+    float * L = logits + (size_t) job.row * n_vocab;
+    const int f = job.flags;
+    const int tid = threadIdx.x;
+    TokenOut res;
+    res.nosp_prob = 0.0f;
+
+    // no_speech probability of the raw logits (whisper.cpp:7186-7196)
+    if (f & LF_NEED_NOSP) {
+        float mx = -INFINITY;
+        for (int i = tid; i < n_vocab; i += LG_THREADS) mx = fmaxf(mx, L[i]);
+        mx = block_max(mx, redf);
+        double s = 0.0;
+        for (int i = tid; i < n_vocab; i += LG_THREADS)
+            if (L[i] > -INFINITY) s += (double) expf(L[i] - mx);
+        s = block_sum(s, redd);
+        const float lse = logf((float) s) + mx;
+        res.nosp_prob = expf(L[vi.nosp] - lse);
+    }
+
+    // temperature + suppression masks (whisper.cpp:6200-6330)
+    for (int i = tid; i < n_vocab; i += LG_THREADS) {
+        float v = L[i];
+        if (job.temperature > 0.0f) v /= job.temperature;
+        if (masked(i, f, job.ts_min, vi)) v = -INFINITY;
+        L[i] = v;
+    }
+    __syncthreads();
+    for (int j = tid; j < vi.n_suppress; j += LG_THREADS) L[vi.suppress_list[j]] = -INFINITY;
+    __syncthreads();
+
+    // log_softmax (whisper_compute_logprobs, 6137-6157)
+    float mx = -INFINITY;
+    for (int i = tid; i < n_vocab; i += LG_THREADS) mx = fmaxf(mx, L[i]);
+    mx = block_max(mx, redf);
+    double s = 0.0;
+    for (int i = tid; i < n_vocab; i += LG_THREADS)
+        if (L[i] > -INFINITY) s += (double) expf(L[i] - mx);
+    s = block_sum(s, redd);
+    const float lse = logf((float) s) + mx;
+
+    // timestamp mass vs best text token (6337-6361)
+    float ts_max = -INFINITY, tx_max = -INFINITY;
+    for (int i = tid; i < n_vocab; i += LG_THREADS) {
+        const float lp = L[i] > -INFINITY ? L[i] - lse : -INFINITY;
+        if (i >= vi.beg) ts_max = fmaxf(ts_max, lp); else tx_max = fmaxf(tx_max, lp);
+    }
+    ts_max = block_max(ts_max, redf);
+    tx_max = block_max(tx_max, redf);
+    double ts_sum = 0.0;
+    for (int i = vi.beg + tid; i < n_vocab; i += LG_THREADS) {
+        const float lp = L[i] > -INFINITY ? L[i] - lse : -INFINITY;
+        if (lp > -INFINITY) ts_sum += (double) expf(lp - ts_max);
+    }
+    ts_sum = block_sum(ts_sum, redd);
+    if (tid == 0) {
+        const float ts_lp = ts_sum > 0.0 ? logf((float) ts_sum) + ts_max : -INFINITY;
+        apply_ts_rule = ts_lp > tx_max;
+    }
+    __syncthreads();
+    if (apply_ts_rule)
+        for (int i = tid; i < vi.beg; i += LG_THREADS) L[i] = -INFINITY;
+    __syncthreads();
+
+    // probs + greedy pick (whisper_compute_probs 6159-6171, whisper_sample_token 6460-6517)
+    float best = -1.0f;
+    int best_i = 0x7fffffff;
+    float tbest = -1.0f;
+    int tbest_i = 0x7fffffff;
+    double ts_psum = 0.0;
+    for (int i = tid; i < n_vocab; i += LG_THREADS) {
+        const float lp = L[i] > -INFINITY ? L[i] - lse : -INFINITY;
+        const float p = L[i] == -INFINITY ? 0.0f : expf(lp);
+        if (lp_out) lp_out[(size_t) blockIdx.x * n_vocab + i] = lp;
+        if (pr_out) pr_out[(size_t) blockIdx.x * n_vocab + i] = p;
+        if (p > best) { best = p; best_i = i; }
+        if (i >= vi.beg) {
+            ts_psum += (double) p;
+            if (p > tbest) { tbest = p; tbest_i = i; }
+        }
+    }
+    block_argmax(best, best_i, redf, redi);
+    block_argmax(tbest, tbest_i, redf, redi);
+    ts_psum = block_sum(ts_psum, redd);
+    if (tid == 0) {
+        res.id = best > 0.0f ? best_i : 0;
+        res.p = best > 0.0f ? best : 0.0f;
+        res.plog = L[res.id] > -INFINITY ? L[res.id] - lse : -INFINITY;
+        // max_ts starts at 0 in the reference: tid stays 0 unless some ts prob > 0
+        res.tid = tbest > 0.0f ? tbest_i : 0;
+        const double max_ts = tbest > 0.0f ? (double) tbest : 0.0;
+        res.pt = (float) (max_ts / (ts_psum + 1e-10));
+        res.ptsum = (float) ts_psum;
+        if (res.id >= vi.beg) {
+            res.tid = res.id;
+            res.pt = res.p;
+        }
+        res.pad_ = 0.0f;
+        outv[blockIdx.x] = res;
+    }
+}
+
+// ---------------------------------------------------------------------------------
+// state->logits emulation for the no-speech probability. The reference computes it
+// with whisper_compute_logprobs(state->logits, n_vocab, ...) (ref 7186-7196): the max
+// is taken over the WHOLE [n_tokens][n_vocab] buffer (only the flagged rows of the
+// last decode call are fresh, the others hold stale or zero-initialised values) while
+// the soft-max runs over row 0. The engine keeps row 0 and per-row maxima per clip.
+// ---------------------------------------------------------------------------------
+__global__ __launch_bounds__(LG_THREADS) void k_row_max(const float * __restrict__ logits, int n_vocab,
+                                                       float * __restrict__ out) {
+    __shared__ float redf[LG_WAVES];
+    const float * L = logits + (size_t) blockIdx.x * n_vocab;
+    float mx = -INFINITY;
+    for (int i = threadIdx.x; i < n_vocab; i += LG_THREADS) mx = fmaxf(mx, L[i]);
+    mx = block_max(mx, redf);
+    if (threadIdx.x == 0) out[blockIdx.x] = mx;
+}
+
+void logits_row_max(hipStream_t s, const float * logits, int n_rows, int n_vocab, float * out_dev) {
+    if (n_rows <= 0) return;
+    hipLaunchKernelGGL(k_row_max, dim3(n_rows), dim3(LG_THREADS), 0, s, logits, n_vocab, out_dev);
+}
+
+// dst_rows[i] <- logits row src_rows[i]  (dst index -1: zero fill)
+__global__ void k_copy_rows(const float * __restrict__ logits, int n_vocab, const int2 * __restrict__ map,
+                            float * __restrict__ dst) {
+    const int2 m = map[blockIdx.x];
+    float * d = dst + (size_t) m.y * n_vocab;
+    const float * s = logits + (size_t) m.x * n_vocab;
+    for (int i = threadIdx.x; i < n_vocab; i += blockDim.x) d[i] = m.x >= 0 ? s[i] : 0.0f;
+}
+
+void logits_copy_rows(hipStream_t s, const float * logits, int n_vocab, const int2 * map_dev, int n, float * dst) {
+    if (n <= 0) return;
+    hipLaunchKernelGGL(k_copy_rows, dim3(n), dim3(256), 0, s, logits, n_vocab, map_dev, dst);
+}
+
+// prob[nosp] of soft-max(row) with an externally supplied max
+__global__ __launch_bounds__(LG_THREADS) void k_nosp(const float * __restrict__ rows, int n_vocab,
+                                                    const int * __restrict__ row_idx, const float * __restrict__ mx,
+                                                    int nosp, float * __restrict__ out) {
+    __shared__ double redd[LG_WAVES];
+    const float * L = rows + (size_t) row_idx[blockIdx.x] * n_vocab;
+    const float m = mx[blockIdx.x];
+    double s = 0.0;
+    for (int i = threadIdx.x; i < n_vocab; i += LG_THREADS)
+        if (L[i] > -INFINITY) s += (double) expf(L[i] - m);
+    s = block_sum(s, redd);
+    if (threadIdx.x == 0) {
+        const float lse = logf((float) s) + m;
+        out[blockIdx.x] = expf(L[nosp] - lse);
+    }
+}
+
+void nosp_probs(hipStream_t s, const float * rows, int n_vocab, const int * row_idx_dev, const float * max_dev, int n,
+                int nosp, float * out_dev) {
+    if (n <= 0) return;
+    hipLaunchKernelGGL(k_nosp, dim3(n), dim3(LG_THREADS), 0, s, rows, n_vocab, row_idx_dev, max_dev, nosp, out_dev);
+}
+
+void process_logits(hipStream_t s, float * logits, int n_vocab, const LogitJob * jobs_dev, int n_jobs,
+                    const VocabInfo & vi, TokenOut * out_dev, float * logprobs_out, float * probs_out) {
+    if (n_jobs <= 0) return;
+    hipLaunchKernelGGL(k_process_logits, dim3(n_jobs), dim3(LG_THREADS), 0, s, logits, n_vocab, jobs_dev, vi, out_dev,
+                       logprobs_out, probs_out);
+}
+
+} // namespace owk

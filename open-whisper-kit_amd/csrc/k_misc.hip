@@ -1,0 +1,212 @@
+// Front-end (log-mel), normalisation, embedding and im2col kernels, gfx950.
+#include "kernels.h"
+
+namespace owk {
+
+// ----------------------------------------------------------------------------------
+// wave-level reductions (64 lanes)
+// ----------------------------------------------------------------------------------
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// ----------------------------------------------------------------------------------
+// LayerNorm -> f16 (ggml_compute_forward_norm_f32, ref ggml-cpu/ops.cpp:3578-3623,
+// followed by the separate ggml_mul / ggml_add of whisper.cpp:2103-2108): mean from a
+// double sum rounded to float, variance accumulated in double, scale = 1/sqrtf(var+eps),
+// then ((x-mean)*scale)*w + b with one rounding per op (built with -ffp-contract=off).
+// One wave per row; the f16 output feeds the next GEMM directly.
+// ----------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_layernorm_f16(const float * __restrict__ x, int rows, int d,
+                                                       const float * __restrict__ w, const float * __restrict__ b,
+                                                       float eps, _Float16 * __restrict__ out, int ldo,
+                                                       const int * __restrict__ row_idx, float * __restrict__ out32) {
+    const int lane = threadIdx.x & 63;
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= rows) return;
+    const float * xr = x + (size_t) (row_idx ? row_idx[row] : row) * d;
+    double s = 0.0;
+    for (int i = lane; i < d; i += 64) s += (double) xr[i];
+    s = wave_sum_d(s);
+    const float mean = (float) s / (float) d;
+    double v = 0.0;
+    for (int i = lane; i < d; i += 64) {
+        const float t = xr[i] - mean;
+        v += (double) (t * t);
+    }
+    v = wave_sum_d(v);
+    const float var = (float) (v / (double) d);
+    const float scale = 1.0f / sqrtf(var + eps);
+    _Float16 * o = out + (size_t) row * ldo;
+    for (int i = lane; i < d; i += 64) {
+        float y = (xr[i] - mean) * scale;
+        y = y * w[i];
+        y = y + b[i];
+        o[i] = (_Float16) y;
+        if (out32) out32[(size_t) row * d + i] = y;
+    }
+}
+
+void layernorm_f16(hipStream_t s, const float * x, int rows, int d, const float * w, const float * b, float eps,
+                   _Float16 * out, int ldo, const int * row_idx, float * out32) {
+    if (rows <= 0) return;
+    hipLaunchKernelGGL(k_layernorm_f16, dim3((rows + 3) / 4), dim3(256), 0, s, x, rows, d, w, b, eps, out, ldo,
+                       row_idx, out32);
+}
+
+// token + position embedding (whisper.cpp:2515-2518: get_rows(d_te) + get_rows(d_pe))
+__global__ void k_embed(const _Float16 * __restrict__ te, const float * __restrict__ pe, const int * __restrict__ tok,
+                        const int * __restrict__ pos, int rows, int d, float * __restrict__ x) {
+    const int r = blockIdx.x;
+    if (r >= rows) return;
+    const _Float16 * t = te + (size_t) tok[r] * d;
+    const float * p = pe + (size_t) pos[r] * d;
+    for (int i = threadIdx.x; i < d; i += blockDim.x) x[(size_t) r * d + i] = (float) t[i] + p[i];
+}
+
+void embed_tokens(hipStream_t s, const _Float16 * te, const float * pe, const int * tok, const int * pos, int rows,
+                  int d, float * x) {
+    if (rows <= 0) return;
+    hipLaunchKernelGGL(k_embed, dim3(rows), dim3(256), 0, s, te, pe, tok, pos, rows, d, x);
+}
+
+// ----------------------------------------------------------------------------------
+// Log-mel spectrogram (ref whisper.cpp:3104-3260). Per frame: reflect-padded samples
+// times the periodic Hann window (float product, as the reference), 201-bin DFT of
+// the 400-sample frame evaluated in double (the reference's float radix-2/DFT FFT is
+// a rounding of this), power, mel projection summed in double, log10(max(., 1e-10)).
+// Frames past n_samples/160 hold only zero padding -> log10(1e-10) = -10 exactly.
+// One block per (frame, clip).
+// ----------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_mel(const MelJob * __restrict__ jobs, const float * __restrict__ filters,
+                                             int n_mel, const float * __restrict__ hann,
+                                             const double * __restrict__ tw) {
+    const MelJob job = jobs[blockIdx.y];
+    const int f = blockIdx.x;
+    if (f >= job.n_len) return;
+    const int n = job.n_samples;
+    const int n_w = n + 200;  // samples after the 200-sample reflect pad
+    const int n_compute = min(n_w / 160 + 1, job.n_len);
+    float * mel = job.mel;
+    if (f >= n_compute) {
+        for (int m = threadIdx.x; m < n_mel; m += blockDim.x) mel[(size_t) m * job.n_len + f] = -10.0f;
+        return;
+    }
+    __shared__ double frame[400];
+    __shared__ double power[201];
+    const int off = f * 160;
+    for (int j = threadIdx.x; j < 400; j += blockDim.x) {
+        const int p = off + j;  // index into the padded signal
+        float v = 0.0f;
+        if (p < n_w) {
+            v = p < 200 ? job.pcm[200 - p] : job.pcm[p - 200];
+        }
+        frame[j] = (double) (hann[j] * v);
+    }
+    __syncthreads();
+    for (int k = threadIdx.x; k < 201; k += blockDim.x) {
+        double re = 0.0, im = 0.0;
+        int idx = 0;
+        for (int j = 0; j < 400; ++j) {
+            const double x = frame[j];
+            re += x * tw[idx];
+            im -= x * tw[400 + idx];
+            idx += k;
+            if (idx >= 400) idx -= 400;
+        }
+        power[k] = re * re + im * im;
+    }
+    __syncthreads();
+    for (int m = threadIdx.x; m < n_mel; m += blockDim.x) {
+        const float * fr = filters + (size_t) m * 201;
+        double sum = 0.0;
+        for (int k = 0; k < 201; ++k) sum += power[k] * (double) fr[k];
+        mel[(size_t) m * job.n_len + f] = (float) log10(fmax(sum, 1e-10));
+    }
+}
+
+void mel_spectrogram(hipStream_t s, const MelJob * jobs_dev, int n_jobs, int max_frames, const float * filters,
+                     int n_mel, const double * twiddle, const float * hann) {
+    if (n_jobs <= 0 || max_frames <= 0) return;
+    hipLaunchKernelGGL(k_mel, dim3(max_frames, n_jobs), dim3(256), 0, s, jobs_dev, filters, n_mel, hann, twiddle);
+}
+
+// global max over the whole (padded) clip, clamp to max-8, (x+4)/4 (whisper.cpp:3228-3244)
+__global__ __launch_bounds__(1024) void k_mel_norm(const MelJob * __restrict__ jobs, int n_mel) {
+    const MelJob job = jobs[blockIdx.x];
+    const size_t total = (size_t) n_mel * job.n_len;
+    float m = -1e20f;
+    for (size_t i = threadIdx.x; i < total; i += blockDim.x) m = fmaxf(m, job.mel[i]);
+    __shared__ float red[1024];
+    red[threadIdx.x] = m;
+    __syncthreads();
+    for (int o = 512; o > 0; o >>= 1) {
+        if ((int) threadIdx.x < o) red[threadIdx.x] = fmaxf(red[threadIdx.x], red[threadIdx.x + o]);
+        __syncthreads();
+    }
+    const double mmax = (double) red[0] - 8.0;
+    for (size_t i = threadIdx.x; i < total; i += blockDim.x) {
+        float v = job.mel[i];
+        if ((double) v < mmax) v = (float) mmax;
+        job.mel[i] = (float) (((double) v + 4.0) / 4.0);
+    }
+}
+
+void mel_normalize(hipStream_t s, const MelJob * jobs_dev, int n_jobs, int n_mel) {
+    if (n_jobs <= 0) return;
+    hipLaunchKernelGGL(k_mel_norm, dim3(n_jobs), dim3(1024), 0, s, jobs_dev, n_mel);
+}
+
+// ----------------------------------------------------------------------------------
+// im2col for the two conv1d layers (ggml_conv_1d_ph: im2col to F16 then mul_mat,
+// ref ggml.c:4409-4437; whisper.cpp:2006-2014). Column index = c*3 + k, matching the
+// weight's [out][in][k] memory order; K is zero-padded to the GEMM's 64 granule.
+// ----------------------------------------------------------------------------------
+__global__ void k_conv1_im2col(const MelWindow * __restrict__ wins, int n_mel, int n_ctx2, int kpad,
+                               _Float16 * __restrict__ A) {
+    const int clip = blockIdx.y;
+    const MelWindow w = wins[clip];
+    const size_t per_clip = (size_t) n_ctx2 * kpad;
+    for (size_t e = (size_t) blockIdx.x * blockDim.x + threadIdx.x; e < per_clip; e += (size_t) gridDim.x * blockDim.x) {
+        const int t = (int) (e / kpad), col = (int) (e % kpad);
+        float v = 0.0f;
+        if (col < 3 * n_mel) {
+            const int c = col / 3, k = col - 3 * c;
+            const int u = t + k - 1;  // position inside the window (padding 1)
+            if (u >= 0 && u < n_ctx2) {
+                const int src = w.offset + u;
+                if (src < w.n_len) v = w.mel[(size_t) c * w.n_len + src];
+            }
+        }
+        A[(size_t) clip * per_clip + e] = (_Float16) v;
+    }
+}
+
+void conv1_im2col(hipStream_t s, const MelWindow * win_dev, int n_clips, int n_mel, int n_ctx2, int kpad, _Float16 * A) {
+    hipLaunchKernelGGL(k_conv1_im2col, dim3(512, n_clips), dim3(256), 0, s, win_dev, n_mel, n_ctx2, kpad, A);
+}
+
+// conv2: stride 2, padding 1, input is the f16 conv1 output [clip][t_in][d]
+__global__ void k_conv2_im2col(const _Float16 * __restrict__ x, int t_in, int d, _Float16 * __restrict__ A) {
+    const int clip = blockIdx.y;
+    const int t_out = t_in / 2;
+    const int K = 3 * d;
+    const size_t per_clip = (size_t) t_out * K;
+    const _Float16 * xc = x + (size_t) clip * t_in * d;
+    for (size_t e = (size_t) blockIdx.x * blockDim.x + threadIdx.x; e < per_clip; e += (size_t) gridDim.x * blockDim.x) {
+        const int t = (int) (e / K), col = (int) (e % K);
+        const int c = col / 3, k = col - 3 * c;
+        const int u = 2 * t + k - 1;
+        _Float16 v = (_Float16) 0.0f;
+        if (u >= 0 && u < t_in) v = xc[(size_t) u * d + c];
+        A[(size_t) clip * per_clip + e] = v;
+    }
+}
+
+void conv2_im2col(hipStream_t s, const _Float16 * x, int n_clips, int t_in, int d, _Float16 * A) {
+    hipLaunchKernelGGL(k_conv2_im2col, dim3(1024, n_clips), dim3(256), 0, s, x, t_in, d, A);
+}
+
+} // namespace owk

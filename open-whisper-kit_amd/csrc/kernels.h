@@ -1,0 +1,151 @@
+// Launch interfaces of the gfx950 kernels (implemented in k_*.hip).
+#pragma once
+
+#include "common.h"
+
+namespace owk {
+
+// ---------------------------------------------------------------------------------
+// GEMM epilogues. Every dense op of the Whisper graph is C[M,N] = A[M,K] * W[N,K]^T
+// with A = f16 activations (the reference rounds every mul_mat activation to F16,
+// ggml-cpu vec_dot_type F16) and W = f16 weights, f32 accumulate; what differs is the
+// fused epilogue (bias / scale / GELU / residual / layout scatter).
+// ---------------------------------------------------------------------------------
+enum EpiMode : int {
+    EPI_F16 = 0,        // out16[r*ldo+c] = f16((acc + bias[c]) * scale)
+    EPI_GELU_F16 = 1,   // out16 = gelu_tab(acc + bias)                   (mlp.0, conv1)
+    EPI_RESID_F32 = 2,  // out32[r*ldo+c] = resid[r*ldo+c] + (acc + bias)  (attn.out, mlp.2)
+    EPI_CONV2 = 3,      // out32[r*ldo+c] = pos[(r%T)*ldo+c] + gelu(acc + bias)  (conv2 + e_pe)
+    EPI_QKV_ENC = 4,    // Q/K/V split; V written transposed per (clip, head) for attention
+    EPI_KV_CROSS = 5,   // cross K (scaled) / V (+bias) split into the cross-KV cache
+    EPI_QKV_DEC = 6,    // decoder self-attn: Q (bias, scale), K (scale), V (bias) -> KV cells
+    EPI_F32 = 7,        // out32[r*ldo+c] = acc  (logits)
+};
+
+struct EpiParams {
+    const float * bias = nullptr;   // [N] (or [d] slices for split modes)
+    const float * bias2 = nullptr;  // second bias (V bias in split modes)
+    float scale = 1.0f;
+    const float * resid = nullptr;  // f32 residual input
+    float * out32 = nullptr;
+    _Float16 * out16 = nullptr;
+    _Float16 * out16b = nullptr;    // K (split modes)
+    _Float16 * out16c = nullptr;    // V (split modes)
+    int ldo = 0;                    // leading dim of out32/out16/resid
+    int d = 0;                      // model width for split modes
+    int T = 0;                      // rows per clip (EPI_CONV2, EPI_QKV_ENC)
+    int Tpad = 0;                   // padded key count of the transposed V (EPI_QKV_ENC)
+    const float * pos = nullptr;    // EPI_CONV2 positional embedding [T][d]
+    const uint16_t * gelu_tab = nullptr;  // 65536-entry f16 GELU table
+    const int64_t * row_off = nullptr;    // EPI_QKV_DEC: element offset of each row's KV cell
+    const int * slot_map = nullptr;       // EPI_KV_CROSS: clip index -> cross-KV slot (null = identity)
+};
+
+// large tiles (encoder / conv / cross-KV / long prefill): A [M,lda] f16, W [N,ldw] f16
+void gemm_f16(hipStream_t s, int mode, int M, int N, int K, const _Float16 * A, int lda,
+              const _Float16 * W, int ldw, const EpiParams & ep);
+// skinny (decode steps, M <= 64): split-K across the waves of a block, LDS reduction
+void gemm_f16_skinny(hipStream_t s, int mode, int M, int N, int K, const _Float16 * A, int lda,
+                     const _Float16 * W, int ldw, const EpiParams & ep);
+// dispatch on M
+void gemm(hipStream_t s, int mode, int M, int N, int K, const _Float16 * A, int lda,
+          const _Float16 * W, int ldw, const EpiParams & ep);
+
+// ---------------------------------------------------------------------------------
+// normalisation / elementwise
+// ---------------------------------------------------------------------------------
+// out16[r] = f16(LN(x[r]) * w + b); mean/variance accumulated in double (ref ops.cpp:3578-3623)
+// row_idx (optional): output row i normalises input row row_idx[i]; out32 (optional) f32 copy
+void layernorm_f16(hipStream_t s, const float * x, int rows, int d, const float * w, const float * b,
+                   float eps, _Float16 * out, int ldo, const int * row_idx = nullptr, float * out32 = nullptr);
+// decoder input embedding: x[r] = f32(tok_emb[tok[r]]) + pos_emb[pos[r]]
+void embed_tokens(hipStream_t s, const _Float16 * tok_emb, const float * pos_emb, const int * tokens,
+                  const int * pos, int rows, int d, float * x);
+
+// ---------------------------------------------------------------------------------
+// audio front-end
+// ---------------------------------------------------------------------------------
+struct MelJob {
+    const float * pcm;   // device pointer to this clip's samples
+    int n_samples;
+    int n_len;           // frames (n_samples + 480000) / 160
+    float * mel;         // device [n_mel][n_len]
+};
+// log10 power mel spectrogram, un-normalised (ref whisper.cpp:3104-3167), all jobs in one launch
+// twiddle: cos[400] then sin[400] (double); hann: periodic window [400] (float, host-computed
+// exactly as whisper_global_cache::fill_hann_window, whisper.cpp:3023-3031)
+void mel_spectrogram(hipStream_t s, const MelJob * jobs_dev, int n_jobs, int max_frames,
+                     const float * filters, int n_mel, const double * twiddle, const float * hann);
+// per-job max, clamp to max-8, (x+4)/4 (ref whisper.cpp:3228-3244)
+void mel_normalize(hipStream_t s, const MelJob * jobs_dev, int n_jobs, int n_mel);
+
+// im2col for conv1 (k=3, s=1, p=1) from each clip's mel window: A[(clip*3000 + t)][c*3+k], f16
+struct MelWindow {
+    const float * mel;   // [n_mel][n_len]
+    int n_len;
+    int offset;          // seek (frames)
+};
+void conv1_im2col(hipStream_t s, const MelWindow * win_dev, int n_clips, int n_mel, int n_ctx2,
+                  int kpad, _Float16 * A);
+// im2col for conv2 (k=3, s=2, p=1) over the f16 conv1 output [clips*3000][d]
+void conv2_im2col(hipStream_t s, const _Float16 * x, int n_clips, int t_in, int d, _Float16 * A);
+
+// ---------------------------------------------------------------------------------
+// attention
+// ---------------------------------------------------------------------------------
+// encoder self-attention (flash, MFMA) over T real keys + n_zero_pad all-zero keys
+// (the reference's GGML_PAD(1500,256) kv_pad rows, whisper.cpp:2055,2145-2159).
+// q, k: [clips*T][H*64] f16; vt: [clips][H][64][Tpad] f16; out: [clips*T][H*64] f16
+void attn_encoder(hipStream_t s, const _Float16 * q, const _Float16 * k, const _Float16 * vt,
+                  int n_clips, int T, int Tpad, int H, float scale, int n_zero_pad, _Float16 * out);
+
+// decoder attention row job: one query row attends over a list of KV rows in a given
+// order with the reference flash-attention numerics (one_chunk: F16 V accumulator,
+// ops.cpp:8140-8233; tiled: F32 accumulator, ops.cpp:8275-8546)
+struct AttnRow {
+    int q_row;          // row in q / out
+    int kv_base;        // element offset of KV row 0 for this row's clip (layer-relative)
+    int n_keys;         // number of listed key rows
+    int key_list;       // offset into key_idx (cell indices, in reference visit order); -1 = 0..n_keys-1
+    int n_zero_pad;     // trailing all-zero keys (cross attention padding)
+    int mode;           // 0 = one_chunk (F16 accumulator), 1 = tiled (F32 accumulator)
+};
+void attn_decoder(hipStream_t s, const _Float16 * q, int ldq, const _Float16 * kbase, const _Float16 * vbase,
+                  int ld_kv, const AttnRow * rows_dev, int n_rows, const int * key_idx, int H, float scale,
+                  int max_keys, _Float16 * out, int ldo);
+
+// ---------------------------------------------------------------------------------
+// logits -> token (whisper_process_logits + whisper_sample_token, greedy)
+// ---------------------------------------------------------------------------------
+struct LogitJob {
+    int row;               // logits row
+    int flags;             // bit0 is_initial, bit1 last_was_ts, bit2 penult_was_ts, bit3 has_ts,
+                           // bit4 suppress_blank, bit5 no_timestamps, bit6 tdrz, bit7 suppress_eot,
+                           // bit8 need_nosp (no_speech prob of the raw logits)
+    int ts_min;            // timestamps below token_beg + ts_min are masked (has_ts rule)
+    float temperature;
+};
+struct VocabInfo {
+    int n_vocab, eot, sot, solm, prev, nosp, not_, beg, translate, transcribe, space;
+    int lang_begin, n_lang;
+    int tid0_max;          // max initial timestamp index (max_initial_ts rule)
+    const int * suppress_list; int n_suppress;  // suppress_nst token ids
+};
+struct TokenOut {
+    int id, tid;
+    float p, plog, pt, ptsum;
+    float nosp_prob;
+    float pad_;
+};
+// per-row maxima of raw logits rows
+void logits_row_max(hipStream_t s, const float * logits, int n_rows, int n_vocab, float * out_dev);
+// dst row map[i].y <- logits row map[i].x (x < 0: zeros)
+void logits_copy_rows(hipStream_t s, const float * logits, int n_vocab, const int2 * map_dev, int n, float * dst);
+// out[i] = softmax(rows[row_idx[i]] with max max_dev[i])[nosp]
+void nosp_probs(hipStream_t s, const float * rows, int n_vocab, const int * row_idx_dev, const float * max_dev, int n,
+                int nosp, float * out_dev);
+// processes logits in place (filters applied), writes logprobs/probs when requested
+void process_logits(hipStream_t s, float * logits, int n_vocab, const LogitJob * jobs_dev, int n_jobs,
+                    const VocabInfo & vi, TokenOut * out_dev, float * logprobs_out, float * probs_out);
+
+} // namespace owk

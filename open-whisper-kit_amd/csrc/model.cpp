@@ -1,0 +1,464 @@
+// ggml-bin model loader for the MI355X engine.
+//
+// Reads exactly the file format of the reference loader (whisper_model_load,
+// ref src/whisper.cpp:1485-1956; tensor names src/whisper-arch.h:42-106) and packs
+// the weights for the GEMM kernels in one device allocation:
+//   - attention q/k/v weights concatenated into one [3d][d] matrix per layer (one GEMM)
+//   - cross-attention k/v concatenated into [2d][d] per decoder layer
+//   - conv1 weight [d][n_mels*3] zero-padded along K to a multiple of 64
+// plus device constants: the f16 GELU table, mel filterbank, DFT twiddles, Hann window.
+#include "model.h"
+
+#include <cmath>
+#include <cstdarg>
+#include <cstring>
+#include <memory>
+#include <mutex>
+
+namespace owk {
+
+static ggml_log_callback g_log_cb = nullptr;
+static void * g_log_ud = nullptr;
+
+void set_log_callback(ggml_log_callback cb, void * ud) {
+    g_log_cb = cb;
+    g_log_ud = ud;
+}
+
+void log_msg(ggml_log_level level, const char * fmt, ...) {
+    char buf[2048];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    if (g_log_cb) {
+        g_log_cb(level, buf, g_log_ud);
+    } else if (level >= GGML_LOG_LEVEL_WARN) {
+        fputs(buf, stderr);
+    }
+}
+
+const std::map<std::string, std::pair<int, std::string>> & languages() {
+    static const char * tab[][2] = {
+        {"en", "english"}, {"zh", "chinese"}, {"de", "german"}, {"es", "spanish"}, {"ru", "russian"},
+        {"ko", "korean"}, {"fr", "french"}, {"ja", "japanese"}, {"pt", "portuguese"}, {"tr", "turkish"},
+        {"pl", "polish"}, {"ca", "catalan"}, {"nl", "dutch"}, {"ar", "arabic"}, {"sv", "swedish"},
+        {"it", "italian"}, {"id", "indonesian"}, {"hi", "hindi"}, {"fi", "finnish"}, {"vi", "vietnamese"},
+        {"he", "hebrew"}, {"uk", "ukrainian"}, {"el", "greek"}, {"ms", "malay"}, {"cs", "czech"},
+        {"ro", "romanian"}, {"da", "danish"}, {"hu", "hungarian"}, {"ta", "tamil"}, {"no", "norwegian"},
+        {"th", "thai"}, {"ur", "urdu"}, {"hr", "croatian"}, {"bg", "bulgarian"}, {"lt", "lithuanian"},
+        {"la", "latin"}, {"mi", "maori"}, {"ml", "malayalam"}, {"cy", "welsh"}, {"sk", "slovak"},
+        {"te", "telugu"}, {"fa", "persian"}, {"lv", "latvian"}, {"bn", "bengali"}, {"sr", "serbian"},
+        {"az", "azerbaijani"}, {"sl", "slovenian"}, {"kn", "kannada"}, {"et", "estonian"}, {"mk", "macedonian"},
+        {"br", "breton"}, {"eu", "basque"}, {"is", "icelandic"}, {"hy", "armenian"}, {"ne", "nepali"},
+        {"mn", "mongolian"}, {"bs", "bosnian"}, {"kk", "kazakh"}, {"sq", "albanian"}, {"sw", "swahili"},
+        {"gl", "galician"}, {"mr", "marathi"}, {"pa", "punjabi"}, {"si", "sinhala"}, {"km", "khmer"},
+        {"sn", "shona"}, {"yo", "yoruba"}, {"so", "somali"}, {"af", "afrikaans"}, {"oc", "occitan"},
+        {"ka", "georgian"}, {"be", "belarusian"}, {"tg", "tajik"}, {"sd", "sindhi"}, {"gu", "gujarati"},
+        {"am", "amharic"}, {"yi", "yiddish"}, {"lo", "lao"}, {"uz", "uzbek"}, {"fo", "faroese"},
+        {"ht", "haitian creole"}, {"ps", "pashto"}, {"tk", "turkmen"}, {"nn", "nynorsk"}, {"mt", "maltese"},
+        {"sa", "sanskrit"}, {"lb", "luxembourgish"}, {"my", "myanmar"}, {"bo", "tibetan"}, {"tl", "tagalog"},
+        {"mg", "malagasy"}, {"as", "assamese"}, {"tt", "tatar"}, {"haw", "hawaiian"}, {"ln", "lingala"},
+        {"ha", "hausa"}, {"ba", "bashkir"}, {"jw", "javanese"}, {"su", "sundanese"}, {"yue", "cantonese"},
+    };
+    static std::map<std::string, std::pair<int, std::string>> m;
+    static std::once_flag once;
+    std::call_once(once, [] {
+        for (int i = 0; i < (int) (sizeof(tab) / sizeof(tab[0])); ++i) m[tab[i][0]] = {i, tab[i][1]};
+    });
+    return m;
+}
+
+// ---------------------------------------------------------------------------------
+// GELU table: ggml_table_gelu_f16[i] = fp16(gelu_f32(fp32(i))) with
+// gelu_f32(x) = 0.5*x*(1 + tanh(sqrt(2/pi)*x*(1 + 0.044715*x^2)))  (ggml-cpu/vec.h:975-977).
+// The reference build (gcc, GNU mode, FMA ISA) contracts 1 + a*x*x into one fma; the
+// same contraction is written explicitly here (pinned by tests/test_oracle_pin.py).
+// ---------------------------------------------------------------------------------
+static void build_gelu_table(std::vector<uint16_t> & tab) {
+    const float GELU_COEF_A = 0.044715f;
+    const float SQRT_2_OVER_PI = 0.79788456080286535587989211986876f;
+    tab.resize(65536);
+    for (int i = 0; i < 65536; ++i) {
+        const float x = f16_to_f32_host((uint16_t) i);
+        const float inner = fmaf(GELU_COEF_A * x, x, 1.0f);
+        const float g = 0.5f * x * (1.0f + tanhf(SQRT_2_OVER_PI * x * inner));
+        tab[i] = f32_to_f16_host(g);
+    }
+}
+
+const std::vector<uint16_t> & gelu_table_host() {
+    static std::vector<uint16_t> tab;
+    static std::once_flag once;
+    std::call_once(once, [] { build_gelu_table(tab); });
+    return tab;
+}
+
+namespace {
+
+struct Reader {
+    whisper_model_loader * l;
+    bool ok = true;
+    void read(void * dst, size_t n) {
+        if (!ok) return;
+        if (l->read(l->context, dst, n) != n) ok = false;
+    }
+    template <typename T> T get() {
+        T v{};
+        read(&v, sizeof(T));
+        return v;
+    }
+};
+
+struct TensorSpec {
+    std::string name;
+    std::vector<int64_t> ne;  // ggml order (ne[0] innermost)
+    bool f16;                 // expected storage type in an F16 model
+};
+
+std::vector<TensorSpec> expected_tensors(const HParams & hp) {
+    const int64_t d = hp.n_audio_state, dt = hp.n_text_state;
+    std::vector<TensorSpec> t;
+    auto add = [&](const std::string & n, std::vector<int64_t> ne, bool f16) { t.push_back({n, ne, f16}); };
+    add("encoder.positional_embedding", {d, hp.n_audio_ctx}, false);
+    add("encoder.conv1.weight", {3, hp.n_mels, d}, true);
+    add("encoder.conv1.bias", {1, d}, false);
+    add("encoder.conv2.weight", {3, d, d}, true);
+    add("encoder.conv2.bias", {1, d}, false);
+    add("encoder.ln_post.weight", {d}, false);
+    add("encoder.ln_post.bias", {d}, false);
+    for (int i = 0; i < hp.n_audio_layer; ++i) {
+        const std::string p = "encoder.blocks." + std::to_string(i) + ".";
+        add(p + "mlp_ln.weight", {d}, false);
+        add(p + "mlp_ln.bias", {d}, false);
+        add(p + "mlp.0.weight", {d, 4 * d}, true);
+        add(p + "mlp.0.bias", {4 * d}, false);
+        add(p + "mlp.2.weight", {4 * d, d}, true);
+        add(p + "mlp.2.bias", {d}, false);
+        add(p + "attn_ln.weight", {d}, false);
+        add(p + "attn_ln.bias", {d}, false);
+        add(p + "attn.query.weight", {d, d}, true);
+        add(p + "attn.query.bias", {d}, false);
+        add(p + "attn.key.weight", {d, d}, true);
+        add(p + "attn.value.weight", {d, d}, true);
+        add(p + "attn.value.bias", {d}, false);
+        add(p + "attn.out.weight", {d, d}, true);
+        add(p + "attn.out.bias", {d}, false);
+    }
+    add("decoder.positional_embedding", {dt, hp.n_text_ctx}, false);
+    add("decoder.token_embedding.weight", {dt, hp.n_vocab}, true);
+    add("decoder.ln.weight", {dt}, false);
+    add("decoder.ln.bias", {dt}, false);
+    for (int i = 0; i < hp.n_text_layer; ++i) {
+        const std::string p = "decoder.blocks." + std::to_string(i) + ".";
+        add(p + "mlp_ln.weight", {dt}, false);
+        add(p + "mlp_ln.bias", {dt}, false);
+        add(p + "mlp.0.weight", {dt, 4 * dt}, true);
+        add(p + "mlp.0.bias", {4 * dt}, false);
+        add(p + "mlp.2.weight", {4 * dt, dt}, true);
+        add(p + "mlp.2.bias", {dt}, false);
+        for (const char * a : {"attn", "cross_attn"}) {
+            const std::string q = p + a;
+            add(q + "_ln.weight", {dt}, false);
+            add(q + "_ln.bias", {dt}, false);
+            add(q + ".query.weight", {dt, dt}, true);
+            add(q + ".query.bias", {dt}, false);
+            add(q + ".key.weight", {dt, dt}, true);
+            add(q + ".value.weight", {dt, dt}, true);
+            add(q + ".value.bias", {dt}, false);
+            add(q + ".out.weight", {dt, dt}, true);
+            add(q + ".out.bias", {dt}, false);
+        }
+    }
+    return t;
+}
+
+struct HostTensor {
+    std::vector<uint8_t> data;  // raw bytes as stored
+    bool f16 = false;
+    bool loaded = false;
+    int64_t nelem = 0;
+};
+
+} // namespace
+
+Model * load_model(whisper_model_loader * loader, int device, std::string & err) {
+    Reader r{loader};
+    auto m = std::make_unique<Model>();
+    m->device = device;
+    HParams & hp = m->hp;
+
+    if (r.get<uint32_t>() != 0x67676d6c) { err = "invalid model data (bad magic)"; return nullptr; }
+    hp.n_vocab = r.get<int32_t>();
+    hp.n_audio_ctx = r.get<int32_t>();
+    hp.n_audio_state = r.get<int32_t>();
+    hp.n_audio_head = r.get<int32_t>();
+    hp.n_audio_layer = r.get<int32_t>();
+    hp.n_text_ctx = r.get<int32_t>();
+    hp.n_text_state = r.get<int32_t>();
+    hp.n_text_head = r.get<int32_t>();
+    hp.n_text_layer = r.get<int32_t>();
+    hp.n_mels = r.get<int32_t>();
+    hp.ftype = r.get<int32_t>();
+    if (!r.ok) { err = "truncated header"; return nullptr; }
+    if (hp.n_audio_state != hp.n_text_state || hp.n_audio_state % 64 || hp.n_audio_state / hp.n_audio_head != 64 ||
+        hp.n_text_state / hp.n_text_head != 64) {
+        err = "unsupported hyper-parameters (head dim must be 64)";
+        return nullptr;
+    }
+    switch (hp.n_audio_layer) {
+        case 4: m->type = MODEL_TINY; break;
+        case 6: m->type = MODEL_BASE; break;
+        case 12: m->type = MODEL_SMALL; break;
+        case 24: m->type = MODEL_MEDIUM; break;
+        case 32: m->type = MODEL_LARGE; break;
+        default: m->type = MODEL_UNKNOWN;
+    }
+    const int qntvr = hp.ftype / 1000;
+    (void) qntvr;
+    hp.ftype %= 1000;
+    if (hp.ftype != 1) {  // GGML_FTYPE_MOSTLY_F16
+        err = "unsupported ftype " + std::to_string(hp.ftype) + " (this engine build loads F16 models)";
+        return nullptr;
+    }
+
+    // mel filters
+    m->n_filters_mel = r.get<int32_t>();
+    m->n_filters_fft = r.get<int32_t>();
+    if (m->n_filters_fft != 201 || m->n_filters_mel <= 0 || m->n_filters_mel > 512) { err = "bad mel filters"; return nullptr; }
+    m->filters.resize((size_t) m->n_filters_mel * m->n_filters_fft);
+    r.read(m->filters.data(), m->filters.size() * sizeof(float));
+
+    // vocab (ref 1589-1675)
+    Vocab & v = m->vocab;
+    const int32_t n_vocab_file = r.get<int32_t>();
+    if (!r.ok || n_vocab_file < 0 || n_vocab_file > hp.n_vocab) { err = "bad vocab"; return nullptr; }
+    v.id_to_token.resize(std::max<int>(hp.n_vocab, n_vocab_file));
+    std::string word;
+    for (int i = 0; i < n_vocab_file; ++i) {
+        const uint32_t len = r.get<uint32_t>();
+        if (!r.ok || len > (1u << 20)) { err = "bad vocab entry"; return nullptr; }
+        word.assign(len, '\0');
+        if (len) r.read(&word[0], len);
+        v.token_to_id[word] = i;
+        v.id_to_token[i] = word;
+    }
+    v.n_vocab = hp.n_vocab;
+    if (v.is_multilingual()) {
+        v.eot++;
+        v.sot++;
+        const int dt = v.num_languages() - 98;
+        v.translate += dt; v.transcribe += dt; v.solm += dt; v.prev += dt; v.nosp += dt; v.not_ += dt; v.beg += dt;
+    }
+    if (n_vocab_file < hp.n_vocab) {
+        // reverse map of language ids for the synthesized "[_LANG_xx]" names
+        std::vector<std::string> lang_code(200);
+        for (const auto & kv : languages()) lang_code[kv.second.first] = kv.first;
+        for (int i = n_vocab_file; i < hp.n_vocab; ++i) {
+            if (i > v.beg) word = "[_TT_" + std::to_string(i - v.beg) + "]";
+            else if (i == v.eot) word = "[_EOT_]";
+            else if (i == v.sot) word = "[_SOT_]";
+            else if (i == v.translate) word = "[_TRANSLATE_]";
+            else if (i == v.transcribe) word = "[_TRANSCRIBE_]";
+            else if (i == v.solm) word = "[_SOLM_]";
+            else if (i == v.prev) word = "[_PREV_]";
+            else if (i == v.nosp) word = "[_NOSP_]";
+            else if (i == v.not_) word = "[_NOT_]";
+            else if (i == v.beg) word = "[_BEG_]";
+            else if (i > v.sot && i <= v.sot + v.num_languages()) {
+                const int lid = i - v.sot - 1;
+                word = "[_LANG_" + (lid < (int) lang_code.size() ? lang_code[lid] : std::string("")) + "]";
+            } else word = "[_extra_token_" + std::to_string(i) + "]";
+            v.token_to_id[word] = i;
+            v.id_to_token[i] = word;
+        }
+    }
+    if (!r.ok) { err = "truncated vocab"; return nullptr; }
+
+    // tensors
+    const auto specs = expected_tensors(hp);
+    std::map<std::string, size_t> idx;
+    for (size_t i = 0; i < specs.size(); ++i) idx[specs[i].name] = i;
+    std::vector<HostTensor> ht(specs.size());
+    int n_loaded = 0;
+    for (;;) {
+        int32_t n_dims = 0, name_len = 0, ttype = 0;
+        r.read(&n_dims, 4);
+        r.read(&name_len, 4);
+        r.read(&ttype, 4);
+        if (!r.ok || loader->eof(loader->context)) break;
+        if (n_dims < 1 || n_dims > 4 || name_len <= 0 || name_len > 512) { err = "bad tensor header"; return nullptr; }
+        int64_t ne[4] = {1, 1, 1, 1}, nel = 1;
+        for (int i = 0; i < n_dims; ++i) { ne[i] = r.get<int32_t>(); nel *= ne[i]; }
+        std::string name(name_len, '\0');
+        r.read(&name[0], name_len);
+        auto it = idx.find(name);
+        if (it == idx.end()) { err = "unknown tensor '" + name + "' in model file"; return nullptr; }
+        const TensorSpec & sp = specs[it->second];
+        int64_t expect = 1;
+        for (auto e : sp.ne) expect *= e;
+        for (size_t i = 0; i < sp.ne.size(); ++i)
+            if (ne[i] != sp.ne[i]) { err = "tensor '" + name + "' has wrong shape in model file"; return nullptr; }
+        if (nel != expect) { err = "tensor '" + name + "' has wrong size in model file"; return nullptr; }
+        if (ttype != 0 && ttype != 1) { err = "tensor '" + name + "': unsupported type " + std::to_string(ttype); return nullptr; }
+        if (sp.f16 && ttype != 1) { err = "tensor '" + name + "': expected F16 weights"; return nullptr; }
+        HostTensor & t = ht[it->second];
+        t.f16 = ttype == 1;
+        t.nelem = nel;
+        t.data.resize((size_t) nel * (t.f16 ? 2 : 4));
+        r.read(t.data.data(), t.data.size());
+        if (!r.ok) { err = "truncated tensor data for '" + name + "'"; return nullptr; }
+        t.loaded = true;
+        ++n_loaded;
+    }
+    m->n_loaded = n_loaded;
+    if (n_loaded == 0) {
+        log_msg(GGML_LOG_LEVEL_WARN, "whisper_model_load: WARN no tensors loaded from model file - assuming empty model for testing\n");
+    } else if (n_loaded != (int) specs.size()) {
+        err = "not all tensors loaded from model file - expected " + std::to_string(specs.size()) + ", got " +
+              std::to_string(n_loaded);
+        return nullptr;
+    }
+
+    // ---- device packing ----
+    OWK_HIP_CHECK(hipSetDevice(device));
+    const int64_t d = hp.n_audio_state;
+    m->kpad_conv1 = (int) (((3 * hp.n_mels) + 63) / 64 * 64);
+
+    // layout plan: (offset, bytes) per packed item, 256-byte aligned
+    size_t off = 0;
+    auto reserve = [&](size_t bytes) { size_t o = off; off += (bytes + 255) & ~(size_t) 255; return o; };
+    const auto & S = specs;
+    auto bytes_of = [&](const std::string & n) {
+        const TensorSpec & sp = S[idx.at(n)];
+        int64_t e = 1;
+        for (auto x : sp.ne) e *= x;
+        return (size_t) e * (sp.f16 ? 2 : 4);
+    };
+    std::map<std::string, size_t> place;  // simple tensors -> offset
+    for (const auto & sp : S) place[sp.name] = 0;
+    // packed matrices
+    const size_t o_conv1 = reserve((size_t) d * m->kpad_conv1 * 2);
+    std::vector<size_t> o_enc_qkv(hp.n_audio_layer), o_dec_qkv(hp.n_text_layer), o_dec_ckv(hp.n_text_layer);
+    for (int i = 0; i < hp.n_audio_layer; ++i) o_enc_qkv[i] = reserve((size_t) 3 * d * d * 2);
+    for (int i = 0; i < hp.n_text_layer; ++i) {
+        o_dec_qkv[i] = reserve((size_t) 3 * d * d * 2);
+        o_dec_ckv[i] = reserve((size_t) 2 * d * d * 2);
+    }
+    for (auto & kv : place) {
+        const std::string & n = kv.first;
+        const bool packed = n == "encoder.conv1.weight" ||
+                            (n.find(".key.weight") != std::string::npos) ||
+                            (n.find(".value.weight") != std::string::npos) ||
+                            (n.find("attn.query.weight") != std::string::npos && n.find("cross_attn") == std::string::npos);
+        kv.second = packed ? (size_t) -1 : reserve(bytes_of(n));
+    }
+    const size_t o_gelu = reserve(65536 * 2);
+    const size_t o_filt = reserve(m->filters.size() * 4);
+    const size_t o_tw = reserve(800 * 8);
+    const size_t o_hann = reserve(400 * 4);
+
+    m->blob.alloc(off);
+    OWK_HIP_CHECK(hipMemset(m->blob.ptr, 0, off));
+    char * base = (char *) m->blob.ptr;
+    auto up = [&](size_t o, const void * src, size_t n) { OWK_HIP_CHECK(hipMemcpy(base + o, src, n, hipMemcpyHostToDevice)); };
+    auto host = [&](const std::string & n) -> const HostTensor & { return ht[idx.at(n)]; };
+
+    if (n_loaded > 0) {
+        for (const auto & kv : place)
+            if (kv.second != (size_t) -1) up(kv.second, host(kv.first).data.data(), host(kv.first).data.size());
+        // conv1 [d][n_mels][3] -> [d][kpad]
+        {
+            const HostTensor & t = host("encoder.conv1.weight");
+            std::vector<uint16_t> p((size_t) d * m->kpad_conv1, 0);
+            const uint16_t * src = (const uint16_t *) t.data.data();
+            for (int64_t o = 0; o < d; ++o)
+                memcpy(&p[(size_t) o * m->kpad_conv1], src + (size_t) o * 3 * hp.n_mels, (size_t) 3 * hp.n_mels * 2);
+            up(o_conv1, p.data(), p.size() * 2);
+        }
+        auto cat = [&](size_t o, std::initializer_list<std::string> parts) {
+            size_t at = o;
+            for (const auto & n : parts) {
+                const HostTensor & t = host(n);
+                up(at, t.data.data(), t.data.size());
+                at += t.data.size();
+            }
+        };
+        for (int i = 0; i < hp.n_audio_layer; ++i) {
+            const std::string p = "encoder.blocks." + std::to_string(i) + ".attn.";
+            cat(o_enc_qkv[i], {p + "query.weight", p + "key.weight", p + "value.weight"});
+        }
+        for (int i = 0; i < hp.n_text_layer; ++i) {
+            const std::string p = "decoder.blocks." + std::to_string(i) + ".";
+            cat(o_dec_qkv[i], {p + "attn.query.weight", p + "attn.key.weight", p + "attn.value.weight"});
+            cat(o_dec_ckv[i], {p + "cross_attn.key.weight", p + "cross_attn.value.weight"});
+        }
+    }
+    up(o_gelu, gelu_table_host().data(), 65536 * 2);
+    up(o_filt, m->filters.data(), m->filters.size() * 4);
+    {
+        // twiddles for the 400-point DFT (double) and the periodic Hann window computed like
+        // whisper_global_cache::fill_hann_window (whisper.cpp:3023-3031): float cosf of a
+        // double argument, 0.5*(1-c) in double, stored as float.
+        std::vector<double> tw(800);
+        for (int i = 0; i < 400; ++i) {
+            const double th = 2.0 * M_PI * i / 400.0;
+            tw[i] = cos(th);
+            tw[400 + i] = sin(th);
+        }
+        up(o_tw, tw.data(), tw.size() * 8);
+        std::vector<float> hann(400);
+        for (int i = 0; i < 400; ++i) hann[i] = (float) (0.5 * (1.0 - cosf((float) ((2.0 * M_PI * i) / (400 + 0)))));
+        up(o_hann, hann.data(), hann.size() * 4);
+    }
+
+    auto F = [&](const std::string & n) { return (const float *) (base + place.at(n)); };
+    auto H = [&](const std::string & n) { return (const _Float16 *) (base + place.at(n)); };
+    m->conv1_w = (const _Float16 *) (base + o_conv1);
+    m->conv1_b = F("encoder.conv1.bias");
+    m->conv2_w = H("encoder.conv2.weight");
+    m->conv2_b = F("encoder.conv2.bias");
+    m->e_pe = F("encoder.positional_embedding");
+    m->e_ln_w = F("encoder.ln_post.weight");
+    m->e_ln_b = F("encoder.ln_post.bias");
+    m->enc.resize(hp.n_audio_layer);
+    for (int i = 0; i < hp.n_audio_layer; ++i) {
+        const std::string p = "encoder.blocks." + std::to_string(i) + ".";
+        EncLayerW & L = m->enc[i];
+        L.attn_ln_w = F(p + "attn_ln.weight"); L.attn_ln_b = F(p + "attn_ln.bias");
+        L.mlp_ln_w = F(p + "mlp_ln.weight"); L.mlp_ln_b = F(p + "mlp_ln.bias");
+        L.w_qkv = (const _Float16 *) (base + o_enc_qkv[i]);
+        L.b_q = F(p + "attn.query.bias"); L.b_v = F(p + "attn.value.bias");
+        L.w_o = H(p + "attn.out.weight"); L.b_o = F(p + "attn.out.bias");
+        L.w_mlp0 = H(p + "mlp.0.weight"); L.b_mlp0 = F(p + "mlp.0.bias");
+        L.w_mlp1 = H(p + "mlp.2.weight"); L.b_mlp1 = F(p + "mlp.2.bias");
+    }
+    m->d_te = H("decoder.token_embedding.weight");
+    m->d_pe = F("decoder.positional_embedding");
+    m->d_ln_w = F("decoder.ln.weight");
+    m->d_ln_b = F("decoder.ln.bias");
+    m->dec.resize(hp.n_text_layer);
+    for (int i = 0; i < hp.n_text_layer; ++i) {
+        const std::string p = "decoder.blocks." + std::to_string(i) + ".";
+        DecLayerW & L = m->dec[i];
+        L.attn_ln_w = F(p + "attn_ln.weight"); L.attn_ln_b = F(p + "attn_ln.bias");
+        L.cross_ln_w = F(p + "cross_attn_ln.weight"); L.cross_ln_b = F(p + "cross_attn_ln.bias");
+        L.mlp_ln_w = F(p + "mlp_ln.weight"); L.mlp_ln_b = F(p + "mlp_ln.bias");
+        L.w_qkv = (const _Float16 *) (base + o_dec_qkv[i]);
+        L.b_q = F(p + "attn.query.bias"); L.b_v = F(p + "attn.value.bias");
+        L.w_o = H(p + "attn.out.weight"); L.b_o = F(p + "attn.out.bias");
+        L.cw_q = H(p + "cross_attn.query.weight"); L.cb_q = F(p + "cross_attn.query.bias");
+        L.cw_kv = (const _Float16 *) (base + o_dec_ckv[i]);
+        L.cb_v = F(p + "cross_attn.value.bias");
+        L.cw_o = H(p + "cross_attn.out.weight"); L.cb_o = F(p + "cross_attn.out.bias");
+        L.w_mlp0 = H(p + "mlp.0.weight"); L.b_mlp0 = F(p + "mlp.0.bias");
+        L.w_mlp1 = H(p + "mlp.2.weight"); L.b_mlp1 = F(p + "mlp.2.bias");
+    }
+    m->gelu_tab = (const uint16_t *) (base + o_gelu);
+    m->mel_filters = (const float *) (base + o_filt);
+    m->twiddle = (const double *) (base + o_tw);
+    m->hann = (const float *) (base + o_hann);
+    return m.release();
+}
+
+} // namespace owk

@@ -1,0 +1,90 @@
+// Internal definitions of whisper_context / whisper_state for the MI355X engine.
+#pragma once
+
+#include <memory>
+#include <mutex>
+#include <random>
+#include <string>
+#include <vector>
+
+#include "engine.h"
+#include "kv_cells.h"
+#include "model.h"
+#include "owk.h"
+#include "whisper.h"
+
+namespace owk {
+
+struct Segment {
+    int64_t t0 = 0, t1 = 0;
+    std::string text;
+    float no_speech_prob = 0.0f;
+    std::vector<whisper_token_data> tokens;
+    bool speaker_turn_next = false;
+};
+
+// whisper_sequence (ref src/whisper.cpp:783-794)
+struct Sequence {
+    std::vector<whisper_token_data> tokens;
+    int result_len = 0;
+    double sum_logprobs_all = 0, sum_logprobs = 0, avg_logprobs = 0, entropy = 0, score = 0;
+};
+
+// whisper_decoder (ref 797-820) minus grammar state
+struct Decoder {
+    Sequence sequence;
+    int i_batch = 0;        // logits row of this decoder in the current decode call
+    int seek_delta = 0;
+    bool failed = false, completed = false, has_ts = false;
+    std::vector<float> probs, logits, logprobs;  // host copies (sampling / beam / callback paths)
+    TokenOut gtok{};        // device-side greedy pick for the current logits
+    std::mt19937 rng;
+};
+
+constexpr int MAX_DECODERS = 8;  // WHISPER_MAX_DECODERS (ref 142)
+
+} // namespace owk
+
+struct whisper_state {
+    std::unique_ptr<owk::Engine> eng;
+    int64_t t_sample_us = 0, t_encode_us = 0, t_decode_us = 0, t_batchd_us = 0, t_prompt_us = 0, t_mel_us = 0;
+    int32_t n_sample = 0, n_encode = 0, n_decode = 0, n_batchd = 0, n_prompt = 0, n_fail_p = 0, n_fail_h = 0;
+    int32_t kv_self_n_dec = 1;
+    owk::KvCells kv;  // cell map of slot 0 (staged API) / of this clip in batch mode
+    int mel_n_len = 0, mel_n_len_org = 0, mel_n_mel = 0;
+    std::vector<float> logits;  // whisper_get_logits
+    std::vector<float> logits_rowmax;  // per-row maxima of the emulated state->logits buffer
+    std::vector<owk::Segment> result_all;
+    std::vector<whisper_token> prompt_past0, prompt_past1;
+    int lang_id = 0;
+    owk::Decoder decoders[owk::MAX_DECODERS];
+    float no_speech_prob = 0.0f;
+    std::vector<float> energy;
+    int64_t t_beg = 0, t_last = 0;
+    whisper_token tid_last = 0;
+};
+
+struct whisper_context {
+    int64_t t_load_us = 0, t_start_us = 0;
+    whisper_context_params params{};
+    std::unique_ptr<owk::Model> model;
+    whisper_state * state = nullptr;
+    std::string path_model;
+    owk::Prof prof;
+    std::mutex mu;
+    whisper_timings timings{};
+};
+
+namespace owk {
+int64_t time_us();
+owk::VocabInfo vocab_info(const whisper_context * ctx, const whisper_full_params & p, std::vector<int> & suppress);
+struct CallToken {  // one token of a reference decode call (whisper_batch entry)
+    int token, pos, seq;
+    bool logits;
+};
+// allocate KV cells for one reference decode call of one clip and emit engine rows
+int prepare_decode_call(whisper_state * st, int slot, const std::vector<CallToken> & toks,
+                        std::vector<DecodeRow> & rows, std::vector<int> & keys, int & n_logit);
+int full_batch(whisper_context * ctx, whisper_state ** states, const whisper_full_params * params,
+               const owk_full_ext * ext, const float * const * samples, const int * n_samples, int n_clips);
+} // namespace owk

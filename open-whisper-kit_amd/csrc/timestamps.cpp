@@ -1,0 +1,206 @@
+// Heuristic token-level timestamps (params.token_timestamps; used by the Swift SDK's
+// WhisperContext). Host-side, per emitted segment; restates the reference
+// whisper_exp_compute_token_level_timestamps (ref src/whisper.cpp:8455-8680) with its
+// helpers voice_length (8400-8422), get_signal_energy (8425-8441), the segment-relative
+// sample mapping (8443-8453) and whisper_wrap_segment (6077-6128).
+#include <algorithm>
+#include <cmath>
+
+#include "state.h"
+
+namespace owk {
+
+static float voice_length(const std::string & text) {
+    float res = 0.0f;
+    for (char c : text) {
+        if (c == ' ') res += 0.01f;
+        else if (c == ',') res += 2.00f;
+        else if (c == '.' || c == '!' || c == '?') res += 3.00f;
+        else if (c >= '0' && c <= '9') res += 3.00f;
+        else res += 1.00f;
+    }
+    return res;
+}
+
+std::vector<float> signal_energy(const float * signal, int n_samples, int hw) {
+    std::vector<float> out(n_samples);
+    for (int i = 0; i < n_samples; i++) {
+        float sum = 0;
+        for (int j = -hw; j <= hw; j++)
+            if (i + j >= 0 && i + j < n_samples) sum += fabsf(signal[i + j]);
+        out[i] = sum / (2 * hw + 1);
+    }
+    return out;
+}
+
+static int ts_to_sample(int64_t t, int64_t seg_t0, int n_samples) {
+    const int64_t rel = t - seg_t0;
+    const int s = (int) ((rel * WHISPER_SAMPLE_RATE) / 100);
+    return std::max(0, std::min(n_samples - 1, s));
+}
+
+static int64_t sample_to_ts(int i_sample, int64_t seg_t0) { return (100ll * i_sample) / WHISPER_SAMPLE_RATE + seg_t0; }
+
+void compute_token_timestamps(whisper_context * ctx, whisper_state * st, int i_segment, float thold_pt, float thold_ptsum) {
+    const Vocab & v = ctx->model->vocab;
+    Segment & seg = st->result_all[i_segment];
+    auto & tk = seg.tokens;
+    const int n_samples = (int) st->energy.size();
+    if (n_samples == 0) {
+        log_msg(GGML_LOG_LEVEL_ERROR, "whisper_exp_compute_token_level_timestamps: no signal data available\n");
+        return;
+    }
+    const int64_t t0 = seg.t0, t1 = seg.t1;
+    const int n = (int) tk.size();
+    if (n == 0) return;
+    if (n == 1) {
+        tk[0].t0 = t0;
+        tk[0].t1 = t1;
+        return;
+    }
+    int64_t & t_beg = st->t_beg;
+    int64_t & t_last = st->t_last;
+    whisper_token & tid_last = st->tid_last;
+
+    for (int j = 0; j < n; ++j) {
+        auto & token = tk[j];
+        if (j == 0) {
+            if (token.id == v.beg) {
+                tk[j].t0 = t0;
+                tk[j].t1 = t0;
+                tk[j + 1].t0 = t0;
+                t_beg = t0;
+                t_last = t0;
+                tid_last = v.beg;
+            } else {
+                tk[j].t0 = t_last;
+            }
+        }
+        const int64_t tt = t_beg + 2 * (token.tid - v.beg);
+        tk[j].vlen = voice_length(v.id_to_token[token.id]);
+        if (token.pt > thold_pt && token.ptsum > thold_ptsum && token.tid > tid_last && tt <= t1) {
+            if (j > 0) tk[j - 1].t1 = tt;
+            tk[j].t0 = tt;
+            tid_last = token.tid;
+        }
+    }
+    tk[n - 2].t1 = t1;
+    tk[n - 1].t0 = t1;
+    tk[n - 1].t1 = t1;
+    t_last = t1;
+
+    // split runs of tokens without timestamps proportionally to voice length
+    {
+        int p0 = 0, p1 = 0;
+        for (;;) {
+            while (p1 < n && tk[p1].t1 < 0) p1++;
+            if (p1 >= n) p1--;
+            if (p1 > p0) {
+                double psum = 0.0;
+                for (int j = p0; j <= p1; j++) psum += tk[j].vlen;
+                const double dt = tk[p1].t1 - tk[p0].t0;
+                for (int j = p0 + 1; j <= p1; j++) {
+                    const double ct = tk[j - 1].t0 + dt * tk[j - 1].vlen / psum;
+                    tk[j - 1].t1 = ct;
+                    tk[j].t0 = ct;
+                }
+            }
+            p1++;
+            p0 = p1;
+            if (p1 >= n) break;
+        }
+    }
+    for (int j = 0; j < n - 1; j++) {
+        if (tk[j].t1 < 0) tk[j + 1].t0 = tk[j].t1;
+        if (j > 0 && tk[j - 1].t1 > tk[j].t0) {
+            tk[j].t0 = tk[j - 1].t1;
+            tk[j].t1 = std::max(tk[j].t0, tk[j].t1);
+        }
+    }
+    // snap to voice activity
+    const int hw = WHISPER_SAMPLE_RATE / 8;
+    const auto & e = st->energy;
+    for (int j = 0; j < n; j++) {
+        if (tk[j].id >= v.eot) continue;
+        int s0 = ts_to_sample(tk[j].t0, seg.t0, n_samples);
+        int s1 = ts_to_sample(tk[j].t1, seg.t0, n_samples);
+        const int ss0 = std::max(s0 - hw, 0);
+        const int ss1 = std::min(s1 + hw, n_samples);
+        const int ns = ss1 - ss0;
+        float sum = 0.0f;
+        for (int k = ss0; k < ss1; k++) sum += e[k];
+        const float thold = 0.5 * sum / ns;
+        {
+            int k = s0;
+            if (e[k] > thold && j > 0) {
+                while (k > 0 && e[k] > thold) k--;
+                tk[j].t0 = sample_to_ts(k, seg.t0);
+                if (tk[j].t0 < tk[j - 1].t1) tk[j].t0 = tk[j - 1].t1;
+                else s0 = k;
+            } else {
+                while (e[k] < thold && k < s1) k++;
+                s0 = k;
+                tk[j].t0 = sample_to_ts(k, seg.t0);
+            }
+        }
+        {
+            int k = s1;
+            if (e[k] > thold) {
+                while (k < n_samples - 1 && e[k] > thold) k++;
+                tk[j].t1 = sample_to_ts(k, seg.t0);
+                if (j < n - 1 && tk[j].t1 > tk[j + 1].t0) tk[j].t1 = tk[j + 1].t0;
+                else s1 = k;
+            } else {
+                while (e[k] < thold && k > s0) k--;
+                s1 = k;
+                tk[j].t1 = sample_to_ts(k, seg.t0);
+            }
+        }
+    }
+}
+
+static int utf8_len(const char * s) {
+    int c = 0;
+    for (; *s; ++s)
+        if ((*s & 0xC0) != 0x80) c++;
+    return c;
+}
+
+int wrap_segment(whisper_context * ctx, whisper_state * st, int max_len, bool split_on_word) {
+    const Vocab & v = ctx->model->vocab;
+    Segment seg = st->result_all.back();
+    int res = 1, acc = 0;
+    std::string text;
+    for (int i = 0; i < (int) seg.tokens.size(); i++) {
+        const auto & token = seg.tokens[i];
+        if (token.id >= v.eot) continue;
+        const std::string & txt = v.id_to_token[token.id];
+        const int cur = utf8_len(txt.c_str());
+        const bool split_ok = !split_on_word || txt[0] == ' ';
+        if (acc + cur > max_len && i > 0 && split_ok) {
+            st->result_all.back().text = std::move(text);
+            st->result_all.back().t1 = token.t0;
+            st->result_all.back().tokens.resize(i);
+            st->result_all.back().speaker_turn_next = false;
+            Segment ns;
+            ns.t0 = token.t0;
+            ns.t1 = seg.t1;
+            ns.tokens.insert(ns.tokens.end(), seg.tokens.begin() + i, seg.tokens.end());
+            ns.speaker_turn_next = seg.speaker_turn_next;
+            ns.no_speech_prob = 0.0f;
+            st->result_all.push_back(ns);
+            acc = 0;
+            text = "";
+            seg = st->result_all.back();
+            i = -1;
+            res++;
+        } else {
+            acc += cur;
+            text += txt;
+        }
+    }
+    st->result_all.back().text = std::move(text);
+    return res;
+}
+
+} // namespace owk

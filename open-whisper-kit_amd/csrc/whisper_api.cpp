@@ -1,0 +1,973 @@
+// The drop-in C ABI (include/whisper.h) of the MI355X engine.
+//
+// Lifecycle, getters, staged encode/decode and error conventions follow the reference
+// implementation cited per function; the compute behind them is the batch engine.
+#include <algorithm>
+#include <cfloat>
+#include <cmath>
+#include <cstring>
+#include <fstream>
+#include <regex>
+#include <thread>
+
+#include "state.h"
+
+using namespace owk;
+
+namespace owk {
+void set_log_callback(ggml_log_callback cb, void * ud);
+const std::vector<uint16_t> & gelu_table_host();
+}
+
+static whisper_state * new_state(whisper_context * ctx) {
+    auto * st = new whisper_state();
+    try {
+        st->eng.reset(new Engine(ctx->model.get(), &ctx->prof));
+    } catch (const std::exception & e) {
+        log_msg(GGML_LOG_LEVEL_ERROR, "whisper_init_state: %s\n", e.what());
+        delete st;
+        return nullptr;
+    }
+    const int cells = (ctx->model->hp.n_text_ctx + 255) / 256 * 256;  // GGML_PAD(n_text_ctx, 256), ref 3387-3390
+    st->kv.init(cells);
+    st->kv_self_n_dec = 1;
+    st->decoders[0].rng = std::mt19937(0);  // ref 3470
+    return st;
+}
+
+extern "C" {
+
+void ggml_backend_load_all(void) {}
+
+const char * whisper_version(void) { return "1.8.3-mi355x"; }
+
+// ---------------------------------------------------------------------------------
+// defaults (ref whisper.cpp:3606-3622, 5928-6034)
+// ---------------------------------------------------------------------------------
+struct whisper_context_params whisper_context_default_params(void) {
+    whisper_context_params r{};
+    r.use_gpu = true;
+    r.flash_attn = true;
+    r.gpu_device = 0;
+    r.dtw_token_timestamps = false;
+    r.dtw_aheads_preset = WHISPER_AHEADS_NONE;
+    r.dtw_n_top = -1;
+    r.dtw_aheads = {0, nullptr};
+    r.dtw_mem_size = 1024 * 1024 * 128;
+    return r;
+}
+
+struct whisper_context_params * whisper_context_default_params_by_ref(void) {
+    return new whisper_context_params(whisper_context_default_params());
+}
+
+struct whisper_vad_params whisper_vad_default_params(void) {
+    // ref whisper.cpp:4438-4449
+    whisper_vad_params r{};
+    r.threshold = 0.5f;
+    r.min_speech_duration_ms = 250;
+    r.min_silence_duration_ms = 100;
+    r.max_speech_duration_s = FLT_MAX;
+    r.speech_pad_ms = 30;
+    r.samples_overlap = 0.1f;
+    return r;
+}
+
+struct whisper_vad_context_params whisper_vad_default_context_params(void) {
+    whisper_vad_context_params r{};
+    r.n_threads = 4;
+    r.use_gpu = false;
+    r.gpu_device = 0;
+    return r;
+}
+
+struct whisper_full_params whisper_full_default_params(enum whisper_sampling_strategy strategy) {
+    whisper_full_params r{};
+    r.strategy = strategy;
+    r.n_threads = std::min(4, (int32_t) std::thread::hardware_concurrency());
+    r.n_max_text_ctx = 16384;
+    r.offset_ms = 0;
+    r.duration_ms = 0;
+    r.translate = false;
+    r.no_context = true;
+    r.no_timestamps = false;
+    r.single_segment = false;
+    r.print_special = false;
+    r.print_progress = true;
+    r.print_realtime = false;
+    r.print_timestamps = true;
+    r.token_timestamps = false;
+    r.thold_pt = 0.01f;
+    r.thold_ptsum = 0.01f;
+    r.max_len = 0;
+    r.split_on_word = false;
+    r.max_tokens = 0;
+    r.debug_mode = false;
+    r.audio_ctx = 0;
+    r.tdrz_enable = false;
+    r.suppress_regex = nullptr;
+    r.initial_prompt = nullptr;
+    r.carry_initial_prompt = false;
+    r.prompt_tokens = nullptr;
+    r.prompt_n_tokens = 0;
+    r.language = "en";
+    r.detect_language = false;
+    r.suppress_blank = true;
+    r.suppress_nst = false;
+    r.temperature = 0.0f;
+    r.max_initial_ts = 1.0f;
+    r.length_penalty = -1.0f;
+    r.temperature_inc = 0.2f;
+    r.entropy_thold = 2.4f;
+    r.logprob_thold = -1.0f;
+    r.no_speech_thold = 0.6f;
+    r.greedy.best_of = -1;
+    r.beam_search.beam_size = -1;
+    r.beam_search.patience = -1.0f;
+    r.grammar_rules = nullptr;
+    r.n_grammar_rules = 0;
+    r.i_start_rule = 0;
+    r.grammar_penalty = 100.0f;
+    r.vad = false;
+    r.vad_model_path = nullptr;
+    r.vad_params = whisper_vad_default_params();
+    if (strategy == WHISPER_SAMPLING_GREEDY) r.greedy.best_of = 5;
+    else r.beam_search.beam_size = 5;
+    return r;
+}
+
+struct whisper_full_params * whisper_full_default_params_by_ref(enum whisper_sampling_strategy strategy) {
+    return new whisper_full_params(whisper_full_default_params(strategy));
+}
+
+void whisper_free_params(struct whisper_full_params * params) { delete params; }
+void whisper_free_context_params(struct whisper_context_params * params) { delete params; }
+
+// ---------------------------------------------------------------------------------
+// init / free (ref 3624-3861)
+// ---------------------------------------------------------------------------------
+struct whisper_context * whisper_init_with_params_no_state(struct whisper_model_loader * loader,
+                                                           struct whisper_context_params params) {
+    const int64_t t0 = time_us();
+    if (params.flash_attn && params.dtw_token_timestamps) {
+        log_msg(GGML_LOG_LEVEL_WARN, "%s: dtw_token_timestamps is not supported with flash_attn - disabling\n", __func__);
+        params.dtw_token_timestamps = false;
+    }
+    if (params.dtw_token_timestamps) {
+        log_msg(GGML_LOG_LEVEL_WARN, "%s: dtw_token_timestamps is not available in this engine build - disabling\n",
+                __func__);
+        params.dtw_token_timestamps = false;
+    }
+    int n_dev = 0;
+    if (hipGetDeviceCount(&n_dev) != hipSuccess || n_dev <= 0) {
+        log_msg(GGML_LOG_LEVEL_ERROR, "%s: no MI355X (gfx950) device available\n", __func__);
+        loader->close(loader->context);
+        return nullptr;
+    }
+    const int dev = std::max(0, std::min(params.gpu_device, n_dev - 1));
+    std::string err;
+    Model * m = nullptr;
+    try {
+        m = load_model(loader, dev, err);
+    } catch (const std::exception & e) {
+        err = e.what();
+    }
+    loader->close(loader->context);
+    if (!m) {
+        log_msg(GGML_LOG_LEVEL_ERROR, "whisper_model_load: %s\n", err.c_str());
+        log_msg(GGML_LOG_LEVEL_ERROR, "%s: failed to load model\n", __func__);
+        return nullptr;
+    }
+    auto * ctx = new whisper_context();
+    ctx->params = params;
+    ctx->model.reset(m);
+    ctx->t_start_us = t0;
+    ctx->t_load_us = time_us() - t0;
+    return ctx;
+}
+
+struct whisper_context * whisper_init_from_file_with_params_no_state(const char * path_model,
+                                                                     struct whisper_context_params params) {
+    auto * fin = new std::ifstream(path_model, std::ios::binary);
+    if (!*fin) {
+        log_msg(GGML_LOG_LEVEL_ERROR, "%s: failed to open '%s'\n", __func__, path_model);
+        delete fin;
+        return nullptr;
+    }
+    whisper_model_loader loader = {};
+    loader.context = fin;
+    loader.read = [](void * c, void * out, size_t n) {
+        auto * f = (std::ifstream *) c;
+        f->read((char *) out, n);
+        return (size_t) f->gcount();
+    };
+    loader.eof = [](void * c) { return ((std::ifstream *) c)->eof(); };
+    loader.close = [](void * c) {
+        auto * f = (std::ifstream *) c;
+        f->close();
+        delete f;
+    };
+    auto * ctx = whisper_init_with_params_no_state(&loader, params);
+    if (ctx) ctx->path_model = path_model;
+    return ctx;
+}
+
+struct whisper_context * whisper_init_from_buffer_with_params_no_state(void * buffer, size_t buffer_size,
+                                                                       struct whisper_context_params params) {
+    struct Buf {
+        uint8_t * p;
+        size_t size, off;
+    } buf = {(uint8_t *) buffer, buffer_size, 0};
+    whisper_model_loader loader = {};
+    loader.context = &buf;
+    loader.read = [](void * c, void * out, size_t n) {
+        Buf * b = (Buf *) c;
+        const size_t k = b->off + n < b->size ? n : b->size - b->off;
+        memcpy(out, b->p + b->off, k);
+        b->off += k;
+        return k;
+    };
+    loader.eof = [](void * c) { Buf * b = (Buf *) c; return b->off >= b->size; };
+    loader.close = [](void *) {};
+    return whisper_init_with_params_no_state(&loader, params);
+}
+
+static whisper_context * with_state(whisper_context * ctx) {
+    if (!ctx) return nullptr;
+    ctx->state = whisper_init_state(ctx);
+    if (!ctx->state) {
+        whisper_free(ctx);
+        return nullptr;
+    }
+    return ctx;
+}
+
+struct whisper_context * whisper_init_from_file_with_params(const char * path_model, struct whisper_context_params params) {
+    return with_state(whisper_init_from_file_with_params_no_state(path_model, params));
+}
+struct whisper_context * whisper_init_from_buffer_with_params(void * buffer, size_t buffer_size,
+                                                              struct whisper_context_params params) {
+    return with_state(whisper_init_from_buffer_with_params_no_state(buffer, buffer_size, params));
+}
+struct whisper_context * whisper_init_with_params(struct whisper_model_loader * loader, struct whisper_context_params params) {
+    return with_state(whisper_init_with_params_no_state(loader, params));
+}
+struct whisper_context * whisper_init_from_file(const char * path_model) {
+    return whisper_init_from_file_with_params(path_model, whisper_context_default_params());
+}
+struct whisper_context * whisper_init_from_buffer(void * buffer, size_t buffer_size) {
+    return whisper_init_from_buffer_with_params(buffer, buffer_size, whisper_context_default_params());
+}
+struct whisper_context * whisper_init(struct whisper_model_loader * loader) {
+    return whisper_init_with_params(loader, whisper_context_default_params());
+}
+struct whisper_context * whisper_init_from_file_no_state(const char * path_model) {
+    return whisper_init_from_file_with_params_no_state(path_model, whisper_context_default_params());
+}
+struct whisper_context * whisper_init_from_buffer_no_state(void * buffer, size_t buffer_size) {
+    return whisper_init_from_buffer_with_params_no_state(buffer, buffer_size, whisper_context_default_params());
+}
+struct whisper_context * whisper_init_no_state(struct whisper_model_loader * loader) {
+    return whisper_init_with_params_no_state(loader, whisper_context_default_params());
+}
+
+struct whisper_state * whisper_init_state(struct whisper_context * ctx) {
+    if (!ctx) return nullptr;
+    return new_state(ctx);
+}
+
+int whisper_ctx_init_openvino_encoder_with_state(struct whisper_context *, struct whisper_state *, const char *,
+                                                 const char *, const char *) {
+    return 1;
+}
+int whisper_ctx_init_openvino_encoder(struct whisper_context *, const char *, const char *, const char *) { return 1; }
+
+void whisper_free_state(struct whisper_state * state) { delete state; }
+
+void whisper_free(struct whisper_context * ctx) {
+    if (!ctx) return;
+    whisper_free_state(ctx->state);
+    ctx->state = nullptr;
+    delete ctx;
+}
+
+// ---------------------------------------------------------------------------------
+// staged API (ref 3875-3955)
+// ---------------------------------------------------------------------------------
+static Engine & eng_of(whisper_context * ctx, whisper_state * st) {
+    if (!st->eng) st->eng.reset(new Engine(ctx->model.get(), &ctx->prof));
+    const int cells = std::max<int>((int) st->kv.size, (ctx->model->hp.n_text_ctx + 255) / 256 * 256);
+    st->eng->reserve(1, std::max(cells, st->eng->kv_cells));
+    return *st->eng;
+}
+
+int whisper_pcm_to_mel_with_state(struct whisper_context * ctx, struct whisper_state * st, const float * samples,
+                                  int n_samples, int) {
+    try {
+        OWK_HIP_CHECK(hipSetDevice(ctx->model->device));
+        Engine & e = eng_of(ctx, st);
+        const int64_t t0 = time_us();
+        e.compute_mel({0}, {samples}, {n_samples});
+        st->t_mel_us += time_us() - t0;
+        st->mel_n_len = e.mel_len(0);
+        st->mel_n_len_org = 1 + (n_samples + 200 - 400) / 160;
+        st->mel_n_mel = ctx->model->n_filters_mel;
+    } catch (const std::exception & ex) {
+        log_msg(GGML_LOG_LEVEL_ERROR, "%s: failed to compute mel spectrogram: %s\n", __func__, ex.what());
+        return -1;
+    }
+    return 0;
+}
+
+int whisper_pcm_to_mel(struct whisper_context * ctx, const float * samples, int n_samples, int n_threads) {
+    return whisper_pcm_to_mel_with_state(ctx, ctx->state, samples, n_samples, n_threads);
+}
+
+int whisper_set_mel_with_state(struct whisper_context * ctx, struct whisper_state * st, const float * data, int n_len,
+                               int n_mel) {
+    if (n_mel != ctx->model->n_filters_mel) {
+        log_msg(GGML_LOG_LEVEL_ERROR, "%s: invalid number of mel bands: %d (expected %d)\n", __func__, n_mel,
+                ctx->model->n_filters_mel);
+        return -1;
+    }
+    try {
+        OWK_HIP_CHECK(hipSetDevice(ctx->model->device));
+        eng_of(ctx, st).set_mel(0, data, n_len, n_mel);
+    } catch (const std::exception & ex) {
+        log_msg(GGML_LOG_LEVEL_ERROR, "%s: %s\n", __func__, ex.what());
+        return -1;
+    }
+    st->mel_n_len = n_len;
+    st->mel_n_len_org = n_len;
+    st->mel_n_mel = n_mel;
+    return 0;
+}
+
+int whisper_set_mel(struct whisper_context * ctx, const float * data, int n_len, int n_mel) {
+    return whisper_set_mel_with_state(ctx, ctx->state, data, n_len, n_mel);
+}
+
+int whisper_encode_with_state(struct whisper_context * ctx, struct whisper_state * st, int offset, int) {
+    try {
+        OWK_HIP_CHECK(hipSetDevice(ctx->model->device));
+        Engine & e = eng_of(ctx, st);
+        const int64_t t0 = time_us();
+        e.encode({0}, {offset});
+        e.sync();
+        st->t_encode_us += time_us() - t0;
+        st->n_encode++;
+    } catch (const std::exception & ex) {
+        log_msg(GGML_LOG_LEVEL_ERROR, "%s: failed to eval: %s\n", __func__, ex.what());
+        return -1;
+    }
+    return 0;
+}
+
+int whisper_encode(struct whisper_context * ctx, int offset, int n_threads) {
+    return whisper_encode_with_state(ctx, ctx->state, offset, n_threads);
+}
+
+int whisper_decode_with_state(struct whisper_context * ctx, struct whisper_state * st, const whisper_token * tokens,
+                              int n_tokens, int n_past, int) {
+    if (n_tokens <= 0) return 1;
+    try {
+        OWK_HIP_CHECK(hipSetDevice(ctx->model->device));
+        Engine & e = eng_of(ctx, st);
+        // whisper_batch_prep_legacy + seq_rm (ref 511-523, 3935-3946)
+        std::vector<CallToken> toks(n_tokens);
+        for (int i = 0; i < n_tokens; ++i) toks[i] = CallToken{tokens[i], n_past + i, 0, i == n_tokens - 1};
+        st->kv.seq_rm(0, n_past, -1);
+        std::vector<DecodeRow> rows;
+        std::vector<int> keys;
+        int n_logit = 0;
+        if (prepare_decode_call(st, 0, toks, rows, keys, n_logit) < 0) {
+            log_msg(GGML_LOG_LEVEL_ERROR, "%s: failed to eval\n", __func__);
+            return 1;
+        }
+        const int64_t t0 = time_us();
+        e.decode(rows, keys, n_logit);
+        const int nv = ctx->model->hp.n_vocab;
+        st->logits.resize((size_t) n_tokens * nv);
+        e.download_logits(0, st->logits.data() + (size_t) (n_tokens - 1) * nv);
+        // keep the no-speech emulation consistent for a following whisper_full on this state
+        std::vector<float> rmax;
+        e.logits_maxes(n_logit, rmax);
+        st->logits_rowmax.resize(n_tokens, 0.0f);
+        st->logits_rowmax[n_tokens - 1] = rmax[0];
+        if (n_tokens == 1) e.row0_update({{0, 0}});
+        const int64_t dt = time_us() - t0;
+        if (n_tokens == 1) { st->t_decode_us += dt; st->n_decode++; }
+        else if (n_tokens < 16) { st->t_batchd_us += dt; st->n_batchd += n_tokens; }
+        else { st->t_prompt_us += dt; st->n_prompt += n_tokens; }
+    } catch (const std::exception & ex) {
+        log_msg(GGML_LOG_LEVEL_ERROR, "%s: failed to eval: %s\n", __func__, ex.what());
+        return 1;
+    }
+    return 0;
+}
+
+int whisper_decode(struct whisper_context * ctx, const whisper_token * tokens, int n_tokens, int n_past, int n_threads) {
+    if (ctx->state == nullptr) {
+        log_msg(GGML_LOG_LEVEL_ERROR, "%s: ERROR state was not loaded.\n", __func__);
+        return -1;
+    }
+    return whisper_decode_with_state(ctx, ctx->state, tokens, n_tokens, n_past, n_threads);
+}
+
+// ---------------------------------------------------------------------------------
+// tokenizer (greedy longest match over regex-split words, ref 3272-3320)
+// ---------------------------------------------------------------------------------
+int whisper_tokenize(struct whisper_context * ctx, const char * text, whisper_token * tokens, int n_max_tokens) {
+    const Vocab & v = ctx->model->vocab;
+    std::vector<std::string> words;
+    {
+        std::string str = text;
+        const std::regex re(R"('s|'t|'re|'ve|'m|'ll|'d| ?[[:alpha:]]+| ?[[:digit:]]+| ?[^\s[:alpha:][:digit:]]+|\s+(?!\S)|\s+)");
+        std::smatch m;
+        while (std::regex_search(str, m, re)) {
+            for (auto x : m) words.push_back(x);
+            str = m.suffix();
+        }
+    }
+    std::vector<whisper_token> res;
+    for (const auto & w : words) {
+        if (w.empty()) continue;
+        int i = 0;
+        const int n = (int) w.size();
+        while (i < n) {
+            bool found = false;
+            for (int j = n; j > i; --j) {
+                auto it = v.token_to_id.find(w.substr(i, j - i));
+                if (it != v.token_to_id.end()) {
+                    res.push_back(it->second);
+                    i = j;
+                    found = true;
+                    break;
+                }
+            }
+            if (!found) {
+                log_msg(GGML_LOG_LEVEL_ERROR, "unknown token\n");
+                ++i;
+            }
+        }
+    }
+    if (n_max_tokens < (int) res.size()) {
+        if (n_max_tokens > 0)
+            log_msg(GGML_LOG_LEVEL_ERROR, "%s: too many resulting tokens: %d (max %d)\n", __func__, (int) res.size(),
+                    n_max_tokens);
+        return -(int) res.size();
+    }
+    for (size_t i = 0; i < res.size(); ++i) tokens[i] = res[i];
+    return (int) res.size();
+}
+
+int whisper_token_count(struct whisper_context * ctx, const char * text) { return -whisper_tokenize(ctx, text, NULL, 0); }
+
+// ---------------------------------------------------------------------------------
+// languages (ref 3976-4102)
+// ---------------------------------------------------------------------------------
+int whisper_lang_max_id(void) {
+    int mx = 0;
+    for (const auto & kv : languages()) mx = std::max(mx, kv.second.first);
+    return mx;
+}
+
+int whisper_lang_id(const char * lang) {
+    const auto & L = languages();
+    if (!L.count(lang)) {
+        for (const auto & kv : L)
+            if (kv.second.second == lang) return kv.second.first;
+        log_msg(GGML_LOG_LEVEL_ERROR, "%s: unknown language '%s'\n", __func__, lang);
+        return -1;
+    }
+    return L.at(lang).first;
+}
+
+const char * whisper_lang_str(int id) {
+    for (const auto & kv : languages())
+        if (kv.second.first == id) return kv.first.c_str();
+    log_msg(GGML_LOG_LEVEL_ERROR, "%s: unknown language id %d\n", __func__, id);
+    return nullptr;
+}
+
+const char * whisper_lang_str_full(int id) {
+    for (const auto & kv : languages())
+        if (kv.second.first == id) return kv.second.second.c_str();
+    log_msg(GGML_LOG_LEVEL_ERROR, "%s: unknown language id %d\n", __func__, id);
+    return nullptr;
+}
+
+int whisper_lang_auto_detect_with_state(struct whisper_context * ctx, struct whisper_state * st, int offset_ms,
+                                        int n_threads, float * lang_probs) {
+    const int seek = offset_ms / 10;
+    if (seek < 0) return -1;
+    if (seek >= st->mel_n_len_org) return -2;
+    if (whisper_encode_with_state(ctx, st, seek, n_threads) != 0) return -6;
+    const whisper_token sot = ctx->model->vocab.sot;
+    if (whisper_decode_with_state(ctx, st, &sot, 1, 0, n_threads) != 0) return -7;
+    std::vector<std::pair<float, int>> lid;
+    for (const auto & kv : languages()) lid.emplace_back(st->logits[sot + 1 + kv.second.first], kv.second.first);
+    std::sort(lid.begin(), lid.end(), [](const std::pair<float, int> & a, const std::pair<float, int> & b) {
+        return a.first > b.first;
+    });
+    const float mx = lid[0].first;
+    double sum = 0.0;
+    for (auto & kv : lid) { kv.first = exp(kv.first - mx); sum += kv.first; }
+    for (auto & kv : lid) kv.first /= sum;
+    if (lang_probs)
+        for (const auto & kv : lid) lang_probs[kv.second] = kv.first;
+    return lid[0].second;
+}
+
+int whisper_lang_auto_detect(struct whisper_context * ctx, int offset_ms, int n_threads, float * lang_probs) {
+    return whisper_lang_auto_detect_with_state(ctx, ctx->state, offset_ms, n_threads, lang_probs);
+}
+
+// ---------------------------------------------------------------------------------
+// model / vocab queries (ref 4104-4243)
+// ---------------------------------------------------------------------------------
+int whisper_model_n_vocab(struct whisper_context * ctx) { return ctx->model->hp.n_vocab; }
+int whisper_model_n_audio_ctx(struct whisper_context * ctx) { return ctx->model->hp.n_audio_ctx; }
+int whisper_model_n_audio_state(struct whisper_context * ctx) { return ctx->model->hp.n_audio_state; }
+int whisper_model_n_audio_head(struct whisper_context * ctx) { return ctx->model->hp.n_audio_head; }
+int whisper_model_n_audio_layer(struct whisper_context * ctx) { return ctx->model->hp.n_audio_layer; }
+int whisper_model_n_text_ctx(struct whisper_context * ctx) { return ctx->model->hp.n_text_ctx; }
+int whisper_model_n_text_state(struct whisper_context * ctx) { return ctx->model->hp.n_text_state; }
+int whisper_model_n_text_head(struct whisper_context * ctx) { return ctx->model->hp.n_text_head; }
+int whisper_model_n_text_layer(struct whisper_context * ctx) { return ctx->model->hp.n_text_layer; }
+int whisper_model_n_mels(struct whisper_context * ctx) { return ctx->model->hp.n_mels; }
+int whisper_model_ftype(struct whisper_context * ctx) { return ctx->model->hp.ftype; }
+int whisper_model_type(struct whisper_context * ctx) { return (int) ctx->model->type; }
+
+const char * whisper_model_type_readable(struct whisper_context * ctx) {
+    switch (ctx->model->type) {
+        case MODEL_TINY: return "tiny";
+        case MODEL_BASE: return "base";
+        case MODEL_SMALL: return "small";
+        case MODEL_MEDIUM: return "medium";
+        case MODEL_LARGE: return "large";
+        default: return "unknown";
+    }
+}
+
+int whisper_n_len_from_state(struct whisper_state * state) { return state->mel_n_len_org; }
+int whisper_n_len(struct whisper_context * ctx) { return ctx->state->mel_n_len_org; }
+int whisper_n_vocab(struct whisper_context * ctx) { return ctx->model->vocab.n_vocab; }
+int whisper_n_text_ctx(struct whisper_context * ctx) { return ctx->model->hp.n_text_ctx; }
+int whisper_n_audio_ctx(struct whisper_context * ctx) { return ctx->model->hp.n_audio_ctx; }
+int whisper_is_multilingual(struct whisper_context * ctx) { return ctx->model->vocab.is_multilingual() ? 1 : 0; }
+float * whisper_get_logits(struct whisper_context * ctx) { return ctx->state->logits.data(); }
+float * whisper_get_logits_from_state(struct whisper_state * state) { return state->logits.data(); }
+const char * whisper_token_to_str(struct whisper_context * ctx, whisper_token token) {
+    return ctx->model->vocab.id_to_token.at(token).c_str();
+}
+whisper_token whisper_token_eot(struct whisper_context * ctx) { return ctx->model->vocab.eot; }
+whisper_token whisper_token_sot(struct whisper_context * ctx) { return ctx->model->vocab.sot; }
+whisper_token whisper_token_solm(struct whisper_context * ctx) { return ctx->model->vocab.solm; }
+whisper_token whisper_token_prev(struct whisper_context * ctx) { return ctx->model->vocab.prev; }
+whisper_token whisper_token_nosp(struct whisper_context * ctx) { return ctx->model->vocab.nosp; }
+whisper_token whisper_token_not(struct whisper_context * ctx) { return ctx->model->vocab.not_; }
+whisper_token whisper_token_beg(struct whisper_context * ctx) { return ctx->model->vocab.beg; }
+whisper_token whisper_token_lang(struct whisper_context * ctx, int lang_id) { return ctx->model->vocab.sot + 1 + lang_id; }
+whisper_token whisper_token_translate(struct whisper_context * ctx) { return ctx->model->vocab.translate; }
+whisper_token whisper_token_transcribe(struct whisper_context * ctx) { return ctx->model->vocab.transcribe; }
+
+// ---------------------------------------------------------------------------------
+// timings (ref 4245-4297)
+// ---------------------------------------------------------------------------------
+struct whisper_timings * whisper_get_timings(struct whisper_context * ctx) {
+    if (!ctx->state) return nullptr;
+    const whisper_state * s = ctx->state;
+    // the reference returns a heap object the caller never frees; a context-owned one here
+    whisper_timings & t = ctx->timings;
+    t.sample_ms = 1e-3f * s->t_sample_us / std::max(1, s->n_sample);
+    t.encode_ms = 1e-3f * s->t_encode_us / std::max(1, s->n_encode);
+    t.decode_ms = 1e-3f * s->t_decode_us / std::max(1, s->n_decode);
+    t.batchd_ms = 1e-3f * s->t_batchd_us / std::max(1, s->n_batchd);
+    t.prompt_ms = 1e-3f * s->t_prompt_us / std::max(1, s->n_prompt);
+    return &t;
+}
+
+void whisper_print_timings(struct whisper_context * ctx) {
+    const int64_t t_end = time_us();
+    log_msg(GGML_LOG_LEVEL_INFO, "\nwhisper_print_timings:     load time = %8.2f ms\n", ctx->t_load_us / 1000.0f);
+    if (ctx->state) {
+        const whisper_state * s = ctx->state;
+        const int ns = std::max(1, s->n_sample), ne = std::max(1, s->n_encode), nd = std::max(1, s->n_decode),
+                  nb = std::max(1, s->n_batchd), np = std::max(1, s->n_prompt);
+        log_msg(GGML_LOG_LEVEL_INFO, "whisper_print_timings:     fallbacks = %3d p / %3d h\n", s->n_fail_p, s->n_fail_h);
+        log_msg(GGML_LOG_LEVEL_INFO, "whisper_print_timings:      mel time = %8.2f ms\n", s->t_mel_us / 1000.0f);
+        log_msg(GGML_LOG_LEVEL_INFO, "whisper_print_timings:   sample time = %8.2f ms / %5d runs ( %8.2f ms per run)\n",
+                1e-3f * s->t_sample_us, ns, 1e-3f * s->t_sample_us / ns);
+        log_msg(GGML_LOG_LEVEL_INFO, "whisper_print_timings:   encode time = %8.2f ms / %5d runs ( %8.2f ms per run)\n",
+                1e-3f * s->t_encode_us, ne, 1e-3f * s->t_encode_us / ne);
+        log_msg(GGML_LOG_LEVEL_INFO, "whisper_print_timings:   decode time = %8.2f ms / %5d runs ( %8.2f ms per run)\n",
+                1e-3f * s->t_decode_us, nd, 1e-3f * s->t_decode_us / nd);
+        log_msg(GGML_LOG_LEVEL_INFO, "whisper_print_timings:   batchd time = %8.2f ms / %5d runs ( %8.2f ms per run)\n",
+                1e-3f * s->t_batchd_us, nb, 1e-3f * s->t_batchd_us / nb);
+        log_msg(GGML_LOG_LEVEL_INFO, "whisper_print_timings:   prompt time = %8.2f ms / %5d runs ( %8.2f ms per run)\n",
+                1e-3f * s->t_prompt_us, np, 1e-3f * s->t_prompt_us / np);
+    }
+    log_msg(GGML_LOG_LEVEL_INFO, "whisper_print_timings:    total time = %8.2f ms\n", (t_end - ctx->t_start_us) / 1000.0f);
+}
+
+void whisper_reset_timings(struct whisper_context * ctx) {
+    ctx->t_start_us = time_us();
+    if (whisper_state * s = ctx->state) {
+        s->t_mel_us = s->t_sample_us = s->t_encode_us = s->t_decode_us = s->t_batchd_us = s->t_prompt_us = 0;
+        s->n_sample = s->n_encode = s->n_decode = s->n_batchd = s->n_prompt = 0;
+    }
+}
+
+const char * whisper_print_system_info(void) {
+    static std::string s;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+    s = "MI355X/HIP : devices = " + std::to_string(n) + " | gfx950 MFMA f16 | ";
+    return s.c_str();
+}
+
+// ---------------------------------------------------------------------------------
+// whisper_full (ref 6827-7929)
+// ---------------------------------------------------------------------------------
+int whisper_full_with_state(struct whisper_context * ctx, struct whisper_state * state, struct whisper_full_params params,
+                            const float * samples, int n_samples) {
+    try {
+        return full_batch(ctx, &state, &params, nullptr, &samples, &n_samples, 1);
+    } catch (const std::exception & e) {
+        log_msg(GGML_LOG_LEVEL_ERROR, "whisper_full_with_state: %s\n", e.what());
+        return -6;
+    }
+}
+
+int whisper_full(struct whisper_context * ctx, struct whisper_full_params params, const float * samples, int n_samples) {
+    return whisper_full_with_state(ctx, ctx->state, params, samples, n_samples);
+}
+
+// Splits the audio into n_processors chunks (ref 7801-7929). The chunks run as one
+// batch on the device instead of n_processors CPU threads; merging is unchanged.
+int whisper_full_parallel(struct whisper_context * ctx, struct whisper_full_params params, const float * samples,
+                          int n_samples, int n_processors) {
+    if (n_processors == 1) return whisper_full(ctx, params, samples, n_samples);
+    if (params.vad) {
+        log_msg(GGML_LOG_LEVEL_ERROR, "whisper_full_parallel: VAD is not supported by this engine build\n");
+        return -1;
+    }
+    const int offset_samples = (WHISPER_SAMPLE_RATE * params.offset_ms) / 1000;
+    const int per = (n_samples - offset_samples) / n_processors;
+    std::vector<whisper_state *> states(n_processors);
+    std::vector<whisper_full_params> ps(n_processors, params);
+    std::vector<const float *> ptr(n_processors);
+    std::vector<int> ns(n_processors);
+    states[0] = ctx->state;
+    ps[0].print_realtime = false;
+    ptr[0] = samples;
+    ns[0] = offset_samples + per;
+    for (int i = 1; i < n_processors; ++i) {
+        states[i] = whisper_init_state(ctx);
+        if (!states[i]) return -1;
+        const int start = offset_samples + i * per;
+        ns[i] = (i == n_processors - 1) ? n_samples - start : per;
+        ptr[i] = samples + start;
+        ps[i].offset_ms = 0;
+        ps[i].print_progress = false;
+        ps[i].print_realtime = false;
+        ps[i].new_segment_callback = nullptr;
+        ps[i].new_segment_callback_user_data = nullptr;
+        ps[i].progress_callback = nullptr;
+        ps[i].progress_callback_user_data = nullptr;
+    }
+    int ret = 0;
+    try {
+        ret = full_batch(ctx, states.data(), ps.data(), nullptr, ptr.data(), ns.data(), n_processors);
+    } catch (const std::exception & e) {
+        log_msg(GGML_LOG_LEVEL_ERROR, "whisper_full_parallel: %s\n", e.what());
+        ret = -6;
+    }
+    const int64_t offset_t = (int64_t) (params.offset_ms / 10.0);
+    for (int i = 1; i < n_processors; ++i) {
+        for (auto & r : states[i]->result_all) {
+            r.t0 += 100 * ((i) * per) / WHISPER_SAMPLE_RATE + offset_t;
+            r.t1 += 100 * ((i) * per) / WHISPER_SAMPLE_RATE + offset_t;
+            if (!ctx->state->result_all.empty()) r.t0 = std::max(r.t0, ctx->state->result_all.back().t1);
+            ctx->state->result_all.push_back(std::move(r));
+            if (params.new_segment_callback)
+                params.new_segment_callback(ctx, ctx->state, 1, params.new_segment_callback_user_data);
+        }
+        whisper_state * s = states[i];
+        ctx->state->t_mel_us += s->t_mel_us;
+        ctx->state->t_sample_us += s->t_sample_us;
+        ctx->state->t_encode_us += s->t_encode_us;
+        ctx->state->t_decode_us += s->t_decode_us;
+        ctx->state->t_batchd_us += s->t_batchd_us;
+        ctx->state->t_prompt_us += s->t_prompt_us;
+        ctx->state->n_sample += s->n_sample;
+        ctx->state->n_encode += s->n_encode;
+        ctx->state->n_decode += s->n_decode;
+        ctx->state->n_batchd += s->n_batchd;
+        ctx->state->n_prompt += s->n_prompt;
+        whisper_free_state(s);
+    }
+    ctx->state->t_mel_us /= n_processors;
+    ctx->state->t_sample_us /= n_processors;
+    ctx->state->t_encode_us /= n_processors;
+    ctx->state->t_decode_us /= n_processors;
+    return ret;
+}
+
+int whisper_full_n_segments_from_state(struct whisper_state * state) { return (int) state->result_all.size(); }
+int whisper_full_n_segments(struct whisper_context * ctx) { return (int) ctx->state->result_all.size(); }
+int whisper_full_lang_id_from_state(struct whisper_state * state) { return state->lang_id; }
+int whisper_full_lang_id(struct whisper_context * ctx) { return ctx->state->lang_id; }
+int64_t whisper_full_get_segment_t0_from_state(struct whisper_state * state, int i) { return state->result_all[i].t0; }
+int64_t whisper_full_get_segment_t1_from_state(struct whisper_state * state, int i) { return state->result_all[i].t1; }
+int64_t whisper_full_get_segment_t0(struct whisper_context * ctx, int i) { return ctx->state->result_all[i].t0; }
+int64_t whisper_full_get_segment_t1(struct whisper_context * ctx, int i) { return ctx->state->result_all[i].t1; }
+bool whisper_full_get_segment_speaker_turn_next_from_state(struct whisper_state * state, int i) {
+    return state->result_all[i].speaker_turn_next;
+}
+bool whisper_full_get_segment_speaker_turn_next(struct whisper_context * ctx, int i) {
+    return ctx->state->result_all[i].speaker_turn_next;
+}
+const char * whisper_full_get_segment_text_from_state(struct whisper_state * state, int i) {
+    return state->result_all[i].text.c_str();
+}
+const char * whisper_full_get_segment_text(struct whisper_context * ctx, int i) { return ctx->state->result_all[i].text.c_str(); }
+int whisper_full_n_tokens_from_state(struct whisper_state * state, int i) { return (int) state->result_all[i].tokens.size(); }
+int whisper_full_n_tokens(struct whisper_context * ctx, int i) { return (int) ctx->state->result_all[i].tokens.size(); }
+const char * whisper_full_get_token_text_from_state(struct whisper_context * ctx, struct whisper_state * state, int i, int j) {
+    return ctx->model->vocab.id_to_token[state->result_all[i].tokens[j].id].c_str();
+}
+const char * whisper_full_get_token_text(struct whisper_context * ctx, int i, int j) {
+    return ctx->model->vocab.id_to_token[ctx->state->result_all[i].tokens[j].id].c_str();
+}
+whisper_token whisper_full_get_token_id_from_state(struct whisper_state * state, int i, int j) {
+    return state->result_all[i].tokens[j].id;
+}
+whisper_token whisper_full_get_token_id(struct whisper_context * ctx, int i, int j) { return ctx->state->result_all[i].tokens[j].id; }
+struct whisper_token_data whisper_full_get_token_data_from_state(struct whisper_state * state, int i, int j) {
+    return state->result_all[i].tokens[j];
+}
+struct whisper_token_data whisper_full_get_token_data(struct whisper_context * ctx, int i, int j) {
+    return ctx->state->result_all[i].tokens[j];
+}
+float whisper_full_get_token_p_from_state(struct whisper_state * state, int i, int j) { return state->result_all[i].tokens[j].p; }
+float whisper_full_get_token_p(struct whisper_context * ctx, int i, int j) { return ctx->state->result_all[i].tokens[j].p; }
+float whisper_full_get_segment_no_speech_prob(struct whisper_context * ctx, int i) {
+    return ctx->state->result_all[i].no_speech_prob;
+}
+float whisper_full_get_segment_no_speech_prob_from_state(struct whisper_state * state, int i) {
+    return state->result_all[i].no_speech_prob;
+}
+
+// ---------------------------------------------------------------------------------
+// VAD: not part of this engine build (SURVEY 2.1 N9, next-row candidate)
+// ---------------------------------------------------------------------------------
+struct whisper_vad_context * whisper_vad_init_from_file_with_params(const char *, struct whisper_vad_context_params) {
+    log_msg(GGML_LOG_LEVEL_ERROR, "whisper_vad_init: Silero VAD is not available in this engine build\n");
+    return nullptr;
+}
+struct whisper_vad_context * whisper_vad_init_with_params(struct whisper_model_loader * loader, struct whisper_vad_context_params) {
+    if (loader && loader->close) loader->close(loader->context);
+    log_msg(GGML_LOG_LEVEL_ERROR, "whisper_vad_init: Silero VAD is not available in this engine build\n");
+    return nullptr;
+}
+bool whisper_vad_detect_speech(struct whisper_vad_context *, const float *, int) { return false; }
+bool whisper_vad_detect_speech_stateful(struct whisper_vad_context *, const float *, int) { return false; }
+void whisper_vad_reset_state(struct whisper_vad_context *) {}
+int whisper_vad_n_probs(struct whisper_vad_context *) { return 0; }
+float * whisper_vad_probs(struct whisper_vad_context *) { return nullptr; }
+struct whisper_vad_segments * whisper_vad_segments_from_probs(struct whisper_vad_context *, struct whisper_vad_params) {
+    return nullptr;
+}
+struct whisper_vad_segments * whisper_vad_segments_from_samples(struct whisper_vad_context *, struct whisper_vad_params,
+                                                                 const float *, int) {
+    return nullptr;
+}
+int whisper_vad_segments_n_segments(struct whisper_vad_segments *) { return 0; }
+float whisper_vad_segments_get_segment_t0(struct whisper_vad_segments *, int) { return 0.0f; }
+float whisper_vad_segments_get_segment_t1(struct whisper_vad_segments *, int) { return 0.0f; }
+void whisper_vad_free_segments(struct whisper_vad_segments *) {}
+void whisper_vad_free(struct whisper_vad_context *) {}
+
+// ---------------------------------------------------------------------------------
+// microbenchmarks (ref 8107-8375: memcpy and ggml_mul_mat GFLOPS) on the device
+// ---------------------------------------------------------------------------------
+static std::string g_bench_str;
+
+int whisper_bench_memcpy(int n_threads) {
+    fputs(whisper_bench_memcpy_str(n_threads), stderr);
+    return 0;
+}
+
+const char * whisper_bench_memcpy_str(int) {
+    g_bench_str.clear();
+    try {
+        const size_t n = (size_t) 1 << 30;
+        DevBuf a, b;
+        a.alloc(n);
+        b.alloc(n);
+        OWK_HIP_CHECK(hipMemset(a.ptr, 1, n));
+        hipEvent_t e0, e1;
+        OWK_HIP_CHECK(hipEventCreate(&e0));
+        OWK_HIP_CHECK(hipEventCreate(&e1));
+        OWK_HIP_CHECK(hipMemcpy(b.ptr, a.ptr, n, hipMemcpyDeviceToDevice));
+        OWK_HIP_CHECK(hipEventRecord(e0, nullptr));
+        for (int i = 0; i < 10; ++i) OWK_HIP_CHECK(hipMemcpyAsync(b.ptr, a.ptr, n, hipMemcpyDeviceToDevice, nullptr));
+        OWK_HIP_CHECK(hipEventRecord(e1, nullptr));
+        OWK_HIP_CHECK(hipEventSynchronize(e1));
+        float ms = 0;
+        OWK_HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
+        char buf[256];
+        snprintf(buf, sizeof(buf), "memcpy: %.2f GB/s (device to device, 1 GiB x 10, read+write)\n",
+                 2.0 * 10.0 * n / (ms * 1e-3) / 1e9);
+        g_bench_str = buf;
+        (void) hipEventDestroy(e0);
+        (void) hipEventDestroy(e1);
+    } catch (const std::exception & e) {
+        g_bench_str = std::string("memcpy: failed: ") + e.what() + "\n";
+    }
+    return g_bench_str.c_str();
+}
+
+int whisper_bench_ggml_mul_mat(int n_threads) {
+    fputs(whisper_bench_ggml_mul_mat_str(n_threads), stderr);
+    return 0;
+}
+
+const char * whisper_bench_ggml_mul_mat_str(int) {
+    g_bench_str.clear();
+    try {
+        for (int N : {1024, 2048, 4096, 8192}) {
+            DevBuf a, w, c;
+            a.alloc((size_t) N * N * 2);
+            w.alloc((size_t) N * N * 2);
+            c.alloc((size_t) N * N * 2);
+            OWK_HIP_CHECK(hipMemset(a.ptr, 0x11, a.bytes));
+            OWK_HIP_CHECK(hipMemset(w.ptr, 0x11, w.bytes));
+            EpiParams ep;
+            ep.out16 = c.as<_Float16>();
+            ep.ldo = N;
+            gemm_f16(nullptr, EPI_F16, N, N, N, a.as<_Float16>(), N, w.as<_Float16>(), N, ep);
+            OWK_HIP_CHECK(hipDeviceSynchronize());
+            hipEvent_t e0, e1;
+            OWK_HIP_CHECK(hipEventCreate(&e0));
+            OWK_HIP_CHECK(hipEventCreate(&e1));
+            const int iters = N >= 4096 ? 10 : 50;
+            OWK_HIP_CHECK(hipEventRecord(e0, nullptr));
+            for (int i = 0; i < iters; ++i)
+                gemm_f16(nullptr, EPI_F16, N, N, N, a.as<_Float16>(), N, w.as<_Float16>(), N, ep);
+            OWK_HIP_CHECK(hipEventRecord(e1, nullptr));
+            OWK_HIP_CHECK(hipEventSynchronize(e1));
+            float ms = 0;
+            OWK_HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
+            char buf[256];
+            snprintf(buf, sizeof(buf), "%5zu x %5zu: F16 %8.1f TFLOPS (MFMA gemm, %d runs)\n", (size_t) N, (size_t) N,
+                     2.0 * N * (double) N * N * iters / (ms * 1e-3) / 1e12, iters);
+            g_bench_str += buf;
+            (void) hipEventDestroy(e0);
+            (void) hipEventDestroy(e1);
+        }
+    } catch (const std::exception & e) {
+        g_bench_str += std::string("mul_mat: failed: ") + e.what() + "\n";
+    }
+    return g_bench_str.c_str();
+}
+
+void whisper_log_set(ggml_log_callback log_callback, void * user_data) { set_log_callback(log_callback, user_data); }
+
+// ---------------------------------------------------------------------------------
+// owk.h extensions
+// ---------------------------------------------------------------------------------
+int owk_full_batch(struct whisper_context * ctx, struct whisper_state ** states, struct whisper_full_params params,
+                   const struct owk_full_ext * ext, const float * const * samples, const int * n_samples, int n_clips) {
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    std::vector<whisper_full_params> ps(std::max(n_clips, 1), params);
+    try {
+        return full_batch(ctx, states, ps.data(), ext, samples, n_samples, n_clips);
+    } catch (const std::exception & e) {
+        log_msg(GGML_LOG_LEVEL_ERROR, "owk_full_batch: %s\n", e.what());
+        return -6;
+    }
+}
+
+void owk_prof_enable(struct whisper_context * ctx, int enable) {
+    ctx->prof.flush();
+    ctx->prof.on = enable != 0;
+}
+
+void owk_prof_reset(struct whisper_context * ctx) { ctx->prof.reset(); }
+
+int owk_prof_read(struct whisper_context * ctx, const char * cls, double * total_ms, long * launches) {
+    ctx->prof.flush();
+    for (size_t i = 0; i < ctx->prof.names.size(); ++i)
+        if (ctx->prof.names[i] == cls) {
+            if (total_ms) *total_ms = ctx->prof.tot[i].ms;
+            if (launches) *launches = ctx->prof.tot[i].n;
+            return 0;
+        }
+    return -1;
+}
+
+int owk_prof_work(struct whisper_context * ctx, const char * cls, double * flops, double * bytes) {
+    ctx->prof.flush();
+    for (size_t i = 0; i < ctx->prof.names.size(); ++i)
+        if (ctx->prof.names[i] == cls) {
+            if (flops) *flops = ctx->prof.tot[i].flops;
+            if (bytes) *bytes = ctx->prof.tot[i].bytes;
+            return 0;
+        }
+    return -1;
+}
+
+const char * owk_prof_classes(struct whisper_context * ctx) {
+    ctx->prof.flush();
+    ctx->prof.classes_csv.clear();
+    for (size_t i = 0; i < ctx->prof.names.size(); ++i) {
+        if (i) ctx->prof.classes_csv += ",";
+        ctx->prof.classes_csv += ctx->prof.names[i];
+    }
+    return ctx->prof.classes_csv.c_str();
+}
+
+int owk_device_ok(int device) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || device >= n) return 0;
+    hipDeviceProp_t p;
+    if (hipGetDeviceProperties(&p, device) != hipSuccess) return 0;
+    return strncmp(p.gcnArchName, "gfx950", 6) == 0 ? 1 : 0;
+}
+
+const char * owk_build_info(void) { return "open-whisper-kit MI355X engine: gfx950 HIP kernels (MFMA f16), batch-major"; }
+
+// debug / test hooks: reference intermediates of the last staged call on a state
+int owk_debug_mel(struct whisper_state * st, float * out, int cap) {
+    if (!st->eng) return -1;
+    const int n = st->mel_n_mel * st->eng->mel_len(0);
+    if (out) {
+        if (cap < n) return -1;
+        st->eng->download_mel(0, out);
+    }
+    return n;
+}
+
+int owk_debug_enc(struct whisper_context * ctx, struct whisper_state * st, int index, float * out, int cap) {
+    const int n = ctx->model->hp.n_audio_ctx * ctx->model->hp.n_audio_state;
+    if (!st->eng) return -1;
+    if (out) {
+        if (cap < n) return -1;
+        st->eng->download_enc(index, out);
+    }
+    return n;
+}
+
+int owk_debug_cross(struct whisper_context * ctx, struct whisper_state * st, int slot, int layer, uint16_t * k, uint16_t * v) {
+    if (!st->eng) return -1;
+    const int n = ctx->model->hp.n_audio_ctx * ctx->model->hp.n_text_state;
+    if (k && v) st->eng->download_cross(slot, layer, k, v);
+    return n;
+}
+
+const uint16_t * owk_debug_gelu_table(void) { return gelu_table_host().data(); }
+
+}  // extern "C"

@@ -1,0 +1,269 @@
+"""ctypes binding of the drop-in C ABI (include/whisper.h + include/owk.h).
+
+This is how tests/, bench.py and __graft_entry__.py drive the MI355X engine: through
+the exact exported symbols a reference caller would bind (the same calls the Swift
+SDK / examples/cli make). Struct layouts mirror the reference header
+(ref include/whisper.h:116-151, 487-591) field for field.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.normpath(os.path.join(HERE, "..", "lib", "libwhisper.so"))
+
+WHISPER_SAMPLING_GREEDY = 0
+WHISPER_SAMPLING_BEAM_SEARCH = 1
+
+
+class Aheads(C.Structure):
+    _fields_ = [("n_heads", C.c_size_t), ("heads", C.c_void_p)]
+
+
+class ContextParams(C.Structure):
+    _fields_ = [("use_gpu", C.c_bool), ("flash_attn", C.c_bool), ("gpu_device", C.c_int),
+                ("dtw_token_timestamps", C.c_bool), ("dtw_aheads_preset", C.c_int), ("dtw_n_top", C.c_int),
+                ("dtw_aheads", Aheads), ("dtw_mem_size", C.c_size_t)]
+
+
+class TokenData(C.Structure):
+    _fields_ = [("id", C.c_int32), ("tid", C.c_int32), ("p", C.c_float), ("plog", C.c_float), ("pt", C.c_float),
+                ("ptsum", C.c_float), ("t0", C.c_int64), ("t1", C.c_int64), ("t_dtw", C.c_int64),
+                ("vlen", C.c_float)]
+
+
+class VadParams(C.Structure):
+    _fields_ = [("threshold", C.c_float), ("min_speech_duration_ms", C.c_int), ("min_silence_duration_ms", C.c_int),
+                ("max_speech_duration_s", C.c_float), ("speech_pad_ms", C.c_int), ("samples_overlap", C.c_float)]
+
+
+class _Greedy(C.Structure):
+    _fields_ = [("best_of", C.c_int)]
+
+
+class _Beam(C.Structure):
+    _fields_ = [("beam_size", C.c_int), ("patience", C.c_float)]
+
+
+LOGITS_FILTER_CB = C.CFUNCTYPE(None, C.c_void_p, C.c_void_p, C.POINTER(TokenData), C.c_int, C.POINTER(C.c_float),
+                               C.c_void_p)
+
+
+class FullParams(C.Structure):
+    _fields_ = [
+        ("strategy", C.c_int),
+        ("n_threads", C.c_int), ("n_max_text_ctx", C.c_int), ("offset_ms", C.c_int), ("duration_ms", C.c_int),
+        ("translate", C.c_bool), ("no_context", C.c_bool), ("no_timestamps", C.c_bool), ("single_segment", C.c_bool),
+        ("print_special", C.c_bool), ("print_progress", C.c_bool), ("print_realtime", C.c_bool),
+        ("print_timestamps", C.c_bool),
+        ("token_timestamps", C.c_bool), ("thold_pt", C.c_float), ("thold_ptsum", C.c_float), ("max_len", C.c_int),
+        ("split_on_word", C.c_bool), ("max_tokens", C.c_int),
+        ("debug_mode", C.c_bool), ("audio_ctx", C.c_int),
+        ("tdrz_enable", C.c_bool),
+        ("suppress_regex", C.c_char_p),
+        ("initial_prompt", C.c_char_p), ("carry_initial_prompt", C.c_bool), ("prompt_tokens", C.c_void_p),
+        ("prompt_n_tokens", C.c_int),
+        ("language", C.c_char_p), ("detect_language", C.c_bool),
+        ("suppress_blank", C.c_bool), ("suppress_nst", C.c_bool),
+        ("temperature", C.c_float), ("max_initial_ts", C.c_float), ("length_penalty", C.c_float),
+        ("temperature_inc", C.c_float), ("entropy_thold", C.c_float), ("logprob_thold", C.c_float),
+        ("no_speech_thold", C.c_float),
+        ("greedy", _Greedy), ("beam_search", _Beam),
+        ("new_segment_callback", C.c_void_p), ("new_segment_callback_user_data", C.c_void_p),
+        ("progress_callback", C.c_void_p), ("progress_callback_user_data", C.c_void_p),
+        ("encoder_begin_callback", C.c_void_p), ("encoder_begin_callback_user_data", C.c_void_p),
+        ("abort_callback", C.c_void_p), ("abort_callback_user_data", C.c_void_p),
+        ("logits_filter_callback", C.c_void_p), ("logits_filter_callback_user_data", C.c_void_p),
+        ("grammar_rules", C.c_void_p), ("n_grammar_rules", C.c_size_t), ("i_start_rule", C.c_size_t),
+        ("grammar_penalty", C.c_float),
+        ("vad", C.c_bool), ("vad_model_path", C.c_char_p), ("vad_params", VadParams),
+    ]
+
+
+class FullExt(C.Structure):
+    _fields_ = [("suppress_eot", C.c_int), ("reserved", C.c_int * 7)]
+
+
+# every symbol include/whisper.h + include/owk.h declare (checked by tests/test_abi.py)
+def header_symbols(include_dir=None):
+    import re
+    include_dir = include_dir or os.path.normpath(os.path.join(HERE, "..", "..", "include"))
+    syms = []
+    for h in ("whisper.h", "owk.h", "ggml-backend.h"):
+        txt = open(os.path.join(include_dir, h)).read()
+        txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+        for m in re.finditer(r"\b((?:whisper|owk|ggml_backend)_[a-z0-9_]+)\s*\(", txt):
+            name = m.group(1)
+            if name.endswith("_callback"):
+                continue
+            syms.append(name)
+    return sorted(set(syms))
+
+
+_lib = None
+
+
+def load(path: str | None = None) -> C.CDLL:
+    """Load libwhisper.so; raises if the HIP build is missing (no CPU fallback exists)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    path = path or os.environ.get("OWK_LIB", LIB_PATH)
+    if not os.path.exists(path):
+        raise FileNotFoundError(f"libwhisper.so not built at {path} (run `make` / __graft_entry__.build())")
+    L = C.CDLL(path)
+    vp, ip, fp = C.c_void_p, C.c_int, C.POINTER(C.c_float)
+    L.whisper_context_default_params.restype = ContextParams
+    L.whisper_full_default_params.restype = FullParams
+    L.whisper_full_default_params.argtypes = [ip]
+    L.whisper_init_from_file_with_params.restype = vp
+    L.whisper_init_from_file_with_params.argtypes = [C.c_char_p, ContextParams]
+    L.whisper_init_state.restype = vp
+    L.whisper_init_state.argtypes = [vp]
+    L.whisper_free.argtypes = [vp]
+    L.whisper_free_state.argtypes = [vp]
+    L.whisper_full.argtypes = [vp, FullParams, fp, ip]
+    L.whisper_full_with_state.argtypes = [vp, vp, FullParams, fp, ip]
+    L.whisper_full_parallel.argtypes = [vp, FullParams, fp, ip, ip]
+    L.owk_full_batch.argtypes = [vp, C.POINTER(vp), FullParams, C.POINTER(FullExt), C.POINTER(fp), C.POINTER(ip), ip]
+    for n in ("whisper_full_n_segments_from_state",):
+        getattr(L, n).argtypes = [vp]
+    L.whisper_full_n_segments.argtypes = [vp]
+    L.whisper_full_get_segment_t0_from_state.restype = C.c_int64
+    L.whisper_full_get_segment_t0_from_state.argtypes = [vp, ip]
+    L.whisper_full_get_segment_t1_from_state.restype = C.c_int64
+    L.whisper_full_get_segment_t1_from_state.argtypes = [vp, ip]
+    L.whisper_full_get_segment_text_from_state.restype = C.c_char_p
+    L.whisper_full_get_segment_text_from_state.argtypes = [vp, ip]
+    L.whisper_full_get_segment_no_speech_prob_from_state.restype = C.c_float
+    L.whisper_full_get_segment_no_speech_prob_from_state.argtypes = [vp, ip]
+    L.whisper_full_n_tokens_from_state.argtypes = [vp, ip]
+    L.whisper_full_get_token_data_from_state.restype = TokenData
+    L.whisper_full_get_token_data_from_state.argtypes = [vp, ip, ip]
+    L.whisper_pcm_to_mel_with_state.argtypes = [vp, vp, fp, ip, ip]
+    L.whisper_encode_with_state.argtypes = [vp, vp, ip, ip]
+    L.whisper_decode_with_state.argtypes = [vp, vp, C.POINTER(C.c_int32), ip, ip, ip]
+    L.whisper_get_logits_from_state.restype = fp
+    L.whisper_get_logits_from_state.argtypes = [vp]
+    L.whisper_n_vocab.argtypes = [vp]
+    L.whisper_token_sot.argtypes = [vp]
+    L.whisper_token_eot.argtypes = [vp]
+    L.whisper_token_beg.argtypes = [vp]
+    L.whisper_token_not.argtypes = [vp]
+    L.whisper_token_to_str.restype = C.c_char_p
+    L.whisper_token_to_str.argtypes = [vp, ip]
+    L.whisper_model_n_mels.argtypes = [vp]
+    L.whisper_model_n_audio_state.argtypes = [vp]
+    L.whisper_model_n_text_layer.argtypes = [vp]
+    L.whisper_is_multilingual.argtypes = [vp]
+    L.whisper_lang_auto_detect_with_state.argtypes = [vp, vp, ip, ip, fp]
+    L.whisper_lang_max_id.restype = ip
+    L.whisper_log_set.argtypes = [vp, vp]
+    L.owk_prof_enable.argtypes = [vp, ip]
+    L.owk_prof_reset.argtypes = [vp]
+    L.owk_prof_read.argtypes = [vp, C.c_char_p, C.POINTER(C.c_double), C.POINTER(C.c_long)]
+    L.owk_prof_work.argtypes = [vp, C.c_char_p, C.POINTER(C.c_double), C.POINTER(C.c_double)]
+    L.owk_prof_classes.restype = C.c_char_p
+    L.owk_prof_classes.argtypes = [vp]
+    L.owk_device_ok.argtypes = [ip]
+    L.owk_debug_mel.argtypes = [vp, fp, ip]
+    L.owk_debug_enc.argtypes = [vp, vp, ip, fp, ip]
+    L.owk_debug_cross.argtypes = [vp, vp, ip, ip, C.POINTER(C.c_uint16), C.POINTER(C.c_uint16)]
+    L.owk_debug_gelu_table.restype = C.POINTER(C.c_uint16)
+    _lib = L
+    return L
+
+
+_LOG_CB = C.CFUNCTYPE(None, C.c_int, C.c_char_p, C.c_void_p)
+_quiet_cb = _LOG_CB(lambda lvl, txt, ud: None)
+
+
+def quiet():
+    load().whisper_log_set(C.cast(_quiet_cb, C.c_void_p), None)
+
+
+def fptr(a: np.ndarray):
+    return a.ctypes.data_as(C.POINTER(C.c_float))
+
+
+class Whisper:
+    """Thin owner of a whisper_context (and its default state)."""
+
+    def __init__(self, model_path: str, device: int = 0, flash_attn: bool = True):
+        self.L = load()
+        cp = self.L.whisper_context_default_params()
+        cp.gpu_device = device
+        cp.flash_attn = flash_attn
+        self.ctx = self.L.whisper_init_from_file_with_params(model_path.encode(), cp)
+        if not self.ctx:
+            raise RuntimeError(f"whisper_init_from_file_with_params failed for {model_path}")
+        self.n_vocab = self.L.whisper_n_vocab(self.ctx)
+        self._states = []
+
+    def close(self):
+        for s in self._states:
+            self.L.whisper_free_state(s)
+        self._states = []
+        if self.ctx:
+            self.L.whisper_free(self.ctx)
+            self.ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def new_state(self):
+        s = self.L.whisper_init_state(self.ctx)
+        if not s:
+            raise RuntimeError("whisper_init_state failed")
+        self._states.append(s)
+        return s
+
+    def params(self, strategy=WHISPER_SAMPLING_GREEDY, **kw) -> FullParams:
+        p = self.L.whisper_full_default_params(strategy)
+        p.print_progress = False
+        p.print_timestamps = False
+        for k, v in kw.items():
+            if k == "best_of":
+                p.greedy.best_of = v
+            elif k == "beam_size":
+                p.beam_search.beam_size = v
+            elif k == "language":
+                p.language = v.encode() if isinstance(v, str) else v
+            else:
+                setattr(p, k, v)
+        return p
+
+    def full(self, state, pcm: np.ndarray, params: FullParams) -> int:
+        pcm = np.ascontiguousarray(pcm, dtype=np.float32)
+        return self.L.whisper_full_with_state(self.ctx, state, params, fptr(pcm), len(pcm))
+
+    def full_batch(self, states, pcms, params: FullParams, suppress_eot=False) -> int:
+        n = len(pcms)
+        arrs = [np.ascontiguousarray(p, dtype=np.float32) for p in pcms]
+        ptrs = (C.POINTER(C.c_float) * n)(*[fptr(a) for a in arrs])
+        ns = (C.c_int * n)(*[len(a) for a in arrs])
+        sts = (C.c_void_p * n)(*states)
+        ext = FullExt()
+        ext.suppress_eot = 1 if suppress_eot else 0
+        return self.L.owk_full_batch(self.ctx, sts, params, C.byref(ext), ptrs, ns, n)
+
+    def segments(self, state):
+        L = self.L
+        out = []
+        for i in range(L.whisper_full_n_segments_from_state(state)):
+            toks = []
+            for j in range(L.whisper_full_n_tokens_from_state(state, i)):
+                t = L.whisper_full_get_token_data_from_state(state, i, j)
+                toks.append((t.id, t.tid, t.p, t.plog, t.pt, t.ptsum, t.t0, t.t1))
+            out.append(dict(t0=L.whisper_full_get_segment_t0_from_state(state, i),
+                            t1=L.whisper_full_get_segment_t1_from_state(state, i),
+                            text=L.whisper_full_get_segment_text_from_state(state, i).decode("utf-8", "replace"),
+                            no_speech_prob=L.whisper_full_get_segment_no_speech_prob_from_state(state, i),
+                            tokens=toks))
+        return out

@@ -1,0 +1,152 @@
+// TEST INFRASTRUCTURE — parity oracle probe, never part of the product.
+//
+// Compiles the reference implementation in place (#include of
+// /root/reference/src/whisper.cpp; nothing is copied into this repo) and adds a
+// handful of extern "C" accessors so tests/golden generators and bench.py's
+// cpu_baseline leg can read reference intermediates through ctypes:
+//   - the log-mel spectrogram        (whisper_state::mel, whisper.cpp:3170-3260)
+//   - the encoder output embd_enc    (whisper_build_graph_encoder, whisper.cpp:2038-2269)
+//   - the cross-attention K/V cache  (whisper_build_graph_cross, whisper.cpp:2272-2346)
+//   - decoder logits                 (whisper_decode_internal, whisper.cpp:2848-2978)
+//   - whisper_full with a flat config struct (whisper_full_with_state, whisper.cpp:6827-7776)
+#include "whisper.cpp"
+
+extern "C" {
+
+struct ref_full_cfg {
+    int   strategy;         // 0 greedy, 1 beam search
+    int   n_threads;
+    int   best_of;
+    int   beam_size;
+    float temperature;
+    float temperature_inc;
+    int   no_timestamps;
+    int   max_tokens;
+    int   suppress_eot;     // fixed-work mode: logits_filter_callback sets logits[eot] = -inf
+    int   token_timestamps;
+    int   no_context;
+    int   single_segment;
+    const char * language;
+    int   suppress_nst;
+    float length_penalty;
+};
+
+static void ref_suppress_eot_cb(struct whisper_context * ctx, struct whisper_state * /*state*/,
+                                const whisper_token_data * /*tokens*/, int /*n_tokens*/,
+                                float * logits, void * /*user_data*/) {
+    logits[whisper_token_eot(ctx)] = -INFINITY;
+}
+
+void * ref_init(const char * path, int flash_attn, int dtw_preset) {
+    whisper_log_set([](ggml_log_level, const char *, void *) {}, nullptr);
+    auto cp = whisper_context_default_params();
+    cp.use_gpu    = false;
+    cp.flash_attn = flash_attn != 0;
+    if (dtw_preset > 0) {
+        cp.dtw_token_timestamps = true;
+        cp.dtw_aheads_preset    = (whisper_alignment_heads_preset) dtw_preset;
+    }
+    return whisper_init_from_file_with_params(path, cp);
+}
+
+void ref_free(void * ctx) { whisper_free((whisper_context *) ctx); }
+
+// returns n_mel*n_len floats written (row-major [n_mel][n_len]); -1 on error
+int ref_mel(void * vctx, const float * pcm, int n, int n_threads, float * out, int cap,
+            int * n_len, int * n_len_org, int * n_mel) {
+    auto * ctx = (whisper_context *) vctx;
+    if (whisper_pcm_to_mel(ctx, pcm, n, n_threads) != 0) return -1;
+    const auto & mel = ctx->state->mel;
+    *n_len = mel.n_len; *n_len_org = mel.n_len_org; *n_mel = mel.n_mel;
+    const int total = mel.n_len * mel.n_mel;
+    if (out) {
+        if (cap < total) return -1;
+        memcpy(out, mel.data.data(), total * sizeof(float));
+    }
+    return total;
+}
+
+int ref_encode(void * vctx, int offset, int n_threads) {
+    return whisper_encode((whisper_context *) vctx, offset, n_threads);
+}
+
+static int tensor_f32_out(ggml_tensor * t, float * out, int cap) {
+    if (!t) return -1;
+    const int64_t n = ggml_nelements(t);
+    if (out) {
+        if (cap < n) return -1;
+        if (t->type == GGML_TYPE_F32) {
+            ggml_backend_tensor_get(t, out, 0, n * sizeof(float));
+        } else {
+            return -2;
+        }
+    }
+    return (int) n;
+}
+
+// encoder output [n_ctx][n_state] (token-major)
+int ref_get_enc(void * vctx, float * out, int cap) {
+    return tensor_f32_out(((whisper_context *) vctx)->state->embd_enc, out, cap);
+}
+
+// conv-stack output (layout ggml [n_state (ne0=time? see ref) ...])
+int ref_get_conv(void * vctx, float * out, int cap, int * ne0, int * ne1) {
+    ggml_tensor * t = ((whisper_context *) vctx)->state->embd_conv;
+    if (!t) return -1;
+    *ne0 = (int) t->ne[0]; *ne1 = (int) t->ne[1];
+    return tensor_f32_out(t, out, cap);
+}
+
+// raw F16 cross K/V cache bytes; layout per whisper.cpp:2320-2325 (FA) or 2327-2334 (no FA)
+long ref_get_cross(void * vctx, uint16_t * k, uint16_t * v, long cap) {
+    auto * st = ((whisper_context *) vctx)->state;
+    const long n = ggml_nelements(st->kv_cross.k);
+    if (k && v) {
+        if (cap < n) return -1;
+        ggml_backend_tensor_get(st->kv_cross.k, k, 0, n * 2);
+        ggml_backend_tensor_get(st->kv_cross.v, v, 0, n * 2);
+    }
+    return n;
+}
+
+int ref_decode(void * vctx, const int * tokens, int n_tokens, int n_past, int n_threads) {
+    return whisper_decode((whisper_context *) vctx, tokens, n_tokens, n_past, n_threads);
+}
+
+float * ref_logits(void * vctx) { return whisper_get_logits((whisper_context *) vctx); }
+
+int ref_full(void * vctx, const float * pcm, int n, const ref_full_cfg * cfg) {
+    auto * ctx = (whisper_context *) vctx;
+    auto p = whisper_full_default_params(cfg->strategy == 1 ? WHISPER_SAMPLING_BEAM_SEARCH
+                                                            : WHISPER_SAMPLING_GREEDY);
+    p.n_threads        = cfg->n_threads;
+    p.print_progress   = false;
+    p.print_realtime   = false;
+    p.print_timestamps = false;
+    if (cfg->best_of   > 0) p.greedy.best_of        = cfg->best_of;
+    if (cfg->beam_size > 0) p.beam_search.beam_size = cfg->beam_size;
+    p.temperature      = cfg->temperature;
+    p.temperature_inc  = cfg->temperature_inc;
+    p.no_timestamps    = cfg->no_timestamps != 0;
+    p.max_tokens       = cfg->max_tokens;
+    p.token_timestamps = cfg->token_timestamps != 0;
+    p.no_context       = cfg->no_context != 0;
+    p.single_segment   = cfg->single_segment != 0;
+    p.suppress_nst     = cfg->suppress_nst != 0;
+    p.length_penalty   = cfg->length_penalty;
+    if (cfg->language) p.language = cfg->language;
+    if (cfg->suppress_eot) p.logits_filter_callback = ref_suppress_eot_cb;
+    return whisper_full(ctx, p, pcm, n);
+}
+
+// state counters for the CPU-baseline breakdown (whisper.cpp:835-848)
+void ref_timings(void * vctx, double * t_mel_ms, double * t_enc_ms, double * t_dec_ms,
+                 double * t_batchd_ms, double * t_prompt_ms, double * t_sample_ms, int * n_decode) {
+    auto * st = ((whisper_context *) vctx)->state;
+    *t_mel_ms = st->t_mel_us / 1e3; *t_enc_ms = st->t_encode_us / 1e3;
+    *t_dec_ms = st->t_decode_us / 1e3; *t_batchd_ms = st->t_batchd_us / 1e3;
+    *t_prompt_ms = st->t_prompt_us / 1e3; *t_sample_ms = st->t_sample_us / 1e3;
+    *n_decode = st->n_decode;
+}
+
+} // extern "C"

@@ -1,0 +1,152 @@
+"""TEST INFRASTRUCTURE -- ctypes driver of the compiled reference (oracle/_ref/libwhisper_ref.so).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may use this module.
+It runs the reference ggml CPU implementation (built from /root/reference sources by
+oracle/ref/Makefile) through the accessors of oracle/ref/ref_probe.cpp.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REF_LIB = os.path.join(HERE, "_ref", "libwhisper_ref.so")
+
+
+class RefFullCfg(C.Structure):
+    _fields_ = [("strategy", C.c_int), ("n_threads", C.c_int), ("best_of", C.c_int), ("beam_size", C.c_int),
+                ("temperature", C.c_float), ("temperature_inc", C.c_float), ("no_timestamps", C.c_int),
+                ("max_tokens", C.c_int), ("suppress_eot", C.c_int), ("token_timestamps", C.c_int),
+                ("no_context", C.c_int), ("single_segment", C.c_int), ("language", C.c_char_p),
+                ("suppress_nst", C.c_int), ("length_penalty", C.c_float)]
+
+
+class RefTokenData(C.Structure):
+    _fields_ = [("id", C.c_int32), ("tid", C.c_int32), ("p", C.c_float), ("plog", C.c_float), ("pt", C.c_float),
+                ("ptsum", C.c_float), ("t0", C.c_int64), ("t1", C.c_int64), ("t_dtw", C.c_int64),
+                ("vlen", C.c_float)]
+
+
+def available() -> bool:
+    return os.path.exists(REF_LIB)
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not available():
+            raise FileNotFoundError(f"reference oracle not built: {REF_LIB} (make -C oracle/ref)")
+        L = C.CDLL(REF_LIB)
+        vp, ip, fp = C.c_void_p, C.c_int, C.POINTER(C.c_float)
+        L.ref_init.restype = vp
+        L.ref_init.argtypes = [C.c_char_p, ip, ip]
+        L.ref_free.argtypes = [vp]
+        L.ref_mel.argtypes = [vp, fp, ip, ip, fp, ip, C.POINTER(ip), C.POINTER(ip), C.POINTER(ip)]
+        L.ref_encode.argtypes = [vp, ip, ip]
+        L.ref_get_enc.argtypes = [vp, fp, ip]
+        L.ref_get_cross.restype = C.c_long
+        L.ref_get_cross.argtypes = [vp, C.POINTER(C.c_uint16), C.POINTER(C.c_uint16), C.c_long]
+        L.ref_decode.argtypes = [vp, C.POINTER(C.c_int), ip, ip, ip]
+        L.ref_logits.restype = fp
+        L.ref_logits.argtypes = [vp]
+        L.ref_full.argtypes = [vp, fp, ip, C.POINTER(RefFullCfg)]
+        L.ref_timings.argtypes = [vp] + [C.POINTER(C.c_double)] * 6 + [C.POINTER(ip)]
+        L.whisper_full_n_segments.argtypes = [vp]
+        L.whisper_full_get_segment_t0.restype = C.c_int64
+        L.whisper_full_get_segment_t0.argtypes = [vp, ip]
+        L.whisper_full_get_segment_t1.restype = C.c_int64
+        L.whisper_full_get_segment_t1.argtypes = [vp, ip]
+        L.whisper_full_get_segment_text.restype = C.c_char_p
+        L.whisper_full_get_segment_text.argtypes = [vp, ip]
+        L.whisper_full_get_segment_no_speech_prob.restype = C.c_float
+        L.whisper_full_get_segment_no_speech_prob.argtypes = [vp, ip]
+        L.whisper_full_n_tokens.argtypes = [vp, ip]
+        L.whisper_full_get_token_data.restype = RefTokenData
+        L.whisper_full_get_token_data.argtypes = [vp, ip, ip]
+        L.whisper_n_vocab.argtypes = [vp]
+        L.whisper_token_sot.argtypes = [vp]
+        L.whisper_lang_auto_detect.argtypes = [vp, ip, ip, fp]
+        _lib = L
+    return _lib
+
+
+def fptr(a):
+    return a.ctypes.data_as(C.POINTER(C.c_float))
+
+
+class Ref:
+    def __init__(self, model_path: str, flash_attn: bool = True):
+        self.L = lib()
+        self.ctx = self.L.ref_init(model_path.encode(), 1 if flash_attn else 0, 0)
+        if not self.ctx:
+            raise RuntimeError("reference init failed")
+        self.n_vocab = self.L.whisper_n_vocab(self.ctx)
+
+    def close(self):
+        if self.ctx:
+            self.L.ref_free(self.ctx)
+            self.ctx = None
+
+    def mel(self, pcm, n_threads=8):
+        pcm = np.ascontiguousarray(pcm, np.float32)
+        nl, nlo, nm = C.c_int(), C.c_int(), C.c_int()
+        n = self.L.ref_mel(self.ctx, fptr(pcm), len(pcm), n_threads, None, 0, nl, nlo, nm)
+        out = np.zeros(n, np.float32)
+        self.L.ref_mel(self.ctx, fptr(pcm), len(pcm), n_threads, fptr(out), n, nl, nlo, nm)
+        return out.reshape(nm.value, nl.value), nlo.value
+
+    def encode(self, offset=0, n_threads=8):
+        assert self.L.ref_encode(self.ctx, offset, n_threads) == 0
+        n = self.L.ref_get_enc(self.ctx, None, 0)
+        out = np.zeros(n, np.float32)
+        self.L.ref_get_enc(self.ctx, fptr(out), n)
+        return out
+
+    def cross(self):
+        n = self.L.ref_get_cross(self.ctx, None, None, 0)
+        k = np.zeros(n, np.uint16)
+        v = np.zeros(n, np.uint16)
+        self.L.ref_get_cross(self.ctx, k.ctypes.data_as(C.POINTER(C.c_uint16)),
+                             v.ctypes.data_as(C.POINTER(C.c_uint16)), n)
+        return k, v
+
+    def decode(self, tokens, n_past, n_threads=8):
+        arr = (C.c_int * len(tokens))(*tokens)
+        assert self.L.ref_decode(self.ctx, arr, len(tokens), n_past, n_threads) == 0
+        lg = np.ctypeslib.as_array(self.L.ref_logits(self.ctx), shape=(len(tokens) * self.n_vocab,))
+        return lg[(len(tokens) - 1) * self.n_vocab:].copy()
+
+    def full(self, pcm, strategy=0, n_threads=8, best_of=5, beam_size=5, temperature=0.0, temperature_inc=0.2,
+             no_timestamps=False, max_tokens=0, suppress_eot=False, token_timestamps=False, no_context=True,
+             single_segment=False, language="en", suppress_nst=False, length_penalty=-1.0):
+        cfg = RefFullCfg(strategy, n_threads, best_of, beam_size, temperature, temperature_inc, int(no_timestamps),
+                         max_tokens, int(suppress_eot), int(token_timestamps), int(no_context), int(single_segment),
+                         language.encode() if language else None, int(suppress_nst), length_penalty)
+        pcm = np.ascontiguousarray(pcm, np.float32)
+        ret = self.L.ref_full(self.ctx, fptr(pcm), len(pcm), C.byref(cfg))
+        return ret, self.segments()
+
+    def segments(self):
+        L = self.L
+        out = []
+        for i in range(L.whisper_full_n_segments(self.ctx)):
+            toks = []
+            for j in range(L.whisper_full_n_tokens(self.ctx, i)):
+                t = L.whisper_full_get_token_data(self.ctx, i, j)
+                toks.append((t.id, t.tid, t.p, t.plog, t.pt, t.ptsum, t.t0, t.t1))
+            out.append(dict(t0=L.whisper_full_get_segment_t0(self.ctx, i), t1=L.whisper_full_get_segment_t1(self.ctx, i),
+                            text=L.whisper_full_get_segment_text(self.ctx, i).decode("utf-8", "replace"),
+                            no_speech_prob=L.whisper_full_get_segment_no_speech_prob(self.ctx, i), tokens=toks))
+        return out
+
+    def timings(self):
+        v = [C.c_double() for _ in range(6)]
+        n = C.c_int()
+        self.L.ref_timings(self.ctx, *[C.byref(x) for x in v], C.byref(n))
+        return dict(mel_ms=v[0].value, enc_ms=v[1].value, dec_ms=v[2].value, batchd_ms=v[3].value,
+                    prompt_ms=v[4].value, sample_ms=v[5].value, n_decode=n.value)
