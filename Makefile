@@ -14,7 +14,7 @@ SRC      := $(PKG)/csrc
 OBJDIR   := $(PKG)/build
 LIB      := $(PKG)/lib/libwhisper.so
 
-FLAGS    := -O3 -std=c++17 -fPIC -ffp-contract=off --offload-arch=$(ARCH) -Iinclude -I$(SRC) \
+FLAGS    := -O3 -g -std=c++17 -fPIC -ffp-contract=off --offload-arch=$(ARCH) -Iinclude -I$(SRC) \
             -DWHISPER_SHARED -DWHISPER_BUILD -Wall -Wno-unused-function -Wno-unused-variable
 
 HIP_SRCS := $(wildcard $(SRC)/*.hip)
@@ -27,7 +27,7 @@ all: $(LIB)
 
 $(LIB): $(OBJS)
 	@mkdir -p $(dir $@)
-	$(HIPCC) -shared --offload-arch=$(ARCH) -o $@ $(OBJS) -Wl,--no-undefined -Wl,-soname,libwhisper.so
+	$(HIPCC) -shared --offload-arch=$(ARCH) -o $@ $(OBJS) -rdynamic -Wl,--no-undefined -Wl,-soname,libwhisper.so
 
 $(OBJDIR)/%.hip.o: $(SRC)/%.hip $(HDRS)
 	@mkdir -p $(OBJDIR)
@@ -37,10 +37,17 @@ $(OBJDIR)/%.cpp.o: $(SRC)/%.cpp $(HDRS)
 	@mkdir -p $(OBJDIR)
 	$(HIPCC) $(FLAGS) -x hip -c $< -o $@
 
+SELFTEST := $(PKG)/lib/owk_selftest
+
+$(SELFTEST): tools/owk_selftest.cpp $(LIB)
+	g++ -O1 -g -std=c++17 -Iinclude -o $@ $< -L$(PKG)/lib -lwhisper -Wl,-rpath,'$$ORIGIN'
+
+selftest: $(SELFTEST)
+
 oracle:
 	$(MAKE) -C oracle/ref -j$(JOBS)
 
 clean:
 	rm -rf $(OBJDIR) $(PKG)/lib
 
-.PHONY: all clean oracle
+.PHONY: all clean oracle selftest

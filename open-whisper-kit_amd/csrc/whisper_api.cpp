@@ -19,6 +19,29 @@ void set_log_callback(ggml_log_callback cb, void * ud);
 const std::vector<uint16_t> & gelu_table_host();
 }
 
+// OWK_BACKTRACE=1: print a native backtrace on SIGSEGV/SIGABRT (host-side debugging on
+// the GPU box, where no debugger may attach to a GPU process)
+#include <csignal>
+#include <execinfo.h>
+#include <unistd.h>
+static void owk_crash_handler(int sig) {
+    void * frames[64];
+    const int n = backtrace(frames, 64);
+    const char msg[] = "\n[owk] fatal signal, native backtrace:\n";
+    (void) !write(2, msg, sizeof(msg) - 1);
+    backtrace_symbols_fd(frames, n, 2);
+    signal(sig, SIG_DFL);
+    raise(sig);
+}
+static int owk_install_crash_handler = [] {
+    const char * e = getenv("OWK_BACKTRACE");
+    if (e && e[0] == '1') {
+        signal(SIGSEGV, owk_crash_handler);
+        signal(SIGABRT, owk_crash_handler);
+    }
+    return 0;
+}();
+
 static whisper_state * new_state(whisper_context * ctx) {
     auto * st = new whisper_state();
     try {

@@ -129,8 +129,25 @@ def load(path: str | None = None) -> C.CDLL:
     L.whisper_full_with_state.argtypes = [vp, vp, FullParams, fp, ip]
     L.whisper_full_parallel.argtypes = [vp, FullParams, fp, ip, ip]
     L.owk_full_batch.argtypes = [vp, C.POINTER(vp), FullParams, C.POINTER(FullExt), C.POINTER(fp), C.POINTER(ip), ip]
-    for n in ("whisper_full_n_segments_from_state",):
+    # int f(ctx-or-state) getters: without argtypes ctypes would truncate the pointer to 32 bits
+    for n in ("whisper_full_n_segments_from_state", "whisper_n_len_from_state", "whisper_n_len",
+              "whisper_full_lang_id_from_state", "whisper_full_lang_id", "whisper_n_text_ctx",
+              "whisper_n_audio_ctx", "whisper_model_n_vocab", "whisper_model_n_audio_ctx",
+              "whisper_model_n_audio_head", "whisper_model_n_audio_layer", "whisper_model_n_text_ctx",
+              "whisper_model_n_text_state", "whisper_model_n_text_head", "whisper_model_ftype",
+              "whisper_model_type", "whisper_token_solm", "whisper_token_prev", "whisper_token_nosp",
+              "whisper_token_translate", "whisper_token_transcribe"):
         getattr(L, n).argtypes = [vp]
+    L.whisper_token_lang.argtypes = [vp, ip]
+    L.whisper_lang_id.argtypes = [C.c_char_p]
+    L.whisper_lang_str.restype = C.c_char_p
+    L.whisper_lang_str.argtypes = [ip]
+    L.whisper_tokenize.argtypes = [vp, C.c_char_p, C.POINTER(C.c_int32), ip]
+    L.whisper_get_logits.restype = fp
+    L.whisper_get_logits.argtypes = [vp]
+    L.whisper_full_get_segment_speaker_turn_next_from_state.restype = C.c_bool
+    L.whisper_full_get_segment_speaker_turn_next_from_state.argtypes = [vp, ip]
+    L.whisper_print_system_info.restype = C.c_char_p
     L.whisper_full_n_segments.argtypes = [vp]
     L.whisper_full_get_segment_t0_from_state.restype = C.c_int64
     L.whisper_full_get_segment_t0_from_state.argtypes = [vp, ip]

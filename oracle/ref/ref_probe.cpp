@@ -11,6 +11,8 @@
 //   - whisper_full with a flat config struct (whisper_full_with_state, whisper.cpp:6827-7776)
 #include "whisper.cpp"
 
+#include <mutex>
+
 extern "C" {
 
 struct ref_full_cfg {
@@ -29,7 +31,75 @@ struct ref_full_cfg {
     const char * language;
     int   suppress_nst;
     float length_penalty;
+    int   record_topk;      // record + truncate logits to a top-K set (see ref_record_cb)
 };
+
+// ---------------------------------------------------------------------------------
+// Logit recording for the stochastic strategies (sampling, beam search, temperature
+// fallback). Their outcome depends on where an mt19937 draw lands in the CDF of the
+// probabilities, so any f32 reordering can change a pick. For an exact comparison of
+// the decoding *logic*, the golden run truncates every decoder's logits (at the
+// logits_filter_callback point, whisper.cpp:6254) to a recorded set of entries:
+//   top REC_TEXT finite text tokens (< token_beg), token_eot if finite, and the top
+//   REC_TS finite timestamp tokens; everything else becomes -inf.
+// The GPU test installs a callback that substitutes exactly these recorded values,
+// keyed by the decoder's token prefix (nearest match on values when a prefix repeats).
+static constexpr int REC_TEXT = 24, REC_TS = 16, REC_W = REC_TEXT + 1 + REC_TS;
+static std::vector<int>   g_rec_prefix, g_rec_off, g_rec_idx;
+static std::vector<float> g_rec_val;
+static bool               g_rec_suppress_eot = false;
+static std::mutex         g_rec_mtx;  // whisper_full runs process_logits of the decoders on worker threads
+
+static void ref_record_cb(struct whisper_context * ctx, struct whisper_state * /*state*/,
+                          const whisper_token_data * tokens, int n_tokens, float * logits, void * /*user_data*/) {
+    const int n_vocab = whisper_n_vocab(ctx), eot = whisper_token_eot(ctx), beg = whisper_token_beg(ctx);
+    if (g_rec_suppress_eot) logits[eot] = -INFINITY;
+    auto top = [&](int lo, int hi, int k, std::vector<int> & out) {
+        std::vector<int> ids;
+        for (int i = lo; i < hi; ++i)
+            if (logits[i] > -INFINITY && i != eot) ids.push_back(i);
+        k = std::min<int>(k, (int) ids.size());
+        std::partial_sort(ids.begin(), ids.begin() + k, ids.end(), [&](int a, int b) {
+            return logits[a] > logits[b] || (logits[a] == logits[b] && a < b);
+        });
+        out.insert(out.end(), ids.begin(), ids.begin() + k);
+    };
+    std::vector<int> keep;
+    top(0, beg, REC_TEXT, keep);
+    if (logits[eot] > -INFINITY) keep.push_back(eot);
+    top(beg, n_vocab, REC_TS, keep);
+    {
+        std::lock_guard<std::mutex> lock(g_rec_mtx);
+        g_rec_off.push_back((int) g_rec_prefix.size());
+        for (int i = 0; i < n_tokens; ++i) g_rec_prefix.push_back(tokens[i].id);
+        for (int j = 0; j < REC_W; ++j) {
+            const int id = j < (int) keep.size() ? keep[j] : -1;
+            g_rec_idx.push_back(id);
+            g_rec_val.push_back(id >= 0 ? logits[id] : -INFINITY);
+        }
+    }
+    std::vector<float> kept(keep.size());
+    for (size_t j = 0; j < keep.size(); ++j) kept[j] = logits[keep[j]];
+    for (int i = 0; i < n_vocab; ++i) logits[i] = -INFINITY;
+    for (size_t j = 0; j < keep.size(); ++j) logits[keep[j]] = kept[j];
+}
+
+// recorded entries: returns their count; with non-null outputs copies
+//   off[n+1] (prefix offsets), prefix[off[n]], idx[n*REC_W], val[n*REC_W]
+int ref_record_get(int * off, int * prefix, int * idx, float * val, int * width) {
+    const int n = (int) g_rec_off.size();
+    *width = REC_W;
+    if (off) {
+        for (int i = 0; i < n; ++i) off[i] = g_rec_off[i];
+        off[n] = (int) g_rec_prefix.size();
+        std::copy(g_rec_prefix.begin(), g_rec_prefix.end(), prefix);
+        std::copy(g_rec_idx.begin(), g_rec_idx.end(), idx);
+        std::copy(g_rec_val.begin(), g_rec_val.end(), val);
+    }
+    return n;
+}
+
+int ref_record_prefix_len() { return (int) g_rec_prefix.size(); }
 
 static void ref_suppress_eot_cb(struct whisper_context * ctx, struct whisper_state * /*state*/,
                                 const whisper_token_data * /*tokens*/, int /*n_tokens*/,
@@ -136,6 +206,14 @@ int ref_full(void * vctx, const float * pcm, int n, const ref_full_cfg * cfg) {
     p.length_penalty   = cfg->length_penalty;
     if (cfg->language) p.language = cfg->language;
     if (cfg->suppress_eot) p.logits_filter_callback = ref_suppress_eot_cb;
+    // every golden run starts from a freshly initialised state's sampler (whisper.cpp:3470):
+    // decoders[0].rng otherwise carries the draws of earlier runs on this context
+    ctx->state->decoders[0].rng = std::mt19937(0);
+    g_rec_prefix.clear(); g_rec_off.clear(); g_rec_idx.clear(); g_rec_val.clear();
+    if (cfg->record_topk) {
+        g_rec_suppress_eot = cfg->suppress_eot != 0;
+        p.logits_filter_callback = ref_record_cb;
+    }
     return whisper_full(ctx, p, pcm, n);
 }
 

@@ -20,7 +20,8 @@ class RefFullCfg(C.Structure):
                 ("temperature", C.c_float), ("temperature_inc", C.c_float), ("no_timestamps", C.c_int),
                 ("max_tokens", C.c_int), ("suppress_eot", C.c_int), ("token_timestamps", C.c_int),
                 ("no_context", C.c_int), ("single_segment", C.c_int), ("language", C.c_char_p),
-                ("suppress_nst", C.c_int), ("length_penalty", C.c_float)]
+                ("suppress_nst", C.c_int), ("length_penalty", C.c_float),
+                ("record_topk", C.c_int)]
 
 
 class RefTokenData(C.Structure):
@@ -55,6 +56,7 @@ def lib():
         L.ref_logits.restype = fp
         L.ref_logits.argtypes = [vp]
         L.ref_full.argtypes = [vp, fp, ip, C.POINTER(RefFullCfg)]
+        L.ref_record_get.argtypes = [C.POINTER(ip), C.POINTER(ip), C.POINTER(ip), fp, C.POINTER(ip)]
         L.ref_timings.argtypes = [vp] + [C.POINTER(C.c_double)] * 6 + [C.POINTER(ip)]
         L.whisper_full_n_segments.argtypes = [vp]
         L.whisper_full_get_segment_t0.restype = C.c_int64
@@ -123,13 +125,28 @@ class Ref:
 
     def full(self, pcm, strategy=0, n_threads=8, best_of=5, beam_size=5, temperature=0.0, temperature_inc=0.2,
              no_timestamps=False, max_tokens=0, suppress_eot=False, token_timestamps=False, no_context=True,
-             single_segment=False, language="en", suppress_nst=False, length_penalty=-1.0):
+             single_segment=False, language="en", suppress_nst=False, length_penalty=-1.0, record_topk=False):
         cfg = RefFullCfg(strategy, n_threads, best_of, beam_size, temperature, temperature_inc, int(no_timestamps),
                          max_tokens, int(suppress_eot), int(token_timestamps), int(no_context), int(single_segment),
-                         language.encode() if language else None, int(suppress_nst), length_penalty)
+                         language.encode() if language else None, int(suppress_nst), length_penalty,
+                         int(record_topk))
         pcm = np.ascontiguousarray(pcm, np.float32)
         ret = self.L.ref_full(self.ctx, fptr(pcm), len(pcm), C.byref(cfg))
         return ret, self.segments()
+
+    def recorded(self):
+        """Logit entries recorded by the last full(record_topk=True): (off, prefix, idx, val)."""
+        w = C.c_int()
+        n = self.L.ref_record_get(None, None, None, None, C.byref(w))
+        off = np.zeros(n + 1, np.int32)
+        # prefix length is off[n]; query it through a first copy of the offsets
+        plen = self.L.ref_record_prefix_len()
+        prefix = np.zeros(max(plen, 1), np.int32)
+        idx = np.zeros(n * w.value, np.int32)
+        val = np.zeros(n * w.value, np.float32)
+        P = lambda a: a.ctypes.data_as(C.POINTER(C.c_int))
+        self.L.ref_record_get(P(off), P(prefix), P(idx), fptr(val), C.byref(w))
+        return off, prefix[:plen], idx.reshape(n, w.value), val.reshape(n, w.value)
 
     def segments(self):
         L = self.L

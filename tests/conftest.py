@@ -9,6 +9,7 @@ ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
 GOLDEN = os.path.join(ROOT, "tests", "golden")
 sys.path.insert(0, os.path.join(ROOT, "open-whisper-kit_amd", "python"))
 sys.path.insert(0, os.path.join(ROOT, "oracle"))
+sys.path.insert(0, GOLDEN)
 
 
 def pytest_configure(config):

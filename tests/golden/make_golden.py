@@ -17,9 +17,11 @@ import numpy as np
 
 ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), "..", ".."))
 sys.path.insert(0, os.path.join(ROOT, "oracle"))
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "open-whisper-kit_amd", "python"))
 import owk_synth as S  # noqa: E402
 import ref_oracle as R  # noqa: E402
+from recording import prefix_hash  # noqa: E402
 
 OUT = os.path.dirname(os.path.abspath(__file__))
 SEED = 1234
@@ -33,6 +35,11 @@ CONFIGS = {
     "token_ts": dict(temperature_inc=0.0, token_timestamps=True),
     "sampled": dict(temperature=0.4, temperature_inc=0.0, best_of=5),
 }
+# Configs whose result depends on mt19937 draws (sampling at t > 0, beam search's
+# topk draws, temperature fallback). Their golden runs record and truncate the logits
+# at the logits_filter_callback point (oracle/ref/ref_probe.cpp ref_record_cb); the GPU
+# test substitutes the recorded values so the decoding logic is compared exactly.
+STOCHASTIC = ("greedy_fallback", "beam5", "sampled")
 
 
 def clips():
@@ -101,8 +108,16 @@ def main():
             for cfg_name, cfg in CONFIGS.items():
                 if model in ("base.en", "l3-mini") and cfg_name in ("sampled", "greedy_fallback") and cname == "synth30":
                     continue
-                ret, segs = ref.full(pcm, language=lang, **cfg)
+                rec = cfg_name in STOCHASTIC
+                ret, segs = ref.full(pcm, language=lang, record_topk=rec, **cfg)
                 meta["results"][f"{key}/full/{cfg_name}"] = {"ret": ret, "segments": segs}
+                if rec:
+                    off, prefix, idx, val = ref.recorded()
+                    k = f"{key}/full/{cfg_name}"
+                    arrays[k + "/rec_hash"] = np.array(
+                        [prefix_hash(prefix[off[i]:off[i + 1]]) for i in range(len(off) - 1)], np.uint64)
+                    arrays[k + "/rec_idx"] = np.where(idx < 0, 65535, idx).astype(np.uint16)
+                    arrays[k + "/rec_val"] = val
             print(model, cname, "done", flush=True)
         if multilingual:
             ret, segs = ref.full(audio["jfk"], language="auto", temperature_inc=0.0)
