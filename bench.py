@@ -1,0 +1,238 @@
+#!/usr/bin/env python3
+"""Throughput of the whisper_full() hot path on MI355X: real-time factor (audio s / wall s).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--model large-v3] [--batch 32]
+
+N > 1 is launched by the driver as
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N ...
+One process per GPU. Clips are sharded across ranks: every rank runs its own
+batch of `--batch` independent 30 s clips; there is no data-path collective. The process group
+(gloo) only carries the start/end barriers and the max-over-ranks of the timed region.
+
+A "step" is one owk_full_batch() call (include/owk.h) = whisper_full() semantics for each of the
+`--batch` clips of this rank: log-mel -> conv + encoder -> cross-KV -> prefill -> greedy decode.
+Workload (DESIGN.md "Measurement"): synthetic-weight large-v3 (F16 ggml-bin, real shapes),
+synthetic 16 kHz 30 s clips already resident in HBM, language "en", temperature_inc = 0,
+no_timestamps, <|endoftext|> suppressed and max_tokens = 219, i.e. exactly 220 sampled tokens
+per clip (the n_text_ctx/2 - 4 decode-step ceiling of whisper_full, ref whisper.cpp:7190):
+fixed work, identical on the CPU reference.
+
+Roofline: per kernel class the engine records HIP events on its own stream around every launch
+(owk_prof_*); `roofline` reports the class with the largest device time. The rocprofv3 summary
+of the same command is committed under profiles/.
+
+cpu_baseline: the reference ggml CPU path (oracle/_ref/libwhisper_ref.so, compiled from the
+reference sources by oracle/ref/Makefile) runs ONE clip of the same workload on this host's
+cores (rank 0, N = 1 only) -- a bounded sample of ~10-30 s.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "open-whisper-kit_amd", "python"))
+
+PEAK_F16_TFLOPS = 2500.0  # MI355X dense FP16/BF16 MFMA (MI355X_MICROARCH.md)
+PEAK_HBM_GBS = 8000.0     # HBM3E spec
+CLIP_SAMPLES = 480000     # 30 s at 16 kHz
+MAX_TOKENS = 219          # completion at i >= max_tokens -> 220 tokens per clip
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=2)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--model", default="large-v3")
+    ap.add_argument("--batch", type=int, default=32, help="clips per GPU per step")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-prof", action="store_true", help="disable per-class HIP-event timing")
+    ap.add_argument("--verbose", action="store_true")
+    return ap.parse_args()
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_threads():
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.isdigit():
+        n = min(n, int(env))
+    return max(1, n)
+
+
+def cpu_baseline(model_path, pcm):
+    """Reference ggml CPU path on one clip of the same fixed workload (bounded sample)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import ref_oracle as R  # test/measurement infrastructure only
+
+    if not R.available():
+        return None
+    nt = cpu_threads()
+    ref = R.Ref(model_path)
+    t0 = time.perf_counter()
+    ret, segs = ref.full(pcm, n_threads=nt, language="en", no_timestamps=True, max_tokens=MAX_TOKENS,
+                         suppress_eot=True, temperature_inc=0.0)
+    wall = time.perf_counter() - t0
+    ntok = sum(len(s["tokens"]) for s in segs)
+    tm = ref.timings()
+    ref.close()
+    return {"value": round(len(pcm) / 16000.0 / wall, 4), "unit": "audio-s/wall-s", "cores": nt,
+            "kind": "reference",
+            "sample": f"1 clip x 30 s, same model/params, {ntok} tokens, ret={ret}, wall {wall:.1f} s "
+                      f"(encode {tm['enc_ms'] / 1e3:.1f} s, decode {tm['dec_ms'] / 1e3:.1f} s), "
+                      f"ggml CPU n_threads={nt}"}
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    local = int(os.environ.get("LOCAL_RANK", 0))
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    import owk
+    import owk_synth as S
+
+    if world > 1:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    # synthetic weights of the real architecture (rank 0 writes, the others wait)
+    cache = os.environ.get("OWK_MODEL_CACHE", "/tmp/owk_models")
+    if rank == 0:
+        t = time.perf_counter()
+        model_path = S.ensure_model(args.model, cache_dir=cache)
+        log(f"[bench] model {model_path} ready in {time.perf_counter() - t:.1f} s")
+    barrier()
+    model_path = S.ensure_model(args.model, cache_dir=cache)
+
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    L = owk.load()
+    if L.owk_device_ok(local) != 1:
+        raise RuntimeError("libwhisper.so: no usable gfx950 device / code object")
+    owk.quiet()
+    w = owk.Whisper(model_path, device=local)
+    B = args.batch
+    # clips of this rank, resident in HBM for the timed region
+    host = [S.synth_audio(CLIP_SAMPLES, rank * B + i) for i in range(B)]
+    audio = torch.from_numpy(np.stack(host)).to(dev).contiguous()
+    ptrs = [audio[i].data_ptr() for i in range(B)]
+    ns = [CLIP_SAMPLES] * B
+    states = [w.new_state() for _ in range(B)]
+    p = w.params(0, language="en", temperature_inc=0.0, no_timestamps=True, max_tokens=MAX_TOKENS)
+    torch.cuda.synchronize()
+
+    def step():
+        ret = w.full_batch_device(states, ptrs, ns, p, suppress_eot=True)
+        if ret != 0:
+            raise RuntimeError(f"owk_full_batch returned {ret}")
+
+    for i in range(args.warmup):
+        t = time.perf_counter()
+        step()
+        log(f"[bench] warmup {i}: {time.perf_counter() - t:.3f} s")
+
+    prof = not args.no_prof
+    w.L.owk_prof_enable(w.ctx, 1 if prof else 0)
+    w.L.owk_prof_reset(w.ctx)
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step()
+        if args.verbose:
+            log(f"[bench] step {i}: {time.perf_counter() - t0:.3f} s")
+    torch.cuda.synchronize()
+    barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+
+    # every clip must have done the full fixed work (no skipped decoding)
+    ntok = [sum(len(s["tokens"]) for s in w.segments(st)) for st in states]
+    if min(ntok) != MAX_TOKENS + 1:
+        raise RuntimeError(f"fixed-work violation: tokens per clip {sorted(set(ntok))}")
+
+    classes = {}
+    if prof:
+        for c in w.prof_classes():
+            classes[c] = w.prof(c)
+    roof = None
+    if classes:
+        dom = max(classes, key=lambda c: classes[c]["ms"])
+        d = classes[dom]
+        avg_ms = d["ms"] / max(1, d["launches"])
+        mfma = dom.startswith("gemm") or dom == "attn_encoder"
+        if mfma:
+            ach = d["flops"] / (d["ms"] * 1e-3) / 1e12
+            roof = {"bound": "mfma", "achieved": round(ach, 2), "peak": PEAK_F16_TFLOPS, "unit": "TFLOP/s",
+                    "frac": round(ach / PEAK_F16_TFLOPS, 4), "traffic": None}
+        else:
+            ach = d["bytes"] / (d["ms"] * 1e-3) / 1e9
+            roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                    "frac": round(ach / PEAK_HBM_GBS, 4), "traffic": None}
+        roof["kernel_class"] = dom
+        roof["avg_launch_ms"] = round(avg_ms, 5)
+        roof["launches"] = d["launches"]
+        if rank == 0:
+            tot = sum(v["ms"] for v in classes.values())
+            for c, v in sorted(classes.items(), key=lambda kv: -kv[1]["ms"]):
+                log(f"[bench] {c:16s} {v['ms']:10.2f} ms {100 * v['ms'] / tot:5.1f}%  launches {v['launches']:7d}"
+                    f"  {v['flops'] / max(v['ms'], 1e-9) / 1e9:8.1f} TFLOP/s  "
+                    f"{v['bytes'] / max(v['ms'], 1e-9) / 1e6:8.1f} GB/s")
+
+    audio_s = world * B * args.steps * CLIP_SAMPLES / 16000.0
+    out = {
+        "metric": "real-time factor (audio-sec/wall-sec) large-v3 30s clips, 1/2/4/8 MI355X",
+        "value": round(audio_s / dt, 2),
+        "unit": "audio-s/wall-s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(1e3 * dt / args.steps, 2),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f16",
+        "data": "synthetic: seeded 30 s 16 kHz clips; random-init weights of the named architecture",
+        "config": {"workload": f"{args.model} F16, {B} x 30 s clips per GPU per step, greedy "
+                               f"(temperature_inc=0), no_timestamps, EOT suppressed, {MAX_TOKENS + 1} "
+                               f"tokens/clip, audio resident in HBM",
+                   "model": args.model, "clips_per_gpu": B, "global_batch": world * B,
+                   "tokens_per_clip": MAX_TOKENS + 1, "parallelism": f"clip-sharded x{world} (no collectives)"},
+        "roofline": roof,
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        try:
+            out["cpu_baseline"] = cpu_baseline(model_path, host[0])
+        except Exception as e:  # report, never hide the GPU number
+            log(f"[bench] cpu baseline failed: {e}")
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

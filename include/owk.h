@@ -22,7 +22,10 @@ struct owk_full_ext {
     /* fixed-work mode for throughput runs: mask <|endoftext|> on the device, equivalent
      * to a logits_filter_callback doing logits[eot] = -INF (ref whisper.cpp:6254-6256) */
     int suppress_eot;
-    int reserved[7];
+    /* samples[i] are device pointers (f32, on the context's GPU) instead of host memory:
+     * lets a caller keep the audio resident in HBM (bench.py times the pipeline this way) */
+    int samples_on_device;
+    int reserved[6];
 };
 
 /* run n_clips clips; states[i] receives clip i's segments. Returns 0 if every clip

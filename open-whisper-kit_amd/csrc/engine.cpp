@@ -116,13 +116,13 @@ void Engine::reserve(int slots, int cells) {
 }
 
 void Engine::compute_mel(const std::vector<int> & slots, const std::vector<const float *> & pcm,
-                         const std::vector<int> & n_samples) {
+                         const std::vector<int> & n_samples, bool pcm_on_device) {
     const int n = (int) slots.size();
     if (n == 0) return;
     const int n_mel = m->n_filters_mel;
     size_t total_pcm = 0;
     for (int i = 0; i < n; ++i) total_pcm += (size_t) n_samples[i];
-    pcm_tmp_.alloc(std::max<size_t>(total_pcm, 1) * 4);
+    if (!pcm_on_device) pcm_tmp_.alloc(std::max<size_t>(total_pcm, 1) * 4);
     std::vector<MelJob> jobs(n);
     size_t at = 0;
     int max_frames = 0;
@@ -132,9 +132,13 @@ void Engine::compute_mel(const std::vector<int> & slots, const std::vector<const
         DevBuf * b = mel_[s];
         b->alloc((size_t) n_mel * n_len * 4);
         mel_len_[s] = n_len;
-        OWK_HIP_CHECK(hipMemcpyAsync(pcm_tmp_.as<float>() + at, pcm[i], (size_t) n_samples[i] * 4,
-                                     hipMemcpyHostToDevice, stream));
-        jobs[i] = MelJob{pcm_tmp_.as<float>() + at, n_samples[i], n_len, b->as<float>()};
+        const float * src = pcm[i];
+        if (!pcm_on_device) {
+            OWK_HIP_CHECK(hipMemcpyAsync(pcm_tmp_.as<float>() + at, pcm[i], (size_t) n_samples[i] * 4,
+                                         hipMemcpyHostToDevice, stream));
+            src = pcm_tmp_.as<float>() + at;
+        }
+        jobs[i] = MelJob{src, n_samples[i], n_len, b->as<float>()};
         at += n_samples[i];
         max_frames = std::max(max_frames, n_len);
     }

@@ -74,7 +74,7 @@ public:
     // ---- mel ----
     // computes normalised log-mel for clips into slots[i]
     void compute_mel(const std::vector<int> & slots, const std::vector<const float *> & pcm,
-                     const std::vector<int> & n_samples);
+                     const std::vector<int> & n_samples, bool pcm_on_device = false);
     void set_mel(int slot, const float * host, int n_len, int n_mel);
     int mel_len(int slot) const { return slot < (int) mel_len_.size() ? mel_len_[slot] : 0; }
     void download_mel(int slot, float * host) const;

@@ -242,6 +242,7 @@ struct Clip {
     int ret = 0;
     bool device_logits = true;  // greedy path on the device
     bool suppress_eot = false;
+    bool pcm_on_device = false;  // owk_full_ext::samples_on_device
 
     int seek = 0, seek_start = 0, seek_end = 0;
     const int delta_min = 10;
@@ -300,7 +301,13 @@ struct Clip {
             st->t_beg = 0;
             st->t_last = 0;
             st->tid_last = 0;
-            if (n > 0) st->energy = signal_energy(pcm, n, 32);
+            if (n > 0 && pcm_on_device) {
+                std::vector<float> host(n);
+                OWK_HIP_CHECK(hipMemcpy(host.data(), pcm, (size_t) n * 4, hipMemcpyDeviceToHost));
+                st->energy = signal_energy(host.data(), n, 32);
+            } else if (n > 0) {
+                st->energy = signal_energy(pcm, n, 32);
+            }
         }
         seek_start = p.offset_ms / 10;
         seek_end = p.duration_ms == 0 ? st->mel_n_len_org : seek_start + p.duration_ms / 10;
@@ -796,6 +803,7 @@ int full_batch(whisper_context * ctx, whisper_state ** states, const whisper_ful
         k.slot = c;
         k.device_logits = params.logits_filter_callback == nullptr;
         k.suppress_eot = ext && ext->suppress_eot;
+        k.pcm_on_device = ext && ext->samples_on_device;
         whisper_state * st = states[c];
         st->result_all.clear();
         if (st->kv.size == 0 || st->kv.size < (uint32_t) base_cells) st->kv.init(base_cells * (st->kv_self_n_dec > 1 ? st->kv_self_n_dec + 2 : 1));
@@ -808,7 +816,7 @@ int full_batch(whisper_context * ctx, whisper_state ** states, const whisper_ful
         for (int c = 0; c < n_clips; ++c)
             if (n_samples[c] > 0) { slots.push_back(c); pcm.push_back(samples[c]); ns.push_back(n_samples[c]); }
         const int64_t t0 = time_us();
-        eng.compute_mel(slots, pcm, ns);
+        eng.compute_mel(slots, pcm, ns, ext && ext->samples_on_device);
         const int64_t dt = time_us() - t0;
         for (size_t i = 0; i < slots.size(); ++i) {
             whisper_state * st = states[slots[i]];

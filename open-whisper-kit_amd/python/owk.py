@@ -84,7 +84,7 @@ class FullParams(C.Structure):
 
 
 class FullExt(C.Structure):
-    _fields_ = [("suppress_eot", C.c_int), ("reserved", C.c_int * 7)]
+    _fields_ = [("suppress_eot", C.c_int), ("samples_on_device", C.c_int), ("reserved", C.c_int * 6)]
 
 
 # every symbol include/whisper.h + include/owk.h declare (checked by tests/test_abi.py)
@@ -269,6 +269,27 @@ class Whisper:
         ext = FullExt()
         ext.suppress_eot = 1 if suppress_eot else 0
         return self.L.owk_full_batch(self.ctx, sts, params, C.byref(ext), ptrs, ns, n)
+
+    def full_batch_device(self, states, dev_ptrs, n_samples, params: FullParams, suppress_eot=False) -> int:
+        """owk_full_batch over audio already resident in HBM (dev_ptrs: device addresses)."""
+        n = len(dev_ptrs)
+        ptrs = (C.POINTER(C.c_float) * n)(*[C.cast(C.c_void_p(p), C.POINTER(C.c_float)) for p in dev_ptrs])
+        ns = (C.c_int * n)(*n_samples)
+        sts = (C.c_void_p * n)(*states)
+        ext = FullExt()
+        ext.suppress_eot = 1 if suppress_eot else 0
+        ext.samples_on_device = 1
+        return self.L.owk_full_batch(self.ctx, sts, params, C.byref(ext), ptrs, ns, n)
+
+    def prof_classes(self):
+        s = self.L.owk_prof_classes(self.ctx)
+        return [c for c in (s.decode() if s else "").split(",") if c]
+
+    def prof(self, cls):
+        ms, n, fl, by = C.c_double(), C.c_long(), C.c_double(), C.c_double()
+        self.L.owk_prof_read(self.ctx, cls.encode(), C.byref(ms), C.byref(n))
+        self.L.owk_prof_work(self.ctx, cls.encode(), C.byref(fl), C.byref(by))
+        return dict(ms=ms.value, launches=n.value, flops=fl.value, bytes=by.value)
 
     def segments(self, state):
         L = self.L
