@@ -80,6 +80,20 @@ ProfScope::~ProfScope() {
 Engine::Engine(const Model * m_, Prof * prof_) : m(m_), prof(prof_) {
     OWK_HIP_CHECK(hipSetDevice(m->device));
     OWK_HIP_CHECK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+    // split-K workspace for every decoder GEMM shape (K = d or 4d; N up to n_vocab)
+    const HParams & hp = m->hp;
+    const int d = hp.n_text_state, nv = hp.n_vocab;
+    size_t fl = 0;
+    for (int N : {3 * d, d, 4 * d, nv})
+        for (int K : {d, 4 * d}) fl = std::max(fl, gemm_ws_floats(N, K));
+    const int tickets = (std::max(4 * d, nv) + 15) / 16;
+    gws_part_.alloc(std::max<size_t>(fl, 1) * 4);
+    gws_tick_.alloc((size_t) tickets * 4);
+    OWK_HIP_CHECK(hipMemsetAsync(gws_tick_.ptr, 0, (size_t) tickets * 4, stream));
+    gws_.partial = gws_part_.as<float>();
+    gws_.partial_floats = fl;
+    gws_.tickets = gws_tick_.as<int>();
+    gws_.n_tickets = tickets;
 }
 
 Engine::~Engine() {
@@ -364,6 +378,7 @@ void Engine::decode(const std::vector<DecodeRow> & rows, const std::vector<int> 
     std::vector<int64_t> rowoff(R);
     std::vector<AttnRow> rs(R), rc(R);
     int max_keys = 1;
+    bool self_oc = false, self_tl = false, cross_oc = false, cross_tl = false;
     for (int r = 0; r < R; ++r) {
         const DecodeRow & x = rows[r];
         tok[r] = x.token;
@@ -372,6 +387,8 @@ void Engine::decode(const std::vector<DecodeRow> & rows, const std::vector<int> 
         rs[r] = AttnRow{r, (int) ((int64_t) x.slot * kv_cells * d), x.n_keys, x.key_off, 0, x.mode_self};
         rc[r] = AttnRow{r, (int) ((int64_t) x.slot * T * d), T, -1, n_ctx_pad - T, x.mode_cross};
         max_keys = std::max(max_keys, x.n_keys);
+        (x.mode_self ? self_tl : self_oc) = true;
+        (x.mode_cross ? cross_tl : cross_oc) = true;
         if (x.logit_row >= 0) lsel[x.logit_row] = r;
     }
     d_keys_.alloc(std::max<size_t>(key_list.size(), 1) * 4);
@@ -397,7 +414,7 @@ void Engine::decode(const std::vector<DecodeRow> & rows, const std::vector<int> 
         ProfScope ps(prof, stream, Mr <= 64 ? "gemm_dec" : "gemm_dec_big", gemm_flops(Mr, N, K),
                      2.0 * ((double) Mr * K + (double) N * K));
         (void) cls;
-        gemm(stream, mode, Mr, N, K, A, K, W, K, ep);
+        gemm(stream, mode, Mr, N, K, A, K, W, K, ep, &gws_);
     };
 
     {
@@ -431,7 +448,7 @@ void Engine::decode(const std::vector<DecodeRow> & rows, const std::vector<int> 
         {
             ProfScope ps(prof, stream, "attn_self");
             attn_decoder(stream, d_q_.as<_Float16>(), d, Kl, Vl, d, d_rows_self_.as<AttnRow>(), R, d_keys_.as<int>(), H,
-                         1.0f, max_keys, d_ao_.as<_Float16>(), d);
+                         1.0f, max_keys, d_ao_.as<_Float16>(), d, self_oc, self_tl);
         }
         {
             EpiParams ep;
@@ -457,7 +474,7 @@ void Engine::decode(const std::vector<DecodeRow> & rows, const std::vector<int> 
             ProfScope ps(prof, stream, "attn_cross", 4.0 * R * (double) n_ctx_pad * d, 2.0 * 2.0 * R * (double) T * d);
             attn_decoder(stream, d_q_.as<_Float16>(), d, cross_k_.as<_Float16>() + l * cross_stride,
                          cross_v_.as<_Float16>() + l * cross_stride, d, d_rows_cross_.as<AttnRow>(), R, nullptr, H,
-                         kq_scale, T, d_ao_.as<_Float16>(), d);
+                         kq_scale, T, d_ao_.as<_Float16>(), d, cross_oc, cross_tl);
         }
         {
             EpiParams ep;
@@ -499,7 +516,7 @@ void Engine::decode(const std::vector<DecodeRow> & rows, const std::vector<int> 
         ep.ldo = nv;
         ProfScope ps(prof, stream, n_logit_rows <= 64 ? "gemm_logits" : "gemm_logits_big",
                      gemm_flops(n_logit_rows, nv, d), 2.0 * (double) nv * d);
-        gemm(stream, EPI_F32, n_logit_rows, nv, d, d_xl_.as<_Float16>(), d, m->d_te, d, ep);
+        gemm(stream, EPI_F32, n_logit_rows, nv, d, d_xl_.as<_Float16>(), d, m->d_te, d, ep, &gws_);
     }
 }
 

@@ -124,6 +124,8 @@ private:
     int dec_rows_cap_ = 0;
 
     DevBuf mel_jobs_, pcm_tmp_;
+    DevBuf gws_part_, gws_tick_;  // split-K workspace of the decode-row GEMMs
+    GemmWs gws_;
 };
 
 } // namespace owk

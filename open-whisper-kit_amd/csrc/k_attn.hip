@@ -176,12 +176,169 @@ void attn_encoder(hipStream_t s, const _Float16 * q, const _Float16 * k, const _
 }
 
 // ----------------------------------------------------------------------------------
-// Decoder attention, reference-order emulation. Block = 4 waves = 4 heads of one row.
-// Phase 1 (parallel): scores s_i = dot(K_i, Q) * scale for all listed keys -> LDS.
-// Phase 2 (sequential over keys, lanes = the 64 head dims):
-//   one_chunk: if s > M { M = s; ms = exp(Mold-M); acc = f16(acc*ms); vs = 1 }
-//              else    { vs = exp(s-M) };  acc = f16(fma(v, vs, acc)); S = S*ms + vs
-//   tiled:     tiles of 16 keys, F32 accumulator (ops.cpp:8417-8510)
+// Decode-step attention, reference-order emulation of the one_chunk path
+// (ops.cpp:8140-8233), one wave per (query row, head):
+//   for each key in visit order:
+//     if s > M { M = s; ms = exp(Mold-M); acc = f16(acc*ms); vs = 1 } else { vs = exp(s-M) }
+//     acc = f16(fma(v, vs, acc));  S = S*ms + vs
+// Only the acc/S recurrences are sequential. Per chunk of 64 keys:
+//   1. K and V tiles stream HBM -> LDS with global_load_lds, AS_NBUF chunks in flight
+//      (the HBM-bound part: K + V of the row's clip, 2 x 128 B per key and head);
+//   2. lane = key: s = (q . k) * scale; an inclusive max-scan over the wave gives each
+//      key's running max before it (Mex), hence its (ms, vs) pair in parallel;
+//   3. lane = head dim: the exact per-key recurrence, with ms/vs broadcast by readlane
+//      and the rescale branch taken only on the (wave-uniform) new-maximum keys.
+// ----------------------------------------------------------------------------------
+constexpr int AS_KC = 64;       // keys per chunk
+constexpr int AS_NBUF = 3;      // chunks in flight
+constexpr int AS_TILE = AS_KC * 128;
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+    static_assert(N >= 0 && N < 64, "vmcnt range");
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+constexpr int AS_MAX_LIST = 2048;  // listed keys (self-attention cells) per row
+
+template <bool LIST>
+__global__ __launch_bounds__(64) void k_attn_step(const _Float16 * __restrict__ q, int ldq,
+                                                  const _Float16 * __restrict__ kb, const _Float16 * __restrict__ vb,
+                                                  int ld_kv, const AttnRow * __restrict__ rows,
+                                                  const int * __restrict__ key_idx, float scale,
+                                                  _Float16 * __restrict__ out, int ldo) {
+    __shared__ __attribute__((aligned(1024))) char smem[AS_NBUF * 2 * AS_TILE];
+    __shared__ int s_list[LIST ? AS_MAX_LIST : 1];
+    const int lane = threadIdx.x;
+    const AttnRow job = rows[blockIdx.y];
+    if (job.mode != 0) return;  // tiled (F32) rows: k_attn_decoder
+    const int h = blockIdx.x;
+    const int n = job.n_keys;
+    if (n <= 0) {
+        out[(size_t) job.q_row * ldo + h * 64 + lane] = (_Float16) 0.0f;
+        return;
+    }
+    if constexpr (LIST) {
+        // cell indices to LDS up front: the stage loop then issues no global loads whose
+        // results it must wait for (a vmcnt wait would also drain the in-flight K/V tiles)
+        const int * list = key_idx + job.key_list;
+        for (int i = lane; i < n; i += 64) s_list[i] = job.key_list >= 0 ? list[i] : i;
+        __builtin_amdgcn_s_waitcnt(0);
+        __builtin_amdgcn_wave_barrier();
+    }
+    const _Float16 * kh = kb + job.kv_base + h * 64;
+    const _Float16 * vh = vb + job.kv_base + h * 64;
+
+    // q of this (row, head): uniform -> scalar registers
+    const half8 * qp = (const half8 *) (q + (size_t) job.q_row * ldq + h * 64);
+    half8 qv[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) qv[c] = qp[c];
+
+    const int nchunks = (n + AS_KC - 1) / AS_KC;
+    // stage chunk c into buffer b: 8 + 8 loads of 1 KB (8 keys x 128 B each)
+    auto stage = [&](int b, int c) {
+        char * sK = smem + b * 2 * AS_TILE;
+        char * sV = sK + AS_TILE;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int kk = i * 8 + (lane >> 3);
+            const int key = min(c * AS_KC + kk, n - 1);
+            const int cell = LIST ? s_list[key] : key;
+            const int seg = (lane & 7) ^ (kk & 7);  // K rows XOR-swizzled for the lane-per-key reads
+            __builtin_amdgcn_global_load_lds((const void *) (kh + (size_t) cell * ld_kv + seg * 8),
+                                             (lds_ptr_t) (sK + i * 1024), 16, 0, 0);
+            __builtin_amdgcn_global_load_lds((const void *) (vh + (size_t) cell * ld_kv + (lane & 7) * 8),
+                                             (lds_ptr_t) (sV + i * 1024), 16, 0, 0);
+        }
+    };
+
+    float M = -INFINITY, S = 0.0f;
+    _Float16 acc = (_Float16) 0.0f;  // the reference's F16 VKQ accumulator (VKQ16)
+#pragma unroll
+    for (int c = 0; c < AS_NBUF - 1; ++c)
+        if (c < nchunks) stage(c, c);
+
+    for (int c = 0; c < nchunks; ++c) {
+        if (c + AS_NBUF - 1 < nchunks) {
+            stage((c + AS_NBUF - 1) % AS_NBUF, c + AS_NBUF - 1);
+            wait_vmcnt<16 * (AS_NBUF - 1)>();
+        } else if (c + 1 < nchunks) {
+            wait_vmcnt<16>();
+        } else {
+            wait_vmcnt<0>();
+        }
+        const char * sK = smem + (c % AS_NBUF) * 2 * AS_TILE;
+        const char * sV = sK + AS_TILE;
+        const int base = c * AS_KC;
+        const int nk = min(AS_KC, n - base);
+
+        // 2. scores, lane = key
+        float s;
+        {
+            const char * kr = sK + lane * 128;
+            float a = 0.0f;
+#pragma unroll
+            for (int cc = 0; cc < 8; ++cc) {
+                const half8 kv = *(const half8 *) (kr + ((cc ^ (lane & 7)) << 4));
+#pragma unroll
+                for (int e = 0; e < 8; ++e) a = fmaf((float) kv[e], (float) qv[cc][e], a);
+            }
+            s = lane < nk ? a * scale : -INFINITY;
+        }
+        float pm = s;  // inclusive running max over the chunk
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const float t = __shfl_up(pm, off, 64);
+            if (lane >= off) pm = fmaxf(pm, t);
+        }
+        float mex = __shfl_up(pm, 1, 64);
+        mex = lane == 0 ? M : fmaxf(mex, M);
+        const bool nm = lane < nk && s > mex;
+        const float ms = nm ? expf(mex - s) : 1.0f;
+        const float vs = nm ? 1.0f : expf(s - mex);
+        M = fmaxf(M, __shfl(pm, 63, 64));
+
+        // 3. recurrence, lane = head dim
+        const _Float16 * vcol = (const _Float16 *) sV + lane;
+        // acc*ms with ms == 1 is exact, so the rescale is applied unconditionally (branch-free)
+        // and each key costs two dependent mixed-precision FMAs (f32 math, f16 result)
+        if (nk == AS_KC) {
+#pragma unroll
+            for (int kk = 0; kk < AS_KC; ++kk) {
+                const float msk = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, ms), kk));
+                const float vsk = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, vs), kk));
+                acc = (_Float16) ((float) acc * msk);
+                acc = (_Float16) fmaf((float) vcol[kk * 64], vsk, (float) acc);
+                S = fmaf(S, msk, vsk);
+            }
+        } else {
+            for (int kk = 0; kk < nk; ++kk) {
+                const float msk = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, ms), kk));
+                const float vsk = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, vs), kk));
+                acc = (_Float16) ((float) acc * msk);
+                acc = (_Float16) fmaf((float) vcol[kk * 64], vsk, (float) acc);
+                S = fmaf(S, msk, vsk);
+            }
+        }
+    }
+    for (int j = 0; j < job.n_zero_pad; ++j) {  // all-zero keys: s = 0, v = 0 (acc + 0*vs == acc)
+        if (0.0f > M) {
+            const float ms = expf(M - 0.0f);
+            M = 0.0f;
+            acc = (_Float16) ((float) acc * ms);
+            S = fmaf(S, ms, 1.0f);
+        } else {
+            S = fmaf(S, 1.0f, expf(0.0f - M));
+        }
+    }
+    const float S_inv = S == 0.0f ? 0.0f : 1.0f / S;
+    out[(size_t) job.q_row * ldo + h * 64 + lane] = (_Float16) ((float) acc * S_inv);
+}
+
+// ----------------------------------------------------------------------------------
+// Decoder attention for rows on the tiled path (prefills of >= 32 tokens: F32
+// accumulator over tiles of 16 keys, ops.cpp:8417-8510). Block = 4 waves = 4 heads.
 // ----------------------------------------------------------------------------------
 constexpr int DA_MAX_KEYS = 2048;
 
@@ -194,6 +351,7 @@ __global__ __launch_bounds__(256) void k_attn_decoder(const _Float16 * __restric
     __shared__ _Float16 qs[4][64];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const AttnRow job = rows[blockIdx.y];
+    if (job.mode == 0) return;  // one_chunk rows: k_attn_step
     const int h = blockIdx.x * 4 + wave;
     if (h >= H) return;
     const int n = job.n_keys;
@@ -291,11 +449,23 @@ __global__ __launch_bounds__(256) void k_attn_decoder(const _Float16 * __restric
 
 void attn_decoder(hipStream_t s, const _Float16 * q, int ldq, const _Float16 * kbase, const _Float16 * vbase, int ld_kv,
                   const AttnRow * rows_dev, int n_rows, const int * key_idx, int H, float scale, int max_keys,
-                  _Float16 * out, int ldo) {
+                  _Float16 * out, int ldo, bool any_one_chunk, bool any_tiled) {
     if (n_rows <= 0) return;
-    if (max_keys > DA_MAX_KEYS) throw std::runtime_error("attn_decoder: too many keys");
-    hipLaunchKernelGGL(k_attn_decoder, dim3((H + 3) / 4, n_rows), dim3(256), 0, s, q, ldq, kbase, vbase, ld_kv, rows_dev,
-                       key_idx, H, scale, out, ldo);
+    if (any_one_chunk) {
+        if (key_idx) {
+            if (max_keys > AS_MAX_LIST) throw std::runtime_error("attn_decoder: too many listed keys");
+            hipLaunchKernelGGL(k_attn_step<true>, dim3(H, n_rows), dim3(64), 0, s, q, ldq, kbase, vbase, ld_kv, rows_dev,
+                               key_idx, scale, out, ldo);
+        } else {
+            hipLaunchKernelGGL(k_attn_step<false>, dim3(H, n_rows), dim3(64), 0, s, q, ldq, kbase, vbase, ld_kv, rows_dev,
+                               key_idx, scale, out, ldo);
+        }
+    }
+    if (any_tiled) {
+        if (max_keys > DA_MAX_KEYS) throw std::runtime_error("attn_decoder: too many keys");
+        hipLaunchKernelGGL(k_attn_decoder, dim3((H + 3) / 4, n_rows), dim3(256), 0, s, q, ldq, kbase, vbase, ld_kv,
+                           rows_dev, key_idx, H, scale, out, ldo);
+    }
 }
 
 } // namespace owk

@@ -7,6 +7,8 @@
 // the f32 additions differs from the reference SIMD dot product.
 #include "kernels.h"
 
+#include <algorithm>
+
 namespace owk {
 
 __device__ __forceinline__ float gelu_lookup(const uint16_t * tab, float x) {
@@ -236,6 +238,97 @@ __global__ __launch_bounds__(512) void k_gemm_skinny(int M, int N, int K, const 
     }
 }
 
+// ---------------------------------------------------------------------------------
+// Decode-row GEMM (M <= 32 rows, the per-step decoder matmuls): weight-streaming.
+// One 16-column tile per block, 8 waves; wave w takes J consecutive k-steps of 32 and
+// issues ALL of its weight and activation loads before the first MFMA, so a launch
+// has (close to) the whole weight matrix in flight at once -- the decode GEMMs are a
+// single HBM round trip, not a pipeline. K beyond 8*J*32 is split over gridDim.y
+// blocks whose partial tiles go to a workspace; the last block to finish a tile (an
+// atomic ticket) adds them in fixed k order, so results do not depend on timing.
+// ---------------------------------------------------------------------------------
+constexpr int GR_WAVES = 8;
+constexpr int GR_JMAX = 8;
+
+template <int MODE, int MT>
+__global__ __launch_bounds__(GR_WAVES * 64) void k_gemm_rows(int M, int N, int K, const _Float16 * __restrict__ A,
+                                                             int lda, const _Float16 * __restrict__ W, int ldw,
+                                                             EpiParams ep, int J, float * __restrict__ part,
+                                                             int * __restrict__ tickets) {
+    __shared__ floatx4 red[GR_WAVES][MT][64];
+    __shared__ int s_last;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int n0 = blockIdx.x * 16;
+    const int nsteps = K >> 5;
+    const int ks0 = (blockIdx.y * GR_WAVES + wave) * J;
+    const int nj = max(0, min(J, nsteps - ks0));
+
+    const int n = min(n0 + (lane & 15), N - 1);
+    const _Float16 * wp = W + (size_t) n * ldw + 8 * (lane >> 4) + ks0 * 32;
+    half8 b[GR_JMAX], a[MT][GR_JMAX];
+#pragma unroll
+    for (int j = 0; j < GR_JMAX; ++j)
+        if (j < nj) b[j] = *(const half8 *) (wp + j * 32);
+#pragma unroll
+    for (int i = 0; i < MT; ++i) {
+        const _Float16 * ap = A + (size_t) min(i * 16 + (lane & 15), M - 1) * lda + 8 * (lane >> 4) + ks0 * 32;
+#pragma unroll
+        for (int j = 0; j < GR_JMAX; ++j)
+            if (j < nj) a[i][j] = *(const half8 *) (ap + j * 32);
+    }
+    floatx4 acc[MT];
+#pragma unroll
+    for (int i = 0; i < MT; ++i) acc[i] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < GR_JMAX; ++j)
+        if (j < nj)
+#pragma unroll
+            for (int i = 0; i < MT; ++i) acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[i][j], b[j], acc[i], 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < MT; ++i) red[wave][i][lane] = acc[i];
+    __syncthreads();
+
+    const int KS = gridDim.y;
+    if (tid < MT * 64) {
+        const int i = tid >> 6, ln = tid & 63;
+        floatx4 sum = red[0][i][ln];
+#pragma unroll
+        for (int w = 1; w < GR_WAVES; ++w) sum += red[w][i][ln];
+        if (KS == 1) {
+            const int c = n0 + (ln & 15);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int r = i * 16 + 4 * (ln >> 4) + e;
+                if (r < M && c < N) epi_store<MODE>(ep, r, c, sum[e]);
+            }
+            return;
+        }
+        // split K: partial tile [ks][tile][i][lane] -> workspace
+        floatx4 * pp = (floatx4 *) part + (((size_t) blockIdx.y * gridDim.x + blockIdx.x) * MT + i) * 64 + ln;
+        *pp = sum;
+    }
+    if (KS == 1) return;
+    __threadfence();
+    __syncthreads();
+    if (tid == 0) s_last = atomicAdd(&tickets[blockIdx.x], 1) == KS - 1;
+    __syncthreads();
+    if (!s_last) return;
+    __threadfence();
+    if (tid < MT * 64) {
+        const int i = tid >> 6, ln = tid & 63;
+        floatx4 sum = floatx4{0.f, 0.f, 0.f, 0.f};
+        for (int ks = 0; ks < KS; ++ks)
+            sum += *((const volatile floatx4 *) part + (((size_t) ks * gridDim.x + blockIdx.x) * MT + i) * 64 + ln);
+        const int c = n0 + (ln & 15);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int r = i * 16 + 4 * (ln >> 4) + e;
+            if (r < M && c < N) epi_store<MODE>(ep, r, c, sum[e]);
+        }
+    }
+    if (tid == 0) tickets[blockIdx.x] = 0;  // re-armed for the next launch on this workspace
+}
+
 template <template <int> class L, typename... Args> static void dispatch_mode(int mode, Args &&... args) {
     switch (mode) {
         case EPI_F16: L<EPI_F16>::run(args...); break;
@@ -264,6 +357,30 @@ template <int MODE> struct LaunchSkinny {
     }
 };
 
+template <int MODE> struct LaunchRows {
+    static void run(hipStream_t s, int M, int N, int K, const _Float16 * A, int lda, const _Float16 * W, int ldw,
+                    const EpiParams & ep, const GemmWs * ws) {
+        const int nsteps = K / 32;
+        int J = std::min(GR_JMAX, (nsteps + GR_WAVES - 1) / GR_WAVES);
+        const int KS = (nsteps + GR_WAVES * J - 1) / (GR_WAVES * J);
+        const int tiles = (N + 15) / 16;
+        float * part = nullptr;
+        int * tick = nullptr;
+        if (KS > 1) {
+            const size_t need = (size_t) KS * tiles * 2 * 64 * 4;  // floats (MT <= 2)
+            if (!ws || ws->partial_floats < need || ws->n_tickets < tiles)
+                throw std::runtime_error("gemm_rows: split-K workspace too small");
+            part = ws->partial;
+            tick = ws->tickets;
+        }
+        const dim3 grid(tiles, KS), block(GR_WAVES * 64);
+        if (M <= 16)
+            hipLaunchKernelGGL((k_gemm_rows<MODE, 1>), grid, block, 0, s, M, N, K, A, lda, W, ldw, ep, J, part, tick);
+        else
+            hipLaunchKernelGGL((k_gemm_rows<MODE, 2>), grid, block, 0, s, M, N, K, A, lda, W, ldw, ep, J, part, tick);
+    }
+};
+
 static void check_shape(int M, int N, int K, int lda, int ldw, int kmul) {
     if (M <= 0 || N <= 0 || K <= 0 || K % kmul != 0 || lda < K || ldw < K || (lda % 8) || (ldw % 8))
         throw std::runtime_error("gemm: unsupported shape M=" + std::to_string(M) + " N=" + std::to_string(N) +
@@ -283,12 +400,23 @@ void gemm_f16_skinny(hipStream_t s, int mode, int M, int N, int K, const _Float1
     dispatch_mode<LaunchSkinny>(mode, s, M, N, K, A, lda, W, ldw, ep);
 }
 
+size_t gemm_ws_floats(int N, int K) {
+    const int nsteps = K / 32;
+    const int J = std::min(GR_JMAX, (nsteps + GR_WAVES - 1) / GR_WAVES);
+    const int KS = (nsteps + GR_WAVES * J - 1) / (GR_WAVES * J);
+    return KS > 1 ? (size_t) KS * ((N + 15) / 16) * 2 * 64 * 4 : 0;
+}
+
 void gemm(hipStream_t s, int mode, int M, int N, int K, const _Float16 * A, int lda, const _Float16 * W, int ldw,
-          const EpiParams & ep) {
-    if (M <= 64 && K % 32 == 0)
+          const EpiParams & ep, const GemmWs * ws) {
+    if (M <= 32 && K % 32 == 0) {
+        check_shape(M, N, K, lda, ldw, 32);
+        dispatch_mode<LaunchRows>(mode, s, M, N, K, A, lda, W, ldw, ep, ws);
+    } else if (M <= 64 && K % 32 == 0) {
         gemm_f16_skinny(s, mode, M, N, K, A, lda, W, ldw, ep);
-    else
+    } else {
         gemm_f16(s, mode, M, N, K, A, lda, W, ldw, ep);
+    }
 }
 
 } // namespace owk

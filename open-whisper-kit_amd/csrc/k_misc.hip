@@ -19,6 +19,8 @@ __device__ __forceinline__ double wave_sum_d(double v) {
 // then ((x-mean)*scale)*w + b with one rounding per op (built with -ffp-contract=off).
 // One wave per row; the f16 output feeds the next GEMM directly.
 // ----------------------------------------------------------------------------------
+constexpr int LN_V4 = 8;  // float4 per lane held in registers -> d <= 2048
+
 __global__ __launch_bounds__(256) void k_layernorm_f16(const float * __restrict__ x, int rows, int d,
                                                        const float * __restrict__ w, const float * __restrict__ b,
                                                        float eps, _Float16 * __restrict__ out, int ldo,
@@ -26,32 +28,57 @@ __global__ __launch_bounds__(256) void k_layernorm_f16(const float * __restrict_
     const int lane = threadIdx.x & 63;
     const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (row >= rows) return;
-    const float * xr = x + (size_t) (row_idx ? row_idx[row] : row) * d;
+    const float4 * xr = (const float4 * ) (x + (size_t) (row_idx ? row_idx[row] : row) * d);
+    const int n4 = d >> 2;
+    // the whole row is loaded once, up front (one memory round trip per launch)
+    float4 xv[LN_V4];
+#pragma unroll
+    for (int j = 0; j < LN_V4; ++j) {
+        const int i = lane + 64 * j;
+        xv[j] = i < n4 ? xr[i] : float4{0.f, 0.f, 0.f, 0.f};
+    }
     double s = 0.0;
-    for (int i = lane; i < d; i += 64) s += (double) xr[i];
+#pragma unroll
+    for (int j = 0; j < LN_V4; ++j)
+        s += ((double) xv[j].x + (double) xv[j].y) + ((double) xv[j].z + (double) xv[j].w);
     s = wave_sum_d(s);
     const float mean = (float) s / (float) d;
     double v = 0.0;
-    for (int i = lane; i < d; i += 64) {
-        const float t = xr[i] - mean;
-        v += (double) (t * t);
+#pragma unroll
+    for (int j = 0; j < LN_V4; ++j) {
+        if (lane + 64 * j < n4) {
+            const float tx = xv[j].x - mean, ty = xv[j].y - mean, tz = xv[j].z - mean, tw = xv[j].w - mean;
+            v += ((double) (tx * tx) + (double) (ty * ty)) + ((double) (tz * tz) + (double) (tw * tw));
+        }
     }
     v = wave_sum_d(v);
     const float var = (float) (v / (double) d);
     const float scale = 1.0f / sqrtf(var + eps);
+    const float4 * w4 = (const float4 *) w;
+    const float4 * b4 = (const float4 *) b;
     _Float16 * o = out + (size_t) row * ldo;
-    for (int i = lane; i < d; i += 64) {
-        float y = (xr[i] - mean) * scale;
-        y = y * w[i];
-        y = y + b[i];
-        o[i] = (_Float16) y;
-        if (out32) out32[(size_t) row * d + i] = y;
+#pragma unroll
+    for (int j = 0; j < LN_V4; ++j) {
+        const int i = lane + 64 * j;
+        if (i < n4) {
+            const float4 ww = w4[i], bb = b4[i];
+            float4 y;
+            y.x = (xv[j].x - mean) * scale * ww.x + bb.x;
+            y.y = (xv[j].y - mean) * scale * ww.y + bb.y;
+            y.z = (xv[j].z - mean) * scale * ww.z + bb.z;
+            y.w = (xv[j].w - mean) * scale * ww.w + bb.w;
+            half4 h;
+            h[0] = (_Float16) y.x; h[1] = (_Float16) y.y; h[2] = (_Float16) y.z; h[3] = (_Float16) y.w;
+            *(half4 *) (o + 4 * i) = h;
+            if (out32) *(float4 *) (out32 + (size_t) row * d + 4 * i) = y;
+        }
     }
 }
 
 void layernorm_f16(hipStream_t s, const float * x, int rows, int d, const float * w, const float * b, float eps,
                    _Float16 * out, int ldo, const int * row_idx, float * out32) {
     if (rows <= 0) return;
+    if (d % 4 != 0 || d > 4 * 64 * LN_V4 || ldo % 4 != 0) throw std::runtime_error("layernorm_f16: unsupported width");
     hipLaunchKernelGGL(k_layernorm_f16, dim3((rows + 3) / 4), dim3(256), 0, s, x, rows, d, w, b, eps, out, ldo,
                        row_idx, out32);
 }

@@ -47,9 +47,17 @@ void gemm_f16(hipStream_t s, int mode, int M, int N, int K, const _Float16 * A, 
 // skinny (decode steps, M <= 64): split-K across the waves of a block, LDS reduction
 void gemm_f16_skinny(hipStream_t s, int mode, int M, int N, int K, const _Float16 * A, int lda,
                      const _Float16 * W, int ldw, const EpiParams & ep);
-// dispatch on M
+// split-K workspace of the decode-row GEMM (owned by the caller: one per stream)
+struct GemmWs {
+    float * partial = nullptr;  // partial tiles
+    size_t partial_floats = 0;
+    int * tickets = nullptr;    // per-column-tile arrival counters, zero-initialised, self-resetting
+    int n_tickets = 0;
+};
+size_t gemm_ws_floats(int N, int K);  // partial floats a (N, K) decode-row GEMM needs (0 = no split)
+// dispatch on M: <= 32 rows decode-row GEMM, <= 64 skinny, else 128x128 tiles
 void gemm(hipStream_t s, int mode, int M, int N, int K, const _Float16 * A, int lda,
-          const _Float16 * W, int ldw, const EpiParams & ep);
+          const _Float16 * W, int ldw, const EpiParams & ep, const GemmWs * ws = nullptr);
 
 // ---------------------------------------------------------------------------------
 // normalisation / elementwise
@@ -112,7 +120,7 @@ struct AttnRow {
 };
 void attn_decoder(hipStream_t s, const _Float16 * q, int ldq, const _Float16 * kbase, const _Float16 * vbase,
                   int ld_kv, const AttnRow * rows_dev, int n_rows, const int * key_idx, int H, float scale,
-                  int max_keys, _Float16 * out, int ldo);
+                  int max_keys, _Float16 * out, int ldo, bool any_one_chunk, bool any_tiled);
 
 // ---------------------------------------------------------------------------------
 // logits -> token (whisper_process_logits + whisper_sample_token, greedy)

@@ -84,13 +84,24 @@ def log_mel(pcm, filters):
 
 
 # ------------------------------------------------------------------------------------
+def _tanhf(x):
+    """The C library's tanhf (what the reference calls); numpy's float32 tanh differs in
+    the last ulp for some inputs, which flips f16 table entries."""
+    import ctypes
+
+    libm = ctypes.CDLL("libm.so.6")
+    libm.tanhf.restype = ctypes.c_float
+    libm.tanhf.argtypes = [ctypes.c_float]
+    return np.array([libm.tanhf(float(v)) for v in np.asarray(x, f32)], f32)
+
+
 def gelu_table():
     x = np.arange(65536, dtype=np.uint16).view(f16).astype(f32)
     a = f32(0.044715)
     c = f32(0.79788456080286535587989211986876)
     with np.errstate(all="ignore"):
         inner = (((a * x).astype(np.float64) * x.astype(np.float64)) + 1.0).astype(f32)  # fma(a*x, x, 1)
-        g = (f32(0.5) * x * (f32(1.0) + np.tanh(c * x * inner).astype(f32))).astype(f32)
+        g = (f32(0.5) * x * (f32(1.0) + _tanhf(c * x * inner))).astype(f32)
     return g.astype(f16).view(np.uint16)
 
 
