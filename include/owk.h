@@ -52,6 +52,8 @@ WHISPER_API int owk_debug_enc(struct whisper_context * ctx, struct whisper_state
 WHISPER_API int owk_debug_cross(struct whisper_context * ctx, struct whisper_state * st, int slot, int layer,
                                 uint16_t * k, uint16_t * v);
 WHISPER_API const uint16_t * owk_debug_gelu_table(void);
+/* out[M][N] = A[M][K] . W[N][K]^T (f16 bits in, f32 out) through the engine's GEMM dispatch */
+WHISPER_API int owk_debug_gemm(int device, int M, int N, int K, const uint16_t * a, const uint16_t * w, float * out);
 
 /* library identity: 1 when the gfx950 HIP code object is present and a device is usable */
 WHISPER_API int owk_device_ok(int device);

@@ -63,4 +63,27 @@ struct DevBuf {
     template <typename T> T * as() const { return (T *) ptr; }
 };
 
+// RAII pinned (page-locked) host allocation: async H2D/D2H copies from it are true DMA
+struct PinnedBuf {
+    void * ptr = nullptr;
+    size_t bytes = 0;
+    PinnedBuf() = default;
+    PinnedBuf(const PinnedBuf &) = delete;
+    PinnedBuf & operator=(const PinnedBuf &) = delete;
+    ~PinnedBuf() { release(); }
+    void release() {
+        if (ptr) (void) hipHostFree(ptr);
+        ptr = nullptr;
+        bytes = 0;
+    }
+    void alloc(size_t n) {
+        if (n <= bytes && ptr) return;
+        release();
+        if (n == 0) return;
+        OWK_HIP_CHECK(hipHostMalloc(&ptr, n, hipHostMallocDefault));
+        bytes = n;
+    }
+    template <typename T> T * as() const { return (T *) ptr; }
+};
+
 } // namespace owk

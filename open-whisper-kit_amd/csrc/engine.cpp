@@ -86,17 +86,13 @@ Engine::Engine(const Model * m_, Prof * prof_) : m(m_), prof(prof_) {
     size_t fl = 0;
     for (int N : {3 * d, d, 4 * d, nv})
         for (int K : {d, 4 * d}) fl = std::max(fl, gemm_ws_floats(N, K));
-    const int tickets = (std::max(4 * d, nv) + 15) / 16;
     gws_part_.alloc(std::max<size_t>(fl, 1) * 4);
-    gws_tick_.alloc((size_t) tickets * 4);
-    OWK_HIP_CHECK(hipMemsetAsync(gws_tick_.ptr, 0, (size_t) tickets * 4, stream));
     gws_.partial = gws_part_.as<float>();
     gws_.partial_floats = fl;
-    gws_.tickets = gws_tick_.as<int>();
-    gws_.n_tickets = tickets;
 }
 
 Engine::~Engine() {
+    clear_graphs();
     for (auto * b : mel_) delete b;
     if (stream) (void) hipStreamDestroy(stream);
 }
@@ -346,39 +342,84 @@ void Engine::download_cross(int slot, int layer, uint16_t * kh, uint16_t * vh) c
     OWK_HIP_CHECK(hipMemcpy(vh, cross_v_.as<_Float16>() + o, per * 2, hipMemcpyDeviceToHost));
 }
 
+// decode staging: one pinned host image + its device copy, fixed sections sized by the
+// row/key capacities so the pointers captured in decode graphs stay valid
+void Engine::stage_layout(int C, int KC) {
+    size_t o = 0;
+    auto sec = [&](size_t bytes) {
+        const size_t at = o;
+        o += (bytes + 255) / 256 * 256;
+        return at;
+    };
+    st_tok_ = sec((size_t) C * 4);
+    st_pos_ = sec((size_t) C * 4);
+    st_rowoff_ = sec((size_t) C * 8);
+    st_rs_ = sec((size_t) C * sizeof(AttnRow));
+    st_rc_ = sec((size_t) C * sizeof(AttnRow));
+    st_lsel_ = sec((size_t) C * 4);
+    st_keys_ = sec((size_t) KC * 4);
+    st_bytes_ = o;
+}
+
+void Engine::clear_graphs() {
+    for (auto & kv : graphs_) (void) hipGraphExecDestroy(kv.second);
+    graphs_.clear();
+}
+
+uint64_t Engine::buffers_signature() const {
+    uint64_t h = 1469598103934665603ull;
+    for (const void * p : {d_x_.ptr, d_xn_.ptr, d_q_.ptr, d_ao_.ptr, d_h_.ptr, d_xl_.ptr, logits_.ptr, d_stg_.ptr,
+                           self_k_.ptr, self_v_.ptr, cross_k_.ptr, cross_v_.ptr, gws_part_.ptr})
+        h = (h ^ (uint64_t) (uintptr_t) p) * 1099511628211ull;
+    return h;
+}
+
 void Engine::decode(const std::vector<DecodeRow> & rows, const std::vector<int> & key_list, int n_logit_rows) {
     const HParams & hp = m->hp;
     const int R = (int) rows.size();
     if (R == 0) return;
-    const int d = hp.n_text_state, H = hp.n_text_head, T = hp.n_audio_ctx;
+    const int d = hp.n_text_state, T = hp.n_audio_ctx;
     const int n_ctx_pad = (T + 255) / 256 * 256;
     const int nv = hp.n_vocab;
 
-    if (R > dec_rows_cap_) {
+    const int nk = (int) key_list.size();
+    if (R > dec_rows_cap_ || nk > dec_keys_cap_) {
         sync();
-        dec_rows_cap_ = std::max(R, 64);
-        const int C = dec_rows_cap_;
-        d_x_.alloc((size_t) C * d * 4);
-        d_xn_.alloc((size_t) C * d * 2);
-        d_q_.alloc((size_t) C * d * 2);
-        d_ao_.alloc((size_t) C * d * 2);
-        d_h_.alloc((size_t) C * 4 * d * 2);
-        d_tok_.alloc((size_t) C * 4);
-        d_pos_.alloc((size_t) C * 4);
-        d_rowoff_.alloc((size_t) C * 8);
-        d_rows_self_.alloc(sizeof(AttnRow) * C);
-        d_rows_cross_.alloc(sizeof(AttnRow) * C);
-        d_lsel_.alloc((size_t) C * 4);
-        d_xl_.alloc((size_t) C * d * 2);
+        if (R > dec_rows_cap_) {
+            dec_rows_cap_ = std::max(R, 64);
+            const int C = dec_rows_cap_;
+            d_x_.alloc((size_t) C * d * 4);
+            d_xn_.alloc((size_t) C * d * 2);
+            d_q_.alloc((size_t) C * d * 2);
+            d_ao_.alloc((size_t) C * d * 2);
+            d_h_.alloc((size_t) C * 4 * d * 2);
+            d_xl_.alloc((size_t) C * d * 2);
+            logits_.alloc((size_t) C * nv * 4);
+        }
+        dec_keys_cap_ = std::max(nk, std::max(dec_keys_cap_ * 2, 4096));
+        stage_layout(dec_rows_cap_, dec_keys_cap_);
+        stg_.alloc(st_bytes_);
+        d_stg_.alloc(st_bytes_);
     }
-    if (n_logit_rows > 0) logits_.alloc((size_t) std::max(n_logit_rows, 1) * nv * 4);
+    if (n_logit_rows > R) throw std::runtime_error("decode: more logit rows than rows");
 
-    // host-side staging
-    std::vector<int> tok(R), pos(R), lsel(std::max(n_logit_rows, 1), 0);
-    std::vector<int64_t> rowoff(R);
-    std::vector<AttnRow> rs(R), rc(R);
-    int max_keys = 1;
-    bool self_oc = false, self_tl = false, cross_oc = false, cross_tl = false;
+    // checks the kernels rely on (fail loudly rather than read out of bounds)
+    if ((int64_t) cap_slots * std::max(kv_cells, T) * d >= (int64_t) 1 << 31)
+        throw std::runtime_error("decode: KV offsets exceed 32 bits");
+    for (const auto & x : rows)
+        if (x.slot < 0 || x.slot >= cap_slots || x.cell < 0 || x.cell >= kv_cells || x.token < 0 || x.token >= nv ||
+            x.pos < 0 || x.pos >= hp.n_text_ctx || x.n_keys < 0 || x.key_off < 0 || x.key_off + x.n_keys > nk)
+            throw std::runtime_error("decode: row out of range");
+
+    // host image -> one H2D copy
+    char * h = stg_.as<char>();
+    int * tok = (int *) (h + st_tok_);
+    int * pos = (int *) (h + st_pos_);
+    int64_t * rowoff = (int64_t *) (h + st_rowoff_);
+    AttnRow * rs = (AttnRow *) (h + st_rs_);
+    AttnRow * rc = (AttnRow *) (h + st_rc_);
+    int * lsel = (int *) (h + st_lsel_);
+    DecShape sh{R, n_logit_rows, false, false, false, false, 1};
     for (int r = 0; r < R; ++r) {
         const DecodeRow & x = rows[r];
         tok[r] = x.token;
@@ -386,40 +427,79 @@ void Engine::decode(const std::vector<DecodeRow> & rows, const std::vector<int> 
         rowoff[r] = ((int64_t) x.slot * kv_cells + x.cell) * d;
         rs[r] = AttnRow{r, (int) ((int64_t) x.slot * kv_cells * d), x.n_keys, x.key_off, 0, x.mode_self};
         rc[r] = AttnRow{r, (int) ((int64_t) x.slot * T * d), T, -1, n_ctx_pad - T, x.mode_cross};
-        max_keys = std::max(max_keys, x.n_keys);
-        (x.mode_self ? self_tl : self_oc) = true;
-        (x.mode_cross ? cross_tl : cross_oc) = true;
+        sh.max_keys = std::max(sh.max_keys, x.n_keys);
+        (x.mode_self ? sh.self_tl : sh.self_oc) = true;
+        (x.mode_cross ? sh.cross_tl : sh.cross_oc) = true;
         if (x.logit_row >= 0) lsel[x.logit_row] = r;
     }
-    d_keys_.alloc(std::max<size_t>(key_list.size(), 1) * 4);
-    OWK_HIP_CHECK(hipMemcpyAsync(d_tok_.ptr, tok.data(), R * 4, hipMemcpyHostToDevice, stream));
-    OWK_HIP_CHECK(hipMemcpyAsync(d_pos_.ptr, pos.data(), R * 4, hipMemcpyHostToDevice, stream));
-    OWK_HIP_CHECK(hipMemcpyAsync(d_rowoff_.ptr, rowoff.data(), R * 8, hipMemcpyHostToDevice, stream));
-    OWK_HIP_CHECK(hipMemcpyAsync(d_rows_self_.ptr, rs.data(), sizeof(AttnRow) * R, hipMemcpyHostToDevice, stream));
-    OWK_HIP_CHECK(hipMemcpyAsync(d_rows_cross_.ptr, rc.data(), sizeof(AttnRow) * R, hipMemcpyHostToDevice, stream));
-    if (!key_list.empty())
-        OWK_HIP_CHECK(hipMemcpyAsync(d_keys_.ptr, key_list.data(), key_list.size() * 4, hipMemcpyHostToDevice, stream));
-    OWK_HIP_CHECK(hipMemcpyAsync(d_lsel_.ptr, lsel.data(), lsel.size() * 4, hipMemcpyHostToDevice, stream));
+    if (nk) memcpy(h + st_keys_, key_list.data(), (size_t) nk * 4);
+    OWK_HIP_CHECK(hipMemcpyAsync(d_stg_.ptr, h, st_keys_ + (size_t) nk * 4, hipMemcpyHostToDevice, stream));
+    if (sh.self_oc && sh.max_keys > attn_max_listed_keys()) throw std::runtime_error("decode: too many self-attention keys");
+    if (sh.self_tl && sh.max_keys > attn_max_tiled_keys()) throw std::runtime_error("decode: too many self-attention keys");
 
-    // checks the kernels rely on (fail loudly rather than read out of bounds)
-    if ((int64_t) cap_slots * std::max(kv_cells, T) * d >= (int64_t) 1 << 31)
-        throw std::runtime_error("decode: KV offsets exceed 32 bits");
-    for (const auto & x : rows)
-        if (x.slot < 0 || x.slot >= cap_slots || x.cell < 0 || x.cell >= kv_cells || x.token < 0 || x.token >= nv ||
-            x.pos < 0 || x.pos >= hp.n_text_ctx)
-            throw std::runtime_error("decode: row out of range");
+    static const bool no_graph = getenv("OWK_NO_GRAPH") && atoi(getenv("OWK_NO_GRAPH")) != 0;
+    if ((prof && prof->on) || no_graph) {  // per-kernel events (or debugging): eager launches
+        launch_decode(sh);
+        return;
+    }
+    // replay a captured graph of the whole decoder pass (one launch instead of ~10 per layer)
+    const uint64_t sig = buffers_signature();
+    if (sig != graphs_sig_) {
+        clear_graphs();
+        graphs_sig_ = sig;
+    }
+    const uint64_t key = (uint64_t) R | ((uint64_t) n_logit_rows << 20) | ((uint64_t) sh.self_oc << 40) |
+                         ((uint64_t) sh.self_tl << 41) | ((uint64_t) sh.cross_oc << 42) | ((uint64_t) sh.cross_tl << 43);
+    auto it = graphs_.find(key);
+    if (it == graphs_.end()) {
+        if (graphs_.size() >= 64) clear_graphs();
+        hipGraph_t g = nullptr;
+        OWK_HIP_CHECK(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal));
+        try {
+            launch_decode(sh);
+        } catch (...) {
+            (void) hipStreamEndCapture(stream, &g);
+            if (g) (void) hipGraphDestroy(g);
+            throw;
+        }
+        OWK_HIP_CHECK(hipStreamEndCapture(stream, &g));
+        hipGraphExec_t ex = nullptr;
+        const hipError_t e = hipGraphInstantiate(&ex, g, nullptr, nullptr, 0);
+        (void) hipGraphDestroy(g);
+        OWK_HIP_CHECK(e);
+        it = graphs_.emplace(key, ex).first;
+    }
+    OWK_HIP_CHECK(hipGraphLaunch(it->second, stream));
+}
 
-    auto G = [&](const char * cls, int mode, int N, int K, const _Float16 * A, const _Float16 * W, const EpiParams & ep,
-                 int Mr) {
+void Engine::launch_decode(const DecShape & sh) {
+    const HParams & hp = m->hp;
+    const int R = sh.R, n_logit_rows = sh.n_logit;
+    const int d = hp.n_text_state, H = hp.n_text_head, T = hp.n_audio_ctx;
+    const int n_ctx_pad = (T + 255) / 256 * 256;
+    const int nv = hp.n_vocab;
+    char * dv = d_stg_.as<char>();
+    const int * d_tok = (const int *) (dv + st_tok_);
+    const int * d_pos = (const int *) (dv + st_pos_);
+    const int64_t * d_rowoff = (const int64_t *) (dv + st_rowoff_);
+    const AttnRow * d_rs = (const AttnRow *) (dv + st_rs_);
+    const AttnRow * d_rc = (const AttnRow *) (dv + st_rc_);
+    const int * d_lsel = (const int *) (dv + st_lsel_);
+    const int * d_keys = (const int *) (dv + st_keys_);
+    const int max_keys = sh.max_keys;
+    const bool self_oc = sh.self_oc, self_tl = sh.self_tl, cross_oc = sh.cross_oc, cross_tl = sh.cross_tl;
+
+    auto G = [&](const char * cls, int mode, int N, int K, const _Float16 * A, const _Float16 * W, const _Float16 * Wt,
+                 const EpiParams & ep, int Mr) {
         ProfScope ps(prof, stream, Mr <= 64 ? "gemm_dec" : "gemm_dec_big", gemm_flops(Mr, N, K),
                      2.0 * ((double) Mr * K + (double) N * K));
         (void) cls;
-        gemm(stream, mode, Mr, N, K, A, K, W, K, ep, &gws_);
+        gemm(stream, mode, Mr, N, K, A, K, W, K, ep, &gws_, Wt);
     };
 
     {
         ProfScope ps(prof, stream, "embed");
-        embed_tokens(stream, m->d_te, m->d_pe, d_tok_.as<int>(), d_pos_.as<int>(), R, d, d_x_.as<float>());
+        embed_tokens(stream, m->d_te, m->d_pe, d_tok, d_pos, R, d, d_x_.as<float>());
     }
     const float kq_scale = powf(64.0f, -0.25f);
     const size_t self_stride = (size_t) cap_slots * kv_cells * d;
@@ -442,12 +522,12 @@ void Engine::decode(const std::vector<DecodeRow> & rows, const std::vector<int> 
             ep.out16b = Kl;
             ep.out16c = Vl;
             ep.d = d;
-            ep.row_off = d_rowoff_.as<int64_t>();
-            G("qkv", EPI_QKV_DEC, 3 * d, d, d_xn_.as<_Float16>(), L.w_qkv, ep, R);
+            ep.row_off = d_rowoff;
+            G("qkv", EPI_QKV_DEC, 3 * d, d, d_xn_.as<_Float16>(), L.w_qkv, L.t_qkv, ep, R);
         }
         {
             ProfScope ps(prof, stream, "attn_self");
-            attn_decoder(stream, d_q_.as<_Float16>(), d, Kl, Vl, d, d_rows_self_.as<AttnRow>(), R, d_keys_.as<int>(), H,
+            attn_decoder(stream, d_q_.as<_Float16>(), d, Kl, Vl, d, d_rs, R, d_keys, H,
                          1.0f, max_keys, d_ao_.as<_Float16>(), d, self_oc, self_tl);
         }
         {
@@ -456,7 +536,7 @@ void Engine::decode(const std::vector<DecodeRow> & rows, const std::vector<int> 
             ep.resid = d_x_.as<float>();
             ep.out32 = d_x_.as<float>();
             ep.ldo = d;
-            G("o", EPI_RESID_F32, d, d, d_ao_.as<_Float16>(), L.w_o, ep, R);
+            G("o", EPI_RESID_F32, d, d, d_ao_.as<_Float16>(), L.w_o, L.t_o, ep, R);
         }
         {
             ProfScope ps(prof, stream, "layernorm");
@@ -467,13 +547,13 @@ void Engine::decode(const std::vector<DecodeRow> & rows, const std::vector<int> 
             ep.bias = L.cb_q;
             ep.out16 = d_q_.as<_Float16>();
             ep.ldo = d;
-            G("cq", EPI_F16, d, d, d_xn_.as<_Float16>(), L.cw_q, ep, R);
+            G("cq", EPI_F16, d, d, d_xn_.as<_Float16>(), L.cw_q, L.t_cq, ep, R);
         }
         {
             // bytes: cross K and V of each row's clip (the HBM-bound part of a decode step)
             ProfScope ps(prof, stream, "attn_cross", 4.0 * R * (double) n_ctx_pad * d, 2.0 * 2.0 * R * (double) T * d);
             attn_decoder(stream, d_q_.as<_Float16>(), d, cross_k_.as<_Float16>() + l * cross_stride,
-                         cross_v_.as<_Float16>() + l * cross_stride, d, d_rows_cross_.as<AttnRow>(), R, nullptr, H,
+                         cross_v_.as<_Float16>() + l * cross_stride, d, d_rc, R, nullptr, H,
                          kq_scale, T, d_ao_.as<_Float16>(), d, cross_oc, cross_tl);
         }
         {
@@ -482,7 +562,7 @@ void Engine::decode(const std::vector<DecodeRow> & rows, const std::vector<int> 
             ep.resid = d_x_.as<float>();
             ep.out32 = d_x_.as<float>();
             ep.ldo = d;
-            G("co", EPI_RESID_F32, d, d, d_ao_.as<_Float16>(), L.cw_o, ep, R);
+            G("co", EPI_RESID_F32, d, d, d_ao_.as<_Float16>(), L.cw_o, L.t_co, ep, R);
         }
         {
             ProfScope ps(prof, stream, "layernorm");
@@ -494,7 +574,7 @@ void Engine::decode(const std::vector<DecodeRow> & rows, const std::vector<int> 
             ep.gelu_tab = m->gelu_tab;
             ep.out16 = d_h_.as<_Float16>();
             ep.ldo = 4 * d;
-            G("mlp0", EPI_GELU_F16, 4 * d, d, d_xn_.as<_Float16>(), L.w_mlp0, ep, R);
+            G("mlp0", EPI_GELU_F16, 4 * d, d, d_xn_.as<_Float16>(), L.w_mlp0, L.t_mlp0, ep, R);
         }
         {
             EpiParams ep;
@@ -502,62 +582,22 @@ void Engine::decode(const std::vector<DecodeRow> & rows, const std::vector<int> 
             ep.resid = d_x_.as<float>();
             ep.out32 = d_x_.as<float>();
             ep.ldo = d;
-            G("mlp1", EPI_RESID_F32, d, 4 * d, d_h_.as<_Float16>(), L.w_mlp1, ep, R);
+            G("mlp1", EPI_RESID_F32, d, 4 * d, d_h_.as<_Float16>(), L.w_mlp1, L.t_mlp1, ep, R);
         }
     }
     if (n_logit_rows > 0) {
         {
             ProfScope ps(prof, stream, "layernorm");
             layernorm_f16(stream, d_x_.as<float>(), n_logit_rows, d, m->d_ln_w, m->d_ln_b, hp.eps, d_xl_.as<_Float16>(),
-                          d, d_lsel_.as<int>());
+                          d, d_lsel);
         }
         EpiParams ep;
         ep.out32 = logits_.as<float>();
         ep.ldo = nv;
         ProfScope ps(prof, stream, n_logit_rows <= 64 ? "gemm_logits" : "gemm_logits_big",
                      gemm_flops(n_logit_rows, nv, d), 2.0 * (double) nv * d);
-        gemm(stream, EPI_F32, n_logit_rows, nv, d, d_xl_.as<_Float16>(), d, m->d_te, d, ep, &gws_);
+        gemm(stream, EPI_F32, n_logit_rows, nv, d, d_xl_.as<_Float16>(), d, m->d_te, d, ep, &gws_, m->d_te_t);
     }
-}
-
-void Engine::logits_maxes(int n, std::vector<float> & out) {
-    out.resize(n);
-    if (n <= 0) return;
-    lmax_.alloc((size_t) n * 4);
-    logits_row_max(stream, logits_.as<float>(), n, m->hp.n_vocab, lmax_.as<float>());
-    OWK_HIP_CHECK(hipMemcpyAsync(out.data(), lmax_.ptr, (size_t) n * 4, hipMemcpyDeviceToHost, stream));
-    sync();
-}
-
-void Engine::row0_update(const std::vector<std::pair<int, int>> & map) {
-    if (map.empty()) return;
-    const int nv = m->hp.n_vocab;
-    row0_.alloc((size_t) cap_slots * nv * 4);
-    std::vector<int2> h(map.size());
-    for (size_t i = 0; i < map.size(); ++i) h[i] = make_int2(map[i].first, map[i].second);
-    map_.alloc(h.size() * sizeof(int2));
-    OWK_HIP_CHECK(hipMemcpyAsync(map_.ptr, h.data(), h.size() * sizeof(int2), hipMemcpyHostToDevice, stream));
-    logits_copy_rows(stream, logits_.as<float>(), nv, map_.as<int2>(), (int) h.size(), row0_.as<float>());
-}
-
-void Engine::nosp(const std::vector<std::pair<int, float>> & req, std::vector<float> & out) {
-    const int n = (int) req.size();
-    out.resize(n);
-    if (n == 0) return;
-    const int nv = m->hp.n_vocab;
-    row0_.alloc((size_t) cap_slots * nv * 4);
-    std::vector<int> idx(n);
-    std::vector<float> mx(n);
-    for (int i = 0; i < n; ++i) { idx[i] = req[i].first; mx[i] = req[i].second; }
-    nosp_idx_.alloc(n * 4);
-    nosp_max_.alloc(n * 4);
-    nosp_out_.alloc(n * 4);
-    OWK_HIP_CHECK(hipMemcpyAsync(nosp_idx_.ptr, idx.data(), n * 4, hipMemcpyHostToDevice, stream));
-    OWK_HIP_CHECK(hipMemcpyAsync(nosp_max_.ptr, mx.data(), n * 4, hipMemcpyHostToDevice, stream));
-    nosp_probs(stream, row0_.as<float>(), nv, nosp_idx_.as<int>(), nosp_max_.as<float>(), n, m->vocab.nosp,
-               nosp_out_.as<float>());
-    OWK_HIP_CHECK(hipMemcpyAsync(out.data(), nosp_out_.ptr, n * 4, hipMemcpyDeviceToHost, stream));
-    sync();
 }
 
 void Engine::download_logits(int logit_row, float * host) const {
@@ -573,38 +613,109 @@ void Engine::upload_logits(int logit_row, const float * host) {
     sync();
 }
 
-void Engine::process_logits(const std::vector<LogitJob> & jobs, const VocabInfo & vi_in, std::vector<TokenOut> & out,
-                            float * probs_host, float * logprobs_host) {
-    const int n = (int) jobs.size();
-    out.resize(n);
-    if (n == 0) return;
+void Engine::step_post(const StepPost & post, const std::vector<LogitJob> & jobs, const VocabInfo & vi_in,
+                       std::vector<TokenOut> & out, std::vector<float> & nosp_out, float * probs_host,
+                       float * logprobs_host) {
     const int nv = m->hp.n_vocab;
-    VocabInfo vi = vi_in;
-    suppress_.alloc(std::max(vi.n_suppress, 1) * 4);
-    if (vi.n_suppress > 0)
-        OWK_HIP_CHECK(hipMemcpyAsync(suppress_.ptr, vi.suppress_list, vi.n_suppress * 4, hipMemcpyHostToDevice, stream));
-    vi.suppress_list = suppress_.as<int>();
-    lg_jobs_.alloc(sizeof(LogitJob) * n);
-    lg_out_.alloc(sizeof(TokenOut) * n);
-    OWK_HIP_CHECK(hipMemcpyAsync(lg_jobs_.ptr, jobs.data(), sizeof(LogitJob) * n, hipMemcpyHostToDevice, stream));
-    float * pr = nullptr;
-    float * lp = nullptr;
-    if (probs_host) {
-        lg_probs_.alloc((size_t) n * nv * 4);
-        pr = lg_probs_.as<float>();
-    }
-    if (logprobs_host) {
-        lg_lp_.alloc((size_t) n * nv * 4);
-        lp = lg_lp_.as<float>();
-    }
+    const int n = (int) jobs.size();
+    const int nn = (int) post.nosp.size();
+    out.resize(n);
+    nosp_out.resize(nn);
+    row0_.alloc((size_t) cap_slots * nv * 4);
+    rmx_.alloc((size_t) cap_slots * RMX * 4);
+    for (const auto & e : post.rowmax)
+        if (e.x < 0 || e.x >= cap_slots || e.y < 0 || e.y >= RMX) throw std::runtime_error("step_post: bad row entry");
+    for (const auto & e : post.nosp)
+        if (e.x < 0 || e.x >= cap_slots || e.y < 1 || e.y > RMX) throw std::runtime_error("step_post: bad nosp entry");
+
+    // one packed upload: row-max entries | row-0 map | nosp requests | jobs | suppress list
+    size_t o = 0;
+    auto sec = [&](size_t bytes) {
+        const size_t at = o;
+        o += (bytes + 63) / 64 * 64;
+        return at;
+    };
+    const size_t o_rm = sec(post.rowmax.size() * sizeof(int4)), o_r0 = sec(post.row0.size() * sizeof(int2)),
+                 o_ns = sec(nn * sizeof(int2)), o_jobs = sec(n * sizeof(LogitJob)),
+                 o_sup = sec((size_t) std::max(vi_in.n_suppress, 0) * 4);
+    post_h_.alloc(std::max<size_t>(o, 64));
+    post_d_.alloc(std::max<size_t>(o, 64));
+    char * h = post_h_.as<char>();
+    if (!post.rowmax.empty()) memcpy(h + o_rm, post.rowmax.data(), post.rowmax.size() * sizeof(int4));
+    if (!post.row0.empty()) memcpy(h + o_r0, post.row0.data(), post.row0.size() * sizeof(int2));
+    if (nn) memcpy(h + o_ns, post.nosp.data(), nn * sizeof(int2));
+    if (n) memcpy(h + o_jobs, jobs.data(), n * sizeof(LogitJob));
+    if (vi_in.n_suppress > 0) memcpy(h + o_sup, vi_in.suppress_list, (size_t) vi_in.n_suppress * 4);
+    char * dv = post_d_.as<char>();
+    if (o) OWK_HIP_CHECK(hipMemcpyAsync(dv, h, o, hipMemcpyHostToDevice, stream));
+
+    // results: token records | nosp probs
+    const size_t r_tok = 0, r_ns = ((size_t) n * sizeof(TokenOut) + 63) / 64 * 64;
+    const size_t r_bytes = r_ns + (size_t) nn * 4;
+    post_out_h_.alloc(std::max<size_t>(r_bytes, 64));
+    post_out_d_.alloc(std::max<size_t>(r_bytes, 64));
     {
         ProfScope ps(prof, stream, "logits_proc");
-        owk::process_logits(stream, logits_.as<float>(), nv, lg_jobs_.as<LogitJob>(), n, vi, lg_out_.as<TokenOut>(), lp,
-                            pr);
+        rowmax_update(stream, logits_.as<float>(), nv, (const int4 *) (dv + o_rm), (int) post.rowmax.size(),
+                      rmx_.as<float>(), RMX);
+        logits_copy_rows(stream, logits_.as<float>(), nv, (const int2 *) (dv + o_r0), (int) post.row0.size(),
+                         row0_.as<float>());
+        nosp_probs(stream, row0_.as<float>(), nv, (const int2 *) (dv + o_ns), nn, rmx_.as<float>(), RMX,
+                   m->vocab.nosp, (float *) (post_out_d_.as<char>() + r_ns));
+        if (n) {
+            VocabInfo vi = vi_in;
+            vi.suppress_list = (const int *) (dv + o_sup);
+            float * pr = nullptr;
+            float * lp = nullptr;
+            if (probs_host) {
+                lg_probs_.alloc((size_t) n * nv * 4);
+                pr = lg_probs_.as<float>();
+            }
+            if (logprobs_host) {
+                lg_lp_.alloc((size_t) n * nv * 4);
+                lp = lg_lp_.as<float>();
+            }
+            owk::process_logits(stream, logits_.as<float>(), nv, (const LogitJob *) (dv + o_jobs), n, vi,
+                                (TokenOut *) (post_out_d_.as<char>() + r_tok), lp, pr);
+            if (pr) OWK_HIP_CHECK(hipMemcpyAsync(probs_host, pr, (size_t) n * nv * 4, hipMemcpyDeviceToHost, stream));
+            if (lp) OWK_HIP_CHECK(hipMemcpyAsync(logprobs_host, lp, (size_t) n * nv * 4, hipMemcpyDeviceToHost, stream));
+        }
     }
-    OWK_HIP_CHECK(hipMemcpyAsync(out.data(), lg_out_.ptr, sizeof(TokenOut) * n, hipMemcpyDeviceToHost, stream));
-    if (pr) OWK_HIP_CHECK(hipMemcpyAsync(probs_host, pr, (size_t) n * nv * 4, hipMemcpyDeviceToHost, stream));
-    if (lp) OWK_HIP_CHECK(hipMemcpyAsync(logprobs_host, lp, (size_t) n * nv * 4, hipMemcpyDeviceToHost, stream));
+    if (r_bytes) OWK_HIP_CHECK(hipMemcpyAsync(post_out_h_.ptr, post_out_d_.ptr, r_bytes, hipMemcpyDeviceToHost, stream));
+    sync();
+    if (n) memcpy(out.data(), post_out_h_.as<char>() + r_tok, (size_t) n * sizeof(TokenOut));
+    if (nn) memcpy(nosp_out.data(), post_out_h_.as<char>() + r_ns, (size_t) nn * 4);
+}
+
+void Engine::save_logits_state(int slot, int n_rows, std::vector<float> & rowmax, std::vector<float> & row0) {
+    const int nv = m->hp.n_vocab;
+    sync();
+    rowmax.resize(std::min(n_rows, RMX));
+    row0.resize(nv);
+    if (!rmx_.ptr || !row0_.ptr || slot >= cap_slots) {
+        std::fill(rowmax.begin(), rowmax.end(), 0.0f);
+        std::fill(row0.begin(), row0.end(), 0.0f);
+        return;
+    }
+    if (!rowmax.empty())
+        OWK_HIP_CHECK(hipMemcpy(rowmax.data(), rmx_.as<float>() + (size_t) slot * RMX, rowmax.size() * 4,
+                                hipMemcpyDeviceToHost));
+    OWK_HIP_CHECK(hipMemcpy(row0.data(), row0_.as<float>() + (size_t) slot * nv, (size_t) nv * 4, hipMemcpyDeviceToHost));
+}
+
+void Engine::load_logits_state(int slot, const std::vector<float> & rowmax, const std::vector<float> & row0) {
+    const int nv = m->hp.n_vocab;
+    row0_.alloc((size_t) cap_slots * nv * 4);
+    rmx_.alloc((size_t) cap_slots * RMX * 4);
+    if (slot >= cap_slots) throw std::runtime_error("load_logits_state: slot out of range");
+    if (!rowmax.empty())
+        OWK_HIP_CHECK(hipMemcpyAsync(rmx_.as<float>() + (size_t) slot * RMX, rowmax.data(),
+                                     std::min<size_t>(rowmax.size(), RMX) * 4, hipMemcpyHostToDevice, stream));
+    if ((int) row0.size() == nv)
+        OWK_HIP_CHECK(hipMemcpyAsync(row0_.as<float>() + (size_t) slot * nv, row0.data(), (size_t) nv * 4,
+                                     hipMemcpyHostToDevice, stream));
+    else
+        OWK_HIP_CHECK(hipMemsetAsync(row0_.as<float>() + (size_t) slot * nv, 0, (size_t) nv * 4, stream));
     sync();
 }
 

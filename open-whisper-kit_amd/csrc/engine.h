@@ -57,6 +57,20 @@ struct DecodeRow {
     int logit_row;   // -1: no logits for this row
 };
 
+// what a decoder pass launches (the key of its captured graph)
+struct DecShape {
+    int R, n_logit;
+    bool self_oc, self_tl, cross_oc, cross_tl;  // attention kernels needed (one_chunk / tiled)
+    int max_keys;
+};
+
+// per-step bookkeeping of the emulated reference state->logits buffer (no-speech prob)
+struct StepPost {
+    std::vector<int4> rowmax;  // (slot, row, logit_row or -1, zero_fill)
+    std::vector<int2> row0;    // (logit_row or -1 = zeros, slot)
+    std::vector<int2> nosp;    // (slot, n_rows): no-speech prob over the slot's buffer
+};
+
 class Engine {
 public:
     Engine(const Model * m, Prof * prof);
@@ -92,19 +106,28 @@ public:
     float * logits_dev() const { return logits_.as<float>(); }
     void download_logits(int logit_row, float * host) const;
     void upload_logits(int logit_row, const float * host);
-    // on-device whisper_process_logits + greedy pick
-    void process_logits(const std::vector<LogitJob> & jobs, const VocabInfo & vi, std::vector<TokenOut> & out,
-                        float * probs_host, float * logprobs_host);
-
-    // state->logits emulation for the no-speech probability (see k_logits.hip)
-    void logits_maxes(int n_logit_rows, std::vector<float> & out);
-    void row0_update(const std::vector<std::pair<int, int>> & map);  // (logit row or -1 = zeros, slot)
-    void nosp(const std::vector<std::pair<int, float>> & req, std::vector<float> & out);  // (slot, max)
+    // after a decoder pass, ONE upload + ONE synchronisation: state->logits emulation
+    // (row maxima, row 0, no-speech probabilities) and on-device whisper_process_logits +
+    // greedy pick for every job; probs/logprobs are downloaded only when requested
+    void step_post(const StepPost & post, const std::vector<LogitJob> & jobs, const VocabInfo & vi,
+                   std::vector<TokenOut> & out, std::vector<float> & nosp_out, float * probs_host,
+                   float * logprobs_host);
+    // the emulated buffer of a slot <-> host copies (it persists with the whisper_state)
+    void save_logits_state(int slot, int n_rows, std::vector<float> & rowmax, std::vector<float> & row0);
+    void load_logits_state(int slot, const std::vector<float> & rowmax, const std::vector<float> & row0);
+    static constexpr int RMX = 512;  // rows of the emulated buffer tracked per slot (>= n_text_ctx)
 
     void sync();
 
 private:
-    DevBuf row0_, lmax_, map_, nosp_idx_, nosp_max_, nosp_out_;
+    void launch_decode(const DecShape & sh);
+    void stage_layout(int C, int KC);
+    void clear_graphs();
+    uint64_t buffers_signature() const;
+
+    DevBuf row0_, rmx_;         // emulated state->logits: row 0 [slot][n_vocab], row maxima [slot][RMX]
+    PinnedBuf post_h_, post_out_h_;
+    DevBuf post_d_, post_out_d_;
     // slot storage
     DevBuf cross_k_, cross_v_;   // [L][cap_slots][n_audio_ctx][d]
     DevBuf self_k_, self_v_;     // [L][cap_slots][kv_cells][d]
@@ -118,13 +141,17 @@ private:
     int last_enc_n_ = 0;
 
     // decoder workspace
-    DevBuf d_x_, d_xn_, d_q_, d_ao_, d_h_, d_tok_, d_pos_, d_rowoff_, d_rows_self_, d_rows_cross_, d_keys_,
-        d_lsel_, d_xl_;
-    DevBuf logits_, lg_jobs_, lg_out_, lg_probs_, lg_lp_, suppress_;
-    int dec_rows_cap_ = 0;
+    DevBuf d_x_, d_xn_, d_q_, d_ao_, d_h_, d_xl_;
+    DevBuf logits_, lg_probs_, lg_lp_;
+    int dec_rows_cap_ = 0, dec_keys_cap_ = 0;
+    PinnedBuf stg_;   // host image of the per-pass inputs
+    DevBuf d_stg_;    // its device copy (fixed sections, see stage_layout)
+    size_t st_tok_ = 0, st_pos_ = 0, st_rowoff_ = 0, st_rs_ = 0, st_rc_ = 0, st_lsel_ = 0, st_keys_ = 0, st_bytes_ = 0;
+    std::map<uint64_t, hipGraphExec_t> graphs_;
+    uint64_t graphs_sig_ = 0;
 
     DevBuf mel_jobs_, pcm_tmp_;
-    DevBuf gws_part_, gws_tick_;  // split-K workspace of the decode-row GEMMs
+    DevBuf gws_part_;  // split-K workspace of the decode-row GEMMs
     GemmWs gws_;
 };
 

@@ -193,6 +193,26 @@ constexpr int AS_KC = 64;       // keys per chunk
 constexpr int AS_NBUF = 3;      // chunks in flight
 constexpr int AS_TILE = AS_KC * 128;
 
+// inclusive max-scan over the 64 lanes (DPP: row_shr 1/2/4/8, then row_bcast 15/31)
+#define OWK_DPP_MAX(v, ctrl, rmask, bmask)                                                                       \
+    fmaxf(v, __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, -INFINITY),           \
+                                                                   __builtin_bit_cast(int, v), ctrl, rmask, bmask, \
+                                                                   false)))
+__device__ __forceinline__ float wave_incl_max(float v) {
+    v = OWK_DPP_MAX(v, 0x111, 0xf, 0xf);  // row_shr:1
+    v = OWK_DPP_MAX(v, 0x112, 0xf, 0xf);  // row_shr:2
+    v = OWK_DPP_MAX(v, 0x114, 0xf, 0xf);  // row_shr:4
+    v = OWK_DPP_MAX(v, 0x118, 0xf, 0xf);  // row_shr:8
+    v = OWK_DPP_MAX(v, 0x142, 0xa, 0xf);  // row_bcast:15 -> rows 1, 3
+    v = OWK_DPP_MAX(v, 0x143, 0xc, 0xf);  // row_bcast:31 -> rows 2, 3
+    return v;
+}
+// lane i <- lane i-1 of v; lane 0 <- fill (DPP wave_shr:1)
+__device__ __forceinline__ float wave_shr1(float v, float fill) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, fill), __builtin_bit_cast(int, v),
+                                                                 0x138, 0xf, 0xf, false));
+}
+
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
     static_assert(N >= 0 && N < 64, "vmcnt range");
@@ -273,43 +293,45 @@ __global__ __launch_bounds__(64) void k_attn_step(const _Float16 * __restrict__ 
         const int base = c * AS_KC;
         const int nk = min(AS_KC, n - base);
 
-        // 2. scores, lane = key
+        // 2. scores, lane = key (8 independent partial sums: short dependency chains)
         float s;
         {
             const char * kr = sK + lane * 128;
-            float a = 0.0f;
+            float part[8];
 #pragma unroll
             for (int cc = 0; cc < 8; ++cc) {
                 const half8 kv = *(const half8 *) (kr + ((cc ^ (lane & 7)) << 4));
+                float a = 0.0f;
 #pragma unroll
                 for (int e = 0; e < 8; ++e) a = fmaf((float) kv[e], (float) qv[cc][e], a);
+                part[cc] = a;
             }
+            const float a = ((part[0] + part[1]) + (part[2] + part[3])) + ((part[4] + part[5]) + (part[6] + part[7]));
             s = lane < nk ? a * scale : -INFINITY;
         }
-        float pm = s;  // inclusive running max over the chunk
-#pragma unroll
-        for (int off = 1; off < 64; off <<= 1) {
-            const float t = __shfl_up(pm, off, 64);
-            if (lane >= off) pm = fmaxf(pm, t);
-        }
-        float mex = __shfl_up(pm, 1, 64);
-        mex = lane == 0 ? M : fmaxf(mex, M);
+        // running max before each key: DPP inclusive max-scan, then a one-lane wave shift
+        const float pm = wave_incl_max(s);
+        const float mex = fmaxf(wave_shr1(pm, M), M);
         const bool nm = lane < nk && s > mex;
-        const float ms = nm ? expf(mex - s) : 1.0f;
-        const float vs = nm ? 1.0f : expf(s - mex);
-        M = fmaxf(M, __shfl(pm, 63, 64));
+        const float e = expf(nm ? mex - s : s - mex);
+        const float ms = nm ? e : 1.0f;
+        const float vs = nm ? 1.0f : e;
+        M = fmaxf(M, __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, pm), 63)));
 
         // 3. recurrence, lane = head dim
         const _Float16 * vcol = (const _Float16 *) sV + lane;
         // acc*ms with ms == 1 is exact, so the rescale is applied unconditionally (branch-free)
         // and each key costs two dependent mixed-precision FMAs (f32 math, f16 result)
         if (nk == AS_KC) {
+            _Float16 vv[AS_KC];
+#pragma unroll
+            for (int kk = 0; kk < AS_KC; ++kk) vv[kk] = vcol[kk * 64];
 #pragma unroll
             for (int kk = 0; kk < AS_KC; ++kk) {
                 const float msk = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, ms), kk));
                 const float vsk = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, vs), kk));
                 acc = (_Float16) ((float) acc * msk);
-                acc = (_Float16) fmaf((float) vcol[kk * 64], vsk, (float) acc);
+                acc = (_Float16) fmaf((float) vv[kk], vsk, (float) acc);
                 S = fmaf(S, msk, vsk);
             }
         } else {
@@ -446,6 +468,9 @@ __global__ __launch_bounds__(256) void k_attn_decoder(const _Float16 * __restric
     }
     out[(size_t) job.q_row * ldo + h * 64 + lane] = (_Float16) result;
 }
+
+int attn_max_listed_keys() { return AS_MAX_LIST; }
+int attn_max_tiled_keys() { return DA_MAX_KEYS; }
 
 void attn_decoder(hipStream_t s, const _Float16 * q, int ldq, const _Float16 * kbase, const _Float16 * vbase, int ld_kv,
                   const AttnRow * rows_dev, int n_rows, const int * key_idx, int H, float scale, int max_keys,

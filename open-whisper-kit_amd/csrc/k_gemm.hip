@@ -239,94 +239,128 @@ __global__ __launch_bounds__(512) void k_gemm_skinny(int M, int N, int K, const 
 }
 
 // ---------------------------------------------------------------------------------
-// Decode-row GEMM (M <= 32 rows, the per-step decoder matmuls): weight-streaming.
-// One 16-column tile per block, 8 waves; wave w takes J consecutive k-steps of 32 and
-// issues ALL of its weight and activation loads before the first MFMA, so a launch
-// has (close to) the whole weight matrix in flight at once -- the decode GEMMs are a
-// single HBM round trip, not a pipeline. K beyond 8*J*32 is split over gridDim.y
-// blocks whose partial tiles go to a workspace; the last block to finish a tile (an
-// atomic ticket) adds them in fixed k order, so results do not depend on timing.
+// Decode-row GEMM (M <= 32 rows, the per-step decoder matmuls): weight streaming.
+//
+// Weights are read from a TILED copy made once at load time (tile_weights): the
+// 16 x 32 (n x k) block an MFMA step consumes is stored as 1 KB in exactly the lane
+// order of the B operand, so a wave's J k-steps are one contiguous J KB stream.
+// One 16-column tile per block; wave w takes J consecutive k-steps and issues ALL its
+// weight and activation loads before the first MFMA, so a launch has the whole weight
+// matrix in flight -- the decode GEMM is a single HBM round trip. K beyond
+// waves*J*32 is split over gridDim.y blocks; their partial tiles go to a workspace and
+// a second small launch adds them in fixed k order (deterministic; no device-scope
+// fence, which is costly across the 8 XCDs).
 // ---------------------------------------------------------------------------------
-constexpr int GR_WAVES = 8;
-constexpr int GR_JMAX = 8;
+constexpr int GR_MAXW = 16;  // waves per block
 
-template <int MODE, int MT>
-__global__ __launch_bounds__(GR_WAVES * 64) void k_gemm_rows(int M, int N, int K, const _Float16 * __restrict__ A,
-                                                             int lda, const _Float16 * __restrict__ W, int ldw,
-                                                             EpiParams ep, int J, float * __restrict__ part,
-                                                             int * __restrict__ tickets) {
-    __shared__ floatx4 red[GR_WAVES][MT][64];
-    __shared__ int s_last;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int n0 = blockIdx.x * 16;
+__global__ void k_tile_weights(const _Float16 * __restrict__ W, int N, int K, _Float16 * __restrict__ out) {
     const int nsteps = K >> 5;
-    const int ks0 = (blockIdx.y * GR_WAVES + wave) * J;
+    const size_t total = (size_t) ((N + 15) >> 4) * nsteps * 64;
+    for (size_t p = (size_t) blockIdx.x * blockDim.x + threadIdx.x; p < total; p += (size_t) gridDim.x * blockDim.x) {
+        const int l = (int) (p & 63);
+        const size_t ts = p >> 6;
+        const int st = (int) (ts % nsteps);
+        const int t = (int) (ts / nsteps);
+        const int n = t * 16 + (l & 15), k = st * 32 + 8 * (l >> 4);
+        half8 v = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (n < N) v = *(const half8 *) (W + (size_t) n * K + k);
+        *(half8 *) (out + p * 8) = v;
+    }
+}
+
+void tile_weights(hipStream_t s, const _Float16 * W, int N, int K, _Float16 * out) {
+    if (K % 32) throw std::runtime_error("tile_weights: K % 32");
+    hipLaunchKernelGGL(k_tile_weights, dim3(2048), dim3(256), 0, s, W, N, K, out);
+}
+
+size_t tiled_weight_elems(int N, int K) { return (size_t) ((N + 15) / 16) * 16 * K; }
+
+template <int MODE, int MT, int J>
+__global__ __launch_bounds__(GR_MAXW * 64) void k_gemm_rows(int M, int N, int K, const _Float16 * __restrict__ A,
+                                                            int lda, const _Float16 * __restrict__ Wt, EpiParams ep,
+                                                            float * __restrict__ part) {
+    __shared__ floatx4 red[GR_MAXW][MT][64];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = blockDim.x >> 6;
+    const int tile = blockIdx.x, n0 = tile * 16;
+    const int nsteps = K >> 5;
+    const int ks0 = (blockIdx.y * nw + wave) * J;
     const int nj = max(0, min(J, nsteps - ks0));
 
-    const int n = min(n0 + (lane & 15), N - 1);
-    const _Float16 * wp = W + (size_t) n * ldw + 8 * (lane >> 4) + ks0 * 32;
-    half8 b[GR_JMAX], a[MT][GR_JMAX];
+    // branch-free: every load is issued (k-step clamped into the matrix); operands past
+    // this wave's k range are zeros so the extra MFMAs add exact zeros
+    const half8 z8 = {0, 0, 0, 0, 0, 0, 0, 0};
+    const _Float16 * wp = Wt + ((size_t) tile * nsteps) * 512 + lane * 8;
+    half8 b[J], a[MT][J];
 #pragma unroll
-    for (int j = 0; j < GR_JMAX; ++j)
-        if (j < nj) b[j] = *(const half8 *) (wp + j * 32);
+    for (int j = 0; j < J; ++j) {
+        const half8 t = *(const half8 *) (wp + (size_t) min(ks0 + j, nsteps - 1) * 512);
+        b[j] = j < nj ? t : z8;
+    }
 #pragma unroll
     for (int i = 0; i < MT; ++i) {
-        const _Float16 * ap = A + (size_t) min(i * 16 + (lane & 15), M - 1) * lda + 8 * (lane >> 4) + ks0 * 32;
+        const _Float16 * ap = A + (size_t) min(i * 16 + (lane & 15), M - 1) * lda + 8 * (lane >> 4);
 #pragma unroll
-        for (int j = 0; j < GR_JMAX; ++j)
-            if (j < nj) a[i][j] = *(const half8 *) (ap + j * 32);
+        for (int j = 0; j < J; ++j) {
+            const half8 t = *(const half8 *) (ap + min(ks0 + j, nsteps - 1) * 32);
+            a[i][j] = j < nj ? t : z8;
+        }
     }
+    __builtin_amdgcn_sched_barrier(0);  // keep every load issued ahead of the first wait
     floatx4 acc[MT];
 #pragma unroll
     for (int i = 0; i < MT; ++i) acc[i] = floatx4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int j = 0; j < GR_JMAX; ++j)
-        if (j < nj)
+    for (int j = 0; j < J; ++j)
 #pragma unroll
-            for (int i = 0; i < MT; ++i) acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[i][j], b[j], acc[i], 0, 0, 0);
+        for (int i = 0; i < MT; ++i) acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[i][j], b[j], acc[i], 0, 0, 0);
 #pragma unroll
     for (int i = 0; i < MT; ++i) red[wave][i][lane] = acc[i];
     __syncthreads();
 
-    const int KS = gridDim.y;
     if (tid < MT * 64) {
         const int i = tid >> 6, ln = tid & 63;
         floatx4 sum = red[0][i][ln];
-#pragma unroll
-        for (int w = 1; w < GR_WAVES; ++w) sum += red[w][i][ln];
-        if (KS == 1) {
+        for (int w = 1; w < nw; ++w) sum += red[w][i][ln];
+        if (gridDim.y == 1) {
             const int c = n0 + (ln & 15);
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
                 const int r = i * 16 + 4 * (ln >> 4) + e;
                 if (r < M && c < N) epi_store<MODE>(ep, r, c, sum[e]);
             }
-            return;
+        } else {
+            ((floatx4 *) part)[(((size_t) blockIdx.y * gridDim.x + tile) * MT + i) * 64 + ln] = sum;
         }
-        // split K: partial tile [ks][tile][i][lane] -> workspace
-        floatx4 * pp = (floatx4 *) part + (((size_t) blockIdx.y * gridDim.x + blockIdx.x) * MT + i) * 64 + ln;
-        *pp = sum;
     }
-    if (KS == 1) return;
-    __threadfence();
-    __syncthreads();
-    if (tid == 0) s_last = atomicAdd(&tickets[blockIdx.x], 1) == KS - 1;
-    __syncthreads();
-    if (!s_last) return;
-    __threadfence();
-    if (tid < MT * 64) {
-        const int i = tid >> 6, ln = tid & 63;
-        floatx4 sum = floatx4{0.f, 0.f, 0.f, 0.f};
-        for (int ks = 0; ks < KS; ++ks)
-            sum += *((const volatile floatx4 *) part + (((size_t) ks * gridDim.x + blockIdx.x) * MT + i) * 64 + ln);
-        const int c = n0 + (ln & 15);
+}
+
+template <int MODE, int MT>
+__global__ __launch_bounds__(MT * 64) void k_gemm_rows_reduce(int M, int N, int KS, const float * __restrict__ part,
+                                                              EpiParams ep) {
+    const int tid = threadIdx.x, i = tid >> 6, ln = tid & 63;
+    const int n0 = blockIdx.x * 16;
+    floatx4 sum = floatx4{0.f, 0.f, 0.f, 0.f};
+    for (int ks = 0; ks < KS; ++ks) sum += ((const floatx4 *) part)[(((size_t) ks * gridDim.x + blockIdx.x) * MT + i) * 64 + ln];
+    const int c = n0 + (ln & 15);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            const int r = i * 16 + 4 * (ln >> 4) + e;
-            if (r < M && c < N) epi_store<MODE>(ep, r, c, sum[e]);
-        }
+    for (int e = 0; e < 4; ++e) {
+        const int r = i * 16 + 4 * (ln >> 4) + e;
+        if (r < M && c < N) epi_store<MODE>(ep, r, c, sum[e]);
     }
-    if (tid == 0) tickets[blockIdx.x] = 0;  // re-armed for the next launch on this workspace
+}
+
+// launch geometry of the decode-row GEMM: J k-steps per wave, nw waves, KS k-splits
+struct RowsPlan {
+    int J, nw, KS;
+};
+static RowsPlan rows_plan(int K) {
+    const int nsteps = K / 32;
+    RowsPlan p;
+    p.J = nsteps <= 32 ? 2 : nsteps <= 64 ? 4 : 8;
+    p.KS = (nsteps + GR_MAXW * p.J - 1) / (GR_MAXW * p.J);
+    const int per = (nsteps + p.KS - 1) / p.KS;
+    p.nw = (per + p.J - 1) / p.J;
+    return p;
 }
 
 template <template <int> class L, typename... Args> static void dispatch_mode(int mode, Args &&... args) {
@@ -358,26 +392,31 @@ template <int MODE> struct LaunchSkinny {
 };
 
 template <int MODE> struct LaunchRows {
-    static void run(hipStream_t s, int M, int N, int K, const _Float16 * A, int lda, const _Float16 * W, int ldw,
+    template <int MT, int J>
+    static void go(hipStream_t s, dim3 grid, int nw, int M, int N, int K, const _Float16 * A, int lda,
+                   const _Float16 * Wt, const EpiParams & ep, float * part) {
+        hipLaunchKernelGGL((k_gemm_rows<MODE, MT, J>), grid, dim3(nw * 64), 0, s, M, N, K, A, lda, Wt, ep, part);
+        if (grid.y > 1)
+            hipLaunchKernelGGL((k_gemm_rows_reduce<MODE, MT>), dim3(grid.x), dim3(MT * 64), 0, s, M, N, (int) grid.y,
+                               part, ep);
+    }
+    static void run(hipStream_t s, int M, int N, int K, const _Float16 * A, int lda, const _Float16 * Wt,
                     const EpiParams & ep, const GemmWs * ws) {
-        const int nsteps = K / 32;
-        int J = std::min(GR_JMAX, (nsteps + GR_WAVES - 1) / GR_WAVES);
-        const int KS = (nsteps + GR_WAVES * J - 1) / (GR_WAVES * J);
+        const RowsPlan pl = rows_plan(K);
         const int tiles = (N + 15) / 16;
         float * part = nullptr;
-        int * tick = nullptr;
-        if (KS > 1) {
-            const size_t need = (size_t) KS * tiles * 2 * 64 * 4;  // floats (MT <= 2)
-            if (!ws || ws->partial_floats < need || ws->n_tickets < tiles)
-                throw std::runtime_error("gemm_rows: split-K workspace too small");
+        if (pl.KS > 1) {
+            const size_t need = (size_t) pl.KS * tiles * 2 * 64 * 4;  // floats (MT <= 2)
+            if (!ws || ws->partial_floats < need) throw std::runtime_error("gemm_rows: split-K workspace too small");
             part = ws->partial;
-            tick = ws->tickets;
         }
-        const dim3 grid(tiles, KS), block(GR_WAVES * 64);
-        if (M <= 16)
-            hipLaunchKernelGGL((k_gemm_rows<MODE, 1>), grid, block, 0, s, M, N, K, A, lda, W, ldw, ep, J, part, tick);
-        else
-            hipLaunchKernelGGL((k_gemm_rows<MODE, 2>), grid, block, 0, s, M, N, K, A, lda, W, ldw, ep, J, part, tick);
+        const dim3 grid(tiles, pl.KS);
+        const bool one = M <= 16;
+        switch (pl.J) {
+            case 2: one ? go<1, 2>(s, grid, pl.nw, M, N, K, A, lda, Wt, ep, part) : go<2, 2>(s, grid, pl.nw, M, N, K, A, lda, Wt, ep, part); break;
+            case 4: one ? go<1, 4>(s, grid, pl.nw, M, N, K, A, lda, Wt, ep, part) : go<2, 4>(s, grid, pl.nw, M, N, K, A, lda, Wt, ep, part); break;
+            default: one ? go<1, 8>(s, grid, pl.nw, M, N, K, A, lda, Wt, ep, part) : go<2, 8>(s, grid, pl.nw, M, N, K, A, lda, Wt, ep, part); break;
+        }
     }
 };
 
@@ -401,17 +440,15 @@ void gemm_f16_skinny(hipStream_t s, int mode, int M, int N, int K, const _Float1
 }
 
 size_t gemm_ws_floats(int N, int K) {
-    const int nsteps = K / 32;
-    const int J = std::min(GR_JMAX, (nsteps + GR_WAVES - 1) / GR_WAVES);
-    const int KS = (nsteps + GR_WAVES * J - 1) / (GR_WAVES * J);
-    return KS > 1 ? (size_t) KS * ((N + 15) / 16) * 2 * 64 * 4 : 0;
+    const RowsPlan p = rows_plan(K);
+    return p.KS > 1 ? (size_t) p.KS * ((N + 15) / 16) * 2 * 64 * 4 : 0;
 }
 
 void gemm(hipStream_t s, int mode, int M, int N, int K, const _Float16 * A, int lda, const _Float16 * W, int ldw,
-          const EpiParams & ep, const GemmWs * ws) {
-    if (M <= 32 && K % 32 == 0) {
+          const EpiParams & ep, const GemmWs * ws, const _Float16 * Wt) {
+    if (M <= 32 && K % 32 == 0 && Wt) {
         check_shape(M, N, K, lda, ldw, 32);
-        dispatch_mode<LaunchRows>(mode, s, M, N, K, A, lda, W, ldw, ep, ws);
+        dispatch_mode<LaunchRows>(mode, s, M, N, K, A, lda, Wt, ep, ws);
     } else if (M <= 64 && K % 32 == 0) {
         gemm_f16_skinny(s, mode, M, N, K, A, lda, W, ldw, ep);
     } else {

@@ -222,27 +222,69 @@ void logits_copy_rows(hipStream_t s, const float * logits, int n_vocab, const in
     hipLaunchKernelGGL(k_copy_rows, dim3(n), dim3(256), 0, s, logits, n_vocab, map_dev, dst);
 }
 
-// prob[nosp] of soft-max(row) with an externally supplied max
-__global__ __launch_bounds__(LG_THREADS) void k_nosp(const float * __restrict__ rows, int n_vocab,
-                                                    const int * __restrict__ row_idx, const float * __restrict__ mx,
-                                                    int nosp, float * __restrict__ out) {
-    __shared__ double redd[LG_WAVES];
-    const float * L = rows + (size_t) row_idx[blockIdx.x] * n_vocab;
-    const float m = mx[blockIdx.x];
-    double s = 0.0;
-    for (int i = threadIdx.x; i < n_vocab; i += LG_THREADS)
-        if (L[i] > -INFINITY) s += (double) expf(L[i] - m);
-    s = block_sum(s, redd);
+// Emulated state->logits row maxima (see whisper_full.cpp): entry (slot, row, logit_row,
+// zero_fill) sets rmx[slot][row] to the max of logits row logit_row, or to 0 for a row
+// that a resize of the reference buffer would have zero-filled, or leaves the stale value.
+__global__ __launch_bounds__(LG_THREADS) void k_rowmax_update(const float * __restrict__ logits, int n_vocab,
+                                                            const int4 * __restrict__ ent, float * __restrict__ rmx,
+                                                            int stride) {
+    __shared__ float redf[LG_WAVES];
+    const int4 e = ent[blockIdx.x];
+    float * dst = rmx + (size_t) e.x * stride + e.y;
+    if (e.z < 0) {
+        if (e.w && threadIdx.x == 0) *dst = 0.0f;
+        return;
+    }
+    const float * L = logits + (size_t) e.z * n_vocab;
+    float mx = -INFINITY;
+    for (int i = threadIdx.x; i < n_vocab; i += LG_THREADS) mx = fmaxf(mx, L[i]);
+    mx = block_max(mx, redf);
+    if (threadIdx.x == 0) *dst = mx;
+}
+
+void rowmax_update(hipStream_t s, const float * logits, int n_vocab, const int4 * ent_dev, int n, float * rmx,
+                   int stride) {
+    if (n <= 0) return;
+    hipLaunchKernelGGL(k_rowmax_update, dim3(n), dim3(LG_THREADS), 0, s, logits, n_vocab, ent_dev, rmx, stride);
+}
+
+// No-speech probability after a prefill (ref whisper.cpp:7185-7195): soft-max of the
+// emulated buffer's row 0 with the max over the whole buffer (rows 0..n_rows of rmx),
+// whisper_compute_logprobs' float sum taken in the reference's sequential order.
+constexpr int NS_CHUNK = 4096;
+__global__ __launch_bounds__(LG_THREADS) void k_nosp(const float * __restrict__ row0, int n_vocab,
+                                                    const int2 * __restrict__ req, const float * __restrict__ rmx,
+                                                    int stride, int nosp, float * __restrict__ out) {
+    __shared__ float redf[LG_WAVES];
+    __shared__ float ex[NS_CHUNK];
+    const int2 q = req[blockIdx.x];
+    const float * L = row0 + (size_t) q.x * n_vocab;
+    const float * R = rmx + (size_t) q.x * stride;
+    float m = -INFINITY;
+    for (int i = threadIdx.x; i < q.y; i += LG_THREADS) m = fmaxf(m, R[i]);
+    m = block_max(m, redf);
+    float sum = 0.0f;  // meaningful in thread 0
+    for (int c0 = 0; c0 < n_vocab; c0 += NS_CHUNK) {
+        const int n = min(NS_CHUNK, n_vocab - c0);
+        __syncthreads();
+        for (int i = threadIdx.x; i < n; i += LG_THREADS) {
+            const float v = L[c0 + i];
+            ex[i] = v > -INFINITY ? expf(v - m) : 0.0f;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0)
+            for (int i = 0; i < n; ++i) sum += ex[i];
+    }
     if (threadIdx.x == 0) {
-        const float lse = logf((float) s) + m;
-        out[blockIdx.x] = expf(L[nosp] - lse);
+        const float lse = logf(sum) + m;
+        out[blockIdx.x] = L[nosp] == -INFINITY ? 0.0f : expf(L[nosp] - lse);
     }
 }
 
-void nosp_probs(hipStream_t s, const float * rows, int n_vocab, const int * row_idx_dev, const float * max_dev, int n,
-                int nosp, float * out_dev) {
+void nosp_probs(hipStream_t s, const float * row0, int n_vocab, const int2 * req_dev, int n, const float * rmx,
+                int stride, int nosp, float * out_dev) {
     if (n <= 0) return;
-    hipLaunchKernelGGL(k_nosp, dim3(n), dim3(LG_THREADS), 0, s, rows, n_vocab, row_idx_dev, max_dev, nosp, out_dev);
+    hipLaunchKernelGGL(k_nosp, dim3(n), dim3(LG_THREADS), 0, s, row0, n_vocab, req_dev, rmx, stride, nosp, out_dev);
 }
 
 void process_logits(hipStream_t s, float * logits, int n_vocab, const LogitJob * jobs_dev, int n_jobs,

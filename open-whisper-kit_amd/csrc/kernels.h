@@ -49,15 +49,18 @@ void gemm_f16_skinny(hipStream_t s, int mode, int M, int N, int K, const _Float1
                      const _Float16 * W, int ldw, const EpiParams & ep);
 // split-K workspace of the decode-row GEMM (owned by the caller: one per stream)
 struct GemmWs {
-    float * partial = nullptr;  // partial tiles
+    float * partial = nullptr;  // partial tiles [k split][column tile][rows][16]
     size_t partial_floats = 0;
-    int * tickets = nullptr;    // per-column-tile arrival counters, zero-initialised, self-resetting
-    int n_tickets = 0;
 };
 size_t gemm_ws_floats(int N, int K);  // partial floats a (N, K) decode-row GEMM needs (0 = no split)
-// dispatch on M: <= 32 rows decode-row GEMM, <= 64 skinny, else 128x128 tiles
+// dispatch on M: <= 32 rows decode-row GEMM (needs the tiled copy Wt), <= 64 skinny,
+// else 128x128 tiles (row-major W)
 void gemm(hipStream_t s, int mode, int M, int N, int K, const _Float16 * A, int lda,
-          const _Float16 * W, int ldw, const EpiParams & ep, const GemmWs * ws = nullptr);
+          const _Float16 * W, int ldw, const EpiParams & ep, const GemmWs * ws = nullptr,
+          const _Float16 * Wt = nullptr);
+// tiled weight copy for the decode-row GEMM: [ceil(N/16)][K/32][64 lanes][8] f16
+size_t tiled_weight_elems(int N, int K);
+void tile_weights(hipStream_t s, const _Float16 * W, int N, int K, _Float16 * out);
 
 // ---------------------------------------------------------------------------------
 // normalisation / elementwise
@@ -121,6 +124,8 @@ struct AttnRow {
 void attn_decoder(hipStream_t s, const _Float16 * q, int ldq, const _Float16 * kbase, const _Float16 * vbase,
                   int ld_kv, const AttnRow * rows_dev, int n_rows, const int * key_idx, int H, float scale,
                   int max_keys, _Float16 * out, int ldo, bool any_one_chunk, bool any_tiled);
+int attn_max_listed_keys();  // per-row limit of the one_chunk kernel's key list
+int attn_max_tiled_keys();   // per-row limit of the tiled decoder kernel
 
 // ---------------------------------------------------------------------------------
 // logits -> token (whisper_process_logits + whisper_sample_token, greedy)
@@ -147,11 +152,11 @@ struct TokenOut {
 };
 // per-row maxima of raw logits rows
 void logits_row_max(hipStream_t s, const float * logits, int n_rows, int n_vocab, float * out_dev);
-// dst row map[i].y <- logits row map[i].x (x < 0: zeros)
 void logits_copy_rows(hipStream_t s, const float * logits, int n_vocab, const int2 * map_dev, int n, float * dst);
-// out[i] = softmax(rows[row_idx[i]] with max max_dev[i])[nosp]
-void nosp_probs(hipStream_t s, const float * rows, int n_vocab, const int * row_idx_dev, const float * max_dev, int n,
-                int nosp, float * out_dev);
+void rowmax_update(hipStream_t s, const float * logits, int n_vocab, const int4 * ent_dev, int n, float * rmx,
+                   int stride);
+void nosp_probs(hipStream_t s, const float * row0, int n_vocab, const int2 * req_dev, int n, const float * rmx,
+                int stride, int nosp, float * out_dev);
 // processes logits in place (filters applied), writes logprobs/probs when requested
 void process_logits(hipStream_t s, float * logits, int n_vocab, const LogitJob * jobs_dev, int n_jobs,
                     const VocabInfo & vi, TokenOut * out_dev, float * logprobs_out, float * probs_out);

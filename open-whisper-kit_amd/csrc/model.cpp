@@ -8,6 +8,7 @@
 //   - conv1 weight [d][n_mels*3] zero-padded along K to a multiple of 64
 // plus device constants: the f16 GELU table, mel filterbank, DFT twiddles, Hann window.
 #include "model.h"
+#include "kernels.h"
 
 #include <cmath>
 #include <cstdarg>
@@ -453,6 +454,35 @@ Model * load_model(whisper_model_loader * loader, int device, std::string & err)
         L.cw_o = H(p + "cross_attn.out.weight"); L.cb_o = F(p + "cross_attn.out.bias");
         L.w_mlp0 = H(p + "mlp.0.weight"); L.b_mlp0 = F(p + "mlp.0.bias");
         L.w_mlp1 = H(p + "mlp.2.weight"); L.b_mlp1 = F(p + "mlp.2.bias");
+    }
+    {
+        // decoder weights re-laid out for the decode-row GEMM (an extra 1.6 GB for large-v3;
+        // HBM holds both layouts comfortably, the row-major one still feeds prefills)
+        const int d = hp.n_text_state;
+        size_t tot = tiled_weight_elems(hp.n_vocab, d);
+        const size_t per_layer = tiled_weight_elems(3 * d, d) + 3 * tiled_weight_elems(d, d) +
+                                 tiled_weight_elems(4 * d, d) + tiled_weight_elems(d, 4 * d);
+        tot += per_layer * hp.n_text_layer;
+        m->tiled.alloc(tot * 2);
+        _Float16 * t = m->tiled.as<_Float16>();
+        size_t at = 0;
+        auto tile = [&](const _Float16 * W, int N, int K) {
+            _Float16 * out = t + at;
+            tile_weights(nullptr, W, N, K, out);
+            at += tiled_weight_elems(N, K);
+            return (const _Float16 *) out;
+        };
+        for (int i = 0; i < hp.n_text_layer; ++i) {
+            DecLayerW & L = m->dec[i];
+            L.t_qkv = tile(L.w_qkv, 3 * d, d);
+            L.t_o = tile(L.w_o, d, d);
+            L.t_cq = tile(L.cw_q, d, d);
+            L.t_co = tile(L.cw_o, d, d);
+            L.t_mlp0 = tile(L.w_mlp0, 4 * d, d);
+            L.t_mlp1 = tile(L.w_mlp1, d, 4 * d);
+        }
+        m->d_te_t = tile(m->d_te, hp.n_vocab, d);
+        OWK_HIP_CHECK(hipDeviceSynchronize());
     }
     m->gelu_tab = (const uint16_t *) (base + o_gelu);
     m->mel_filters = (const float *) (base + o_filt);

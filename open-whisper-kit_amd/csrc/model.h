@@ -58,6 +58,8 @@ struct DecLayerW {
     const float *cb_o;
     const _Float16 *w_mlp0, *w_mlp1;
     const float *b_mlp0, *b_mlp1;
+    // tiled copies for the decode-row GEMM (tile_weights layout)
+    const _Float16 *t_qkv, *t_o, *t_cq, *t_co, *t_mlp0, *t_mlp1;
 };
 
 struct Model {
@@ -79,6 +81,8 @@ struct Model {
     const float *e_ln_w = nullptr, *e_ln_b = nullptr;
     std::vector<EncLayerW> enc;
     const _Float16 * d_te = nullptr;     // [n_vocab][d]
+    const _Float16 * d_te_t = nullptr;   // tiled copy (logits of decode steps)
+    DevBuf tiled;                        // all tiled decoder weights
     const float * d_pe = nullptr;        // [n_text_ctx][d]
     const float *d_ln_w = nullptr, *d_ln_b = nullptr;
     std::vector<DecLayerW> dec;

@@ -53,7 +53,12 @@ struct whisper_state {
     owk::KvCells kv;  // cell map of slot 0 (staged API) / of this clip in batch mode
     int mel_n_len = 0, mel_n_len_org = 0, mel_n_mel = 0;
     std::vector<float> logits;  // whisper_get_logits
-    std::vector<float> logits_rowmax;  // per-row maxima of the emulated state->logits buffer
+    // emulated reference state->logits buffer (only what the no-speech probability reads):
+    // its row count, per-row maxima and row 0; live on the device during a call, host
+    // copies persist with the state between calls
+    int logits_rows = 0;
+    std::vector<float> logits_rowmax;
+    std::vector<float> logits_row0;
     std::vector<owk::Segment> result_all;
     std::vector<whisper_token> prompt_past0, prompt_past1;
     int lang_id = 0;

@@ -413,11 +413,21 @@ int whisper_decode_with_state(struct whisper_context * ctx, struct whisper_state
         st->logits.resize((size_t) n_tokens * nv);
         e.download_logits(0, st->logits.data() + (size_t) (n_tokens - 1) * nv);
         // keep the no-speech emulation consistent for a following whisper_full on this state
-        std::vector<float> rmax;
-        e.logits_maxes(n_logit, rmax);
-        st->logits_rowmax.resize(n_tokens, 0.0f);
-        st->logits_rowmax[n_tokens - 1] = rmax[0];
-        if (n_tokens == 1) e.row0_update({{0, 0}});
+        StepPost post;
+        const int old = st->logits_rows;
+        for (int r = 0; r < n_tokens && r < Engine::RMX; ++r) {
+            const bool zero = r >= old;
+            const int lrow = r == n_tokens - 1 ? 0 : -1;
+            if (lrow >= 0 || zero) post.rowmax.push_back(make_int4(0, r, lrow, zero ? 1 : 0));
+        }
+        if (n_tokens == 1) post.row0.push_back(make_int2(0, 0));
+        else if (old == 0) post.row0.push_back(make_int2(-1, 0));
+        std::vector<TokenOut> outs;
+        std::vector<float> ns;
+        VocabInfo vi{};
+        e.step_post(post, {}, vi, outs, ns, nullptr, nullptr);
+        st->logits_rows = n_tokens;
+        e.save_logits_state(0, n_tokens, st->logits_rowmax, st->logits_row0);
         const int64_t dt = time_us() - t0;
         if (n_tokens == 1) { st->t_decode_us += dt; st->n_decode++; }
         else if (n_tokens < 16) { st->t_batchd_us += dt; st->n_batchd += n_tokens; }
@@ -992,5 +1002,40 @@ int owk_debug_cross(struct whisper_context * ctx, struct whisper_state * st, int
 }
 
 const uint16_t * owk_debug_gelu_table(void) { return gelu_table_host().data(); }
+
+int owk_debug_gemm(int device, int M, int N, int K, const uint16_t * a, const uint16_t * w, float * out) {
+    try {
+        OWK_HIP_CHECK(hipSetDevice(device));
+        hipStream_t s;
+        OWK_HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+        DevBuf da, dw, dout, part;
+        da.alloc((size_t) M * K * 2);
+        dw.alloc((size_t) N * K * 2);
+        dout.alloc((size_t) M * N * 4);
+        OWK_HIP_CHECK(hipMemcpy(da.ptr, a, (size_t) M * K * 2, hipMemcpyHostToDevice));
+        OWK_HIP_CHECK(hipMemcpy(dw.ptr, w, (size_t) N * K * 2, hipMemcpyHostToDevice));
+        GemmWs ws;
+        const size_t fl = gemm_ws_floats(N, K);
+        part.alloc(std::max<size_t>(fl, 1) * 4);
+        ws.partial = part.as<float>();
+        ws.partial_floats = fl;
+        EpiParams ep;
+        ep.out32 = dout.as<float>();
+        ep.ldo = N;
+        DevBuf dwt;
+        dwt.alloc(tiled_weight_elems(N, K) * 2);
+        tile_weights(s, dw.as<_Float16>(), N, K, dwt.as<_Float16>());
+        gemm(s, EPI_F32, M, N, K, da.as<_Float16>(), K, dw.as<_Float16>(), K, ep, &ws, dwt.as<_Float16>());
+        // a second launch on the same workspace (results must not depend on its history)
+        gemm(s, EPI_F32, M, N, K, da.as<_Float16>(), K, dw.as<_Float16>(), K, ep, &ws, dwt.as<_Float16>());
+        OWK_HIP_CHECK(hipStreamSynchronize(s));
+        OWK_HIP_CHECK(hipMemcpy(out, dout.ptr, (size_t) M * N * 4, hipMemcpyDeviceToHost));
+        OWK_HIP_CHECK(hipStreamDestroy(s));
+    } catch (const std::exception & ex) {
+        log_msg(GGML_LOG_LEVEL_ERROR, "owk_debug_gemm: %s\n", ex.what());
+        return -1;
+    }
+    return 0;
+}
 
 }  // extern "C"

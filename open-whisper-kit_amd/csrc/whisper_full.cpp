@@ -807,7 +807,10 @@ int full_batch(whisper_context * ctx, whisper_state ** states, const whisper_ful
         whisper_state * st = states[c];
         st->result_all.clear();
         if (st->kv.size == 0 || st->kv.size < (uint32_t) base_cells) st->kv.init(base_cells * (st->kv_self_n_dec > 1 ? st->kv_self_n_dec + 2 : 1));
+        st->logits_rows = (int) st->logits_rowmax.size();
+        eng.load_logits_state(c, st->logits_rowmax, st->logits_row0);
     }
+    eng.sync();
 
     // mel for every clip with samples (whisper_pcm_to_mel_with_state)
     {
@@ -874,43 +877,34 @@ int full_batch(whisper_context * ctx, whisper_state ** states, const whisper_ful
         const int64_t t0 = time_us();
         eng.decode(rows, keys, n_logit);
 
-        // state->logits emulation -> no-speech probability after each prefill
-        {
-            std::vector<float> rmax;
-            eng.logits_maxes(n_logit, rmax);
-            std::vector<std::pair<int, int>> r0map;
-            std::vector<std::pair<int, float>> nreq;
-            std::vector<Clip *> nclip;
-            for (size_t ci = 0; ci < dec.size(); ++ci) {
-                Clip * c = dec[ci];
-                if (c->done() || spans[ci].n == 0) continue;
-                auto & rm = c->st->logits_rowmax;
-                const size_t old = rm.size();
-                const int nt = spans[ci].n;
-                rm.resize(nt, 0.0f);
-                for (int r = 0; r < nt; ++r) {
-                    const DecodeRow & x = rows[spans[ci].row0 + r];
-                    if (x.logit_row >= 0) rm[r] = rmax[x.logit_row];
-                }
-                const DecodeRow & x0 = rows[spans[ci].row0];
-                if (x0.logit_row >= 0) r0map.push_back({x0.logit_row, c->slot});
-                else if (old == 0) r0map.push_back({-1, c->slot});
-                if (c->phase == Phase::WAIT_PREFILL) {
-                    float mx = -INFINITY;
-                    for (float v : rm) mx = std::max(mx, v);
-                    nreq.push_back({c->slot, mx});
-                    nclip.push_back(c);
-                }
+        // state->logits emulation (no-speech probability after each prefill, ref 7185-7195):
+        // the reference resizes state->logits to the call's rows and overwrites only rows
+        // that request logits; the rest keep stale values (zeros where the buffer grew)
+        StepPost post;
+        std::vector<Clip *> nclip;
+        for (size_t ci = 0; ci < dec.size(); ++ci) {
+            Clip * c = dec[ci];
+            if (c->done() || spans[ci].n == 0) continue;
+            const int old = c->st->logits_rows;
+            const int nt = spans[ci].n;
+            for (int r = 0; r < nt; ++r) {
+                const DecodeRow & x = rows[spans[ci].row0 + r];
+                const bool zero = r >= old;
+                if (x.logit_row >= 0 || zero) post.rowmax.push_back(make_int4(c->slot, r, x.logit_row, zero ? 1 : 0));
             }
-            eng.row0_update(r0map);
-            std::vector<float> ns;
-            eng.nosp(nreq, ns);
-            for (size_t q = 0; q < nclip.size(); ++q) nclip[q]->st->no_speech_prob = ns[q];
+            c->st->logits_rows = nt;
+            const DecodeRow & x0 = rows[spans[ci].row0];
+            if (x0.logit_row >= 0) post.row0.push_back(make_int2(x0.logit_row, c->slot));
+            else if (old == 0) post.row0.push_back(make_int2(-1, c->slot));
+            if (c->phase == Phase::WAIT_PREFILL) {
+                post.nosp.push_back(make_int2(c->slot, nt));
+                nclip.push_back(c);
+            }
         }
 
         // logits -> tokens: device path for every decoder row that needs no host callback
         std::vector<LogitJob> jobs;
-        std::vector<std::pair<Clip *, int>> job_owner;  // (clip, decoder index or -1 = lang detect)
+        std::vector<std::pair<Clip *, int>> job_owner;  // (clip, decoder index)
         bool want_probs = false;
         for (size_t ci = 0; ci < dec.size(); ++ci) {
             Clip * c = dec[ci];
@@ -954,10 +948,10 @@ int full_batch(whisper_context * ctx, whisper_state ** states, const whisper_ful
         // host path (logits_filter_callback): raw logits for every row, processed on the host
         const bool host_path = !clips.empty() && !clips[0].device_logits;
         std::vector<TokenOut> outs;
-        std::vector<float> probs_h, lp_h;
-        if (!jobs.empty()) {
+        std::vector<float> ns_out, probs_h, lp_h;
+        if (host_path || jobs.empty()) {
+            eng.step_post(post, {}, vi, outs, ns_out, nullptr, nullptr);
             if (host_path) {
-                outs.resize(jobs.size());
                 hostbuf.resize(nv);
                 for (size_t q = 0; q < jobs.size(); ++q) {
                     Clip * c = job_owner[q].first;
@@ -965,23 +959,25 @@ int full_batch(whisper_context * ctx, whisper_state ** states, const whisper_ful
                     eng.download_logits(jobs[q].row, hostbuf.data());
                     host_process_logits(ctx, c->st, d, c->p, c->t_cur, hostbuf.data(), vi);
                 }
-            } else {
+            }
+        } else {
+            if (want_probs) {
+                probs_h.resize(jobs.size() * (size_t) nv);
+                lp_h.resize(jobs.size() * (size_t) nv);
+            }
+            eng.step_post(post, jobs, vi, outs, ns_out, want_probs ? probs_h.data() : nullptr,
+                          want_probs ? lp_h.data() : nullptr);
+            for (size_t q = 0; q < jobs.size(); ++q) {
+                Clip * c = job_owner[q].first;
+                Decoder & d = c->st->decoders[job_owner[q].second];
+                d.gtok = outs[q];
                 if (want_probs) {
-                    probs_h.resize(jobs.size() * (size_t) nv);
-                    lp_h.resize(jobs.size() * (size_t) nv);
-                }
-                eng.process_logits(jobs, vi, outs, want_probs ? probs_h.data() : nullptr, want_probs ? lp_h.data() : nullptr);
-                for (size_t q = 0; q < jobs.size(); ++q) {
-                    Clip * c = job_owner[q].first;
-                    Decoder & d = c->st->decoders[job_owner[q].second];
-                    d.gtok = outs[q];
-                    if (want_probs) {
-                        d.probs.assign(probs_h.begin() + q * nv, probs_h.begin() + (q + 1) * nv);
-                        d.logprobs.assign(lp_h.begin() + q * nv, lp_h.begin() + (q + 1) * nv);
-                    }
+                    d.probs.assign(probs_h.begin() + q * nv, probs_h.begin() + (q + 1) * nv);
+                    d.logprobs.assign(lp_h.begin() + q * nv, lp_h.begin() + (q + 1) * nv);
                 }
             }
         }
+        for (size_t q = 0; q < nclip.size(); ++q) nclip[q]->st->no_speech_prob = ns_out[q];
         const int64_t dt = time_us() - t0;
         // completions
         for (size_t ci = 0; ci < dec.size(); ++ci) {
@@ -1021,6 +1017,8 @@ int full_batch(whisper_context * ctx, whisper_state ** states, const whisper_ful
             else c->on_step();
         }
     }
+    for (int c = 0; c < n_clips; ++c)
+        eng.save_logits_state(c, states[c]->logits_rows, states[c]->logits_rowmax, states[c]->logits_row0);
     int ret = 0;
     for (auto & c : clips)
         if (c.ret != 0 && ret == 0) ret = c.ret;

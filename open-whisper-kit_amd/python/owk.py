@@ -190,6 +190,8 @@ def load(path: str | None = None) -> C.CDLL:
     L.owk_debug_enc.argtypes = [vp, vp, ip, fp, ip]
     L.owk_debug_cross.argtypes = [vp, vp, ip, ip, C.POINTER(C.c_uint16), C.POINTER(C.c_uint16)]
     L.owk_debug_gelu_table.restype = C.POINTER(C.c_uint16)
+    u16p = C.POINTER(C.c_uint16)
+    L.owk_debug_gemm.argtypes = [ip, ip, ip, ip, u16p, u16p, fp]
     _lib = L
     return L
 
