@@ -54,6 +54,8 @@ WHISPER_API int owk_debug_cross(struct whisper_context * ctx, struct whisper_sta
 WHISPER_API const uint16_t * owk_debug_gelu_table(void);
 /* out[M][N] = A[M][K] . W[N][K]^T (f16 bits in, f32 out) through the engine's GEMM dispatch */
 WHISPER_API int owk_debug_gemm(int device, int M, int N, int K, const uint16_t * a, const uint16_t * w, float * out);
+/* average microseconds per launch of `iters` back-to-back engine GEMMs (epilogue `mode`, zero data) */
+WHISPER_API double owk_debug_gemm_bench(int device, int mode, int M, int N, int K, int iters);
 
 /* library identity: 1 when the gfx950 HIP code object is present and a device is usable */
 WHISPER_API int owk_device_ok(int device);

@@ -86,6 +86,7 @@ Engine::Engine(const Model * m_, Prof * prof_) : m(m_), prof(prof_) {
     size_t fl = 0;
     for (int N : {3 * d, d, 4 * d, nv})
         for (int K : {d, 4 * d}) fl = std::max(fl, gemm_ws_floats(N, K));
+    for (int K : {d, 4 * d}) fl = std::max(fl, gemm_partial_floats(d, K));
     gws_part_.alloc(std::max<size_t>(fl, 1) * 4);
     gws_.partial = gws_part_.as<float>();
     gws_.partial_floats = fl;
@@ -426,6 +427,15 @@ void Engine::decode(const std::vector<DecodeRow> & rows, const std::vector<int> 
         pos[r] = x.pos;
         rowoff[r] = ((int64_t) x.slot * kv_cells + x.cell) * d;
         rs[r] = AttnRow{r, (int) ((int64_t) x.slot * kv_cells * d), x.n_keys, x.key_off, 0, x.mode_self};
+        if (x.mode_self == 0 && x.n_keys > 0) {  // one contiguous run of cells: no list needed
+            const int * kl = key_list.data() + x.key_off;
+            bool run = true;
+            for (int i = 1; i < x.n_keys && run; ++i) run = kl[i] == kl[0] + i;
+            if (run) {
+                rs[r].kv_base += kl[0] * d;
+                rs[r].key_list = -1;
+            }
+        }
         rc[r] = AttnRow{r, (int) ((int64_t) x.slot * T * d), T, -1, n_ctx_pad - T, x.mode_cross};
         sh.max_keys = std::max(sh.max_keys, x.n_keys);
         (x.mode_self ? sh.self_tl : sh.self_oc) = true;
@@ -504,14 +514,36 @@ void Engine::launch_decode(const DecShape & sh) {
     const float kq_scale = powf(64.0f, -0.25f);
     const size_t self_stride = (size_t) cap_slots * kv_cells * d;
     const size_t cross_stride = (size_t) cap_slots * T * d;
+    // R <= 32 rows: the residual matmuls (attn.out, cross_attn.out, mlp.2) emit partial tiles
+    // that one fused kernel finishes together with the following LayerNorm (3 launches
+    // fewer per layer); larger passes use the full-epilogue GEMMs and separate LayerNorms
+    const bool fused = R <= 32;
+    float * part = gws_.partial;
+    auto resid_ln = [&](const _Float16 * A, const _Float16 * W, const _Float16 * Wt, int K, const float * bias,
+                        const float * lnw, const float * lnb) {
+        EpiParams ep;
+        G("part", EPI_PARTIAL, d, K, A, W, Wt, ep, R);
+        ProfScope ps(prof, stream, "layernorm");
+        resid_layernorm(stream, R, d, gemm_partial_splits(K), part, bias, d_x_.as<float>(), lnw, lnb, hp.eps,
+                        d_xn_.as<_Float16>(), d);
+    };
+    auto resid_full = [&](const _Float16 * A, const _Float16 * W, const _Float16 * Wt, int K, const float * bias) {
+        EpiParams ep;
+        ep.bias = bias;
+        ep.resid = d_x_.as<float>();
+        ep.out32 = d_x_.as<float>();
+        ep.ldo = d;
+        G("resid", EPI_RESID_F32, d, K, A, W, Wt, ep, R);
+    };
+    auto ln = [&](const float * w, const float * b) {
+        ProfScope ps(prof, stream, "layernorm");
+        layernorm_f16(stream, d_x_.as<float>(), R, d, w, b, hp.eps, d_xn_.as<_Float16>(), d);
+    };
     for (int l = 0; l < hp.n_text_layer; ++l) {
         const DecLayerW & L = m->dec[l];
         _Float16 * Kl = self_k_.as<_Float16>() + l * self_stride;
         _Float16 * Vl = self_v_.as<_Float16>() + l * self_stride;
-        {
-            ProfScope ps(prof, stream, "layernorm");
-            layernorm_f16(stream, d_x_.as<float>(), R, d, L.attn_ln_w, L.attn_ln_b, hp.eps, d_xn_.as<_Float16>(), d);
-        }
+        if (!fused || l == 0) ln(L.attn_ln_w, L.attn_ln_b);
         {
             EpiParams ep;
             ep.bias = L.b_q;
@@ -530,17 +562,11 @@ void Engine::launch_decode(const DecShape & sh) {
             attn_decoder(stream, d_q_.as<_Float16>(), d, Kl, Vl, d, d_rs, R, d_keys, H,
                          1.0f, max_keys, d_ao_.as<_Float16>(), d, self_oc, self_tl);
         }
-        {
-            EpiParams ep;
-            ep.bias = L.b_o;
-            ep.resid = d_x_.as<float>();
-            ep.out32 = d_x_.as<float>();
-            ep.ldo = d;
-            G("o", EPI_RESID_F32, d, d, d_ao_.as<_Float16>(), L.w_o, L.t_o, ep, R);
-        }
-        {
-            ProfScope ps(prof, stream, "layernorm");
-            layernorm_f16(stream, d_x_.as<float>(), R, d, L.cross_ln_w, L.cross_ln_b, hp.eps, d_xn_.as<_Float16>(), d);
+        if (fused) {
+            resid_ln(d_ao_.as<_Float16>(), L.w_o, L.t_o, d, L.b_o, L.cross_ln_w, L.cross_ln_b);
+        } else {
+            resid_full(d_ao_.as<_Float16>(), L.w_o, L.t_o, d, L.b_o);
+            ln(L.cross_ln_w, L.cross_ln_b);
         }
         {
             EpiParams ep;
@@ -556,17 +582,11 @@ void Engine::launch_decode(const DecShape & sh) {
                          cross_v_.as<_Float16>() + l * cross_stride, d, d_rc, R, nullptr, H,
                          kq_scale, T, d_ao_.as<_Float16>(), d, cross_oc, cross_tl);
         }
-        {
-            EpiParams ep;
-            ep.bias = L.cb_o;
-            ep.resid = d_x_.as<float>();
-            ep.out32 = d_x_.as<float>();
-            ep.ldo = d;
-            G("co", EPI_RESID_F32, d, d, d_ao_.as<_Float16>(), L.cw_o, L.t_co, ep, R);
-        }
-        {
-            ProfScope ps(prof, stream, "layernorm");
-            layernorm_f16(stream, d_x_.as<float>(), R, d, L.mlp_ln_w, L.mlp_ln_b, hp.eps, d_xn_.as<_Float16>(), d);
+        if (fused) {
+            resid_ln(d_ao_.as<_Float16>(), L.cw_o, L.t_co, d, L.cb_o, L.mlp_ln_w, L.mlp_ln_b);
+        } else {
+            resid_full(d_ao_.as<_Float16>(), L.cw_o, L.t_co, d, L.cb_o);
+            ln(L.mlp_ln_w, L.mlp_ln_b);
         }
         {
             EpiParams ep;
@@ -576,13 +596,13 @@ void Engine::launch_decode(const DecShape & sh) {
             ep.ldo = 4 * d;
             G("mlp0", EPI_GELU_F16, 4 * d, d, d_xn_.as<_Float16>(), L.w_mlp0, L.t_mlp0, ep, R);
         }
-        {
-            EpiParams ep;
-            ep.bias = L.b_mlp1;
-            ep.resid = d_x_.as<float>();
-            ep.out32 = d_x_.as<float>();
-            ep.ldo = d;
-            G("mlp1", EPI_RESID_F32, d, 4 * d, d_h_.as<_Float16>(), L.w_mlp1, L.t_mlp1, ep, R);
+        if (fused) {
+            const bool last = l + 1 == hp.n_text_layer;
+            const DecLayerW * nx = last ? nullptr : &m->dec[l + 1];
+            resid_ln(d_h_.as<_Float16>(), L.w_mlp1, L.t_mlp1, 4 * d, L.b_mlp1, nx ? nx->attn_ln_w : nullptr,
+                     nx ? nx->attn_ln_b : nullptr);
+        } else {
+            resid_full(d_h_.as<_Float16>(), L.w_mlp1, L.t_mlp1, 4 * d, L.b_mlp1);
         }
     }
     if (n_logit_rows > 0) {

@@ -168,6 +168,161 @@ __global__ __launch_bounds__(256, 2) void k_attn_encoder(const _Float16 * __rest
     }
 }
 
+// ----------------------------------------------------------------------------------
+// Encoder attention WITHOUT flash attention (context flash_attn = false; the mode the
+// reference needs for DTW timestamps, whisper.cpp:2163-2189): KQ = K.Q over exactly T keys
+// (no zero padding), soft_max_ext(KQ * scale) with the exact row max first and a
+// double-accumulated sum (ggml_compute_forward_soft_max_f32, ops.cpp:5160-5272), then the
+// probabilities are ROUNDED TO F16 (mul_mat(V, KQ_soft_max) converts its f32 operand) and
+// multiplied with V. Same block/lane mapping as k_attn_encoder; three sweeps over the keys
+// (max, sum, output).
+// ----------------------------------------------------------------------------------
+__global__ __launch_bounds__(256, 2) void k_attn_encoder_sm(const _Float16 * __restrict__ q,
+                                                            const _Float16 * __restrict__ k,
+                                                            const _Float16 * __restrict__ vt, int T, int Tpad, int H,
+                                                            float scale, _Float16 * __restrict__ out) {
+    __shared__ __attribute__((aligned(1024))) char smem[4 * FA_TILE_BYTES];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int qt = blockIdx.x, h = blockIdx.y, clip = blockIdx.z;
+    const int d = H * 64;
+    const int g = lane >> 4, l16 = lane & 15;
+    const int qi = qt * 64 + wave * 16 + l16;
+    const int qc = min(qi, T - 1);
+    const _Float16 * qrow = q + ((size_t) clip * T + qc) * d + h * 64;
+    const half8 qf0 = *(const half8 *) (qrow + 8 * g);
+    const half8 qf1 = *(const half8 *) (qrow + 32 + 8 * g);
+    const _Float16 * kbase = k + (size_t) clip * T * d + h * 64;
+    const _Float16 * vbase = vt + ((size_t) clip * H + h) * 64 * Tpad;
+
+    auto stage = [&](int buf, int kt, bool with_v) {
+        char * sK = smem + buf * 2 * FA_TILE_BYTES;
+        char * sV = sK + FA_TILE_BYTES;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int grp = wave * 2 + i;
+            const int row = grp * 8 + (lane >> 3);
+            const int c = (lane & 7) ^ ((row >> 1) & 7);
+            const int key = min(kt * FA_KT + row, T - 1);
+            __builtin_amdgcn_global_load_lds((const void *) (kbase + (size_t) key * d + c * 8),
+                                             (lds_ptr_t) (sK + grp * 1024), 16, 0, 0);
+            if (with_v)
+                __builtin_amdgcn_global_load_lds((const void *) (vbase + (size_t) row * Tpad + kt * FA_KT + c * 8),
+                                                 (lds_ptr_t) (sV + grp * 1024), 16, 0, 0);
+        }
+    };
+    // scores of one K tile: sc[t][e] = s(key 16t + 4g + e, query l16) * scale, -inf past T
+    auto scores = [&](const char * sK, int kt, floatx4 (&sc)[4]) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const int row = t * 16 + l16;
+            const half8 a0 = *(const half8 *) (sK + row * 128 + (((0 + g) ^ ((row >> 1) & 7)) << 4));
+            const half8 a1 = *(const half8 *) (sK + row * 128 + (((4 + g) ^ ((row >> 1) & 7)) << 4));
+            floatx4 z = floatx4{0.f, 0.f, 0.f, 0.f};
+            z = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, qf0, z, 0, 0, 0);
+            z = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1, qf1, z, 0, 0, 0);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int key = kt * FA_KT + t * 16 + 4 * g + e;
+                z[e] = key < T ? z[e] * scale : -INFINITY;
+            }
+            sc[t] = z;
+        }
+    };
+    const int ntiles = (T + FA_KT - 1) / FA_KT;
+
+    // sweep 1: exact row max
+    float m = -INFINITY;
+    stage(0, 0, false);
+    __syncthreads();
+    for (int kt = 0; kt < ntiles; ++kt) {
+        const int cur = kt & 1;
+        if (kt + 1 < ntiles) stage(cur ^ 1, kt + 1, false);
+        floatx4 sc[4];
+        scores(smem + cur * 2 * FA_TILE_BYTES, kt, sc);
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) m = fmaxf(m, sc[t][e]);
+        __syncthreads();
+    }
+    m = fmaxf(m, __shfl_xor(m, 16, 64));
+    m = fmaxf(m, __shfl_xor(m, 32, 64));
+
+    // sweep 2: sum of exp(s - max), accumulated in double
+    double l = 0.0;
+    stage(0, 0, false);
+    __syncthreads();
+    for (int kt = 0; kt < ntiles; ++kt) {
+        const int cur = kt & 1;
+        if (kt + 1 < ntiles) stage(cur ^ 1, kt + 1, false);
+        floatx4 sc[4];
+        scores(smem + cur * 2 * FA_TILE_BYTES, kt, sc);
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) l += (double) expf(sc[t][e] - m);
+        __syncthreads();
+    }
+    l += __shfl_xor(l, 16, 64);
+    l += __shfl_xor(l, 32, 64);
+    const float inv = (float) (1.0 / l);
+
+    // sweep 3: P = f16(exp(s - max) * inv), O = P . V
+    floatx4 o[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) o[i] = floatx4{0.f, 0.f, 0.f, 0.f};
+    stage(0, 0, true);
+    __syncthreads();
+    for (int kt = 0; kt < ntiles; ++kt) {
+        const int cur = kt & 1;
+        if (kt + 1 < ntiles) stage(cur ^ 1, kt + 1, true);
+        const char * sK = smem + cur * 2 * FA_TILE_BYTES;
+        const char * sV = sK + FA_TILE_BYTES;
+        floatx4 sc[4];
+        scores(sK, kt, sc);
+        half8 pb[2];
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) pb[t >> 1][(t & 1) * 4 + e] = (_Float16) (expf(sc[t][e] - m) * inv);
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) {
+            const int row = dt * 16 + l16;
+            const char * vr = sV + row * 128;
+            const int sw = (row >> 1) & 7;
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks) {
+                const int b0 = ks * 64 + 8 * g;
+                const int b1 = ks * 64 + 32 + 8 * g;
+                const half4 lo = *(const half4 *) (vr + ((((b0 >> 4) ^ sw) << 4) | (b0 & 15)));
+                const half4 hi = *(const half4 *) (vr + ((((b1 >> 4) ^ sw) << 4) | (b1 & 15)));
+                half8 a;
+                a[0] = lo[0]; a[1] = lo[1]; a[2] = lo[2]; a[3] = lo[3];
+                a[4] = hi[0]; a[5] = hi[1]; a[6] = hi[2]; a[7] = hi[3];
+                o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, pb[ks], o[dt], 0, 0, 0);
+            }
+        }
+        __syncthreads();
+    }
+    if (qi < T) {
+        _Float16 * orow = out + ((size_t) clip * T + qi) * d + h * 64;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) {
+            half4 r;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) r[e] = (_Float16) o[dt][e];
+            *(half4 *) (orow + dt * 16 + 4 * g) = r;
+        }
+    }
+}
+
+void attn_encoder_softmax(hipStream_t s, const _Float16 * q, const _Float16 * k, const _Float16 * vt, int n_clips, int T,
+                          int Tpad, int H, float scale, _Float16 * out) {
+    if (Tpad < ((T + FA_KT - 1) / FA_KT) * FA_KT) throw std::runtime_error("attn_encoder_softmax: Tpad too small");
+    hipLaunchKernelGGL(k_attn_encoder_sm, dim3((T + 63) / 64, H, n_clips), dim3(256), 0, s, q, k, vt, T, Tpad, H, scale,
+                       out);
+}
+
 void attn_encoder(hipStream_t s, const _Float16 * q, const _Float16 * k, const _Float16 * vt, int n_clips, int T,
                   int Tpad, int H, float scale, int n_zero_pad, _Float16 * out) {
     if (Tpad < ((T + FA_KT - 1) / FA_KT) * FA_KT) throw std::runtime_error("attn_encoder: Tpad too small");
@@ -238,11 +393,14 @@ __global__ __launch_bounds__(64) void k_attn_step(const _Float16 * __restrict__ 
         out[(size_t) job.q_row * ldo + h * 64 + lane] = (_Float16) 0.0f;
         return;
     }
-    if constexpr (LIST) {
+    // a listed row whose cells are not one contiguous run (the host passes contiguous runs
+    // as key_list = -1 with kv_base at the first cell)
+    const bool listed = LIST && job.key_list >= 0;
+    if (listed) {
         // cell indices to LDS up front: the stage loop then issues no global loads whose
         // results it must wait for (a vmcnt wait would also drain the in-flight K/V tiles)
         const int * list = key_idx + job.key_list;
-        for (int i = lane; i < n; i += 64) s_list[i] = job.key_list >= 0 ? list[i] : i;
+        for (int i = lane; i < n; i += 64) s_list[i] = list[i];
         __builtin_amdgcn_s_waitcnt(0);
         __builtin_amdgcn_wave_barrier();
     }
@@ -264,7 +422,7 @@ __global__ __launch_bounds__(64) void k_attn_step(const _Float16 * __restrict__ 
         for (int i = 0; i < 8; ++i) {
             const int kk = i * 8 + (lane >> 3);
             const int key = min(c * AS_KC + kk, n - 1);
-            const int cell = LIST ? s_list[key] : key;
+            const int cell = listed ? s_list[key] : key;
             const int seg = (lane & 7) ^ (kk & 7);  // K rows XOR-swizzled for the lane-per-key reads
             __builtin_amdgcn_global_load_lds((const void *) (kh + (size_t) cell * ld_kv + seg * 8),
                                              (lds_ptr_t) (sK + i * 1024), 16, 0, 0);
@@ -373,7 +531,7 @@ __global__ __launch_bounds__(256) void k_attn_decoder(const _Float16 * __restric
     __shared__ _Float16 qs[4][64];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const AttnRow job = rows[blockIdx.y];
-    if (job.mode == 0) return;  // one_chunk rows: k_attn_step
+    if (job.mode != 1) return;  // one_chunk rows: k_attn_step; soft_max rows: k_attn_softmax
     const int h = blockIdx.x * 4 + wave;
     if (h >= H) return;
     const int n = job.n_keys;
@@ -467,6 +625,107 @@ __global__ __launch_bounds__(256) void k_attn_decoder(const _Float16 * __restric
         result = acc * S_inv;
     }
     out[(size_t) job.q_row * ldo + h * 64 + lane] = (_Float16) result;
+}
+
+// ----------------------------------------------------------------------------------
+// Decoder attention WITHOUT flash attention (flash_attn = false contexts; rows with
+// mode 2): KQ over the listed keys (self: visible cells; cross: exactly n_audio_ctx),
+// soft_max with the exact max and a double sum, probabilities rounded to F16 for the
+// P.V product (whisper.cpp:2616-2628 self, 2697-2738 cross). Optionally the f32
+// probabilities of alignment heads are captured for DTW timestamps (whisper.cpp:2720-2736):
+// cap[a][key][cap_row] for alignment head a = amap[h] >= 0.
+// Block = 4 waves per (row, head).
+// ----------------------------------------------------------------------------------
+constexpr int SM_MAX_KEYS = 2048;
+
+__global__ __launch_bounds__(256) void k_attn_softmax(const _Float16 * __restrict__ q, int ldq,
+                                                      const _Float16 * __restrict__ kb, const _Float16 * __restrict__ vb,
+                                                      int ld_kv, const AttnRow * __restrict__ rows,
+                                                      const int * __restrict__ key_idx, float scale,
+                                                      _Float16 * __restrict__ out, int ldo,
+                                                      const int * __restrict__ amap, float * __restrict__ cap,
+                                                      int cap_rows) {
+    __shared__ float sp[SM_MAX_KEYS];
+    __shared__ _Float16 p16[SM_MAX_KEYS];
+    __shared__ float redf[4];
+    __shared__ double redd[4];
+    __shared__ floatx4 acc4[4][16];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const AttnRow job = rows[blockIdx.y];
+    if (job.mode != 2) return;
+    const int h = blockIdx.x;
+    const int n = job.n_keys;
+    const int * list = job.key_list >= 0 ? key_idx + job.key_list : nullptr;
+    const _Float16 * kh = kb + job.kv_base + h * 64;
+    const _Float16 * vh = vb + job.kv_base + h * 64;
+    const _Float16 * qr = q + (size_t) job.q_row * ldq + h * 64;
+
+    // scores
+    float mx = -INFINITY;
+    for (int i = tid; i < n; i += 256) {
+        const int cell = list ? list[i] : i;
+        const half8 * kr = (const half8 *) (kh + (size_t) cell * ld_kv);
+        float part[8];
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+            const half8 kv = kr[c];
+            const half8 qv = ((const half8 *) qr)[c];
+            float a = 0.0f;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) a = fmaf((float) kv[e], (float) qv[e], a);
+            part[c] = a;
+        }
+        const float s = (((part[0] + part[1]) + (part[2] + part[3])) + ((part[4] + part[5]) + (part[6] + part[7]))) * scale;
+        sp[i] = s;
+        mx = fmaxf(mx, s);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+    if (lane == 0) redf[wave] = mx;
+    __syncthreads();
+    mx = fmaxf(fmaxf(redf[0], redf[1]), fmaxf(redf[2], redf[3]));
+    // exp and the double-accumulated sum
+    double sum = 0.0;
+    for (int i = tid; i < n; i += 256) {
+        const float e = expf(sp[i] - mx);
+        sp[i] = e;
+        sum += (double) e;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o, 64);
+    if (lane == 0) redd[wave] = sum;
+    __syncthreads();
+    sum = (redd[0] + redd[1]) + (redd[2] + redd[3]);
+    const float inv = (float) (1.0 / sum);
+    const int a = amap ? amap[h] : -1;
+    for (int i = tid; i < n; i += 256) {
+        const float p = sp[i] * inv;
+        p16[i] = (_Float16) p;
+        if (a >= 0) cap[((size_t) a * n + i) * cap_rows + job.q_row] = p;
+    }
+    __syncthreads();
+    // P . V: wave w takes keys w, w+4, ...; lane = head dim
+    float acc = 0.0f;
+    for (int i = wave; i < n; i += 4) {
+        const int cell = list ? list[i] : i;
+        acc = fmaf((float) p16[i], (float) vh[(size_t) cell * ld_kv + lane], acc);
+    }
+    ((float *) acc4)[wave * 64 + lane] = acc;
+    __syncthreads();
+    if (wave == 0) {
+        const float * a4 = (const float *) acc4;
+        const float r = (a4[lane] + a4[64 + lane]) + (a4[128 + lane] + a4[192 + lane]);
+        out[(size_t) job.q_row * ldo + h * 64 + lane] = (_Float16) r;
+    }
+}
+
+void attn_decoder_softmax(hipStream_t s, const _Float16 * q, int ldq, const _Float16 * kbase, const _Float16 * vbase,
+                          int ld_kv, const AttnRow * rows_dev, int n_rows, const int * key_idx, int H, float scale,
+                          int max_keys, _Float16 * out, int ldo, const int * amap, float * cap, int cap_rows) {
+    if (n_rows <= 0) return;
+    if (max_keys > SM_MAX_KEYS) throw std::runtime_error("attn_decoder_softmax: too many keys");
+    hipLaunchKernelGGL(k_attn_softmax, dim3(H, n_rows), dim3(256), 0, s, q, ldq, kbase, vbase, ld_kv, rows_dev, key_idx,
+                       scale, out, ldo, amap, cap, cap_rows);
 }
 
 int attn_max_listed_keys() { return AS_MAX_LIST; }

@@ -73,6 +73,7 @@ __device__ __forceinline__ void epi_store(const EpiParams & p, int r, int c, flo
         p.out32[(size_t) r * p.ldo + c] = acc;
     }
 }
+template <> __device__ __forceinline__ void epi_store<EPI_PARTIAL>(const EpiParams &, int, int, float) {}
 
 typedef __attribute__((address_space(3))) void * lds_ptr_t;
 
@@ -317,19 +318,30 @@ __global__ __launch_bounds__(GR_MAXW * 64) void k_gemm_rows(int M, int N, int K,
     for (int i = 0; i < MT; ++i) red[wave][i][lane] = acc[i];
     __syncthreads();
 
-    if (tid < MT * 64) {
-        const int i = tid >> 6, ln = tid & 63;
-        floatx4 sum = red[0][i][ln];
-        for (int w = 1; w < nw; ++w) sum += red[w][i][ln];
-        if (gridDim.y == 1) {
-            const int c = n0 + (ln & 15);
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const int r = i * 16 + 4 * (ln >> 4) + e;
-                if (r < M && c < N) epi_store<MODE>(ep, r, c, sum[e]);
-            }
-        } else {
+    if (MODE != EPI_PARTIAL && gridDim.y > 1) {  // split-K partial tiles for k_gemm_rows_reduce
+        if (tid < MT * 64) {
+            const int i = tid >> 6, ln = tid & 63;
+            floatx4 sum = red[0][i][ln];
+            for (int w = 1; w < nw; ++w) sum += red[w][i][ln];
             ((floatx4 *) part)[(((size_t) blockIdx.y * gridDim.x + tile) * MT + i) * 64 + ln] = sum;
+        }
+        return;
+    }
+    // epilogue spread over every thread: one output (row r, column c) each, adjacent
+    // threads on adjacent columns; the wave partials are summed in fixed wave order
+    for (int o = tid; o < MT * 256; o += blockDim.x) {
+        const int r = o >> 4, cc = o & 15;
+        const int i = r >> 4, rr = r & 15;
+        const int ln = 16 * (rr >> 2) + cc, e = rr & 3;
+        const float * rp = (const float *) &red[0][i][ln] + e;
+        float sum = rp[0];
+        for (int w = 1; w < nw; ++w) sum += rp[w * MT * 64 * 4];
+        const int c = n0 + cc;
+        if (r < M && c < N) {
+            if constexpr (MODE == EPI_PARTIAL)
+                part[((size_t) blockIdx.y * M + r) * N + c] = sum;  // row-major [ks][M][N] for resid_layernorm
+            else
+                epi_store<MODE>(ep, r, c, sum);
         }
     }
 }
@@ -353,11 +365,22 @@ __global__ __launch_bounds__(MT * 64) void k_gemm_rows_reduce(int M, int N, int 
 struct RowsPlan {
     int J, nw, KS;
 };
-static RowsPlan rows_plan(int K) {
+static int env_int(const char * name, int dflt) {
+    const char * v = getenv(name);
+    return v && *v ? atoi(v) : dflt;
+}
+// partial (EPI_PARTIAL) launches split K for free (resid_layernorm adds the splits), so
+// they take shorter k ranges per wave and twice the blocks; full-epilogue launches avoid
+// a second (reduce) launch unless K is very long (tools/gemm_sweep.py measurements)
+static RowsPlan rows_plan(int K, bool partial) {
     const int nsteps = K / 32;
     RowsPlan p;
-    p.J = nsteps <= 32 ? 2 : nsteps <= 64 ? 4 : 8;
+    if (partial) p.J = nsteps <= 64 ? 2 : 4;
+    else p.J = nsteps <= 32 ? 2 : nsteps <= 64 ? 4 : 8;
+    static const int j_over = env_int("OWK_GR_J", 0), ks_over = env_int("OWK_GR_KS", 0);  // tuning sweeps
+    if (j_over == 2 || j_over == 4 || j_over == 8) p.J = j_over;
     p.KS = (nsteps + GR_MAXW * p.J - 1) / (GR_MAXW * p.J);
+    if (ks_over > p.KS && ks_over <= nsteps / p.J) p.KS = ks_over;
     const int per = (nsteps + p.KS - 1) / p.KS;
     p.nw = (per + p.J - 1) / p.J;
     return p;
@@ -396,16 +419,16 @@ template <int MODE> struct LaunchRows {
     static void go(hipStream_t s, dim3 grid, int nw, int M, int N, int K, const _Float16 * A, int lda,
                    const _Float16 * Wt, const EpiParams & ep, float * part) {
         hipLaunchKernelGGL((k_gemm_rows<MODE, MT, J>), grid, dim3(nw * 64), 0, s, M, N, K, A, lda, Wt, ep, part);
-        if (grid.y > 1)
+        if (grid.y > 1 && MODE != EPI_PARTIAL)
             hipLaunchKernelGGL((k_gemm_rows_reduce<MODE, MT>), dim3(grid.x), dim3(MT * 64), 0, s, M, N, (int) grid.y,
                                part, ep);
     }
     static void run(hipStream_t s, int M, int N, int K, const _Float16 * A, int lda, const _Float16 * Wt,
                     const EpiParams & ep, const GemmWs * ws) {
-        const RowsPlan pl = rows_plan(K);
+        const RowsPlan pl = rows_plan(K, MODE == EPI_PARTIAL);
         const int tiles = (N + 15) / 16;
         float * part = nullptr;
-        if (pl.KS > 1) {
+        if (pl.KS > 1 || MODE == EPI_PARTIAL) {
             const size_t need = (size_t) pl.KS * tiles * 2 * 64 * 4;  // floats (MT <= 2)
             if (!ws || ws->partial_floats < need) throw std::runtime_error("gemm_rows: split-K workspace too small");
             part = ws->partial;
@@ -440,12 +463,20 @@ void gemm_f16_skinny(hipStream_t s, int mode, int M, int N, int K, const _Float1
 }
 
 size_t gemm_ws_floats(int N, int K) {
-    const RowsPlan p = rows_plan(K);
+    const RowsPlan p = rows_plan(K, false);
     return p.KS > 1 ? (size_t) p.KS * ((N + 15) / 16) * 2 * 64 * 4 : 0;
 }
+size_t gemm_partial_floats(int N, int K) { return (size_t) rows_plan(K, true).KS * ((N + 15) / 16) * 2 * 64 * 4; }
+int gemm_partial_splits(int K) { return rows_plan(K, true).KS; }
 
 void gemm(hipStream_t s, int mode, int M, int N, int K, const _Float16 * A, int lda, const _Float16 * W, int ldw,
           const EpiParams & ep, const GemmWs * ws, const _Float16 * Wt) {
+    if (mode == EPI_PARTIAL) {
+        if (!(M <= 32 && K % 32 == 0 && Wt && N % 16 == 0)) throw std::runtime_error("gemm: EPI_PARTIAL needs the decode-row path");
+        check_shape(M, N, K, lda, ldw, 32);
+        LaunchRows<EPI_PARTIAL>::run(s, M, N, K, A, lda, Wt, ep, ws);
+        return;
+    }
     if (M <= 32 && K % 32 == 0 && Wt) {
         check_shape(M, N, K, lda, ldw, 32);
         dispatch_mode<LaunchRows>(mode, s, M, N, K, A, lda, Wt, ep, ws);

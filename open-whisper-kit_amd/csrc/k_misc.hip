@@ -21,22 +21,12 @@ __device__ __forceinline__ double wave_sum_d(double v) {
 // ----------------------------------------------------------------------------------
 constexpr int LN_V4 = 8;  // float4 per lane held in registers -> d <= 2048
 
-__global__ __launch_bounds__(256) void k_layernorm_f16(const float * __restrict__ x, int rows, int d,
-                                                       const float * __restrict__ w, const float * __restrict__ b,
-                                                       float eps, _Float16 * __restrict__ out, int ldo,
-                                                       const int * __restrict__ row_idx, float * __restrict__ out32) {
-    const int lane = threadIdx.x & 63;
-    const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (row >= rows) return;
-    const float4 * xr = (const float4 * ) (x + (size_t) (row_idx ? row_idx[row] : row) * d);
+// LayerNorm of one row held in registers (lane owns float4 groups lane + 64 j); shared by
+// k_layernorm_f16 and k_resid_layernorm so both produce identical bits
+__device__ __forceinline__ void ln_row_regs(const float4 (&xv)[LN_V4], int lane, int d, const float * __restrict__ w,
+                                            const float * __restrict__ b, float eps, _Float16 * __restrict__ o,
+                                            float * __restrict__ o32) {
     const int n4 = d >> 2;
-    // the whole row is loaded once, up front (one memory round trip per launch)
-    float4 xv[LN_V4];
-#pragma unroll
-    for (int j = 0; j < LN_V4; ++j) {
-        const int i = lane + 64 * j;
-        xv[j] = i < n4 ? xr[i] : float4{0.f, 0.f, 0.f, 0.f};
-    }
     double s = 0.0;
 #pragma unroll
     for (int j = 0; j < LN_V4; ++j)
@@ -56,7 +46,6 @@ __global__ __launch_bounds__(256) void k_layernorm_f16(const float * __restrict_
     const float scale = 1.0f / sqrtf(var + eps);
     const float4 * w4 = (const float4 *) w;
     const float4 * b4 = (const float4 *) b;
-    _Float16 * o = out + (size_t) row * ldo;
 #pragma unroll
     for (int j = 0; j < LN_V4; ++j) {
         const int i = lane + 64 * j;
@@ -70,9 +59,73 @@ __global__ __launch_bounds__(256) void k_layernorm_f16(const float * __restrict_
             half4 h;
             h[0] = (_Float16) y.x; h[1] = (_Float16) y.y; h[2] = (_Float16) y.z; h[3] = (_Float16) y.w;
             *(half4 *) (o + 4 * i) = h;
-            if (out32) *(float4 *) (out32 + (size_t) row * d + 4 * i) = y;
+            if (o32) *(float4 *) (o32 + 4 * i) = y;
         }
     }
+}
+
+__global__ __launch_bounds__(256) void k_layernorm_f16(const float * __restrict__ x, int rows, int d,
+                                                       const float * __restrict__ w, const float * __restrict__ b,
+                                                       float eps, _Float16 * __restrict__ out, int ldo,
+                                                       const int * __restrict__ row_idx, float * __restrict__ out32) {
+    const int lane = threadIdx.x & 63;
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= rows) return;
+    const float4 * xr = (const float4 * ) (x + (size_t) (row_idx ? row_idx[row] : row) * d);
+    const int n4 = d >> 2;
+    // the whole row is loaded once, up front (one memory round trip per launch)
+    float4 xv[LN_V4];
+#pragma unroll
+    for (int j = 0; j < LN_V4; ++j) {
+        const int i = lane + 64 * j;
+        xv[j] = i < n4 ? xr[i] : float4{0.f, 0.f, 0.f, 0.f};
+    }
+    ln_row_regs(xv, lane, d, w, b, eps, out + (size_t) row * ldo, out32 ? out32 + (size_t) row * d : nullptr);
+}
+
+// Finishes an EPI_PARTIAL decode-row GEMM: sums its k splits in order (row-major partial
+// rows [ks][M][N], k_gemm.hip), adds bias and the residual (out = resid + (acc + bias),
+// whisper.cpp's ggml_add(mul_mat + b, inpL)), writes the new residual row, then LayerNorms it
+// for the next matmul.
+__global__ __launch_bounds__(256) void k_resid_layernorm(int M, int N, int KS, const float * __restrict__ part,
+                                                         const float * __restrict__ bias, float * __restrict__ x,
+                                                         const float * __restrict__ w, const float * __restrict__ b,
+                                                         float eps, _Float16 * __restrict__ xn, int ldo) {
+    const int lane = threadIdx.x & 63;
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= M) return;
+    const int n4 = N >> 2;
+    float4 * xr = (float4 *) (x + (size_t) row * N);
+    float4 xv[LN_V4];
+#pragma unroll
+    for (int j = 0; j < LN_V4; ++j) {
+        const int i = lane + 64 * j;
+        float4 r = float4{0.f, 0.f, 0.f, 0.f};
+        if (i < n4) {
+            float4 a = ((const float4 *) (part + (size_t) row * N))[i];
+            for (int ks = 1; ks < KS; ++ks) {
+                const float4 p = ((const float4 *) (part + ((size_t) ks * M + row) * N))[i];
+                a.x += p.x; a.y += p.y; a.z += p.z; a.w += p.w;
+            }
+            const float4 bb = ((const float4 *) bias)[i];
+            const float4 res = xr[i];
+            r.x = res.x + (a.x + bb.x);
+            r.y = res.y + (a.y + bb.y);
+            r.z = res.z + (a.z + bb.z);
+            r.w = res.w + (a.w + bb.w);
+            xr[i] = r;
+        }
+        xv[j] = r;
+    }
+    if (w) ln_row_regs(xv, lane, N, w, b, eps, xn + (size_t) row * ldo, nullptr);
+}
+
+void resid_layernorm(hipStream_t s, int M, int N, int ks, const float * part, const float * bias, float * x,
+                     const float * lnw, const float * lnb, float eps, _Float16 * xn, int ldo) {
+    if (M <= 0) return;
+    if (M > 32 || N % 16 != 0 || N > 4 * 64 * LN_V4) throw std::runtime_error("resid_layernorm: unsupported shape");
+    hipLaunchKernelGGL(k_resid_layernorm, dim3((M + 3) / 4), dim3(256), 0, s, M, N, ks, part, bias, x, lnw, lnb, eps,
+                       xn, ldo);
 }
 
 void layernorm_f16(hipStream_t s, const float * x, int rows, int d, const float * w, const float * b, float eps,

@@ -20,6 +20,8 @@ enum EpiMode : int {
     EPI_KV_CROSS = 5,   // cross K (scaled) / V (+bias) split into the cross-KV cache
     EPI_QKV_DEC = 6,    // decoder self-attn: Q (bias, scale), K (scale), V (bias) -> KV cells
     EPI_F32 = 7,        // out32[r*ldo+c] = acc  (logits)
+    EPI_PARTIAL = 8,    // decode-row GEMM only: raw partial tiles to the workspace, finished by
+                        // resid_layernorm (bias + residual + next LayerNorm in one pass)
 };
 
 struct EpiParams {
@@ -53,6 +55,13 @@ struct GemmWs {
     size_t partial_floats = 0;
 };
 size_t gemm_ws_floats(int N, int K);  // partial floats a (N, K) decode-row GEMM needs (0 = no split)
+size_t gemm_partial_floats(int N, int K);  // workspace of an EPI_PARTIAL decode-row GEMM
+int gemm_partial_splits(int K);            // its k splits (rows of partial tiles)
+// x[r][c] += sum_ks partial + bias[c]  (the reference's mul_mat + bias + residual add), then
+// LayerNorm of the updated row -> xn (f16), unless lnw == nullptr (residual only).
+// `part` holds `ks` splits [ks][M][N] of an EPI_PARTIAL GEMM with M rows (M <= 32) and N columns.
+void resid_layernorm(hipStream_t s, int M, int N, int ks, const float * part, const float * bias, float * x,
+                     const float * lnw, const float * lnb, float eps, _Float16 * xn, int ldo);
 // dispatch on M: <= 32 rows decode-row GEMM (needs the tiled copy Wt), <= 64 skinny,
 // else 128x128 tiles (row-major W)
 void gemm(hipStream_t s, int mode, int M, int N, int K, const _Float16 * A, int lda,
@@ -107,6 +116,9 @@ void conv2_im2col(hipStream_t s, const _Float16 * x, int n_clips, int t_in, int 
 // encoder self-attention (flash, MFMA) over T real keys + n_zero_pad all-zero keys
 // (the reference's GGML_PAD(1500,256) kv_pad rows, whisper.cpp:2055,2145-2159).
 // q, k: [clips*T][H*64] f16; vt: [clips][H][64][Tpad] f16; out: [clips*T][H*64] f16
+// encoder attention of a flash_attn = false context (soft_max path, F16 probabilities)
+void attn_encoder_softmax(hipStream_t s, const _Float16 * q, const _Float16 * k, const _Float16 * vt, int n_clips, int T,
+                          int Tpad, int H, float scale, _Float16 * out);
 void attn_encoder(hipStream_t s, const _Float16 * q, const _Float16 * k, const _Float16 * vt,
                   int n_clips, int T, int Tpad, int H, float scale, int n_zero_pad, _Float16 * out);
 
@@ -119,11 +131,16 @@ struct AttnRow {
     int n_keys;         // number of listed key rows
     int key_list;       // offset into key_idx (cell indices, in reference visit order); -1 = 0..n_keys-1
     int n_zero_pad;     // trailing all-zero keys (cross attention padding)
-    int mode;           // 0 = one_chunk (F16 accumulator), 1 = tiled (F32 accumulator)
+    int mode;           // 0 = one_chunk (F16 accumulator), 1 = tiled (F32 accumulator), 2 = soft_max (no FA)
 };
 void attn_decoder(hipStream_t s, const _Float16 * q, int ldq, const _Float16 * kbase, const _Float16 * vbase,
                   int ld_kv, const AttnRow * rows_dev, int n_rows, const int * key_idx, int H, float scale,
                   int max_keys, _Float16 * out, int ldo, bool any_one_chunk, bool any_tiled);
+// rows with mode 2 (flash_attn = false contexts): soft_max attention, F16 probabilities;
+// optional DTW capture of alignment-head probabilities cap[a][key][row] (amap: head -> a or -1)
+void attn_decoder_softmax(hipStream_t s, const _Float16 * q, int ldq, const _Float16 * kbase, const _Float16 * vbase,
+                          int ld_kv, const AttnRow * rows_dev, int n_rows, const int * key_idx, int H, float scale,
+                          int max_keys, _Float16 * out, int ldo, const int * amap, float * cap, int cap_rows);
 int attn_max_listed_keys();  // per-row limit of the one_chunk kernel's key list
 int attn_max_tiled_keys();   // per-row limit of the tiled decoder kernel
 

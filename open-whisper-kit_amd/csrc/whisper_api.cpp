@@ -1003,6 +1003,58 @@ int owk_debug_cross(struct whisper_context * ctx, struct whisper_state * st, int
 
 const uint16_t * owk_debug_gelu_table(void) { return gelu_table_host().data(); }
 
+// average device microseconds of `iters` back-to-back decode GEMM launches (event-timed)
+double owk_debug_gemm_bench(int device, int mode, int M, int N, int K, int iters) {
+    try {
+        OWK_HIP_CHECK(hipSetDevice(device));
+        hipStream_t s;
+        OWK_HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+        DevBuf da, dw, dwt, d32, d16, dres, part, bias;
+        da.alloc((size_t) M * K * 2);
+        dw.alloc((size_t) N * K * 2);
+        dwt.alloc(tiled_weight_elems(N, K) * 2);
+        d32.alloc((size_t) M * N * 4);
+        d16.alloc((size_t) M * N * 2);
+        dres.alloc((size_t) M * N * 4);
+        bias.alloc((size_t) N * 4);
+        OWK_HIP_CHECK(hipMemset(da.ptr, 0, da.bytes));
+        OWK_HIP_CHECK(hipMemset(dw.ptr, 0, dw.bytes));
+        OWK_HIP_CHECK(hipMemset(dres.ptr, 0, dres.bytes));
+        OWK_HIP_CHECK(hipMemset(bias.ptr, 0, bias.bytes));
+        tile_weights(s, dw.as<_Float16>(), N, K, dwt.as<_Float16>());
+        const size_t fl = std::max(gemm_ws_floats(N, K), gemm_partial_floats(N, K));
+        part.alloc(std::max<size_t>(fl, 1) * 4);
+        GemmWs ws;
+        ws.partial = part.as<float>();
+        ws.partial_floats = fl;
+        EpiParams ep;
+        ep.bias = bias.as<float>();
+        ep.resid = dres.as<float>();
+        ep.out32 = d32.as<float>();
+        ep.out16 = d16.as<_Float16>();
+        ep.ldo = N;
+        hipEvent_t e0, e1;
+        OWK_HIP_CHECK(hipEventCreate(&e0));
+        OWK_HIP_CHECK(hipEventCreate(&e1));
+        for (int i = 0; i < 3; ++i)
+            gemm(s, mode, M, N, K, da.as<_Float16>(), K, dw.as<_Float16>(), K, ep, &ws, dwt.as<_Float16>());
+        OWK_HIP_CHECK(hipEventRecord(e0, s));
+        for (int i = 0; i < iters; ++i)
+            gemm(s, mode, M, N, K, da.as<_Float16>(), K, dw.as<_Float16>(), K, ep, &ws, dwt.as<_Float16>());
+        OWK_HIP_CHECK(hipEventRecord(e1, s));
+        OWK_HIP_CHECK(hipEventSynchronize(e1));
+        float ms = 0;
+        OWK_HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
+        (void) hipEventDestroy(e0);
+        (void) hipEventDestroy(e1);
+        OWK_HIP_CHECK(hipStreamDestroy(s));
+        return 1e3 * ms / iters;
+    } catch (const std::exception & ex) {
+        log_msg(GGML_LOG_LEVEL_ERROR, "owk_debug_gemm_bench: %s\n", ex.what());
+        return -1;
+    }
+}
+
 int owk_debug_gemm(int device, int M, int N, int K, const uint16_t * a, const uint16_t * w, float * out) {
     try {
         OWK_HIP_CHECK(hipSetDevice(device));

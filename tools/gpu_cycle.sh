@@ -14,4 +14,7 @@ if [ "$PROF" = "1" ]; then
   timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/$TAG/prof -o run -- \
       python3 $GRAFT_REPO_ROOT/bench.py --steps 1 --warmup 1 --no-cpu-baseline \
       > $GRAFT_REPO_ROOT/gpurun_out/$TAG/prof_bench.json 2> $GRAFT_REPO_ROOT/gpurun_out/$TAG/prof_bench.err || exit $?
+  cd $GRAFT_REPO_ROOT
+  python3 tools/prof_summary.py gpurun_out/$TAG/prof > gpurun_out/$TAG/kernel_stats.txt
+  rm -f gpurun_out/$TAG/prof/*kernel_trace.csv   # keep the stats, drop the per-dispatch trace
 fi
