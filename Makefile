@@ -13,17 +13,26 @@ PKG      := open-whisper-kit_amd
 SRC      := $(PKG)/csrc
 OBJDIR   := $(PKG)/build
 LIB      := $(PKG)/lib/libwhisper.so
+SFLIB    := $(PKG)/lib/libsortformer.so
 
 FLAGS    := -O3 -g -std=c++17 -fPIC -ffp-contract=off --offload-arch=$(ARCH) -Iinclude -I$(SRC) \
             -DWHISPER_SHARED -DWHISPER_BUILD -Wall -Wno-unused-function -Wno-unused-variable
 
 HIP_SRCS := $(wildcard $(SRC)/*.hip)
 CPP_SRCS := $(wildcard $(SRC)/*.cpp)
-OBJS     := $(patsubst $(SRC)/%.hip,$(OBJDIR)/%.hip.o,$(HIP_SRCS)) \
+ALL_OBJS := $(patsubst $(SRC)/%.hip,$(OBJDIR)/%.hip.o,$(HIP_SRCS)) \
             $(patsubst $(SRC)/%.cpp,$(OBJDIR)/%.cpp.o,$(CPP_SRCS))
+# libsortformer.so: the SortFormer C ABI (include/sortformer.h) + the shared GEMM/LayerNorm kernels
+SF_ONLY  := $(OBJDIR)/sortformer.cpp.o $(OBJDIR)/k_sortformer.hip.o
+OBJS     := $(filter-out $(SF_ONLY),$(ALL_OBJS))
+SF_OBJS  := $(SF_ONLY) $(OBJDIR)/k_gemm.hip.o $(OBJDIR)/k_misc.hip.o
 HDRS     := $(wildcard $(SRC)/*.h) $(wildcard include/*.h)
 
-all: $(LIB)
+all: $(LIB) $(SFLIB)
+
+$(SFLIB): $(SF_OBJS)
+	@mkdir -p $(dir $@)
+	$(HIPCC) -shared --offload-arch=$(ARCH) -o $@ $(SF_OBJS) -Wl,--no-undefined -Wl,-soname,libsortformer.so
 
 $(LIB): $(OBJS)
 	@mkdir -p $(dir $@)

@@ -71,6 +71,26 @@ __device__ __forceinline__ void epi_store(const EpiParams & p, int r, int c, flo
         }
     } else if constexpr (MODE == EPI_F32) {
         p.out32[(size_t) r * p.ldo + c] = acc;
+    } else if constexpr (MODE == EPI_BIAS_F32) {
+        const float v = p.bias ? acc + p.bias[c] : acc;
+        const size_t o = (size_t) r * p.ldo + c;
+        p.out32[o] = v;
+        if (p.out16) p.out16[o] = (_Float16) v;
+    } else if constexpr (MODE == EPI_SILU_F16) {
+        // ggml_silu_f32 (ggml-cpu/vec.h): x / (1 + exp(-x))
+        const float v = acc + p.bias[c];
+        p.out16[(size_t) r * p.ldo + c] = (_Float16) (v / (1.0f + expf(-v)));
+    } else if constexpr (MODE == EPI_HALF_RESID) {
+        // ggml_add(x, b) -> ggml_scale(0.5) -> ggml_add(residual, .) (sortformer.cpp:1163-1167)
+        const float v = (acc + p.bias[c]) * 0.5f;
+        const size_t o = (size_t) r * p.ldo + c;
+        p.out32[o] = p.resid[o] + v;
+    } else if constexpr (MODE == EPI_RELU_F16) {
+        const float v = acc + p.bias[c];
+        p.out16[(size_t) r * p.ldo + c] = (_Float16) (v > 0.0f ? v : 0.0f);
+    } else if constexpr (MODE == EPI_SIGMOID_F32) {
+        const float v = acc + p.bias[c];
+        p.out32[(size_t) r * p.ldo + c] = 1.0f / (1.0f + expf(-v));
     }
 }
 template <> __device__ __forceinline__ void epi_store<EPI_PARTIAL>(const EpiParams &, int, int, float) {}
@@ -396,6 +416,11 @@ template <template <int> class L, typename... Args> static void dispatch_mode(in
         case EPI_KV_CROSS: L<EPI_KV_CROSS>::run(args...); break;
         case EPI_QKV_DEC: L<EPI_QKV_DEC>::run(args...); break;
         case EPI_F32: L<EPI_F32>::run(args...); break;
+        case EPI_BIAS_F32: L<EPI_BIAS_F32>::run(args...); break;
+        case EPI_SILU_F16: L<EPI_SILU_F16>::run(args...); break;
+        case EPI_HALF_RESID: L<EPI_HALF_RESID>::run(args...); break;
+        case EPI_RELU_F16: L<EPI_RELU_F16>::run(args...); break;
+        case EPI_SIGMOID_F32: L<EPI_SIGMOID_F32>::run(args...); break;
         default: throw std::runtime_error("gemm: bad epilogue mode");
     }
 }

@@ -22,6 +22,12 @@ enum EpiMode : int {
     EPI_F32 = 7,        // out32[r*ldo+c] = acc  (logits)
     EPI_PARTIAL = 8,    // decode-row GEMM only: raw partial tiles to the workspace, finished by
                         // resid_layernorm (bias + residual + next LayerNorm in one pass)
+    // SortFormer (streaming-sortformer/src/sortformer.cpp) epilogues
+    EPI_BIAS_F32 = 9,   // out32 = acc (+ bias[c]); out16 (optional) = f16 of the same value
+    EPI_SILU_F16 = 10,  // out16 = f16(silu(acc + bias))              (conformer FFN linear1)
+    EPI_HALF_RESID = 11,// out32 = resid + (acc + bias) * 0.5         (macaron FFN half step)
+    EPI_RELU_F16 = 12,  // out16 = f16(relu(acc + bias))              (transformer FFN, head)
+    EPI_SIGMOID_F32 = 13,// out32 = sigmoid(acc + bias)               (speaker head)
 };
 
 struct EpiParams {

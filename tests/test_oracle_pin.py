@@ -1,6 +1,9 @@
 """CPU: the numpy restatement of the reference numerics (oracle/whisper_np.py) pinned
 against the golden vectors the compiled reference produced (tests/golden/), and the
 host-built pieces of the drop-in library checked against it. No GPU needed."""
+import json
+import os
+
 import numpy as np
 import pytest
 
@@ -8,6 +11,8 @@ import owk
 import whisper_np as O
 
 LOGIT_RTOL = 1e-3
+ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
+GOLDEN = os.path.join(ROOT, "tests", "golden")
 
 
 @pytest.fixture(scope="module")
@@ -66,3 +71,31 @@ def test_gelu_table_matches_library():
     finite = np.isfinite(x) & np.isfinite(ref.view(np.float16))
     assert np.array_equal(lib[finite], ref[finite])
     del C
+
+
+def test_sortformer_oracle_reproduces_golden():
+    """The compiled reference SortFormer (oracle/_ref/libsortformer_ref.so) regenerates the
+    committed staged-API fixtures bit for bit (pins the fixtures to the reference)."""
+    import sortformer as SF
+    import sortformer_synth as SS
+
+    ref = os.path.join(ROOT, "oracle", "_ref", "libsortformer_ref.so")
+    if not os.path.exists(ref):
+        pytest.skip("reference SortFormer oracle not built")
+    meta = json.load(open(os.path.join(GOLDEN, "sf_golden.json")))
+    A = np.load(os.path.join(GOLDEN, "sf_golden.npz"))
+    cache = os.environ.get("OWK_MODEL_CACHE", "/tmp/owk_models")
+    os.makedirs(cache, exist_ok=True)
+    path = os.path.join(cache, f"synth-sortformer-s{meta['seed']}.gguf")
+    if not os.path.exists(path):
+        assert SS.write_model(path, meta["seed"]) == meta["sha256"]
+    import owk_synth as S
+
+    sf = SF.Sortformer(path, lib=ref, n_threads=min(8, os.cpu_count() or 1))
+    x = S.read_wav_16k_mono(os.path.join(GOLDEN, "sf_test60.wav"))[:16000 * 15]
+    mel, seq = sf.mel(x)
+    assert np.array_equal(mel, A["stage/mel"])
+    assert np.array_equal(sf.preenc(A["stage/mel"], seq), A["stage/preenc"])
+    assert np.array_equal(sf.conformer(A["stage/preenc"], 0), A["stage/conf0"])
+    assert np.array_equal(sf.prediction(A["stage/trans17"]), A["stage/pred"])
+    sf.close()
