@@ -55,6 +55,16 @@ WHISPER_API const uint16_t * owk_debug_gelu_table(void);
 /* out[M][N] = A[M][K] . W[N][K]^T (f16 bits in, f32 out) through the engine's GEMM dispatch */
 WHISPER_API int owk_debug_gemm(int device, int M, int N, int K, const uint16_t * a, const uint16_t * w, float * out);
 /* average microseconds per launch of `iters` back-to-back engine GEMMs (epilogue `mode`, zero data) */
+/* test hook (host only): the DTW alignment of captured alignment-head attention
+ * cap[(head * n_audio_ctx + j) * n_tok + t] (the reference's aheads_cross_QKs layout), as
+ * the time index of each text token the reference's placement loop assigns, in order
+ * (whisper_exp_compute_token_level_timestamps_dtw, ref src/whisper.cpp:8837-8998).
+ * Returns the count written (<= cap_out) or -1. */
+WHISPER_API int owk_debug_dtw(const float * cap, int n_ah, int n_audio_ctx, int n_tok, int sot_len, int n_frames,
+                              int medfilt, int * out, int cap_out);
+/* test hook: alignment-head probabilities captured by the state's last DTW re-decode,
+ * [head][n_audio_ctx][rows of that pass]; returns the float count (copies when out != NULL) */
+WHISPER_API long owk_debug_capture(struct whisper_state * state, float * out, long cap);
 WHISPER_API double owk_debug_gemm_bench(int device, int mode, int M, int N, int K, int iters);
 
 /* library identity: 1 when the gfx950 HIP code object is present and a device is usable */

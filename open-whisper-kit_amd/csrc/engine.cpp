@@ -271,8 +271,12 @@ void Engine::encode(const std::vector<int> & slots, const std::vector<int> & off
             // 4*T*Tpad_kv*d flops (QK^T and PV over the 1536 reference keys)
             ProfScope ps(prof, stream, "attn_encoder", 4.0 * n * (double) T * n_ctx_pad * d,
                          2.0 * 4.0 * M * (double) d);
-            attn_encoder(stream, e_q_.as<_Float16>(), e_k_.as<_Float16>(), e_vt_.as<_Float16>(), n, T, Tpad, H, kq_scale,
-                         n_zero_pad, e_ao_.as<_Float16>());
+            if (flash_attn)
+                attn_encoder(stream, e_q_.as<_Float16>(), e_k_.as<_Float16>(), e_vt_.as<_Float16>(), n, T, Tpad, H,
+                             kq_scale, n_zero_pad, e_ao_.as<_Float16>());
+            else  // soft_max path over exactly T keys (whisper.cpp:2163-2189)
+                attn_encoder_softmax(stream, e_q_.as<_Float16>(), e_k_.as<_Float16>(), e_vt_.as<_Float16>(), n, T, Tpad,
+                                     H, kq_scale, e_ao_.as<_Float16>());
         }
         {
             EpiParams ep;
@@ -375,7 +379,27 @@ uint64_t Engine::buffers_signature() const {
     return h;
 }
 
-void Engine::decode(const std::vector<DecodeRow> & rows, const std::vector<int> & key_list, int n_logit_rows) {
+void Engine::set_alignment_heads(const std::vector<int> & amap, int n_aheads) {
+    const HParams & hp = m->hp;
+    if ((int) amap.size() != hp.n_text_layer * hp.n_text_head) throw std::runtime_error("set_alignment_heads: map size");
+    amap_.alloc(amap.size() * sizeof(int));
+    OWK_HIP_CHECK(hipMemcpy(amap_.ptr, amap.data(), amap.size() * sizeof(int), hipMemcpyHostToDevice));
+    n_ah_ = n_aheads;
+}
+
+void Engine::download_capture(int row0, int n, std::vector<float> & out) const {
+    const int T = m->hp.n_audio_ctx;
+    if (!cap_.ptr || row0 < 0 || row0 + n > cap_rows_) throw std::runtime_error("download_capture: no such rows");
+    std::vector<float> all((size_t) n_ah_ * T * cap_rows_);
+    OWK_HIP_CHECK(hipMemcpyAsync(all.data(), cap_.ptr, all.size() * 4, hipMemcpyDeviceToHost, stream));
+    OWK_HIP_CHECK(hipStreamSynchronize(stream));
+    out.resize((size_t) n_ah_ * T * n);
+    for (size_t kj = 0; kj < (size_t) n_ah_ * T; ++kj)
+        memcpy(&out[kj * n], &all[kj * cap_rows_ + row0], (size_t) n * 4);
+}
+
+void Engine::decode(const std::vector<DecodeRow> & rows, const std::vector<int> & key_list, int n_logit_rows,
+                    bool capture) {
     const HParams & hp = m->hp;
     const int R = (int) rows.size();
     if (R == 0) return;
@@ -436,10 +460,11 @@ void Engine::decode(const std::vector<DecodeRow> & rows, const std::vector<int> 
                 rs[r].key_list = -1;
             }
         }
-        rc[r] = AttnRow{r, (int) ((int64_t) x.slot * T * d), T, -1, n_ctx_pad - T, x.mode_cross};
+        // soft_max rows attend over exactly n_audio_ctx keys (no FA padding, whisper.cpp:2700-2712)
+        rc[r] = AttnRow{r, (int) ((int64_t) x.slot * T * d), T, -1, x.mode_cross == 2 ? 0 : n_ctx_pad - T, x.mode_cross};
         sh.max_keys = std::max(sh.max_keys, x.n_keys);
-        (x.mode_self ? sh.self_tl : sh.self_oc) = true;
-        (x.mode_cross ? sh.cross_tl : sh.cross_oc) = true;
+        (x.mode_self == 2 ? sh.self_sm : x.mode_self ? sh.self_tl : sh.self_oc) = true;
+        (x.mode_cross == 2 ? sh.cross_sm : x.mode_cross ? sh.cross_tl : sh.cross_oc) = true;
         if (x.logit_row >= 0) lsel[x.logit_row] = r;
     }
     if (nk) memcpy(h + st_keys_, key_list.data(), (size_t) nk * 4);
@@ -447,8 +472,15 @@ void Engine::decode(const std::vector<DecodeRow> & rows, const std::vector<int> 
     if (sh.self_oc && sh.max_keys > attn_max_listed_keys()) throw std::runtime_error("decode: too many self-attention keys");
     if (sh.self_tl && sh.max_keys > attn_max_tiled_keys()) throw std::runtime_error("decode: too many self-attention keys");
 
+    if (capture) {
+        if (!n_ah_ || !amap_.ptr) throw std::runtime_error("decode: capture without alignment heads");
+        if (!sh.cross_sm) throw std::runtime_error("decode: capture needs soft_max cross attention (flash_attn = false)");
+        cap_.alloc((size_t) n_ah_ * T * R * 4);
+        cap_rows_ = R;
+        sh.capture = true;
+    }
     static const bool no_graph = getenv("OWK_NO_GRAPH") && atoi(getenv("OWK_NO_GRAPH")) != 0;
-    if ((prof && prof->on) || no_graph) {  // per-kernel events (or debugging): eager launches
+    if ((prof && prof->on) || no_graph || capture) {  // per-kernel events, debugging, DTW: eager launches
         launch_decode(sh);
         return;
     }
@@ -459,7 +491,8 @@ void Engine::decode(const std::vector<DecodeRow> & rows, const std::vector<int> 
         graphs_sig_ = sig;
     }
     const uint64_t key = (uint64_t) R | ((uint64_t) n_logit_rows << 20) | ((uint64_t) sh.self_oc << 40) |
-                         ((uint64_t) sh.self_tl << 41) | ((uint64_t) sh.cross_oc << 42) | ((uint64_t) sh.cross_tl << 43);
+                         ((uint64_t) sh.self_tl << 41) | ((uint64_t) sh.cross_oc << 42) | ((uint64_t) sh.cross_tl << 43) |
+                         ((uint64_t) sh.self_sm << 44) | ((uint64_t) sh.cross_sm << 45);
     auto it = graphs_.find(key);
     if (it == graphs_.end()) {
         if (graphs_.size() >= 64) clear_graphs();
@@ -561,6 +594,9 @@ void Engine::launch_decode(const DecShape & sh) {
             ProfScope ps(prof, stream, "attn_self");
             attn_decoder(stream, d_q_.as<_Float16>(), d, Kl, Vl, d, d_rs, R, d_keys, H,
                          1.0f, max_keys, d_ao_.as<_Float16>(), d, self_oc, self_tl);
+            if (sh.self_sm)  // masked soft_max with scale 1 (Q, K pre-scaled; whisper.cpp:2614-2628)
+                attn_decoder_softmax(stream, d_q_.as<_Float16>(), d, Kl, Vl, d, d_rs, R, d_keys, H, 1.0f, max_keys,
+                                     d_ao_.as<_Float16>(), d, nullptr, nullptr, 0);
         }
         if (fused) {
             resid_ln(d_ao_.as<_Float16>(), L.w_o, L.t_o, d, L.b_o, L.cross_ln_w, L.cross_ln_b);
@@ -581,6 +617,11 @@ void Engine::launch_decode(const DecShape & sh) {
             attn_decoder(stream, d_q_.as<_Float16>(), d, cross_k_.as<_Float16>() + l * cross_stride,
                          cross_v_.as<_Float16>() + l * cross_stride, d, d_rc, R, nullptr, H,
                          kq_scale, T, d_ao_.as<_Float16>(), d, cross_oc, cross_tl);
+            if (sh.cross_sm)  // soft_max_ext(KQ, nullptr, KQscale) over n_audio_ctx keys (whisper.cpp:2697-2738)
+                attn_decoder_softmax(stream, d_q_.as<_Float16>(), d, cross_k_.as<_Float16>() + l * cross_stride,
+                                     cross_v_.as<_Float16>() + l * cross_stride, d, d_rc, R, nullptr, H, kq_scale, T,
+                                     d_ao_.as<_Float16>(), d, sh.capture ? amap_.as<int>() + l * H : nullptr,
+                                     sh.capture ? cap_.as<float>() : nullptr, R);
         }
         if (fused) {
             resid_ln(d_ao_.as<_Float16>(), L.cw_o, L.t_co, d, L.cb_o, L.mlp_ln_w, L.mlp_ln_b);

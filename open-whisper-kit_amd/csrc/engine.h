@@ -52,7 +52,7 @@ struct DecodeRow {
     int cell;        // self-KV cell receiving this token's K/V
     int key_off;     // visible self-attention cells: key_list[key_off .. key_off+n_keys)
     int n_keys;
-    int mode_self;   // 0 one_chunk (F16 acc), 1 tiled (F32 acc)
+    int mode_self;   // 0 one_chunk (F16 acc), 1 tiled (F32 acc), 2 soft_max (flash_attn = false)
     int mode_cross;
     int logit_row;   // -1: no logits for this row
 };
@@ -62,6 +62,8 @@ struct DecShape {
     int R, n_logit;
     bool self_oc, self_tl, cross_oc, cross_tl;  // attention kernels needed (one_chunk / tiled)
     int max_keys;
+    bool self_sm = false, cross_sm = false;     // soft_max rows (flash_attn = false contexts)
+    bool capture = false;                       // DTW: capture alignment-head cross-attention
 };
 
 // per-step bookkeeping of the emulated reference state->logits buffer (no-speech prob)
@@ -82,6 +84,9 @@ public:
 
     int cap_slots = 0;   // clip slots with cross-KV storage
     int kv_cells = 0;    // self-KV cells per slot
+    // whisper_context_params.flash_attn: false selects the reference's soft_max attention
+    // (encoder and decoder) -- the numerics DTW timestamps are defined with
+    bool flash_attn = true;
 
     void reserve(int slots, int cells);
 
@@ -102,7 +107,16 @@ public:
     // ---- decoder ----
     // runs all rows through the decoder; raw logits for rows with logit_row >= 0 are
     // left on the device in logits_dev() [n_logit_rows][n_vocab]
-    void decode(const std::vector<DecodeRow> & rows, const std::vector<int> & key_list, int n_logit_rows);
+    void decode(const std::vector<DecodeRow> & rows, const std::vector<int> & key_list, int n_logit_rows,
+                bool capture = false);
+    // DTW alignment heads (whisper.cpp:1160-1273): amap[layer * n_head + head] = global alignment-head
+    // index (layer-major, preset order) or -1. A decode(..., capture = true) pass stores the f32
+    // cross-attention probabilities of those heads; download_capture returns them for rows
+    // [row0, row0 + n) as [head][key][row] (the reference's aheads_cross_QKs layout).
+    void set_alignment_heads(const std::vector<int> & amap, int n_aheads);
+    int n_aheads() const { return n_ah_; }
+    void download_capture(int row0, int n, std::vector<float> & out) const;
+    int capture_rows() const { return cap_rows_; }
     float * logits_dev() const { return logits_.as<float>(); }
     void download_logits(int logit_row, float * host) const;
     void upload_logits(int logit_row, const float * host);
@@ -149,6 +163,9 @@ private:
     size_t st_tok_ = 0, st_pos_ = 0, st_rowoff_ = 0, st_rs_ = 0, st_rc_ = 0, st_lsel_ = 0, st_keys_ = 0, st_bytes_ = 0;
     std::map<uint64_t, hipGraphExec_t> graphs_;
     uint64_t graphs_sig_ = 0;
+
+    DevBuf amap_, cap_;  // DTW: head map [L][H], captured probabilities [n_ah][T][cap_rows_]
+    int n_ah_ = 0, cap_rows_ = 0;
 
     DevBuf mel_jobs_, pcm_tmp_;
     DevBuf gws_part_;  // split-K workspace of the decode-row GEMMs

@@ -67,6 +67,11 @@ struct whisper_state {
     std::vector<float> energy;
     int64_t t_beg = 0, t_last = 0;
     whisper_token tid_last = 0;
+    // context_params.flash_attn of the owning context (selects the attention numerics)
+    bool flash_attn = true;
+    // DTW alignment heads (dtw_token_timestamps): [layer][head] -> global index or -1
+    std::vector<int> dtw_amap;
+    int dtw_n_ah = 0;
 };
 
 struct whisper_context {
@@ -90,6 +95,18 @@ struct CallToken {  // one token of a reference decode call (whisper_batch entry
 // allocate KV cells for one reference decode call of one clip and emit engine rows
 int prepare_decode_call(whisper_state * st, int slot, const std::vector<CallToken> & toks,
                         std::vector<DecodeRow> & rows, std::vector<int> & keys, int & n_logit);
+// alignment heads of a context (ref get_alignment_heads_by_layer 8688-8707 / aheads_masks_init
+// 1160-1273): amap[layer * n_head + head] = index in layer-major preset order, or -1.
+// Returns false (with a logged error) on an invalid preset, like aheads_masks_init.
+bool alignment_heads(const whisper_context * ctx, std::vector<int> & amap, int & n_ah);
+// DTW time index of each text token placed by the path (timestamps.cpp)
+std::vector<int32_t> dtw_time_indices(const float * cap, int n_ah, int n_audio_ctx, int n_tok, int sot_len, int n_frames,
+                                      int medfilt);
+// DTW token timestamps of segments [i_segment, i_segment + n_segments) (timestamps.cpp)
+void dtw_timestamps(whisper_context * ctx, whisper_state * st, int i_segment, int n_segments, int seek, int n_frames,
+                    int medfilt, const std::vector<float> & cap, int n_ah, int n_audio_ctx, int n_tok, int sot_len);
+// configure a state's engine for its context (attention mode, alignment heads)
+void configure_engine(const whisper_context * ctx, whisper_state * st);
 int full_batch(whisper_context * ctx, whisper_state ** states, const whisper_full_params * params,
                const owk_full_ext * ext, const float * const * samples, const int * n_samples, int n_clips);
 } // namespace owk

@@ -203,4 +203,137 @@ int wrap_segment(whisper_context * ctx, whisper_state * st, int max_len, bool sp
     return res;
 }
 
+// ---------------------------------------------------------------------------------
+// DTW token timestamps (ref whisper_exp_compute_token_level_timestamps_dtw, 8837-8998;
+// median_filter 8802-8835; dtw_and_backtrace 8712-8796). `cap` holds the f32 cross-attention
+// probabilities of the alignment heads from the re-decode of [sot (lang) not text.. eot]:
+// cap[(k * n_audio_ctx + j) * n_tok + t] for head k, audio position j, token t -- the layout of
+// the reference's aheads_cross_QKs.
+// ---------------------------------------------------------------------------------
+// DTW over the captured probabilities; returns, for each new text position of the path in
+// order, the DTW time index (what the reference's placement loop assigns token by token)
+std::vector<int32_t> dtw_time_indices(const float * cap, int n_ah, int n_audio_ctx, int n_tok, int sot_len, int n_frames,
+                                      int medfilt) {
+    std::vector<int32_t> out;
+    const int n_audio = n_frames / 2;
+    if (n_ah <= 0 || n_audio <= medfilt || n_tok <= sot_len + 1) return out;
+    // copy the first n_audio positions and normalise over tokens (ggml_norm, eps 1e-9;
+    // ops.cpp:3578-3623: float mean of a double sum, centred variance accumulated in double
+    // over 16-lane partial sums (vec.cpp:472-546), scale = 1/sqrtf(var + eps))
+    std::vector<float> w((size_t) n_ah * n_audio * n_tok);
+    for (int k = 0; k < n_ah; ++k)
+        for (int j = 0; j < n_audio; ++j) {
+            const float * x = &cap[((size_t) k * n_audio_ctx + j) * n_tok];
+            float * y = &w[((size_t) k * n_audio + j) * n_tok];
+            double s = 0.0;
+            for (int t = 0; t < n_tok; ++t) s += (double) x[t];
+            const float mean = (float) s / (float) n_tok;
+            double s2 = 0.0;
+            int t = 0;
+            for (; t + 15 < n_tok; t += 16) {
+                float lane[16];
+                for (int e = 0; e < 16; ++e) {
+                    y[t + e] = x[t + e] - mean;
+                    lane[e] = y[t + e] * y[t + e];
+                }
+                for (int h = 8; h > 0; h >>= 1)  // _mm512_reduce_add_ps: pairwise halves
+                    for (int e = 0; e < h; ++e) lane[e] = lane[e] + lane[e + h];
+                s2 += (double) lane[0];
+            }
+            for (; t < n_tok; ++t) {
+                y[t] = x[t] - mean;
+                s2 += (double) (y[t] * y[t]);
+            }
+            const float var = (float) (s2 / n_tok);
+            const float sc = 1.0f / sqrtf(var + 1e-9f);
+            for (int u = 0; u < n_tok; ++u) y[u] *= sc;
+        }
+    // median filter (width medfilt, reflect padding) along audio, mean over heads, * -1;
+    // the sot sequence and eot columns are dropped
+    const int N = n_tok - sot_len - 1, M = n_audio;
+    std::vector<float> xm((size_t) N * M);  // [audio j][token i]
+    std::vector<float> filt;
+    std::vector<float> med((size_t) n_ah);
+    for (int i = 0; i < N; ++i) {
+        const int t = i + sot_len;
+        for (int j = 0; j < M; ++j) {
+            for (int k = 0; k < n_ah; ++k) {
+                filt.clear();
+                for (int off = -medfilt / 2; off <= medfilt / 2; ++off) {
+                    int idx = j + off;
+                    if (idx < 0) idx = -idx;
+                    else if (idx >= M) idx = 2 * (M - 1) - idx;
+                    filt.push_back(w[((size_t) k * n_audio + idx) * n_tok + t]);
+                }
+                std::sort(filt.begin(), filt.end());
+                med[k] = filt[filt.size() / 2];
+            }
+            double s = 0.0;  // ggml_mean: ggml_vec_sum_f32 (double accumulate -> float) / n
+            for (int k = 0; k < n_ah; ++k) s += (double) med[k];
+            float mval = (float) s;
+            mval /= (float) n_ah;
+            xm[(size_t) j * N + i] = mval * -1.0f;
+        }
+    }
+    // DTW cost / trace over (token i, audio j), then backtrace
+    std::vector<float> cost((size_t) (N + 1) * (M + 1), INFINITY);
+    std::vector<int32_t> trace((size_t) (N + 1) * (M + 1), -1);
+    auto C = [&](int i, int j) -> float & { return cost[(size_t) j * (N + 1) + i]; };
+    auto Tr = [&](int i, int j) -> int32_t & { return trace[(size_t) j * (N + 1) + i]; };
+    C(0, 0) = 0.0f;
+    for (int j = 1; j <= M; ++j)
+        for (int i = 1; i <= N; ++i) {
+            const float c0 = C(i - 1, j - 1), c1 = C(i - 1, j), c2 = C(i, j - 1);
+            float c;
+            int32_t tt;
+            if (c0 < c1 && c0 < c2) { c = c0; tt = 0; }
+            else if (c1 < c0 && c1 < c2) { c = c1; tt = 1; }
+            else { c = c2; tt = 2; }
+            C(i, j) = xm[(size_t) (j - 1) * N + (i - 1)] + c;
+            Tr(i, j) = tt;
+        }
+    for (int j = 0; j <= M; ++j) Tr(0, j) = 2;
+    for (int i = 0; i <= N; ++i) Tr(i, 0) = 1;
+    std::vector<std::pair<int32_t, int32_t>> path;  // (text index, time index), reversed
+    for (int i = N, j = M; i > 0 || j > 0;) {
+        path.emplace_back(i - 1, j - 1);
+        const int32_t tt = Tr(i, j);
+        if (tt == 0) { --i; --j; }
+        else if (tt == 1) { --i; }
+        else if (tt == 2) { --j; }
+        else throw std::runtime_error("dtw: bad trace");
+    }
+    std::reverse(path.begin(), path.end());
+    int32_t last_v = 0;
+    for (const auto & pv : path) {
+        if (pv.first == last_v) continue;
+        last_v = pv.first;
+        out.push_back(pv.second);
+    }
+    return out;
+}
+
+void dtw_timestamps(whisper_context * ctx, whisper_state * st, int i_segment, int n_segments, int seek, int n_frames,
+                    int medfilt, const std::vector<float> & cap, int n_ah, int n_audio_ctx, int n_tok, int sot_len) {
+    const std::vector<int32_t> tix = dtw_time_indices(cap.data(), n_ah, n_audio_ctx, n_tok, sot_len, n_frames, medfilt);
+    // place timestamps on the text tokens of the segments (each DTW step = 20 ms)
+    const whisper_token eot = ctx->model->vocab.eot;
+    auto & res = st->result_all;
+    size_t si = (size_t) i_segment, ti = 0;
+    auto next = [&]() {
+        if (++ti >= res[si].tokens.size()) { ++si; ti = 0; }
+    };
+    for (const int32_t time_index : tix) {
+        while (si < res.size() && (res[si].tokens.empty() || !(res[si].tokens[ti].id < eot))) {
+            if (res[si].tokens.empty()) { ++si; ti = 0; continue; }
+            next();
+        }
+        if (si >= res.size()) break;  // (the reference would run past the last segment here)
+        res[si].tokens[ti].t_dtw = (int64_t) time_index * 2 + seek;
+        next();
+        if (si >= res.size()) break;
+    }
+    (void) n_segments;
+}
+
 } // namespace owk

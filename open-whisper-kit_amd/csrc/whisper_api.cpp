@@ -7,6 +7,7 @@
 #include <cmath>
 #include <cstring>
 #include <fstream>
+#include <map>
 #include <regex>
 #include <thread>
 
@@ -42,10 +43,94 @@ static int owk_install_crash_handler = [] {
     return 0;
 }();
 
+namespace owk {
+
+// alignment-head presets of the reference (whisper.cpp:384-410): {text layer, head}
+static const std::map<int, std::vector<std::pair<int, int>>> & aheads_presets() {
+    static const std::map<int, std::vector<std::pair<int, int>>> m = {
+        {WHISPER_AHEADS_TINY_EN, {{1, 0}, {2, 0}, {2, 5}, {3, 0}, {3, 1}, {3, 2}, {3, 3}, {3, 4}}},
+        {WHISPER_AHEADS_TINY, {{2, 2}, {3, 0}, {3, 2}, {3, 3}, {3, 4}, {3, 5}}},
+        {WHISPER_AHEADS_BASE_EN, {{3, 3}, {4, 7}, {5, 1}, {5, 5}, {5, 7}}},
+        {WHISPER_AHEADS_BASE, {{3, 1}, {4, 2}, {4, 3}, {4, 7}, {5, 1}, {5, 2}, {5, 4}, {5, 6}}},
+        {WHISPER_AHEADS_SMALL_EN, {{6, 6}, {7, 0}, {7, 3}, {7, 8}, {8, 2}, {8, 5}, {8, 7}, {9, 0}, {9, 4}, {9, 8},
+                                   {9, 10}, {10, 0}, {10, 1}, {10, 2}, {10, 3}, {10, 6}, {10, 11}, {11, 2}, {11, 4}}},
+        {WHISPER_AHEADS_SMALL, {{5, 3}, {5, 9}, {8, 0}, {8, 4}, {8, 7}, {8, 8}, {9, 0}, {9, 7}, {9, 9}, {10, 5}}},
+        {WHISPER_AHEADS_MEDIUM_EN, {{11, 4}, {14, 1}, {14, 12}, {14, 14}, {15, 4}, {16, 0}, {16, 4}, {16, 9}, {17, 12},
+                                    {17, 14}, {18, 7}, {18, 10}, {18, 15}, {20, 0}, {20, 3}, {20, 9}, {20, 14}, {21, 12}}},
+        {WHISPER_AHEADS_MEDIUM, {{13, 15}, {15, 4}, {15, 15}, {16, 1}, {20, 0}, {23, 4}}},
+        {WHISPER_AHEADS_LARGE_V1, {{9, 19}, {11, 2}, {11, 4}, {11, 17}, {22, 7}, {22, 11}, {22, 17}, {23, 2}, {23, 15}}},
+        {WHISPER_AHEADS_LARGE_V2, {{10, 12}, {13, 17}, {16, 11}, {16, 12}, {16, 13}, {17, 15}, {17, 16}, {18, 4}, {18, 11},
+                                   {18, 19}, {19, 11}, {21, 2}, {21, 3}, {22, 3}, {22, 9}, {22, 12}, {23, 5}, {23, 7},
+                                   {23, 13}, {25, 5}, {26, 1}, {26, 12}, {27, 15}}},
+        {WHISPER_AHEADS_LARGE_V3, {{7, 0}, {10, 17}, {12, 18}, {13, 12}, {16, 1}, {17, 14}, {19, 11}, {21, 4}, {24, 1}, {25, 6}}},
+        {WHISPER_AHEADS_LARGE_V3_TURBO, {{2, 4}, {2, 11}, {3, 3}, {3, 6}, {3, 11}, {3, 14}}},
+    };
+    return m;
+}
+
+bool alignment_heads(const whisper_context * ctx, std::vector<int> & amap, int & n_ah) {
+    const whisper_context_params & cp = ctx->params;
+    const int L = ctx->model->hp.n_text_layer, H = ctx->model->hp.n_text_head;
+    std::vector<std::pair<int, int>> heads;
+    if (cp.dtw_aheads_preset == WHISPER_AHEADS_NONE) {
+        log_msg(GGML_LOG_LEVEL_ERROR, "aheads_masks_init: dtw_aheads_preset should be != DTW_AHEADS_NONE\n");
+        return false;
+    } else if (cp.dtw_aheads_preset == WHISPER_AHEADS_N_TOP_MOST) {
+        if (cp.dtw_n_top > L || cp.dtw_n_top <= 0) {
+            log_msg(GGML_LOG_LEVEL_ERROR, "aheads_masks_init: dtw_n_top must be between %d and %d for this model.", 1, L);
+            return false;
+        }
+        for (int l = L - cp.dtw_n_top; l < L; ++l)
+            for (int h = 0; h < H; ++h) heads.emplace_back(l, h);
+    } else {
+        if (cp.dtw_aheads_preset == WHISPER_AHEADS_CUSTOM) {
+            if (cp.dtw_aheads.n_heads == 0 || cp.dtw_aheads.heads == nullptr) {
+                log_msg(GGML_LOG_LEVEL_ERROR, "aheads_masks_init: dtw_aheads unset\n");
+                return false;
+            }
+            for (size_t i = 0; i < cp.dtw_aheads.n_heads; ++i)
+                heads.emplace_back(cp.dtw_aheads.heads[i].n_text_layer, cp.dtw_aheads.heads[i].n_head);
+        } else {
+            auto it = aheads_presets().find(cp.dtw_aheads_preset);
+            if (it == aheads_presets().end()) return false;
+            heads = it->second;
+        }
+        for (const auto & hh : heads)
+            if (hh.first < 0 || hh.first >= L || hh.second < 0 || hh.second >= H) {
+                log_msg(GGML_LOG_LEVEL_ERROR, "aheads_masks_init: alignment head (%d, %d) outside the model\n",
+                        hh.first + 1, hh.second + 1);
+                return false;
+            }
+    }
+    // global index: layer-major, and within a layer the preset order (the mask rows)
+    amap.assign((size_t) L * H, -1);
+    n_ah = 0;
+    for (int l = 0; l < L; ++l)
+        for (const auto & hh : heads)
+            if (hh.first == l) amap[(size_t) l * H + hh.second] = n_ah++;
+    return n_ah > 0;
+}
+
+void configure_engine(const whisper_context * ctx, whisper_state * st) {
+    if (!st->eng) return;
+    st->eng->flash_attn = ctx->params.flash_attn;
+    if (ctx->params.dtw_token_timestamps && st->dtw_n_ah > 0 && st->eng->n_aheads() == 0)
+        st->eng->set_alignment_heads(st->dtw_amap, st->dtw_n_ah);
+}
+
+}  // namespace owk
+
 static whisper_state * new_state(whisper_context * ctx) {
     auto * st = new whisper_state();
+    st->flash_attn = ctx->params.flash_attn;
+    if (ctx->params.dtw_token_timestamps && !alignment_heads(ctx, st->dtw_amap, st->dtw_n_ah)) {
+        log_msg(GGML_LOG_LEVEL_ERROR, "whisper_init_state: aheads_masks_init() failed for alignment heads masks\n");
+        delete st;
+        return nullptr;
+    }
     try {
         st->eng.reset(new Engine(ctx->model.get(), &ctx->prof));
+        configure_engine(ctx, st);
     } catch (const std::exception & e) {
         log_msg(GGML_LOG_LEVEL_ERROR, "whisper_init_state: %s\n", e.what());
         delete st;
@@ -174,11 +259,6 @@ struct whisper_context * whisper_init_with_params_no_state(struct whisper_model_
     const int64_t t0 = time_us();
     if (params.flash_attn && params.dtw_token_timestamps) {
         log_msg(GGML_LOG_LEVEL_WARN, "%s: dtw_token_timestamps is not supported with flash_attn - disabling\n", __func__);
-        params.dtw_token_timestamps = false;
-    }
-    if (params.dtw_token_timestamps) {
-        log_msg(GGML_LOG_LEVEL_WARN, "%s: dtw_token_timestamps is not available in this engine build - disabling\n",
-                __func__);
         params.dtw_token_timestamps = false;
     }
     int n_dev = 0;
@@ -319,6 +399,7 @@ void whisper_free(struct whisper_context * ctx) {
 // ---------------------------------------------------------------------------------
 static Engine & eng_of(whisper_context * ctx, whisper_state * st) {
     if (!st->eng) st->eng.reset(new Engine(ctx->model.get(), &ctx->prof));
+    configure_engine(ctx, st);
     const int cells = std::max<int>((int) st->kv.size, (ctx->model->hp.n_text_ctx + 255) / 256 * 256);
     st->eng->reserve(1, std::max(cells, st->eng->kv_cells));
     return *st->eng;
@@ -1004,6 +1085,35 @@ int owk_debug_cross(struct whisper_context * ctx, struct whisper_state * st, int
 const uint16_t * owk_debug_gelu_table(void) { return gelu_table_host().data(); }
 
 // average device microseconds of `iters` back-to-back decode GEMM launches (event-timed)
+long owk_debug_capture(struct whisper_state * st, float * out, long cap) {
+    try {
+        if (!st || !st->eng || st->eng->capture_rows() <= 0) return -1;
+        std::vector<float> v;
+        st->eng->download_capture(0, st->eng->capture_rows(), v);
+        if (out) {
+            if (cap < (long) v.size()) return -1;
+            std::copy(v.begin(), v.end(), out);
+        }
+        return (long) v.size();
+    } catch (const std::exception & ex) {
+        log_msg(GGML_LOG_LEVEL_ERROR, "owk_debug_capture: %s\n", ex.what());
+        return -1;
+    }
+}
+
+int owk_debug_dtw(const float * cap, int n_ah, int n_audio_ctx, int n_tok, int sot_len, int n_frames, int medfilt,
+                  int * out, int cap_out) {
+    try {
+        const auto v = owk::dtw_time_indices(cap, n_ah, n_audio_ctx, n_tok, sot_len, n_frames, medfilt);
+        const int n = std::min<int>((int) v.size(), cap_out);
+        for (int i = 0; i < n; ++i) out[i] = v[i];
+        return n;
+    } catch (const std::exception & ex) {
+        log_msg(GGML_LOG_LEVEL_ERROR, "owk_debug_dtw: %s\n", ex.what());
+        return -1;
+    }
+}
+
 double owk_debug_gemm_bench(int device, int mode, int M, int N, int K, int iters) {
     try {
         OWK_HIP_CHECK(hipSetDevice(device));

@@ -229,7 +229,7 @@ int wrap_segment(whisper_context * ctx, whisper_state * st, int max_len, bool sp
 // per-clip decoding state machine
 // ---------------------------------------------------------------------------------
 enum class Phase { START, WINDOW, WAIT_ENCODE, ATTEMPT, WAIT_PREFILL, STEP, WAIT_STEP, FINISH, EMIT, LANG_WAIT_ENC,
-                   LANG_WAIT_DEC, DONE };
+                   LANG_WAIT_DEC, WAIT_DTW, DONE };
 
 struct Clip {
     whisper_context * ctx;
@@ -266,12 +266,17 @@ struct Clip {
     // pending decode call
     std::vector<CallToken> rows;
     int64_t t_req = 0;
+    // pending DTW re-decode of the window's segments (ref 7744-7756)
+    int dtw_seg0 = 0, dtw_nseg = 0, dtw_seek_delta = 0, dtw_sot_len = 0;
 
     const Vocab & vocab() const { return ctx->model->vocab; }
     const HParams & hp() const { return ctx->model->hp; }
     bool done() const { return phase == Phase::DONE; }
     bool waiting_encode() const { return phase == Phase::WAIT_ENCODE || phase == Phase::LANG_WAIT_ENC; }
-    bool waiting_decode() const { return phase == Phase::WAIT_PREFILL || phase == Phase::WAIT_STEP || phase == Phase::LANG_WAIT_DEC; }
+    bool waiting_decode() const {
+        return phase == Phase::WAIT_PREFILL || phase == Phase::WAIT_STEP || phase == Phase::LANG_WAIT_DEC ||
+               phase == Phase::WAIT_DTW;
+    }
     int encode_offset() const { return phase == Phase::LANG_WAIT_ENC ? 0 : seek; }
 
     void fail(int code) {
@@ -666,6 +671,7 @@ struct Clip {
     void emit() {
         const Decoder & best = st->decoders[best_decoder_id];
         int seek_delta = best.seek_delta;
+        const int n_segments_before = (int) st->result_all.size();
         const int result_len = best.sequence.result_len;
         const auto & toks = best.sequence.tokens;
         auto & result_all = st->result_all;
@@ -728,10 +734,53 @@ struct Clip {
                     p.new_segment_callback(ctx, st, n_new, p.new_segment_callback_user_data);
             }
         }
+        // [EXPERIMENTAL] DTW token timestamps (ref 7744-7756): re-decode the window's text with
+        // soft_max attention, capturing the alignment heads' cross-attention
+        const int n_segments = (int) result_all.size() - n_segments_before;
+        if (ctx->params.dtw_token_timestamps && n_segments) {
+            dtw_seg0 = (int) result_all.size() - n_segments;
+            dtw_nseg = n_segments;
+            dtw_seek_delta = seek_delta;
+            std::vector<whisper_token> tk = {vocab().sot};
+            if (vocab().is_multilingual()) {
+                const int lang_id = whisper_lang_id(p.language);
+                st->lang_id = lang_id;
+                tk.push_back(vocab().sot + 1 + lang_id);
+            }
+            dtw_sot_len = (int) tk.size();
+            tk.push_back(vocab().not_);
+            for (int s = dtw_seg0; s < dtw_seg0 + n_segments; ++s)
+                for (const auto & t : result_all[s].tokens)
+                    if (t.id < eot) tk.push_back(t.id);
+            tk.push_back(eot);
+            st->kv.clear();
+            rows.clear();
+            for (int k = 0; k < (int) tk.size(); ++k) rows.push_back(CallToken{tk[k], k, 0, k == (int) tk.size() - 1});
+            phase = Phase::WAIT_DTW;
+            return;
+        }
+        emit_tail(seek_delta);
+    }
+
+    void emit_tail(int seek_delta) {
+        const auto & toks = st->decoders[best_decoder_id].sequence.tokens;
+        const int beg = vocab().beg;
         const bool single_ts_ending = toks.size() > 1 && toks[toks.size() - 2].id < beg && toks[toks.size() - 1].id > beg;
         if (single_ts_ending) seek_delta = std::min(seek_end - seek, WHISPER_CHUNK_SIZE * 100);
         seek += seek_delta;
         phase = Phase::WINDOW;
+    }
+
+    // captured alignment-head attention of the DTW call: [head][n_audio_ctx][rows]
+    void on_dtw(const std::vector<float> & cap, int n_ah) {
+        const int n_frames = std::min(std::min(WHISPER_CHUNK_SIZE * 100, dtw_seek_delta), seek_end - seek);
+        dtw_timestamps(ctx, st, dtw_seg0, dtw_nseg, seek, n_frames, 7, cap, n_ah, hp().n_audio_ctx, (int) rows.size(),
+                       dtw_sot_len);
+        if (p.new_segment_callback) {  // the reference's loop bounds, verbatim (ref 7750-7754)
+            for (int seg = (int) st->result_all.size() - dtw_nseg; seg < dtw_nseg; seg++)
+                p.new_segment_callback(ctx, st, seg, p.new_segment_callback_user_data);
+        }
+        emit_tail(dtw_seek_delta);
     }
 };
 
@@ -747,8 +796,9 @@ int prepare_decode_call(whisper_state * st, int slot, const std::vector<CallToke
     if (cell0 < 0) return -1;
     st->kv.n = std::min<uint32_t>(st->kv.size, std::max<int32_t>(1, st->kv.cell_max()));
     // reference flash-attention path choice per ggml_flash_attn_ext call (ops.cpp:8624-8628)
-    const int mode_self = (nt >= 32 && st->kv.n % 16 == 0) ? 1 : 0;
-    const int mode_cross = nt >= 32 ? 1 : 0;
+    // (flash_attn = false contexts: the soft_max path for both, whisper.cpp:2614-2628, 2697-2738)
+    const int mode_self = !st->flash_attn ? 2 : (nt >= 32 && st->kv.n % 16 == 0) ? 1 : 0;
+    const int mode_cross = !st->flash_attn ? 2 : nt >= 32 ? 1 : 0;
     for (int r = 0; r < nt; ++r) {
         DecodeRow x;
         x.slot = slot;
@@ -782,6 +832,7 @@ int full_batch(whisper_context * ctx, whisper_state ** states, const whisper_ful
     OWK_HIP_CHECK(hipSetDevice(M.device));
     whisper_state * st0 = states[0];
     if (!st0->eng) st0->eng.reset(new Engine(&M, &ctx->prof));
+    configure_engine(ctx, st0);
     Engine & eng = *st0->eng;
 
     // capacity: one slot per clip; self-KV cells for the largest decoder count
@@ -875,7 +926,9 @@ int full_batch(whisper_context * ctx, whisper_state ** states, const whisper_ful
             c->t_req = time_us();
         }
         const int64_t t0 = time_us();
-        eng.decode(rows, keys, n_logit);
+        bool capture = false;
+        for (Clip * c : dec) capture = capture || c->phase == Phase::WAIT_DTW;
+        eng.decode(rows, keys, n_logit, capture);
 
         // state->logits emulation (no-speech probability after each prefill, ref 7185-7195):
         // the reference resizes state->logits to the call's rows and overwrites only rows
@@ -910,7 +963,7 @@ int full_batch(whisper_context * ctx, whisper_state ** states, const whisper_ful
             Clip * c = dec[ci];
             if (c->done()) continue;
             const Span & sp = spans[ci];
-            if (c->phase == Phase::LANG_WAIT_DEC) continue;  // handled on host below
+            if (c->phase == Phase::LANG_WAIT_DEC || c->phase == Phase::WAIT_DTW) continue;  // handled below
             whisper_state * st = c->st;
             auto add_job = [&](int j, int lrow, bool nosp) {
                 const Decoder & d = st->decoders[j];
@@ -1011,6 +1064,12 @@ int full_batch(whisper_context * ctx, whisper_state ** states, const whisper_ful
                         c->p.language, lid[0].first);
                 if (c->p.detect_language) { c->phase = Phase::DONE; continue; }
                 c->start_after_lang();
+                continue;
+            }
+            if (c->phase == Phase::WAIT_DTW) {
+                std::vector<float> cap;
+                eng.download_capture(spans[ci].row0, nt, cap);
+                c->on_dtw(cap, eng.n_aheads());
                 continue;
             }
             if (c->phase == Phase::WAIT_PREFILL) c->on_prefill();

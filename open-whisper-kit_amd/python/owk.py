@@ -211,11 +211,17 @@ def fptr(a: np.ndarray):
 class Whisper:
     """Thin owner of a whisper_context (and its default state)."""
 
-    def __init__(self, model_path: str, device: int = 0, flash_attn: bool = True):
+    def __init__(self, model_path: str, device: int = 0, flash_attn: bool = True, dtw_preset: int = 0,
+                 dtw_n_top: int = -1):
         self.L = load()
         cp = self.L.whisper_context_default_params()
         cp.gpu_device = device
         cp.flash_attn = flash_attn
+        if dtw_preset > 0:
+            cp.dtw_token_timestamps = True
+            cp.dtw_aheads_preset = dtw_preset
+            cp.dtw_n_top = dtw_n_top
+        self.dtw = dtw_preset > 0
         self.ctx = self.L.whisper_init_from_file_with_params(model_path.encode(), cp)
         if not self.ctx:
             raise RuntimeError(f"whisper_init_from_file_with_params failed for {model_path}")
@@ -300,7 +306,7 @@ class Whisper:
             toks = []
             for j in range(L.whisper_full_n_tokens_from_state(state, i)):
                 t = L.whisper_full_get_token_data_from_state(state, i, j)
-                toks.append((t.id, t.tid, t.p, t.plog, t.pt, t.ptsum, t.t0, t.t1))
+                toks.append((t.id, t.tid, t.p, t.plog, t.pt, t.ptsum, t.t0, t.t1) + ((t.t_dtw,) if self.dtw else ()))
             out.append(dict(t0=L.whisper_full_get_segment_t0_from_state(state, i),
                             t1=L.whisper_full_get_segment_t1_from_state(state, i),
                             text=L.whisper_full_get_segment_text_from_state(state, i).decode("utf-8", "replace"),

@@ -50,6 +50,8 @@ static std::vector<float> g_rec_val;
 static bool               g_rec_suppress_eot = false;
 static std::mutex         g_rec_mtx;  // whisper_full runs process_logits of the decoders on worker threads
 
+static bool g_rec_trace_only = false;  // record_topk == 2: record the prefixes, leave the logits alone
+
 static void ref_record_cb(struct whisper_context * ctx, struct whisper_state * /*state*/,
                           const whisper_token_data * tokens, int n_tokens, float * logits, void * /*user_data*/) {
     const int n_vocab = whisper_n_vocab(ctx), eot = whisper_token_eot(ctx), beg = whisper_token_beg(ctx);
@@ -78,6 +80,7 @@ static void ref_record_cb(struct whisper_context * ctx, struct whisper_state * /
             g_rec_val.push_back(id >= 0 ? logits[id] : -INFINITY);
         }
     }
+    if (g_rec_trace_only) return;
     std::vector<float> kept(keep.size());
     for (size_t j = 0; j < keep.size(); ++j) kept[j] = logits[keep[j]];
     for (int i = 0; i < n_vocab; ++i) logits[i] = -INFINITY;
@@ -115,6 +118,20 @@ void * ref_init(const char * path, int flash_attn, int dtw_preset) {
     if (dtw_preset > 0) {
         cp.dtw_token_timestamps = true;
         cp.dtw_aheads_preset    = (whisper_alignment_heads_preset) dtw_preset;
+    }
+    return whisper_init_from_file_with_params(path, cp);
+}
+
+// as ref_init with the N_TOP_MOST preset's layer count (whisper_context_params.dtw_n_top)
+void * ref_init_ex(const char * path, int flash_attn, int dtw_preset, int dtw_n_top) {
+    whisper_log_set([](ggml_log_level, const char *, void *) {}, nullptr);
+    auto cp = whisper_context_default_params();
+    cp.use_gpu    = false;
+    cp.flash_attn = flash_attn != 0;
+    if (dtw_preset > 0) {
+        cp.dtw_token_timestamps = true;
+        cp.dtw_aheads_preset    = (whisper_alignment_heads_preset) dtw_preset;
+        cp.dtw_n_top            = dtw_n_top;
     }
     return whisper_init_from_file_with_params(path, cp);
 }
@@ -212,10 +229,25 @@ int ref_full(void * vctx, const float * pcm, int n, const ref_full_cfg * cfg) {
     g_rec_prefix.clear(); g_rec_off.clear(); g_rec_idx.clear(); g_rec_val.clear();
     if (cfg->record_topk) {
         g_rec_suppress_eot = cfg->suppress_eot != 0;
+        g_rec_trace_only = cfg->record_topk == 2;
         p.logits_filter_callback = ref_record_cb;
     }
     return whisper_full(ctx, p, pcm, n);
 }
+
+// the alignment-head attention of the last DTW re-decode (state->aheads_cross_QKs_data,
+// whisper.cpp:8910-8912): [head][n_audio_ctx][n_tokens] floats; returns the count
+long ref_dtw_data(void * vctx, float * out, long cap) {
+    const auto & d = ((whisper_context *) vctx)->state->aheads_cross_QKs_data;
+    if (out) {
+        if (cap < (long) d.size()) return -1;
+        std::copy(d.begin(), d.end(), out);
+    }
+    return (long) d.size();
+}
+
+// decoders[j].seek_delta after whisper_full (greedy t = 0: the last window's best decoder)
+int ref_decoder_seek_delta(void * vctx, int j) { return ((whisper_context *) vctx)->state->decoders[j].seek_delta; }
 
 // state counters for the CPU-baseline breakdown (whisper.cpp:835-848)
 void ref_timings(void * vctx, double * t_mel_ms, double * t_enc_ms, double * t_dec_ms,

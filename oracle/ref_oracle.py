@@ -46,6 +46,11 @@ def lib():
         vp, ip, fp = C.c_void_p, C.c_int, C.POINTER(C.c_float)
         L.ref_init.restype = vp
         L.ref_init.argtypes = [C.c_char_p, ip, ip]
+        L.ref_decoder_seek_delta.argtypes = [vp, ip]
+        L.ref_dtw_data.restype = C.c_long
+        L.ref_dtw_data.argtypes = [vp, fp, C.c_long]
+        L.ref_init_ex.restype = vp
+        L.ref_init_ex.argtypes = [C.c_char_p, ip, ip, ip]
         L.ref_free.argtypes = [vp]
         L.ref_mel.argtypes = [vp, fp, ip, ip, fp, ip, C.POINTER(ip), C.POINTER(ip), C.POINTER(ip)]
         L.ref_encode.argtypes = [vp, ip, ip]
@@ -82,12 +87,13 @@ def fptr(a):
 
 
 class Ref:
-    def __init__(self, model_path: str, flash_attn: bool = True):
+    def __init__(self, model_path: str, flash_attn: bool = True, dtw_preset: int = 0, dtw_n_top: int = -1):
         self.L = lib()
-        self.ctx = self.L.ref_init(model_path.encode(), 1 if flash_attn else 0, 0)
+        self.ctx = self.L.ref_init_ex(model_path.encode(), 1 if flash_attn else 0, dtw_preset, dtw_n_top)
         if not self.ctx:
             raise RuntimeError("reference init failed")
         self.n_vocab = self.L.whisper_n_vocab(self.ctx)
+        self.dtw = dtw_preset > 0
 
     def close(self):
         if self.ctx:
@@ -132,7 +138,14 @@ class Ref:
                          int(record_topk))
         pcm = np.ascontiguousarray(pcm, np.float32)
         ret = self.L.ref_full(self.ctx, fptr(pcm), len(pcm), C.byref(cfg))
-        return ret, self.segments()
+        return ret, self.segments(dtw=self.dtw)
+
+    def dtw_data(self):
+        """Alignment-head attention of the last DTW re-decode, flat [head][n_audio_ctx][n_tok]."""
+        n = self.L.ref_dtw_data(self.ctx, None, 0)
+        out = np.zeros(n, np.float32)
+        self.L.ref_dtw_data(self.ctx, fptr(out), n)
+        return out
 
     def recorded(self):
         """Logit entries recorded by the last full(record_topk=True): (off, prefix, idx, val)."""
@@ -148,14 +161,14 @@ class Ref:
         self.L.ref_record_get(P(off), P(prefix), P(idx), fptr(val), C.byref(w))
         return off, prefix[:plen], idx.reshape(n, w.value), val.reshape(n, w.value)
 
-    def segments(self):
+    def segments(self, dtw=False):
         L = self.L
         out = []
         for i in range(L.whisper_full_n_segments(self.ctx)):
             toks = []
             for j in range(L.whisper_full_n_tokens(self.ctx, i)):
                 t = L.whisper_full_get_token_data(self.ctx, i, j)
-                toks.append((t.id, t.tid, t.p, t.plog, t.pt, t.ptsum, t.t0, t.t1))
+                toks.append((t.id, t.tid, t.p, t.plog, t.pt, t.ptsum, t.t0, t.t1) + ((t.t_dtw,) if dtw else ()))
             out.append(dict(t0=L.whisper_full_get_segment_t0(self.ctx, i), t1=L.whisper_full_get_segment_t1(self.ctx, i),
                             text=L.whisper_full_get_segment_text(self.ctx, i).decode("utf-8", "replace"),
                             no_speech_prob=L.whisper_full_get_segment_no_speech_prob(self.ctx, i), tokens=toks))
