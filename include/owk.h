@@ -65,6 +65,10 @@ WHISPER_API int owk_debug_dtw(const float * cap, int n_ah, int n_audio_ctx, int 
 /* test hook: alignment-head probabilities captured by the state's last DTW re-decode,
  * [head][n_audio_ctx][rows of that pass]; returns the float count (copies when out != NULL) */
 WHISPER_API long owk_debug_capture(struct whisper_state * state, float * out, long cap);
+/* test hook: out[M][N] = Q8_0(a) . Q5_0(w)^T through the engine's quantize + Q5 GEMM; a f32 [M][K],
+ * w_blocks ggml block_q5_0 rows [N][K/32]; q_out / d_out (optional) receive the Q8_0 activations */
+WHISPER_API int owk_debug_gemm_q5(int device, int M, int N, int K, const float * a, const uint8_t * w_blocks, float * out,
+                                  int8_t * q_out, float * d_out);
 WHISPER_API double owk_debug_gemm_bench(int device, int mode, int M, int N, int K, int iters);
 
 /* library identity: 1 when the gfx950 HIP code object is present and a device is usable */

@@ -177,6 +177,24 @@ void Engine::download_mel(int slot, float * host) const {
 
 static double gemm_flops(double M, double N, double K) { return 2.0 * M * N * K; }
 
+void Engine::linear(const char * cls, int mode, int M, int N, int K, const _Float16 * A16, const float * A32, int lda,
+                    const _Float16 * W, const Q5W & q, const EpiParams & ep, const _Float16 * Wt, bool dec) {
+    if (!q) {
+        ProfScope ps(prof, stream, cls, gemm_flops(M, N, K), 2.0 * ((double) M * K + (double) N * K));
+        if (dec) gemm(stream, mode, M, N, K, A16, lda, W, K, ep, &gws_, Wt);
+        else gemm_f16(stream, mode, M, N, K, A16, lda, W, K, ep);
+        return;
+    }
+    // the reference rounds each activation row to Q8_0 (x86 quantize_row_q8_0) before the
+    // q5_0 x q8_0 dot; bytes: Q5_0 weights at 22 B per 32 + the int8 activations
+    {
+        ProfScope ps(prof, stream, "quantize_q8");
+        quantize_q8(stream, A32, A16, lda, M, K, q8a_.as<int8_t>(), q8d_.as<float>());
+    }
+    ProfScope ps(prof, stream, cls, gemm_flops(M, N, K), (double) N * K * 22.0 / 32.0 + (double) M * K);
+    gemm_q5(stream, mode, M, N, K, q8a_.as<int8_t>(), q8d_.as<float>(), q, ep);
+}
+
 void Engine::encode(const std::vector<int> & slots, const std::vector<int> & offsets) {
     const HParams & hp = m->hp;
     const int n = (int) slots.size();
@@ -204,6 +222,12 @@ void Engine::encode(const std::vector<int> & slots, const std::vector<int> & off
         e_h_.alloc((size_t) M * 4 * d * 2);
         e_enc_.alloc((size_t) M * d * 2);
         e_enc32_.alloc((size_t) M * d * 4);
+        if (m->q5) {
+            e_xn32_.alloc((size_t) M * d * 4);
+            e_ao32_.alloc((size_t) M * d * 4);
+            q8a_.alloc(std::max(q8a_.bytes, (size_t) M * 4 * d));
+            q8d_.alloc(std::max(q8d_.bytes, (size_t) M * 4 * d / 32 * 4));
+        }
     }
     e_a1_.alloc((size_t) n * T2 * kp1 * 2);
 
@@ -253,7 +277,8 @@ void Engine::encode(const std::vector<int> & slots, const std::vector<int> & off
         const EncLayerW & L = m->enc[l];
         {
             ProfScope ps(prof, stream, "layernorm");
-            layernorm_f16(stream, e_x_.as<float>(), M, d, L.attn_ln_w, L.attn_ln_b, hp.eps, e_xn_.as<_Float16>(), d);
+            layernorm_f16(stream, e_x_.as<float>(), M, d, L.attn_ln_w, L.attn_ln_b, hp.eps, e_xn_.as<_Float16>(), d,
+                          nullptr, m->q5 ? e_xn32_.as<float>() : nullptr);
         }
         {
             EpiParams ep;
@@ -265,7 +290,7 @@ void Engine::encode(const std::vector<int> & slots, const std::vector<int> & off
             ep.d = d;
             ep.T = T;
             ep.Tpad = Tpad;
-            G("gemm_enc", EPI_QKV_ENC, M, 3 * d, d, e_xn_.as<_Float16>(), d, L.w_qkv, ep);
+            linear("gemm_enc", EPI_QKV_ENC, M, 3 * d, d, e_xn_.as<_Float16>(), e_xn32_.as<float>(), d, L.w_qkv, L.q_qkv, ep);
         }
         {
             // 4*T*Tpad_kv*d flops (QK^T and PV over the 1536 reference keys)
@@ -273,10 +298,10 @@ void Engine::encode(const std::vector<int> & slots, const std::vector<int> & off
                          2.0 * 4.0 * M * (double) d);
             if (flash_attn)
                 attn_encoder(stream, e_q_.as<_Float16>(), e_k_.as<_Float16>(), e_vt_.as<_Float16>(), n, T, Tpad, H,
-                             kq_scale, n_zero_pad, e_ao_.as<_Float16>());
+                             kq_scale, n_zero_pad, e_ao_.as<_Float16>(), m->q5 ? e_ao32_.as<float>() : nullptr);
             else  // soft_max path over exactly T keys (whisper.cpp:2163-2189)
                 attn_encoder_softmax(stream, e_q_.as<_Float16>(), e_k_.as<_Float16>(), e_vt_.as<_Float16>(), n, T, Tpad,
-                                     H, kq_scale, e_ao_.as<_Float16>());
+                                     H, kq_scale, e_ao_.as<_Float16>(), m->q5 ? e_ao32_.as<float>() : nullptr);
         }
         {
             EpiParams ep;
@@ -284,11 +309,12 @@ void Engine::encode(const std::vector<int> & slots, const std::vector<int> & off
             ep.resid = e_x_.as<float>();
             ep.out32 = e_x_.as<float>();
             ep.ldo = d;
-            G("gemm_enc", EPI_RESID_F32, M, d, d, e_ao_.as<_Float16>(), d, L.w_o, ep);
+            linear("gemm_enc", EPI_RESID_F32, M, d, d, e_ao_.as<_Float16>(), e_ao32_.as<float>(), d, L.w_o, L.q_o, ep);
         }
         {
             ProfScope ps(prof, stream, "layernorm");
-            layernorm_f16(stream, e_x_.as<float>(), M, d, L.mlp_ln_w, L.mlp_ln_b, hp.eps, e_xn_.as<_Float16>(), d);
+            layernorm_f16(stream, e_x_.as<float>(), M, d, L.mlp_ln_w, L.mlp_ln_b, hp.eps, e_xn_.as<_Float16>(), d,
+                          nullptr, m->q5 ? e_xn32_.as<float>() : nullptr);
         }
         {
             EpiParams ep;
@@ -296,7 +322,8 @@ void Engine::encode(const std::vector<int> & slots, const std::vector<int> & off
             ep.gelu_tab = m->gelu_tab;
             ep.out16 = e_h_.as<_Float16>();
             ep.ldo = 4 * d;
-            G("gemm_enc", EPI_GELU_F16, M, 4 * d, d, e_xn_.as<_Float16>(), d, L.w_mlp0, ep);
+            linear("gemm_enc", EPI_GELU_F16, M, 4 * d, d, e_xn_.as<_Float16>(), e_xn32_.as<float>(), d, L.w_mlp0, L.q_mlp0,
+                   ep);
         }
         {
             EpiParams ep;
@@ -304,7 +331,8 @@ void Engine::encode(const std::vector<int> & slots, const std::vector<int> & off
             ep.resid = e_x_.as<float>();
             ep.out32 = e_x_.as<float>();
             ep.ldo = d;
-            G("gemm_enc", EPI_RESID_F32, M, d, 4 * d, e_h_.as<_Float16>(), 4 * d, L.w_mlp1, ep);
+            // GELU outputs are F16 table values: exact as the f32 tensor the reference quantizes
+            linear("gemm_enc", EPI_RESID_F32, M, d, 4 * d, e_h_.as<_Float16>(), nullptr, 4 * d, L.w_mlp1, L.q_mlp1, ep);
         }
     }
     {
@@ -327,7 +355,8 @@ void Engine::encode(const std::vector<int> & slots, const std::vector<int> & off
         ep.d = d;
         ep.T = T;
         ep.slot_map = e_slotmap_.as<int>();
-        G("gemm_cross", EPI_KV_CROSS, M, 2 * d, d, e_enc_.as<_Float16>(), d, L.cw_kv, ep);
+        linear("gemm_cross", EPI_KV_CROSS, M, 2 * d, d, e_enc_.as<_Float16>(), m->q5 ? e_enc32_.as<float>() : nullptr, d,
+               L.cw_kv, L.q_ckv, ep);
     }
 }
 
@@ -374,6 +403,7 @@ void Engine::clear_graphs() {
 uint64_t Engine::buffers_signature() const {
     uint64_t h = 1469598103934665603ull;
     for (const void * p : {d_x_.ptr, d_xn_.ptr, d_q_.ptr, d_ao_.ptr, d_h_.ptr, d_xl_.ptr, logits_.ptr, d_stg_.ptr,
+                           q8a_.ptr, q8d_.ptr, d_xn32_.ptr, d_ao32_.ptr, d_xl32_.ptr,
                            self_k_.ptr, self_v_.ptr, cross_k_.ptr, cross_v_.ptr, gws_part_.ptr})
         h = (h ^ (uint64_t) (uintptr_t) p) * 1099511628211ull;
     return h;
@@ -419,6 +449,13 @@ void Engine::decode(const std::vector<DecodeRow> & rows, const std::vector<int> 
             d_ao_.alloc((size_t) C * d * 2);
             d_h_.alloc((size_t) C * 4 * d * 2);
             d_xl_.alloc((size_t) C * d * 2);
+            if (m->q5) {
+                d_xn32_.alloc((size_t) C * d * 4);
+                d_ao32_.alloc((size_t) C * d * 4);
+                d_xl32_.alloc((size_t) C * d * 4);
+                q8a_.alloc(std::max(q8a_.bytes, (size_t) C * 4 * d));
+                q8d_.alloc(std::max(q8d_.bytes, (size_t) C * 4 * d / 32 * 4));
+            }
             logits_.alloc((size_t) C * nv * 4);
         }
         dec_keys_cap_ = std::max(nk, std::max(dec_keys_cap_ * 2, 4096));
@@ -532,17 +569,20 @@ void Engine::launch_decode(const DecShape & sh) {
     const int max_keys = sh.max_keys;
     const bool self_oc = sh.self_oc, self_tl = sh.self_tl, cross_oc = sh.cross_oc, cross_tl = sh.cross_tl;
 
-    auto G = [&](const char * cls, int mode, int N, int K, const _Float16 * A, const _Float16 * W, const _Float16 * Wt,
-                 const EpiParams & ep, int Mr) {
-        ProfScope ps(prof, stream, Mr <= 64 ? "gemm_dec" : "gemm_dec_big", gemm_flops(Mr, N, K),
-                     2.0 * ((double) Mr * K + (double) N * K));
+    const bool q5 = m->q5;
+    // A32: the f32 activation a Q5_0 GEMM quantizes (null: the f16 A is exact, e.g. GELU output)
+    auto G = [&](const char * cls, int mode, int N, int K, const _Float16 * A, const float * A32, const _Float16 * W,
+                 const _Float16 * Wt, const Q5W & q, const EpiParams & ep, int Mr) {
         (void) cls;
-        gemm(stream, mode, Mr, N, K, A, K, W, K, ep, &gws_, Wt);
+        linear(Mr <= 64 ? "gemm_dec" : "gemm_dec_big", mode, Mr, N, K, A, A32, K, W, q, ep, Wt, true);
     };
+    float * xn32 = q5 ? d_xn32_.as<float>() : nullptr;
+    float * ao32 = q5 ? d_ao32_.as<float>() : nullptr;
 
     {
         ProfScope ps(prof, stream, "embed");
-        embed_tokens(stream, m->d_te, m->d_pe, d_tok, d_pos, R, d, d_x_.as<float>());
+        if (q5) embed_tokens_q5(stream, m->q_te, m->d_pe, d_tok, d_pos, R, d, d_x_.as<float>());
+        else embed_tokens(stream, m->d_te, m->d_pe, d_tok, d_pos, R, d, d_x_.as<float>());
     }
     const float kq_scale = powf(64.0f, -0.25f);
     const size_t self_stride = (size_t) cap_slots * kv_cells * d;
@@ -550,27 +590,28 @@ void Engine::launch_decode(const DecShape & sh) {
     // R <= 32 rows: the residual matmuls (attn.out, cross_attn.out, mlp.2) emit partial tiles
     // that one fused kernel finishes together with the following LayerNorm (3 launches
     // fewer per layer); larger passes use the full-epilogue GEMMs and separate LayerNorms
-    const bool fused = R <= 32;
+    const bool fused = R <= 32 && !q5;
     float * part = gws_.partial;
     auto resid_ln = [&](const _Float16 * A, const _Float16 * W, const _Float16 * Wt, int K, const float * bias,
                         const float * lnw, const float * lnb) {
         EpiParams ep;
-        G("part", EPI_PARTIAL, d, K, A, W, Wt, ep, R);
+        G("part", EPI_PARTIAL, d, K, A, nullptr, W, Wt, Q5W(), ep, R);
         ProfScope ps(prof, stream, "layernorm");
         resid_layernorm(stream, R, d, gemm_partial_splits(K), part, bias, d_x_.as<float>(), lnw, lnb, hp.eps,
                         d_xn_.as<_Float16>(), d);
     };
-    auto resid_full = [&](const _Float16 * A, const _Float16 * W, const _Float16 * Wt, int K, const float * bias) {
+    auto resid_full = [&](const _Float16 * A, const float * A32, const _Float16 * W, const _Float16 * Wt,
+                          const Q5W & q, int K, const float * bias) {
         EpiParams ep;
         ep.bias = bias;
         ep.resid = d_x_.as<float>();
         ep.out32 = d_x_.as<float>();
         ep.ldo = d;
-        G("resid", EPI_RESID_F32, d, K, A, W, Wt, ep, R);
+        G("resid", EPI_RESID_F32, d, K, A, A32, W, Wt, q, ep, R);
     };
     auto ln = [&](const float * w, const float * b) {
         ProfScope ps(prof, stream, "layernorm");
-        layernorm_f16(stream, d_x_.as<float>(), R, d, w, b, hp.eps, d_xn_.as<_Float16>(), d);
+        layernorm_f16(stream, d_x_.as<float>(), R, d, w, b, hp.eps, d_xn_.as<_Float16>(), d, nullptr, xn32);
     };
     for (int l = 0; l < hp.n_text_layer; ++l) {
         const DecLayerW & L = m->dec[l];
@@ -588,20 +629,20 @@ void Engine::launch_decode(const DecShape & sh) {
             ep.out16c = Vl;
             ep.d = d;
             ep.row_off = d_rowoff;
-            G("qkv", EPI_QKV_DEC, 3 * d, d, d_xn_.as<_Float16>(), L.w_qkv, L.t_qkv, ep, R);
+            G("qkv", EPI_QKV_DEC, 3 * d, d, d_xn_.as<_Float16>(), xn32, L.w_qkv, L.t_qkv, L.q_qkv, ep, R);
         }
         {
             ProfScope ps(prof, stream, "attn_self");
             attn_decoder(stream, d_q_.as<_Float16>(), d, Kl, Vl, d, d_rs, R, d_keys, H,
-                         1.0f, max_keys, d_ao_.as<_Float16>(), d, self_oc, self_tl);
+                         1.0f, max_keys, d_ao_.as<_Float16>(), d, self_oc, self_tl, ao32);
             if (sh.self_sm)  // masked soft_max with scale 1 (Q, K pre-scaled; whisper.cpp:2614-2628)
                 attn_decoder_softmax(stream, d_q_.as<_Float16>(), d, Kl, Vl, d, d_rs, R, d_keys, H, 1.0f, max_keys,
-                                     d_ao_.as<_Float16>(), d, nullptr, nullptr, 0);
+                                     d_ao_.as<_Float16>(), d, nullptr, nullptr, 0, ao32);
         }
         if (fused) {
             resid_ln(d_ao_.as<_Float16>(), L.w_o, L.t_o, d, L.b_o, L.cross_ln_w, L.cross_ln_b);
         } else {
-            resid_full(d_ao_.as<_Float16>(), L.w_o, L.t_o, d, L.b_o);
+            resid_full(d_ao_.as<_Float16>(), ao32, L.w_o, L.t_o, L.q_o, d, L.b_o);
             ln(L.cross_ln_w, L.cross_ln_b);
         }
         {
@@ -609,24 +650,24 @@ void Engine::launch_decode(const DecShape & sh) {
             ep.bias = L.cb_q;
             ep.out16 = d_q_.as<_Float16>();
             ep.ldo = d;
-            G("cq", EPI_F16, d, d, d_xn_.as<_Float16>(), L.cw_q, L.t_cq, ep, R);
+            G("cq", EPI_F16, d, d, d_xn_.as<_Float16>(), xn32, L.cw_q, L.t_cq, L.q_cq, ep, R);
         }
         {
             // bytes: cross K and V of each row's clip (the HBM-bound part of a decode step)
             ProfScope ps(prof, stream, "attn_cross", 4.0 * R * (double) n_ctx_pad * d, 2.0 * 2.0 * R * (double) T * d);
             attn_decoder(stream, d_q_.as<_Float16>(), d, cross_k_.as<_Float16>() + l * cross_stride,
                          cross_v_.as<_Float16>() + l * cross_stride, d, d_rc, R, nullptr, H,
-                         kq_scale, T, d_ao_.as<_Float16>(), d, cross_oc, cross_tl);
+                         kq_scale, T, d_ao_.as<_Float16>(), d, cross_oc, cross_tl, ao32);
             if (sh.cross_sm)  // soft_max_ext(KQ, nullptr, KQscale) over n_audio_ctx keys (whisper.cpp:2697-2738)
                 attn_decoder_softmax(stream, d_q_.as<_Float16>(), d, cross_k_.as<_Float16>() + l * cross_stride,
                                      cross_v_.as<_Float16>() + l * cross_stride, d, d_rc, R, nullptr, H, kq_scale, T,
                                      d_ao_.as<_Float16>(), d, sh.capture ? amap_.as<int>() + l * H : nullptr,
-                                     sh.capture ? cap_.as<float>() : nullptr, R);
+                                     sh.capture ? cap_.as<float>() : nullptr, R, ao32);
         }
         if (fused) {
             resid_ln(d_ao_.as<_Float16>(), L.cw_o, L.t_co, d, L.cb_o, L.mlp_ln_w, L.mlp_ln_b);
         } else {
-            resid_full(d_ao_.as<_Float16>(), L.cw_o, L.t_co, d, L.cb_o);
+            resid_full(d_ao_.as<_Float16>(), ao32, L.cw_o, L.t_co, L.q_co, d, L.cb_o);
             ln(L.mlp_ln_w, L.mlp_ln_b);
         }
         {
@@ -635,7 +676,7 @@ void Engine::launch_decode(const DecShape & sh) {
             ep.gelu_tab = m->gelu_tab;
             ep.out16 = d_h_.as<_Float16>();
             ep.ldo = 4 * d;
-            G("mlp0", EPI_GELU_F16, 4 * d, d, d_xn_.as<_Float16>(), L.w_mlp0, L.t_mlp0, ep, R);
+            G("mlp0", EPI_GELU_F16, 4 * d, d, d_xn_.as<_Float16>(), xn32, L.w_mlp0, L.t_mlp0, L.q_mlp0, ep, R);
         }
         if (fused) {
             const bool last = l + 1 == hp.n_text_layer;
@@ -643,21 +684,20 @@ void Engine::launch_decode(const DecShape & sh) {
             resid_ln(d_h_.as<_Float16>(), L.w_mlp1, L.t_mlp1, 4 * d, L.b_mlp1, nx ? nx->attn_ln_w : nullptr,
                      nx ? nx->attn_ln_b : nullptr);
         } else {
-            resid_full(d_h_.as<_Float16>(), L.w_mlp1, L.t_mlp1, 4 * d, L.b_mlp1);
+            resid_full(d_h_.as<_Float16>(), nullptr, L.w_mlp1, L.t_mlp1, L.q_mlp1, 4 * d, L.b_mlp1);
         }
     }
     if (n_logit_rows > 0) {
         {
             ProfScope ps(prof, stream, "layernorm");
             layernorm_f16(stream, d_x_.as<float>(), n_logit_rows, d, m->d_ln_w, m->d_ln_b, hp.eps, d_xl_.as<_Float16>(),
-                          d, d_lsel);
+                          d, d_lsel, q5 ? d_xl32_.as<float>() : nullptr);
         }
         EpiParams ep;
         ep.out32 = logits_.as<float>();
         ep.ldo = nv;
-        ProfScope ps(prof, stream, n_logit_rows <= 64 ? "gemm_logits" : "gemm_logits_big",
-                     gemm_flops(n_logit_rows, nv, d), 2.0 * (double) nv * d);
-        gemm(stream, EPI_F32, n_logit_rows, nv, d, d_xl_.as<_Float16>(), d, m->d_te, d, ep, &gws_, m->d_te_t);
+        linear(n_logit_rows <= 64 ? "gemm_logits" : "gemm_logits_big", EPI_F32, n_logit_rows, nv, d,
+               d_xl_.as<_Float16>(), q5 ? d_xl32_.as<float>() : nullptr, d, m->d_te, m->q_te, ep, m->d_te_t, true);
     }
 }
 

@@ -164,6 +164,13 @@ private:
     std::map<uint64_t, hipGraphExec_t> graphs_;
     uint64_t graphs_sig_ = 0;
 
+    // Q5_0 models: f32 activations feeding the quantized GEMMs and their Q8_0 copy
+    void linear(const char * cls, int mode, int M, int N, int K, const _Float16 * A16, const float * A32, int lda,
+                const _Float16 * W, const Q5W & q, const EpiParams & ep, const _Float16 * Wt = nullptr,
+                bool dec = false);
+    DevBuf q8a_, q8d_;
+    DevBuf e_xn32_, e_ao32_, d_xn32_, d_ao32_, d_xl32_;
+
     DevBuf amap_, cap_;  // DTW: head map [L][H], captured probabilities [n_ah][T][cap_rows_]
     int n_ah_ = 0, cap_rows_ = 0;
 

@@ -32,7 +32,8 @@ constexpr int FA_TILE_BYTES = FA_KT * 64 * 2; // 8 KB (K tile or Vt tile)
 
 __global__ __launch_bounds__(256, 2) void k_attn_encoder(const _Float16 * __restrict__ q, const _Float16 * __restrict__ k,
                                                          const _Float16 * __restrict__ vt, int T, int Tpad, int H,
-                                                         float scale, int n_zero_pad, _Float16 * __restrict__ out) {
+                                                         float scale, int n_zero_pad, _Float16 * __restrict__ out,
+                                                         float * __restrict__ out32) {
     __shared__ __attribute__((aligned(1024))) char smem[4 * FA_TILE_BYTES];  // 2 stages x (K, Vt)
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int qt = blockIdx.x, h = blockIdx.y, clip = blockIdx.z;
@@ -157,13 +158,19 @@ __global__ __launch_bounds__(256, 2) void k_attn_encoder(const _Float16 * __rest
     }
     if (qi < T) {
         const float inv = lsum == 0.0f ? 0.0f : 1.0f / lsum;
-        _Float16 * orow = out + ((size_t) clip * T + qi) * d + h * 64;
+        const size_t ro = ((size_t) clip * T + qi) * d + h * 64;
 #pragma unroll
         for (int dt = 0; dt < 4; ++dt) {
+            if (out32) {  // f32 output (Q5_0 models quantize it to Q8_0 themselves)
+                float4 r;
+                r.x = o[dt][0] * inv; r.y = o[dt][1] * inv; r.z = o[dt][2] * inv; r.w = o[dt][3] * inv;
+                *(float4 *) (out32 + ro + dt * 16 + 4 * g) = r;
+                continue;
+            }
             half4 r;
 #pragma unroll
             for (int e = 0; e < 4; ++e) r[e] = (_Float16) (o[dt][e] * inv);
-            *(half4 *) (orow + dt * 16 + 4 * g) = r;
+            *(half4 *) (out + ro + dt * 16 + 4 * g) = r;
         }
     }
 }
@@ -180,7 +187,8 @@ __global__ __launch_bounds__(256, 2) void k_attn_encoder(const _Float16 * __rest
 __global__ __launch_bounds__(256, 2) void k_attn_encoder_sm(const _Float16 * __restrict__ q,
                                                             const _Float16 * __restrict__ k,
                                                             const _Float16 * __restrict__ vt, int T, int Tpad, int H,
-                                                            float scale, _Float16 * __restrict__ out) {
+                                                            float scale, _Float16 * __restrict__ out,
+                                                            float * __restrict__ out32) {
     __shared__ __attribute__((aligned(1024))) char smem[4 * FA_TILE_BYTES];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int qt = blockIdx.x, h = blockIdx.y, clip = blockIdx.z;
@@ -305,29 +313,33 @@ __global__ __launch_bounds__(256, 2) void k_attn_encoder_sm(const _Float16 * __r
         __syncthreads();
     }
     if (qi < T) {
-        _Float16 * orow = out + ((size_t) clip * T + qi) * d + h * 64;
+        const size_t ro = ((size_t) clip * T + qi) * d + h * 64;
 #pragma unroll
         for (int dt = 0; dt < 4; ++dt) {
+            if (out32) {
+                *(float4 *) (out32 + ro + dt * 16 + 4 * g) = make_float4(o[dt][0], o[dt][1], o[dt][2], o[dt][3]);
+                continue;
+            }
             half4 r;
 #pragma unroll
             for (int e = 0; e < 4; ++e) r[e] = (_Float16) o[dt][e];
-            *(half4 *) (orow + dt * 16 + 4 * g) = r;
+            *(half4 *) (out + ro + dt * 16 + 4 * g) = r;
         }
     }
 }
 
 void attn_encoder_softmax(hipStream_t s, const _Float16 * q, const _Float16 * k, const _Float16 * vt, int n_clips, int T,
-                          int Tpad, int H, float scale, _Float16 * out) {
+                          int Tpad, int H, float scale, _Float16 * out, float * out32) {
     if (Tpad < ((T + FA_KT - 1) / FA_KT) * FA_KT) throw std::runtime_error("attn_encoder_softmax: Tpad too small");
     hipLaunchKernelGGL(k_attn_encoder_sm, dim3((T + 63) / 64, H, n_clips), dim3(256), 0, s, q, k, vt, T, Tpad, H, scale,
-                       out);
+                       out, out32);
 }
 
 void attn_encoder(hipStream_t s, const _Float16 * q, const _Float16 * k, const _Float16 * vt, int n_clips, int T,
-                  int Tpad, int H, float scale, int n_zero_pad, _Float16 * out) {
+                  int Tpad, int H, float scale, int n_zero_pad, _Float16 * out, float * out32) {
     if (Tpad < ((T + FA_KT - 1) / FA_KT) * FA_KT) throw std::runtime_error("attn_encoder: Tpad too small");
     hipLaunchKernelGGL(k_attn_encoder, dim3((T + 63) / 64, H, n_clips), dim3(256), 0, s, q, k, vt, T, Tpad, H, scale,
-                       n_zero_pad, out);
+                       n_zero_pad, out, out32);
 }
 
 // ----------------------------------------------------------------------------------
@@ -381,7 +393,7 @@ __global__ __launch_bounds__(64) void k_attn_step(const _Float16 * __restrict__ 
                                                   const _Float16 * __restrict__ kb, const _Float16 * __restrict__ vb,
                                                   int ld_kv, const AttnRow * __restrict__ rows,
                                                   const int * __restrict__ key_idx, float scale,
-                                                  _Float16 * __restrict__ out, int ldo) {
+                                                  _Float16 * __restrict__ out, int ldo, float * __restrict__ out32) {
     __shared__ __attribute__((aligned(1024))) char smem[AS_NBUF * 2 * AS_TILE];
     __shared__ int s_list[LIST ? AS_MAX_LIST : 1];
     const int lane = threadIdx.x;
@@ -390,7 +402,8 @@ __global__ __launch_bounds__(64) void k_attn_step(const _Float16 * __restrict__ 
     const int h = blockIdx.x;
     const int n = job.n_keys;
     if (n <= 0) {
-        out[(size_t) job.q_row * ldo + h * 64 + lane] = (_Float16) 0.0f;
+        if (out32) out32[(size_t) job.q_row * ldo + h * 64 + lane] = 0.0f;
+        else out[(size_t) job.q_row * ldo + h * 64 + lane] = (_Float16) 0.0f;
         return;
     }
     // a listed row whose cells are not one contiguous run (the host passes contiguous runs
@@ -513,7 +526,8 @@ __global__ __launch_bounds__(64) void k_attn_step(const _Float16 * __restrict__ 
         }
     }
     const float S_inv = S == 0.0f ? 0.0f : 1.0f / S;
-    out[(size_t) job.q_row * ldo + h * 64 + lane] = (_Float16) ((float) acc * S_inv);
+    if (out32) out32[(size_t) job.q_row * ldo + h * 64 + lane] = (float) acc * S_inv;
+    else out[(size_t) job.q_row * ldo + h * 64 + lane] = (_Float16) ((float) acc * S_inv);
 }
 
 // ----------------------------------------------------------------------------------
@@ -526,7 +540,7 @@ __global__ __launch_bounds__(256) void k_attn_decoder(const _Float16 * __restric
                                                       const _Float16 * __restrict__ kb, const _Float16 * __restrict__ vb,
                                                       int ld_kv, const AttnRow * __restrict__ rows,
                                                       const int * __restrict__ key_idx, int H, float scale,
-                                                      _Float16 * __restrict__ out, int ldo) {
+                                                      _Float16 * __restrict__ out, int ldo, float * __restrict__ out32) {
     __shared__ float sc[4][DA_MAX_KEYS];
     __shared__ _Float16 qs[4][64];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -624,7 +638,8 @@ __global__ __launch_bounds__(256) void k_attn_decoder(const _Float16 * __restric
         const float S_inv = S == 0.0f ? 0.0f : 1.0f / S;
         result = acc * S_inv;
     }
-    out[(size_t) job.q_row * ldo + h * 64 + lane] = (_Float16) result;
+    if (out32) out32[(size_t) job.q_row * ldo + h * 64 + lane] = result;
+    else out[(size_t) job.q_row * ldo + h * 64 + lane] = (_Float16) result;
 }
 
 // ----------------------------------------------------------------------------------
@@ -644,7 +659,7 @@ __global__ __launch_bounds__(256) void k_attn_softmax(const _Float16 * __restric
                                                       const int * __restrict__ key_idx, float scale,
                                                       _Float16 * __restrict__ out, int ldo,
                                                       const int * __restrict__ amap, float * __restrict__ cap,
-                                                      int cap_rows) {
+                                                      int cap_rows, float * __restrict__ out32) {
     __shared__ float sp[SM_MAX_KEYS];
     __shared__ _Float16 p16[SM_MAX_KEYS];
     __shared__ float redf[4];
@@ -715,17 +730,19 @@ __global__ __launch_bounds__(256) void k_attn_softmax(const _Float16 * __restric
     if (wave == 0) {
         const float * a4 = (const float *) acc4;
         const float r = (a4[lane] + a4[64 + lane]) + (a4[128 + lane] + a4[192 + lane]);
-        out[(size_t) job.q_row * ldo + h * 64 + lane] = (_Float16) r;
+        if (out32) out32[(size_t) job.q_row * ldo + h * 64 + lane] = r;
+        else out[(size_t) job.q_row * ldo + h * 64 + lane] = (_Float16) r;
     }
 }
 
 void attn_decoder_softmax(hipStream_t s, const _Float16 * q, int ldq, const _Float16 * kbase, const _Float16 * vbase,
                           int ld_kv, const AttnRow * rows_dev, int n_rows, const int * key_idx, int H, float scale,
-                          int max_keys, _Float16 * out, int ldo, const int * amap, float * cap, int cap_rows) {
+                          int max_keys, _Float16 * out, int ldo, const int * amap, float * cap, int cap_rows,
+                          float * out32) {
     if (n_rows <= 0) return;
     if (max_keys > SM_MAX_KEYS) throw std::runtime_error("attn_decoder_softmax: too many keys");
     hipLaunchKernelGGL(k_attn_softmax, dim3(H, n_rows), dim3(256), 0, s, q, ldq, kbase, vbase, ld_kv, rows_dev, key_idx,
-                       scale, out, ldo, amap, cap, cap_rows);
+                       scale, out, ldo, amap, cap, cap_rows, out32);
 }
 
 int attn_max_listed_keys() { return AS_MAX_LIST; }
@@ -733,22 +750,22 @@ int attn_max_tiled_keys() { return DA_MAX_KEYS; }
 
 void attn_decoder(hipStream_t s, const _Float16 * q, int ldq, const _Float16 * kbase, const _Float16 * vbase, int ld_kv,
                   const AttnRow * rows_dev, int n_rows, const int * key_idx, int H, float scale, int max_keys,
-                  _Float16 * out, int ldo, bool any_one_chunk, bool any_tiled) {
+                  _Float16 * out, int ldo, bool any_one_chunk, bool any_tiled, float * out32) {
     if (n_rows <= 0) return;
     if (any_one_chunk) {
         if (key_idx) {
             if (max_keys > AS_MAX_LIST) throw std::runtime_error("attn_decoder: too many listed keys");
             hipLaunchKernelGGL(k_attn_step<true>, dim3(H, n_rows), dim3(64), 0, s, q, ldq, kbase, vbase, ld_kv, rows_dev,
-                               key_idx, scale, out, ldo);
+                               key_idx, scale, out, ldo, out32);
         } else {
             hipLaunchKernelGGL(k_attn_step<false>, dim3(H, n_rows), dim3(64), 0, s, q, ldq, kbase, vbase, ld_kv, rows_dev,
-                               key_idx, scale, out, ldo);
+                               key_idx, scale, out, ldo, out32);
         }
     }
     if (any_tiled) {
         if (max_keys > DA_MAX_KEYS) throw std::runtime_error("attn_decoder: too many keys");
         hipLaunchKernelGGL(k_attn_decoder, dim3((H + 3) / 4, n_rows), dim3(256), 0, s, q, ldq, kbase, vbase, ld_kv,
-                           rows_dev, key_idx, H, scale, out, ldo);
+                           rows_dev, key_idx, H, scale, out, ldo, out32);
     }
 }
 

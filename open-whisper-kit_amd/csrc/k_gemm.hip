@@ -8,6 +8,7 @@
 #include "kernels.h"
 
 #include <algorithm>
+#include <cstring>
 
 namespace owk {
 
@@ -468,6 +469,198 @@ template <int MODE> struct LaunchRows {
     }
 };
 
+// ---------------------------------------------------------------------------------
+// Q5_0 x Q8_0 (see kernels.h). Activation rows -> Q8_0 with the x86 rounding of
+// quantize_row_q8_0: d = amax / 127 (stored f16), q = rne(x * (127 / amax)).
+// One 32-lane half-wave per block.
+// ---------------------------------------------------------------------------------
+template <typename TA>
+__global__ __launch_bounds__(256) void k_quantize_q8(const TA * __restrict__ A, int lda, int M, int K,
+                                                     int8_t * __restrict__ q, float * __restrict__ dq) {
+    const int nb = K >> 5;
+    const size_t total = (size_t) M * nb;
+    const int lane = threadIdx.x & 31;
+    for (size_t blk = ((size_t) blockIdx.x * blockDim.x + threadIdx.x) >> 5; blk < total;
+         blk += ((size_t) gridDim.x * blockDim.x) >> 5) {
+        const int r = (int) (blk / nb), b = (int) (blk - (size_t) r * nb);
+        const float x = (float) A[(size_t) r * lda + b * 32 + lane];
+        float am = fabsf(x);
+#pragma unroll
+        for (int o = 16; o > 0; o >>= 1) am = fmaxf(am, __shfl_xor(am, o, 32));
+        const float dd = am / 127.f;
+        const float id = am != 0.0f ? 127.f / am : 0.0f;
+        q[(size_t) r * K + b * 32 + lane] = (int8_t) rintf(x * id);
+        if (lane == 0) dq[(size_t) r * nb + b] = (float) (_Float16) dd;
+    }
+}
+
+void quantize_q8(hipStream_t s, const float * A32, const _Float16 * A16, int lda, int M, int K, int8_t * q, float * dq) {
+    if (M <= 0) return;
+    if (K % 32) throw std::runtime_error("quantize_q8: K % 32");
+    const size_t blocks = (size_t) M * (K / 32);
+    const int grid = (int) std::min<size_t>((blocks * 32 + 255) / 256, 65536);
+    if (A32)
+        hipLaunchKernelGGL(k_quantize_q8<float>, dim3(grid), dim3(256), 0, s, A32, lda, M, K, q, dq);
+    else
+        hipLaunchKernelGGL(k_quantize_q8<_Float16>, dim3(grid), dim3(256), 0, s, A16, lda, M, K, q, dq);
+}
+
+typedef int intx4 __attribute__((ext_vector_type(4)));
+
+// 8 consecutive Q5_0 weights of one block as int8 (B/A operand of mfma_i32_16x16x32_i8):
+// group g = elements 8g..8g+7 = low (g < 2) or high nibbles of bytes 8(g&1)..+7, 5th bits
+// qh >> 8g; value - 16 by bytewise SWAR (v | 0x80) - 16 ^ 0x80
+__device__ __forceinline__ long q5_group(const uint8_t * qs_blk, uint32_t qh, int g) {
+    const uint64_t raw = *(const uint64_t *) (qs_blk + (g & 1) * 8);
+    uint64_t v = (g < 2 ? raw : (raw >> 4)) & 0x0F0F0F0F0F0F0F0FULL;
+    const uint32_t h8 = (qh >> (8 * g)) & 0xFFu;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v |= (uint64_t) ((h8 >> e) & 1u) << (8 * e + 4);
+    v = ((v | 0x8080808080808080ULL) - 0x1010101010101010ULL) ^ 0x8080808080808080ULL;
+    return (long) v;
+}
+
+// skinny: M <= 64 rows; one 16-column tile per block, 8 waves split the K blocks, partial
+// tiles reduced through LDS in fixed wave order
+template <int MODE>
+__global__ __launch_bounds__(512) void k_gemm_q5_skinny(int M, int N, int K, const int8_t * __restrict__ qa,
+                                                        const float * __restrict__ da, Q5W w, EpiParams ep) {
+    __shared__ floatx4 red[8][4][64];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int n0 = blockIdx.x * 16;
+    const int MT = (M + 15) >> 4;
+    const int nb = K >> 5;
+    const int kb0 = (wave * nb) >> 3, kb1 = ((wave + 1) * nb) >> 3;
+    const int g = lane >> 4;
+    const int n = min(n0 + (lane & 15), N - 1);
+    floatx4 acc[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc[i] = floatx4{0.f, 0.f, 0.f, 0.f};
+    for (int kb = kb0; kb < kb1; ++kb) {
+        const long b = q5_group(w.qs + (size_t) n * (K / 2) + kb * 16, w.qh[(size_t) n * nb + kb], g);
+        const float dw = (float) w.d[(size_t) n * nb + kb];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            if (i < MT) {
+                const int ra = min(i * 16 + (lane & 15), M - 1);
+                const long a = *(const long *) (qa + (size_t) ra * K + kb * 32 + 8 * g);
+                const intx4 z = {0, 0, 0, 0};
+                const intx4 iv = __builtin_amdgcn_mfma_i32_16x16x32_i8(a, b, z, 0, 0, 0);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int r = min(i * 16 + 4 * g + e, M - 1);
+                    acc[i][e] += (float) iv[e] * (da[(size_t) r * nb + kb] * dw);
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) red[wave][i][lane] = acc[i];
+    __syncthreads();
+    if (tid < 256) {
+        const int i = tid >> 6, ln = tid & 63;
+        if (i < MT) {
+            floatx4 sum = red[0][i][ln];
+#pragma unroll
+            for (int ww = 1; ww < 8; ++ww) sum += red[ww][i][ln];
+            const int c = n0 + (ln & 15);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int r = i * 16 + 4 * (ln >> 4) + e;
+                if (r < M && c < N) epi_store<MODE>(ep, r, c, sum[e]);
+            }
+        }
+    }
+}
+
+// tiles: 64 x 64 per block, 4 waves of 32 x 32; per 32-wide K block the int8 operands are
+// staged in LDS (the Q5 weights expanded to int8 on the way), one MFMA per 16 x 16 tile,
+// then the per-block scale d_a * d_w folds the integer dot into the f32 accumulator
+template <int MODE>
+__global__ __launch_bounds__(256) void k_gemm_q5_big(int M, int N, int K, const int8_t * __restrict__ qa,
+                                                     const float * __restrict__ da, Q5W w, EpiParams ep) {
+    __shared__ __attribute__((aligned(16))) int8_t sA[2][64][40], sB[2][64][40];
+    __shared__ float sdA[2][64], sdB[2][64];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int nbn = (N + 63) / 64;
+    const int bm = blockIdx.x / nbn, bn = blockIdx.x - bm * nbn;
+    const int m0 = bm * 64, n0 = bn * 64;
+    const int nb = K >> 5;
+    const int wm = wave >> 1, wn = wave & 1;
+    const int g = lane >> 4;
+    floatx4 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+    const int srow = tid >> 2, sq = tid & 3;  // staging: row, 8-element group
+    const int ra = min(m0 + srow, M - 1), rb = min(n0 + srow, N - 1);
+    auto stage = [&](int buf, int kb) {
+        *(long *) &sA[buf][srow][sq * 8] = *(const long *) (qa + (size_t) ra * K + kb * 32 + sq * 8);
+        *(long *) &sB[buf][srow][sq * 8] = q5_group(w.qs + (size_t) rb * (K / 2) + kb * 16, w.qh[(size_t) rb * nb + kb], sq);
+        if (sq == 0) {
+            sdA[buf][srow] = da[(size_t) ra * nb + kb];
+            sdB[buf][srow] = (float) w.d[(size_t) rb * nb + kb];
+        }
+    };
+    stage(0, 0);
+    __syncthreads();
+    for (int kb = 0; kb < nb; ++kb) {
+        const int cur = kb & 1;
+        if (kb + 1 < nb) stage(cur ^ 1, kb + 1);
+        long a[2], b[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            a[i] = *(const long *) &sA[cur][wm * 32 + i * 16 + (lane & 15)][8 * g];
+            b[i] = *(const long *) &sB[cur][wn * 32 + i * 16 + (lane & 15)][8 * g];
+        }
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const intx4 z = {0, 0, 0, 0};
+                const intx4 iv = __builtin_amdgcn_mfma_i32_16x16x32_i8(a[i], b[j], z, 0, 0, 0);
+                const float dw = sdB[cur][wn * 32 + j * 16 + (lane & 15)];
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                    acc[i][j][e] += (float) iv[e] * (sdA[cur][wm * 32 + i * 16 + 4 * g + e] * dw);
+            }
+        __syncthreads();
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int c = n0 + wn * 32 + j * 16 + (lane & 15);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int r = m0 + wm * 32 + i * 16 + 4 * g + e;
+                if (r < M && c < N) epi_store<MODE>(ep, r, c, acc[i][j][e]);
+            }
+        }
+}
+
+template <int MODE> struct LaunchQ5 {
+    static void run(hipStream_t s, int M, int N, int K, const int8_t * qa, const float * da, const Q5W & w,
+                    const EpiParams & ep) {
+        if (M <= 64)
+            hipLaunchKernelGGL(k_gemm_q5_skinny<MODE>, dim3((N + 15) / 16), dim3(512), 0, s, M, N, K, qa, da, w, ep);
+        else
+            hipLaunchKernelGGL(k_gemm_q5_big<MODE>, dim3(((M + 63) / 64) * ((N + 63) / 64)), dim3(256), 0, s, M, N, K,
+                               qa, da, w, ep);
+    }
+};
+
+void q5_split_host(const uint8_t * blocks, int N, int K, uint8_t * qs, uint32_t * qh, uint16_t * d) {
+    const int nb = K / 32;
+    for (size_t i = 0; i < (size_t) N * nb; ++i) {
+        const uint8_t * b = blocks + i * 22;  // block_q5_0: d (f16), qh[4], qs[16]
+        memcpy(&d[i], b, 2);
+        memcpy(&qh[i], b + 2, 4);
+        memcpy(qs + i * 16, b + 6, 16);
+    }
+}
+
 static void check_shape(int M, int N, int K, int lda, int ldw, int kmul) {
     if (M <= 0 || N <= 0 || K <= 0 || K % kmul != 0 || lda < K || ldw < K || (lda % 8) || (ldw % 8))
         throw std::runtime_error("gemm: unsupported shape M=" + std::to_string(M) + " N=" + std::to_string(N) +
@@ -485,6 +678,13 @@ void gemm_f16_skinny(hipStream_t s, int mode, int M, int N, int K, const _Float1
     check_shape(M, N, K, lda, ldw, 32);
     if (M > 64) throw std::runtime_error("gemm_skinny: M > 64");
     dispatch_mode<LaunchSkinny>(mode, s, M, N, K, A, lda, W, ldw, ep);
+}
+
+void gemm_q5(hipStream_t s, int mode, int M, int N, int K, const int8_t * qa, const float * da, const Q5W & w,
+             const EpiParams & ep) {
+    if (M <= 0 || N <= 0 || K <= 0 || K % 32) throw std::runtime_error("gemm_q5: unsupported shape");
+    if (!w) throw std::runtime_error("gemm_q5: no Q5_0 weights");
+    dispatch_mode<LaunchQ5>(mode, s, M, N, K, qa, da, w, ep);
 }
 
 size_t gemm_ws_floats(int N, int K) {

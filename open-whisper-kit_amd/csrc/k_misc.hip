@@ -152,6 +152,31 @@ void embed_tokens(hipStream_t s, const _Float16 * te, const float * pe, const in
     hipLaunchKernelGGL(k_embed, dim3(rows), dim3(256), 0, s, te, pe, tok, pos, rows, d, x);
 }
 
+__global__ void k_embed_q5(const uint8_t * __restrict__ qs, const uint32_t * __restrict__ qh,
+                           const _Float16 * __restrict__ dd, const float * __restrict__ pe,
+                           const int * __restrict__ tok, const int * __restrict__ pos, int rows, int d,
+                           float * __restrict__ x) {
+    const int r = blockIdx.x;
+    if (r >= rows) return;
+    const size_t row = (size_t) tok[r];
+    const int nb = d / 32;
+    const float * p = pe + (size_t) pos[r] * d;
+    for (int i = threadIdx.x; i < d; i += blockDim.x) {
+        const int b = i >> 5, j = i & 31;
+        const uint8_t byte = qs[row * (d / 2) + b * 16 + (j & 15)];
+        const int lo = j < 16 ? (byte & 0x0F) : (byte >> 4);
+        const int hi = (qh[row * nb + b] >> j) & 1;
+        const float v = (float) ((lo | (hi << 4)) - 16) * (float) dd[row * nb + b];  // dequantize_row_q5_0
+        x[(size_t) r * d + i] = v + p[i];
+    }
+}
+
+void embed_tokens_q5(hipStream_t s, const Q5W & te, const float * pe, const int * tok, const int * pos, int rows, int d,
+                     float * x) {
+    if (rows <= 0) return;
+    hipLaunchKernelGGL(k_embed_q5, dim3(rows), dim3(256), 0, s, te.qs, te.qh, te.d, pe, tok, pos, rows, d, x);
+}
+
 // ----------------------------------------------------------------------------------
 // Log-mel spectrogram (ref whisper.cpp:3104-3260). Per frame: reflect-padded samples
 // times the periodic Hann window (float product, as the reference), 201-bin DFT of

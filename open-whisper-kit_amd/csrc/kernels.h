@@ -78,6 +78,27 @@ size_t tiled_weight_elems(int N, int K);
 void tile_weights(hipStream_t s, const _Float16 * W, int N, int K, _Float16 * out);
 
 // ---------------------------------------------------------------------------------
+// Q5_0 weights x Q8_0 activations (ggml MOSTLY_Q5_0 models, ftype 2008). The reference
+// quantizes every mul_mat activation row to Q8_0 per 32 (x86 quantize_row_q8_0,
+// ggml-cpu/arch/x86/quants.c:290-360) and takes the integer dot with the Q5_0 block
+// (ggml_vec_dot_q5_0_q8_0, quants.c:845) scaled by d_w * d_a per block. Here the dot is
+// v_mfma_i32_16x16x32_i8 per 32-block (exact integers), scaled and accumulated in f32.
+// ---------------------------------------------------------------------------------
+struct Q5W {
+    const uint8_t * qs = nullptr;   // [N][K/2]: block b = 16 bytes, byte j = element j | element j+16 << 4
+    const uint32_t * qh = nullptr;  // [N][K/32]: 5th bits, bit j = element j
+    const _Float16 * d = nullptr;   // [N][K/32]: block scales
+    explicit operator bool() const { return qs != nullptr; }
+};
+// Q8_0 rows of A (f32 if A32, else f16): q [M][K] int8, dq [M][K/32] (the f16-rounded scale)
+void quantize_q8(hipStream_t s, const float * A32, const _Float16 * A16, int lda, int M, int K, int8_t * q, float * dq);
+// C[M,N] = Q8(A) . Q5(W)^T with the fused epilogue `mode` (any EpiMode except EPI_PARTIAL)
+void gemm_q5(hipStream_t s, int mode, int M, int N, int K, const int8_t * qa, const float * da, const Q5W & w,
+             const EpiParams & ep);
+// host-side split of ggml block_q5_0 rows (22 B per block) into the Q5W arrays
+void q5_split_host(const uint8_t * blocks, int N, int K, uint8_t * qs, uint32_t * qh, uint16_t * d);
+
+// ---------------------------------------------------------------------------------
 // normalisation / elementwise
 // ---------------------------------------------------------------------------------
 // out16[r] = f16(LN(x[r]) * w + b); mean/variance accumulated in double (ref ops.cpp:3578-3623)
@@ -87,6 +108,9 @@ void layernorm_f16(hipStream_t s, const float * x, int rows, int d, const float 
 // decoder input embedding: x[r] = f32(tok_emb[tok[r]]) + pos_emb[pos[r]]
 void embed_tokens(hipStream_t s, const _Float16 * tok_emb, const float * pos_emb, const int * tokens,
                   const int * pos, int rows, int d, float * x);
+// the same from a Q5_0 token embedding (ggml get_rows -> dequantize_row_q5_0: d * (q - 16))
+void embed_tokens_q5(hipStream_t s, const Q5W & te, const float * pos_emb, const int * tokens, const int * pos,
+                     int rows, int d, float * x);
 
 // ---------------------------------------------------------------------------------
 // audio front-end
@@ -123,10 +147,12 @@ void conv2_im2col(hipStream_t s, const _Float16 * x, int n_clips, int t_in, int 
 // (the reference's GGML_PAD(1500,256) kv_pad rows, whisper.cpp:2055,2145-2159).
 // q, k: [clips*T][H*64] f16; vt: [clips][H][64][Tpad] f16; out: [clips*T][H*64] f16
 // encoder attention of a flash_attn = false context (soft_max path, F16 probabilities)
+// out32 (optional): write the f32 output instead of f16 (Q5_0 models quantize it to Q8_0)
 void attn_encoder_softmax(hipStream_t s, const _Float16 * q, const _Float16 * k, const _Float16 * vt, int n_clips, int T,
-                          int Tpad, int H, float scale, _Float16 * out);
+                          int Tpad, int H, float scale, _Float16 * out, float * out32 = nullptr);
 void attn_encoder(hipStream_t s, const _Float16 * q, const _Float16 * k, const _Float16 * vt,
-                  int n_clips, int T, int Tpad, int H, float scale, int n_zero_pad, _Float16 * out);
+                  int n_clips, int T, int Tpad, int H, float scale, int n_zero_pad, _Float16 * out,
+                  float * out32 = nullptr);
 
 // decoder attention row job: one query row attends over a list of KV rows in a given
 // order with the reference flash-attention numerics (one_chunk: F16 V accumulator,
@@ -141,12 +167,13 @@ struct AttnRow {
 };
 void attn_decoder(hipStream_t s, const _Float16 * q, int ldq, const _Float16 * kbase, const _Float16 * vbase,
                   int ld_kv, const AttnRow * rows_dev, int n_rows, const int * key_idx, int H, float scale,
-                  int max_keys, _Float16 * out, int ldo, bool any_one_chunk, bool any_tiled);
+                  int max_keys, _Float16 * out, int ldo, bool any_one_chunk, bool any_tiled, float * out32 = nullptr);
 // rows with mode 2 (flash_attn = false contexts): soft_max attention, F16 probabilities;
 // optional DTW capture of alignment-head probabilities cap[a][key][row] (amap: head -> a or -1)
 void attn_decoder_softmax(hipStream_t s, const _Float16 * q, int ldq, const _Float16 * kbase, const _Float16 * vbase,
                           int ld_kv, const AttnRow * rows_dev, int n_rows, const int * key_idx, int H, float scale,
-                          int max_keys, _Float16 * out, int ldo, const int * amap, float * cap, int cap_rows);
+                          int max_keys, _Float16 * out, int ldo, const int * amap, float * cap, int cap_rows,
+                          float * out32 = nullptr);
 int attn_max_listed_keys();  // per-row limit of the one_chunk kernel's key list
 int attn_max_tiled_keys();   // per-row limit of the tiled decoder kernel
 

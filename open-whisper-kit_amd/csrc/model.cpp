@@ -177,6 +177,7 @@ std::vector<TensorSpec> expected_tensors(const HParams & hp) {
 struct HostTensor {
     std::vector<uint8_t> data;  // raw bytes as stored
     bool f16 = false;
+    bool q5 = false;            // block_q5_0 rows
     bool loaded = false;
     int64_t nelem = 0;
 };
@@ -218,10 +219,11 @@ Model * load_model(whisper_model_loader * loader, int device, std::string & err)
     const int qntvr = hp.ftype / 1000;
     (void) qntvr;
     hp.ftype %= 1000;
-    if (hp.ftype != 1) {  // GGML_FTYPE_MOSTLY_F16
-        err = "unsupported ftype " + std::to_string(hp.ftype) + " (this engine build loads F16 models)";
+    if (hp.ftype != 1 && hp.ftype != 8) {  // GGML_FTYPE_MOSTLY_F16, GGML_FTYPE_MOSTLY_Q5_0 (ggml.h:448)
+        err = "unsupported ftype " + std::to_string(hp.ftype) + " (this engine build loads F16 and Q5_0 models)";
         return nullptr;
     }
+    m->q5 = hp.ftype == 8;
 
     // mel filters
     m->n_filters_mel = r.get<int32_t>();
@@ -301,12 +303,19 @@ Model * load_model(whisper_model_loader * loader, int device, std::string & err)
         for (size_t i = 0; i < sp.ne.size(); ++i)
             if (ne[i] != sp.ne[i]) { err = "tensor '" + name + "' has wrong shape in model file"; return nullptr; }
         if (nel != expect) { err = "tensor '" + name + "' has wrong size in model file"; return nullptr; }
-        if (ttype != 0 && ttype != 1) { err = "tensor '" + name + "': unsupported type " + std::to_string(ttype); return nullptr; }
-        if (sp.f16 && ttype != 1) { err = "tensor '" + name + "': expected F16 weights"; return nullptr; }
+        // Q5_0 models: every 2-D weight is GGML_TYPE_Q5_0 (6), 22 bytes per 32 (whisper-quantize)
+        const bool want_q5 = m->q5 && sp.f16 && sp.ne.size() == 2;
+        if (want_q5 ? ttype != 6 : (ttype != 0 && ttype != 1)) {
+            err = "tensor '" + name + "': unsupported type " + std::to_string(ttype);
+            return nullptr;
+        }
+        if (sp.f16 && !want_q5 && ttype != 1) { err = "tensor '" + name + "': expected F16 weights"; return nullptr; }
+        if (want_q5 && sp.ne[0] % 32) { err = "tensor '" + name + "': row length not a multiple of 32"; return nullptr; }
         HostTensor & t = ht[it->second];
         t.f16 = ttype == 1;
+        t.q5 = want_q5;
         t.nelem = nel;
-        t.data.resize((size_t) nel * (t.f16 ? 2 : 4));
+        t.data.resize(want_q5 ? (size_t) nel / 32 * 22 : (size_t) nel * (t.f16 ? 2 : 4));
         r.read(t.data.data(), t.data.size());
         if (!r.ok) { err = "truncated tensor data for '" + name + "'"; return nullptr; }
         t.loaded = true;
@@ -341,18 +350,24 @@ Model * load_model(whisper_model_loader * loader, int device, std::string & err)
     // packed matrices
     const size_t o_conv1 = reserve((size_t) d * m->kpad_conv1 * 2);
     std::vector<size_t> o_enc_qkv(hp.n_audio_layer), o_dec_qkv(hp.n_text_layer), o_dec_ckv(hp.n_text_layer);
-    for (int i = 0; i < hp.n_audio_layer; ++i) o_enc_qkv[i] = reserve((size_t) 3 * d * d * 2);
-    for (int i = 0; i < hp.n_text_layer; ++i) {
-        o_dec_qkv[i] = reserve((size_t) 3 * d * d * 2);
-        o_dec_ckv[i] = reserve((size_t) 2 * d * d * 2);
+    if (!m->q5) {
+        for (int i = 0; i < hp.n_audio_layer; ++i) o_enc_qkv[i] = reserve((size_t) 3 * d * d * 2);
+        for (int i = 0; i < hp.n_text_layer; ++i) {
+            o_dec_qkv[i] = reserve((size_t) 3 * d * d * 2);
+            o_dec_ckv[i] = reserve((size_t) 2 * d * d * 2);
+        }
     }
+    auto is_q5 = [&](const std::string & n) {
+        const TensorSpec & sp = S[idx.at(n)];
+        return m->q5 && sp.f16 && sp.ne.size() == 2;
+    };
     for (auto & kv : place) {
         const std::string & n = kv.first;
         const bool packed = n == "encoder.conv1.weight" ||
                             (n.find(".key.weight") != std::string::npos) ||
                             (n.find(".value.weight") != std::string::npos) ||
                             (n.find("attn.query.weight") != std::string::npos && n.find("cross_attn") == std::string::npos);
-        kv.second = packed ? (size_t) -1 : reserve(bytes_of(n));
+        kv.second = (packed || is_q5(n)) ? (size_t) -1 : reserve(bytes_of(n));
     }
     const size_t o_gelu = reserve(65536 * 2);
     const size_t o_filt = reserve(m->filters.size() * 4);
@@ -385,11 +400,11 @@ Model * load_model(whisper_model_loader * loader, int device, std::string & err)
                 at += t.data.size();
             }
         };
-        for (int i = 0; i < hp.n_audio_layer; ++i) {
+        for (int i = 0; i < hp.n_audio_layer && !m->q5; ++i) {
             const std::string p = "encoder.blocks." + std::to_string(i) + ".attn.";
             cat(o_enc_qkv[i], {p + "query.weight", p + "key.weight", p + "value.weight"});
         }
-        for (int i = 0; i < hp.n_text_layer; ++i) {
+        for (int i = 0; i < hp.n_text_layer && !m->q5; ++i) {
             const std::string p = "decoder.blocks." + std::to_string(i) + ".";
             cat(o_dec_qkv[i], {p + "attn.query.weight", p + "attn.key.weight", p + "attn.value.weight"});
             cat(o_dec_ckv[i], {p + "cross_attn.key.weight", p + "cross_attn.value.weight"});
@@ -414,7 +429,67 @@ Model * load_model(whisper_model_loader * loader, int device, std::string & err)
     }
 
     auto F = [&](const std::string & n) { return (const float *) (base + place.at(n)); };
-    auto H = [&](const std::string & n) { return (const _Float16 *) (base + place.at(n)); };
+    auto H = [&](const std::string & n) -> const _Float16 * {
+        return place.at(n) == (size_t) -1 ? nullptr : (const _Float16 *) (base + place.at(n));
+    };
+    // Q5_0 matrices: split block arrays (kernels.h Q5W), row groups concatenated like the F16 packs
+    std::map<std::string, Q5W> q5m;
+    if (m->q5 && n_loaded > 0) {
+        std::vector<std::vector<std::string>> groups;
+        groups.push_back({"decoder.token_embedding.weight"});
+        for (int i = 0; i < hp.n_audio_layer; ++i) {
+            const std::string p = "encoder.blocks." + std::to_string(i) + ".";
+            groups.push_back({p + "attn.query.weight", p + "attn.key.weight", p + "attn.value.weight"});
+            for (const char * n : {"attn.out.weight", "mlp.0.weight", "mlp.2.weight"}) groups.push_back({p + n});
+        }
+        for (int i = 0; i < hp.n_text_layer; ++i) {
+            const std::string p = "decoder.blocks." + std::to_string(i) + ".";
+            groups.push_back({p + "attn.query.weight", p + "attn.key.weight", p + "attn.value.weight"});
+            groups.push_back({p + "cross_attn.key.weight", p + "cross_attn.value.weight"});
+            for (const char * n : {"attn.out.weight", "cross_attn.query.weight", "cross_attn.out.weight", "mlp.0.weight",
+                                   "mlp.2.weight"})
+                groups.push_back({p + n});
+        }
+        size_t qoff = 0;
+        struct Plan { size_t qs, qh, d; int N, K; };
+        std::vector<Plan> plans;
+        for (const auto & gr : groups) {
+            int N = 0;
+            const int K = (int) S[idx.at(gr[0])].ne[0];
+            for (const auto & n : gr) N += (int) S[idx.at(n)].ne[1];
+            Plan pl{0, 0, 0, N, K};
+            auto res = [&](size_t bytes) { size_t o = qoff; qoff += (bytes + 255) & ~(size_t) 255; return o; };
+            pl.qs = res((size_t) N * K / 2);
+            pl.qh = res((size_t) N * (K / 32) * 4);
+            pl.d = res((size_t) N * (K / 32) * 2);
+            plans.push_back(pl);
+        }
+        m->q5blob.alloc(qoff);
+        char * qb = (char *) m->q5blob.ptr;
+        for (size_t gi = 0; gi < groups.size(); ++gi) {
+            const Plan & pl = plans[gi];
+            std::vector<uint8_t> qs((size_t) pl.N * pl.K / 2);
+            std::vector<uint32_t> qh((size_t) pl.N * (pl.K / 32));
+            std::vector<uint16_t> dd((size_t) pl.N * (pl.K / 32));
+            int row = 0;
+            for (const auto & n : groups[gi]) {
+                const HostTensor & t = host(n);
+                const int rows = (int) S[idx.at(n)].ne[1];
+                q5_split_host(t.data.data(), rows, pl.K, qs.data() + (size_t) row * pl.K / 2,
+                              qh.data() + (size_t) row * (pl.K / 32), dd.data() + (size_t) row * (pl.K / 32));
+                row += rows;
+            }
+            OWK_HIP_CHECK(hipMemcpy(qb + pl.qs, qs.data(), qs.size(), hipMemcpyHostToDevice));
+            OWK_HIP_CHECK(hipMemcpy(qb + pl.qh, qh.data(), qh.size() * 4, hipMemcpyHostToDevice));
+            OWK_HIP_CHECK(hipMemcpy(qb + pl.d, dd.data(), dd.size() * 2, hipMemcpyHostToDevice));
+            Q5W w;
+            w.qs = (const uint8_t *) (qb + pl.qs);
+            w.qh = (const uint32_t *) (qb + pl.qh);
+            w.d = (const _Float16 *) (qb + pl.d);
+            q5m[groups[gi][0]] = w;
+        }
+    }
+    auto Q = [&](const std::string & n) { auto it = q5m.find(n); return it == q5m.end() ? Q5W() : it->second; };
     m->conv1_w = (const _Float16 *) (base + o_conv1);
     m->conv1_b = F("encoder.conv1.bias");
     m->conv2_w = H("encoder.conv2.weight");
@@ -433,8 +508,16 @@ Model * load_model(whisper_model_loader * loader, int device, std::string & err)
         L.w_o = H(p + "attn.out.weight"); L.b_o = F(p + "attn.out.bias");
         L.w_mlp0 = H(p + "mlp.0.weight"); L.b_mlp0 = F(p + "mlp.0.bias");
         L.w_mlp1 = H(p + "mlp.2.weight"); L.b_mlp1 = F(p + "mlp.2.bias");
+        if (m->q5) {
+            L.w_qkv = nullptr;
+            L.q_qkv = Q(p + "attn.query.weight");
+            L.q_o = Q(p + "attn.out.weight");
+            L.q_mlp0 = Q(p + "mlp.0.weight");
+            L.q_mlp1 = Q(p + "mlp.2.weight");
+        }
     }
     m->d_te = H("decoder.token_embedding.weight");
+    m->q_te = Q("decoder.token_embedding.weight");
     m->d_pe = F("decoder.positional_embedding");
     m->d_ln_w = F("decoder.ln.weight");
     m->d_ln_b = F("decoder.ln.bias");
@@ -454,8 +537,19 @@ Model * load_model(whisper_model_loader * loader, int device, std::string & err)
         L.cw_o = H(p + "cross_attn.out.weight"); L.cb_o = F(p + "cross_attn.out.bias");
         L.w_mlp0 = H(p + "mlp.0.weight"); L.b_mlp0 = F(p + "mlp.0.bias");
         L.w_mlp1 = H(p + "mlp.2.weight"); L.b_mlp1 = F(p + "mlp.2.bias");
+        if (m->q5) {
+            L.w_qkv = nullptr;
+            L.cw_kv = nullptr;
+            L.q_qkv = Q(p + "attn.query.weight");
+            L.q_ckv = Q(p + "cross_attn.key.weight");
+            L.q_o = Q(p + "attn.out.weight");
+            L.q_cq = Q(p + "cross_attn.query.weight");
+            L.q_co = Q(p + "cross_attn.out.weight");
+            L.q_mlp0 = Q(p + "mlp.0.weight");
+            L.q_mlp1 = Q(p + "mlp.2.weight");
+        }
     }
-    {
+    if (!m->q5) {
         // decoder weights re-laid out for the decode-row GEMM (an extra 1.6 GB for large-v3;
         // HBM holds both layouts comfortably, the row-major one still feeds prefills)
         const int d = hp.n_text_state;

@@ -7,6 +7,7 @@
 #include <vector>
 
 #include "common.h"
+#include "kernels.h"
 #include "whisper.h"
 
 namespace owk {
@@ -42,6 +43,7 @@ struct EncLayerW {
     const float *b_o;
     const _Float16 *w_mlp0, *w_mlp1;
     const float *b_mlp0, *b_mlp1;
+    Q5W q_qkv, q_o, q_mlp0, q_mlp1;  // Q5_0 models (the F16 pointers are null then)
 };
 
 struct DecLayerW {
@@ -60,6 +62,7 @@ struct DecLayerW {
     const float *b_mlp0, *b_mlp1;
     // tiled copies for the decode-row GEMM (tile_weights layout)
     const _Float16 *t_qkv, *t_o, *t_cq, *t_co, *t_mlp0, *t_mlp1;
+    Q5W q_qkv, q_o, q_cq, q_ckv, q_co, q_mlp0, q_mlp1;  // Q5_0 models
 };
 
 struct Model {
@@ -80,6 +83,9 @@ struct Model {
     const float * e_pe = nullptr;        // [n_audio_ctx][d]
     const float *e_ln_w = nullptr, *e_ln_b = nullptr;
     std::vector<EncLayerW> enc;
+    bool q5 = false;                     // MOSTLY_Q5_0 model: 2-D linears (and d_te) are Q5W
+    DevBuf q5blob;
+    Q5W q_te;
     const _Float16 * d_te = nullptr;     // [n_vocab][d]
     const _Float16 * d_te_t = nullptr;   // tiled copy (logits of decode steps)
     DevBuf tiled;                        // all tiled decoder weights

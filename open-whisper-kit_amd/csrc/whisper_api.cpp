@@ -1165,6 +1165,50 @@ double owk_debug_gemm_bench(int device, int mode, int M, int N, int K, int iters
     }
 }
 
+int owk_debug_gemm_q5(int device, int M, int N, int K, const float * a, const uint8_t * w_blocks, float * out,
+                      int8_t * q_out, float * d_out) {
+    try {
+        OWK_HIP_CHECK(hipSetDevice(device));
+        hipStream_t s;
+        OWK_HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+        const int nb = K / 32;
+        std::vector<uint8_t> qs((size_t) N * K / 2);
+        std::vector<uint32_t> qh((size_t) N * nb);
+        std::vector<uint16_t> dd((size_t) N * nb);
+        q5_split_host(w_blocks, N, K, qs.data(), qh.data(), dd.data());
+        DevBuf da, dqs, dqh, ddd, dout, q8, q8d;
+        da.alloc((size_t) M * K * 4);
+        dqs.alloc(qs.size());
+        dqh.alloc(qh.size() * 4);
+        ddd.alloc(dd.size() * 2);
+        dout.alloc((size_t) M * N * 4);
+        q8.alloc((size_t) M * K);
+        q8d.alloc((size_t) M * nb * 4);
+        OWK_HIP_CHECK(hipMemcpy(da.ptr, a, (size_t) M * K * 4, hipMemcpyHostToDevice));
+        OWK_HIP_CHECK(hipMemcpy(dqs.ptr, qs.data(), qs.size(), hipMemcpyHostToDevice));
+        OWK_HIP_CHECK(hipMemcpy(dqh.ptr, qh.data(), qh.size() * 4, hipMemcpyHostToDevice));
+        OWK_HIP_CHECK(hipMemcpy(ddd.ptr, dd.data(), dd.size() * 2, hipMemcpyHostToDevice));
+        Q5W w;
+        w.qs = dqs.as<uint8_t>();
+        w.qh = dqh.as<uint32_t>();
+        w.d = ddd.as<_Float16>();
+        quantize_q8(s, da.as<float>(), nullptr, K, M, K, q8.as<int8_t>(), q8d.as<float>());
+        EpiParams ep;
+        ep.out32 = dout.as<float>();
+        ep.ldo = N;
+        gemm_q5(s, EPI_F32, M, N, K, q8.as<int8_t>(), q8d.as<float>(), w, ep);
+        OWK_HIP_CHECK(hipStreamSynchronize(s));
+        OWK_HIP_CHECK(hipMemcpy(out, dout.ptr, (size_t) M * N * 4, hipMemcpyDeviceToHost));
+        if (q_out) OWK_HIP_CHECK(hipMemcpy(q_out, q8.ptr, (size_t) M * K, hipMemcpyDeviceToHost));
+        if (d_out) OWK_HIP_CHECK(hipMemcpy(d_out, q8d.ptr, (size_t) M * nb * 4, hipMemcpyDeviceToHost));
+        OWK_HIP_CHECK(hipStreamDestroy(s));
+    } catch (const std::exception & ex) {
+        log_msg(GGML_LOG_LEVEL_ERROR, "owk_debug_gemm_q5: %s\n", ex.what());
+        return -1;
+    }
+    return 0;
+}
+
 int owk_debug_gemm(int device, int M, int N, int K, const uint16_t * a, const uint16_t * w, float * out) {
     try {
         OWK_HIP_CHECK(hipSetDevice(device));

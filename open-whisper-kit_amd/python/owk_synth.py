@@ -188,13 +188,98 @@ def write_model(path: str, model: str, seed: int = 1234) -> str:
     return h.hexdigest()
 
 
+def q5_0_blocks(x: np.ndarray) -> bytes:
+    """ggml Q5_0 blocks (22 B per 32 weights) of a row-major f32 tensor, restating
+    quantize_row_q5_0_ref (/root/reference ggml/src/ggml-quants.c:110-152): d = max / -16 with
+    max the first largest-magnitude value, q = min(31, (int8)(x / d + 16.5)), 4 low bits packed
+    in nibbles (element j low, j + 16 high), 5th bits in a little-endian u32."""
+    b = np.ascontiguousarray(x, np.float32).reshape(-1, 32)
+    am = np.argmax(np.abs(b), axis=1)
+    mx = b[np.arange(len(b)), am]
+    d = (mx / np.float32(-16.0)).astype(np.float32)
+    with np.errstate(divide="ignore"):
+        idv = np.where(d != 0, np.float32(1.0) / d, np.float32(0.0)).astype(np.float32)
+    # x * id + 16.5f is one fused multiply-add in the reference build (gcc contracts it on
+    # FMA targets): the product is exact in double, so a single rounding to f32 follows
+    xs = (b.astype(np.float64) * idv.astype(np.float64)[:, None] + 16.5).astype(np.float32)
+    xi = np.minimum(31, np.trunc(xs).astype(np.int64).astype(np.int8).astype(np.int64) & 0xFF).astype(np.uint8)
+    qs = (xi[:, :16] & 0x0F) | ((xi[:, 16:] & 0x0F) << 4)
+    bits = ((xi >> 4) & 1).astype(np.uint32)
+    qh = (bits << np.arange(32, dtype=np.uint32)[None, :]).sum(axis=1, dtype=np.uint64).astype("<u4")
+    out = np.zeros((len(b), 22), np.uint8)
+    out[:, 0:2] = d.astype("<f2").view(np.uint8).reshape(-1, 2)
+    out[:, 2:6] = qh.view(np.uint8).reshape(-1, 4)
+    out[:, 6:22] = qs
+    return out.tobytes()
+
+
+def quantize_q5_0(src: str, dst: str) -> str:
+    """Q5_0 copy of an F16 ggml-bin model, as whisper-quantize writes it
+    (/root/reference examples/quantize/quantize.cpp:159-168, examples/common-ggml.cpp:97-230):
+    every 2-D tensor except the positional embeddings becomes Q5_0 (ttype 6), ftype becomes
+    2008 (GGML_QNT_VERSION 2 * 1000 + MOSTLY_Q5_0 8). Returns the SHA-256."""
+    skip = {"encoder.conv1.bias", "encoder.conv2.bias", "encoder.positional_embedding", "decoder.positional_embedding"}
+    raw = open(src, "rb").read()
+    off = 0
+
+    def take(n):
+        nonlocal off
+        v = raw[off:off + n]
+        off += n
+        return v
+    h = hashlib.sha256()
+    tmp = dst + ".tmp"
+    with open(tmp, "wb") as f:
+        def w(b):
+            f.write(b)
+            h.update(b)
+        w(take(4))
+        hp = list(struct.unpack("<11i", take(44)))
+        hp[10] = 2000 + 8
+        w(struct.pack("<11i", *hp))
+        n_mel, n_fft = struct.unpack("<ii", take(8))
+        w(struct.pack("<ii", n_mel, n_fft))
+        w(take(n_mel * n_fft * 4))
+        n_vocab = struct.unpack("<i", raw[off:off + 4])[0]
+        vstart = off
+        off += 4
+        for _ in range(n_vocab):
+            ln = struct.unpack("<I", raw[off:off + 4])[0]
+            off += 4 + ln
+        w(raw[vstart:off])
+        while off < len(raw):
+            n_dims, name_len, ttype = struct.unpack("<iii", take(12))
+            ne = struct.unpack("<%di" % n_dims, take(4 * n_dims))
+            name = take(name_len)
+            nel = int(np.prod(ne))
+            data = take(nel * (2 if ttype == 1 else 4))
+            quant = n_dims == 2 and name.decode() not in skip
+            w(struct.pack("<iii", n_dims, name_len, 6 if quant else ttype))
+            w(struct.pack("<%di" % n_dims, *ne))
+            w(name)
+            if quant:
+                x = np.frombuffer(data, "<f2" if ttype == 1 else "<f4").astype(np.float32)
+                w(q5_0_blocks(x))
+            else:
+                w(data)
+    os.replace(tmp, dst)
+    return h.hexdigest()
+
+
 def ensure_model(model: str, seed: int = 1234, cache_dir: str | None = None) -> str:
     """Path to a cached synthetic model (generated on first use)."""
     cache_dir = cache_dir or os.environ.get("OWK_MODEL_CACHE", "/tmp/owk_models")
     os.makedirs(cache_dir, exist_ok=True)
-    path = os.path.join(cache_dir, f"synth-{model}-s{seed}.bin")
+    q5 = model.endswith("-q5_0")
+    base = model[:-5] if q5 else model
+    path = os.path.join(cache_dir, f"synth-{base}-s{seed}.bin")
     if not os.path.exists(path):
-        write_model(path, model, seed)
+        write_model(path, base, seed)
+    if q5:
+        qpath = os.path.join(cache_dir, f"synth-{base}-q5_0-s{seed}.bin")
+        if not os.path.exists(qpath):
+            quantize_q5_0(path, qpath)
+        return qpath
     return path
 
 

@@ -259,4 +259,64 @@ void ref_timings(void * vctx, double * t_mel_ms, double * t_enc_ms, double * t_d
     *n_decode = st->n_decode;
 }
 
+// Node-by-node capture of the encoder graph (debug: localises a numerical divergence).
+// ref_capture_encoder(ctx, n) records the first n f32 nodes the scheduler evaluates on
+// the next whisper_encode; ref_capture_get(i, ...) returns node i's op, shape and data.
+struct ref_node { int op; int64_t ne[4]; std::vector<float> data; };
+static std::vector<ref_node> g_nodes;
+static int g_nodes_max = 0;
+
+static bool ref_eval_cb(struct ggml_tensor * t, bool ask, void *) {
+    if (ask) return (int) g_nodes.size() < g_nodes_max;
+    if ((int) g_nodes.size() >= g_nodes_max) return true;
+    ref_node n;
+    n.op = (int) t->op;
+    for (int i = 0; i < 4; ++i) n.ne[i] = t->ne[i];
+    if (t->type == GGML_TYPE_F32 && ggml_is_contiguous(t)) {
+        n.data.resize(ggml_nelements(t));
+        memcpy(n.data.data(), t->data, n.data.size() * 4);
+    }
+    g_nodes.push_back(std::move(n));
+    return true;
+}
+
+void ref_capture_encoder(void * vctx, int max_nodes) {
+    auto * st = ((whisper_context *) vctx)->state;
+    g_nodes.clear();
+    g_nodes_max = max_nodes;
+    ggml_backend_sched_set_eval_callback(st->sched_encode.sched, max_nodes > 0 ? ref_eval_cb : nullptr, nullptr);
+}
+
+int ref_capture_count() { return (int) g_nodes.size(); }
+
+long ref_capture_get(int i, int * op, int64_t * ne, float * out, long cap) {
+    if (i < 0 || i >= (int) g_nodes.size()) return -1;
+    const ref_node & n = g_nodes[i];
+    *op = n.op;
+    for (int k = 0; k < 4; ++k) ne[k] = n.ne[k];
+    if (out && cap >= (long) n.data.size()) memcpy(out, n.data.data(), n.data.size() * 4);
+    return (long) n.data.size();
+}
+
+// ggml's CPU mul_mat on one weight tensor: w (N rows of K, ggml type wtype, raw blocks)
+// times a (M rows of K, f32) -> out [M][N] f32. Pins the quantized-weight GEMM numerics.
+int ref_mul_mat(int wtype, const void * w, int N, int K, const float * a, int M, float * out, int n_threads) {
+    const size_t wbytes = ggml_row_size((ggml_type) wtype, K) * N;
+    ggml_init_params ip = {wbytes + (size_t) M * K * 4 + (size_t) M * N * 4 + 64 * ggml_tensor_overhead() +
+                               ggml_graph_overhead() + (1 << 20), nullptr, false};
+    ggml_context * c = ggml_init(ip);
+    if (!c) return -1;
+    ggml_tensor * tw = ggml_new_tensor_2d(c, (ggml_type) wtype, K, N);
+    ggml_tensor * ta = ggml_new_tensor_2d(c, GGML_TYPE_F32, K, M);
+    memcpy(tw->data, w, wbytes);
+    memcpy(ta->data, a, (size_t) M * K * 4);
+    ggml_tensor * y = ggml_mul_mat(c, tw, ta);
+    ggml_cgraph * gf = ggml_new_graph(c);
+    ggml_build_forward_expand(gf, y);
+    const int rc = ggml_graph_compute_with_ctx(c, gf, n_threads) == GGML_STATUS_SUCCESS ? 0 : -2;
+    if (rc == 0) memcpy(out, y->data, (size_t) M * N * 4);
+    ggml_free(c);
+    return rc;
+}
+
 } // extern "C"

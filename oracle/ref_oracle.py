@@ -129,6 +129,11 @@ class Ref:
         lg = np.ctypeslib.as_array(self.L.ref_logits(self.ctx), shape=(len(tokens) * self.n_vocab,))
         return lg[(len(tokens) - 1) * self.n_vocab:].copy()
 
+    def decode_steps(self, tokens, n_threads=8):
+        """Teacher-forced decode, one token per call from position 0 (the reference only
+        computes the last row of a call, whisper.cpp:2950-2955): [len(tokens)][n_vocab]."""
+        return np.stack([self.decode([t], i, n_threads) for i, t in enumerate(tokens)])
+
     def full(self, pcm, strategy=0, n_threads=8, best_of=5, beam_size=5, temperature=0.0, temperature_inc=0.2,
              no_timestamps=False, max_tokens=0, suppress_eot=False, token_timestamps=False, no_context=True,
              single_segment=False, language="en", suppress_nst=False, length_penalty=-1.0, record_topk=False):

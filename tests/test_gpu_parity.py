@@ -144,7 +144,7 @@ def _flat(segs):
     return [(si, t) for si, s in enumerate(segs) for t in s["tokens"]]
 
 
-def _compare(got, want, key, exact=False, p_atol=2e-3):
+def _compare(got, want, key, exact=False, p_atol=2e-3, tie=TIE_LOGIT):
     """Token ids, segment bounds, text and token timestamps identical to the reference.
 
     Deterministic configs (exact=False) are compared up to the first step where the two
@@ -157,7 +157,7 @@ def _compare(got, want, key, exact=False, p_atol=2e-3):
     for i, ((sg, g), (sw, r)) in enumerate(zip(fg, fw)):
         if g[0] != r[0]:
             gap = abs(g[3] - r[3])
-            assert not exact and gap < TIE_LOGIT, (
+            assert not exact and gap < tie, (
                 f"{key}: token {i} is {g[0]} vs reference {r[0]} (logprob {g[3]:.5f} vs {r[3]:.5f})")
             # finished segments before the divergence must agree completely
             n_done = min(sg, sw)
