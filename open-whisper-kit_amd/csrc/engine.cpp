@@ -372,8 +372,17 @@ void Engine::download_cross(int slot, int layer, uint16_t * kh, uint16_t * vh) c
     OWK_HIP_CHECK(hipStreamSynchronize(stream));
     const size_t per = (size_t) hp.n_audio_ctx * hp.n_text_state;
     const size_t o = ((size_t) layer * cap_slots + slot) * per;
-    OWK_HIP_CHECK(hipMemcpy(kh, cross_k_.as<_Float16>() + o, per * 2, hipMemcpyDeviceToHost));
-    OWK_HIP_CHECK(hipMemcpy(vh, cross_v_.as<_Float16>() + o, per * 2, hipMemcpyDeviceToHost));
+    // device layout is head-major [head][t][64]; the caller gets the reference's [t][d]
+    const int T = hp.n_audio_ctx, d = hp.n_text_state, H = d / 64;
+    std::vector<uint16_t> tk(per), tv(per);
+    OWK_HIP_CHECK(hipMemcpy(tk.data(), cross_k_.as<_Float16>() + o, per * 2, hipMemcpyDeviceToHost));
+    OWK_HIP_CHECK(hipMemcpy(tv.data(), cross_v_.as<_Float16>() + o, per * 2, hipMemcpyDeviceToHost));
+    for (int h = 0; h < H; ++h)
+        for (int t = 0; t < T; ++t)
+            for (int j = 0; j < 64; ++j) {
+                kh[(size_t) t * d + h * 64 + j] = tk[((size_t) h * T + t) * 64 + j];
+                vh[(size_t) t * d + h * 64 + j] = tv[((size_t) h * T + t) * 64 + j];
+            }
 }
 
 // decode staging: one pinned host image + its device copy, fixed sections sized by the
@@ -497,6 +506,7 @@ void Engine::decode(const std::vector<DecodeRow> & rows, const std::vector<int> 
                 rs[r].key_list = -1;
             }
         }
+        if (x.mode_self == 0 && x.n_keys > 0 && rs[r].key_list >= 0) sh.self_list = true;
         // soft_max rows attend over exactly n_audio_ctx keys (no FA padding, whisper.cpp:2700-2712)
         rc[r] = AttnRow{r, (int) ((int64_t) x.slot * T * d), T, -1, x.mode_cross == 2 ? 0 : n_ctx_pad - T, x.mode_cross};
         sh.max_keys = std::max(sh.max_keys, x.n_keys);
@@ -529,7 +539,8 @@ void Engine::decode(const std::vector<DecodeRow> & rows, const std::vector<int> 
     }
     const uint64_t key = (uint64_t) R | ((uint64_t) n_logit_rows << 20) | ((uint64_t) sh.self_oc << 40) |
                          ((uint64_t) sh.self_tl << 41) | ((uint64_t) sh.cross_oc << 42) | ((uint64_t) sh.cross_tl << 43) |
-                         ((uint64_t) sh.self_sm << 44) | ((uint64_t) sh.cross_sm << 45);
+                         ((uint64_t) sh.self_sm << 44) | ((uint64_t) sh.cross_sm << 45) |
+                         ((uint64_t) sh.self_list << 46);
     auto it = graphs_.find(key);
     if (it == graphs_.end()) {
         if (graphs_.size() >= 64) clear_graphs();
@@ -633,10 +644,11 @@ void Engine::launch_decode(const DecShape & sh) {
         }
         {
             ProfScope ps(prof, stream, "attn_self");
-            attn_decoder(stream, d_q_.as<_Float16>(), d, Kl, Vl, d, d_rs, R, d_keys, H,
-                         1.0f, max_keys, d_ao_.as<_Float16>(), d, self_oc, self_tl, ao32);
+            // one_chunk rows all on contiguous cell runs: the list-free kernel (see k_attn_step)
+            attn_decoder(stream, d_q_.as<_Float16>(), d, Kl, Vl, d, 64, d_rs, R, d_keys, H, 1.0f, max_keys,
+                         d_ao_.as<_Float16>(), d, self_oc, self_tl, ao32, sh.self_list);
             if (sh.self_sm)  // masked soft_max with scale 1 (Q, K pre-scaled; whisper.cpp:2614-2628)
-                attn_decoder_softmax(stream, d_q_.as<_Float16>(), d, Kl, Vl, d, d_rs, R, d_keys, H, 1.0f, max_keys,
+                attn_decoder_softmax(stream, d_q_.as<_Float16>(), d, Kl, Vl, d, 64, d_rs, R, d_keys, H, 1.0f, max_keys,
                                      d_ao_.as<_Float16>(), d, nullptr, nullptr, 0, ao32);
         }
         if (fused) {
@@ -656,11 +668,11 @@ void Engine::launch_decode(const DecShape & sh) {
             // bytes: cross K and V of each row's clip (the HBM-bound part of a decode step)
             ProfScope ps(prof, stream, "attn_cross", 4.0 * R * (double) n_ctx_pad * d, 2.0 * 2.0 * R * (double) T * d);
             attn_decoder(stream, d_q_.as<_Float16>(), d, cross_k_.as<_Float16>() + l * cross_stride,
-                         cross_v_.as<_Float16>() + l * cross_stride, d, d_rc, R, nullptr, H,
+                         cross_v_.as<_Float16>() + l * cross_stride, 64, T * 64, d_rc, R, nullptr, H,
                          kq_scale, T, d_ao_.as<_Float16>(), d, cross_oc, cross_tl, ao32);
             if (sh.cross_sm)  // soft_max_ext(KQ, nullptr, KQscale) over n_audio_ctx keys (whisper.cpp:2697-2738)
                 attn_decoder_softmax(stream, d_q_.as<_Float16>(), d, cross_k_.as<_Float16>() + l * cross_stride,
-                                     cross_v_.as<_Float16>() + l * cross_stride, d, d_rc, R, nullptr, H, kq_scale, T,
+                                     cross_v_.as<_Float16>() + l * cross_stride, 64, T * 64, d_rc, R, nullptr, H, kq_scale, T,
                                      d_ao_.as<_Float16>(), d, sh.capture ? amap_.as<int>() + l * H : nullptr,
                                      sh.capture ? cap_.as<float>() : nullptr, R, ao32);
         }

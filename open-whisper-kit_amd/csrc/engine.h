@@ -64,6 +64,7 @@ struct DecShape {
     int max_keys;
     bool self_sm = false, cross_sm = false;     // soft_max rows (flash_attn = false contexts)
     bool capture = false;                       // DTW: capture alignment-head cross-attention
+    bool self_list = false;                     // a one_chunk self row whose cells are not one run
 };
 
 // per-step bookkeeping of the emulated reference state->logits buffer (no-speech prob)

@@ -388,12 +388,17 @@ __device__ __forceinline__ void wait_vmcnt() {
 
 constexpr int AS_MAX_LIST = 2048;  // listed keys (self-attention cells) per row
 
-template <bool LIST>
+// CROSS: the head-major cross K/V (non-temporal loads; also names the instantiation so cross
+// and self attention are apart in profiles)
+template <bool LIST, bool CROSS>
 __global__ __launch_bounds__(64) void k_attn_step(const _Float16 * __restrict__ q, int ldq,
                                                   const _Float16 * __restrict__ kb, const _Float16 * __restrict__ vb,
-                                                  int ld_kv, const AttnRow * __restrict__ rows,
+                                                  int ld_kv, int hs, const AttnRow * __restrict__ rows,
                                                   const int * __restrict__ key_idx, float scale,
                                                   _Float16 * __restrict__ out, int ldo, float * __restrict__ out32) {
+    // NOTE: any ordinary LDS store in this kernel (s_list below) makes the compiler drain
+    // every in-flight global_load_lds (s_waitcnt vmcnt(0)) before the ring reads of each
+    // chunk; the host therefore launches LIST = true only for passes with a listed row
     __shared__ __attribute__((aligned(1024))) char smem[AS_NBUF * 2 * AS_TILE];
     __shared__ int s_list[LIST ? AS_MAX_LIST : 1];
     const int lane = threadIdx.x;
@@ -417,8 +422,8 @@ __global__ __launch_bounds__(64) void k_attn_step(const _Float16 * __restrict__ 
         __builtin_amdgcn_s_waitcnt(0);
         __builtin_amdgcn_wave_barrier();
     }
-    const _Float16 * kh = kb + job.kv_base + h * 64;
-    const _Float16 * vh = vb + job.kv_base + h * 64;
+    const _Float16 * kh = kb + job.kv_base + (size_t) h * hs;
+    const _Float16 * vh = vb + job.kv_base + (size_t) h * hs;
 
     // q of this (row, head): uniform -> scalar registers
     const half8 * qp = (const half8 *) (q + (size_t) job.q_row * ldq + h * 64);
@@ -437,34 +442,33 @@ __global__ __launch_bounds__(64) void k_attn_step(const _Float16 * __restrict__ 
             const int key = min(c * AS_KC + kk, n - 1);
             const int cell = listed ? s_list[key] : key;
             const int seg = (lane & 7) ^ (kk & 7);  // K rows XOR-swizzled for the lane-per-key reads
+            // cross K/V are read once per decode step (larger than the MALL): non-temporal
             __builtin_amdgcn_global_load_lds((const void *) (kh + (size_t) cell * ld_kv + seg * 8),
-                                             (lds_ptr_t) (sK + i * 1024), 16, 0, 0);
+                                             (lds_ptr_t) (sK + i * 1024), 16, 0, CROSS ? 2 : 0);
             __builtin_amdgcn_global_load_lds((const void *) (vh + (size_t) cell * ld_kv + (lane & 7) * 8),
-                                             (lds_ptr_t) (sV + i * 1024), 16, 0, 0);
+                                             (lds_ptr_t) (sV + i * 1024), 16, 0, CROSS ? 2 : 0);
         }
     };
 
     float M = -INFINITY, S = 0.0f;
     _Float16 acc = (_Float16) 0.0f;  // the reference's F16 VKQ accumulator (VKQ16)
 #pragma unroll
-    for (int c = 0; c < AS_NBUF - 1; ++c)
+    for (int c = 0; c < AS_NBUF; ++c)
         if (c < nchunks) stage(c, c);
 
     for (int c = 0; c < nchunks; ++c) {
-        if (c + AS_NBUF - 1 < nchunks) {
-            stage((c + AS_NBUF - 1) % AS_NBUF, c + AS_NBUF - 1);
-            wait_vmcnt<16 * (AS_NBUF - 1)>();
-        } else if (c + 1 < nchunks) {
-            wait_vmcnt<16>();
-        } else {
-            wait_vmcnt<0>();
-        }
+        // chunk c has landed once at most the chunks staged after it are outstanding
+        const int ahead = min(AS_NBUF - 1, nchunks - 1 - c);
+        static_assert(AS_NBUF == 3, "vmcnt ladder below assumes 3 buffers");
+        if (ahead == 2) wait_vmcnt<32>();
+        else if (ahead == 1) wait_vmcnt<16>();
+        else wait_vmcnt<0>();
         const char * sK = smem + (c % AS_NBUF) * 2 * AS_TILE;
         const char * sV = sK + AS_TILE;
         const int base = c * AS_KC;
         const int nk = min(AS_KC, n - base);
 
-        // 2. scores, lane = key (8 independent partial sums: short dependency chains)
+        // 2. scores, lane = key: f32 dot2 of f16 pairs, 8 independent partial sums
         float s;
         {
             const char * kr = sK + lane * 128;
@@ -474,7 +478,10 @@ __global__ __launch_bounds__(64) void k_attn_step(const _Float16 * __restrict__ 
                 const half8 kv = *(const half8 *) (kr + ((cc ^ (lane & 7)) << 4));
                 float a = 0.0f;
 #pragma unroll
-                for (int e = 0; e < 8; ++e) a = fmaf((float) kv[e], (float) qv[cc][e], a);
+                for (int e = 0; e < 8; e += 2) {
+                    const half2v k2 = {kv[e], kv[e + 1]}, q2 = {qv[cc][e], qv[cc][e + 1]};
+                    a = __builtin_amdgcn_fdot2(k2, q2, a, false);
+                }
                 part[cc] = a;
             }
             const float a = ((part[0] + part[1]) + (part[2] + part[3])) + ((part[4] + part[5]) + (part[6] + part[7]));
@@ -489,14 +496,33 @@ __global__ __launch_bounds__(64) void k_attn_step(const _Float16 * __restrict__ 
         const float vs = nm ? 1.0f : e;
         M = fmaxf(M, __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, pm), 63)));
 
-        // 3. recurrence, lane = head dim
+        // 3. recurrence, lane = head dim. A full chunk's V column goes to registers first, so
+        // the chunk's buffer is refilled (chunk c + AS_NBUF) before the sequential part runs:
+        // AS_NBUF chunks stay in flight across it
         const _Float16 * vcol = (const _Float16 *) sV + lane;
-        // acc*ms with ms == 1 is exact, so the rescale is applied unconditionally (branch-free)
-        // and each key costs two dependent mixed-precision FMAs (f32 math, f16 result)
-        if (nk == AS_KC) {
-            _Float16 vv[AS_KC];
+        const bool full = nk == AS_KC;
+        _Float16 vv[AS_KC];
+        if (full) {
 #pragma unroll
             for (int kk = 0; kk < AS_KC; ++kk) vv[kk] = vcol[kk * 64];
+        }
+        if (c + AS_NBUF < nchunks) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // K and V reads of this buffer done
+            stage(c % AS_NBUF, c + AS_NBUF);
+        }
+        if (full && __builtin_amdgcn_ballot_w64(nm) == 0) {
+            // no new maximum in the chunk (the common case once the first keys are seen):
+            // every ms is 1, so acc*ms and S*ms are exact and each key costs one mixed FMA on
+            // acc and one add on S (vs broadcast by readlane)
+#pragma unroll
+            for (int kk = 0; kk < AS_KC; ++kk) {
+                const float vsk = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, vs), kk));
+                acc = (_Float16) fmaf((float) vv[kk], vsk, (float) acc);
+                S = S + vsk;
+            }
+        } else if (full) {
+            // acc*ms with ms == 1 is exact, so the rescale is applied unconditionally (branch-free)
+            // and each key costs two dependent mixed-precision FMAs (f32 math, f16 result)
 #pragma unroll
             for (int kk = 0; kk < AS_KC; ++kk) {
                 const float msk = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, ms), kk));
@@ -505,7 +531,7 @@ __global__ __launch_bounds__(64) void k_attn_step(const _Float16 * __restrict__ 
                 acc = (_Float16) fmaf((float) vv[kk], vsk, (float) acc);
                 S = fmaf(S, msk, vsk);
             }
-        } else {
+        } else {  // the last, partial chunk (nothing staged after it)
             for (int kk = 0; kk < nk; ++kk) {
                 const float msk = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, ms), kk));
                 const float vsk = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, vs), kk));
@@ -538,7 +564,7 @@ constexpr int DA_MAX_KEYS = 2048;
 
 __global__ __launch_bounds__(256) void k_attn_decoder(const _Float16 * __restrict__ q, int ldq,
                                                       const _Float16 * __restrict__ kb, const _Float16 * __restrict__ vb,
-                                                      int ld_kv, const AttnRow * __restrict__ rows,
+                                                      int ld_kv, int hs, const AttnRow * __restrict__ rows,
                                                       const int * __restrict__ key_idx, int H, float scale,
                                                       _Float16 * __restrict__ out, int ldo, float * __restrict__ out32) {
     __shared__ float sc[4][DA_MAX_KEYS];
@@ -550,8 +576,8 @@ __global__ __launch_bounds__(256) void k_attn_decoder(const _Float16 * __restric
     if (h >= H) return;
     const int n = job.n_keys;
     const int * list = job.key_list >= 0 ? key_idx + job.key_list : nullptr;
-    const _Float16 * kh = kb + job.kv_base + h * 64;
-    const _Float16 * vh = vb + job.kv_base + h * 64;
+    const _Float16 * kh = kb + job.kv_base + (size_t) h * hs;
+    const _Float16 * vh = vb + job.kv_base + (size_t) h * hs;
 
     qs[wave][lane] = q[(size_t) job.q_row * ldq + h * 64 + lane];
     __builtin_amdgcn_wave_barrier();
@@ -655,7 +681,7 @@ constexpr int SM_MAX_KEYS = 2048;
 
 __global__ __launch_bounds__(256) void k_attn_softmax(const _Float16 * __restrict__ q, int ldq,
                                                       const _Float16 * __restrict__ kb, const _Float16 * __restrict__ vb,
-                                                      int ld_kv, const AttnRow * __restrict__ rows,
+                                                      int ld_kv, int hs, const AttnRow * __restrict__ rows,
                                                       const int * __restrict__ key_idx, float scale,
                                                       _Float16 * __restrict__ out, int ldo,
                                                       const int * __restrict__ amap, float * __restrict__ cap,
@@ -671,8 +697,8 @@ __global__ __launch_bounds__(256) void k_attn_softmax(const _Float16 * __restric
     const int h = blockIdx.x;
     const int n = job.n_keys;
     const int * list = job.key_list >= 0 ? key_idx + job.key_list : nullptr;
-    const _Float16 * kh = kb + job.kv_base + h * 64;
-    const _Float16 * vh = vb + job.kv_base + h * 64;
+    const _Float16 * kh = kb + job.kv_base + (size_t) h * hs;
+    const _Float16 * vh = vb + job.kv_base + (size_t) h * hs;
     const _Float16 * qr = q + (size_t) job.q_row * ldq + h * 64;
 
     // scores
@@ -736,12 +762,12 @@ __global__ __launch_bounds__(256) void k_attn_softmax(const _Float16 * __restric
 }
 
 void attn_decoder_softmax(hipStream_t s, const _Float16 * q, int ldq, const _Float16 * kbase, const _Float16 * vbase,
-                          int ld_kv, const AttnRow * rows_dev, int n_rows, const int * key_idx, int H, float scale,
+                          int ld_kv, int hs, const AttnRow * rows_dev, int n_rows, const int * key_idx, int H, float scale,
                           int max_keys, _Float16 * out, int ldo, const int * amap, float * cap, int cap_rows,
                           float * out32) {
     if (n_rows <= 0) return;
     if (max_keys > SM_MAX_KEYS) throw std::runtime_error("attn_decoder_softmax: too many keys");
-    hipLaunchKernelGGL(k_attn_softmax, dim3(H, n_rows), dim3(256), 0, s, q, ldq, kbase, vbase, ld_kv, rows_dev, key_idx,
+    hipLaunchKernelGGL(k_attn_softmax, dim3(H, n_rows), dim3(256), 0, s, q, ldq, kbase, vbase, ld_kv, hs, rows_dev, key_idx,
                        scale, out, ldo, amap, cap, cap_rows, out32);
 }
 
@@ -749,23 +775,27 @@ int attn_max_listed_keys() { return AS_MAX_LIST; }
 int attn_max_tiled_keys() { return DA_MAX_KEYS; }
 
 void attn_decoder(hipStream_t s, const _Float16 * q, int ldq, const _Float16 * kbase, const _Float16 * vbase, int ld_kv,
-                  const AttnRow * rows_dev, int n_rows, const int * key_idx, int H, float scale, int max_keys,
-                  _Float16 * out, int ldo, bool any_one_chunk, bool any_tiled, float * out32) {
+                  int hs, const AttnRow * rows_dev, int n_rows, const int * key_idx, int H, float scale, int max_keys,
+                  _Float16 * out, int ldo, bool any_one_chunk, bool any_tiled, float * out32, bool oc_listed) {
     if (n_rows <= 0) return;
     if (any_one_chunk) {
-        if (key_idx) {
+        if (key_idx && oc_listed) {
             if (max_keys > AS_MAX_LIST) throw std::runtime_error("attn_decoder: too many listed keys");
-            hipLaunchKernelGGL(k_attn_step<true>, dim3(H, n_rows), dim3(64), 0, s, q, ldq, kbase, vbase, ld_kv, rows_dev,
-                               key_idx, scale, out, ldo, out32);
+            hipLaunchKernelGGL((k_attn_step<true, false>), dim3(H, n_rows), dim3(64), 0, s, q, ldq, kbase, vbase, ld_kv, hs,
+                               rows_dev, key_idx, scale, out, ldo, out32);
         } else {
-            hipLaunchKernelGGL(k_attn_step<false>, dim3(H, n_rows), dim3(64), 0, s, q, ldq, kbase, vbase, ld_kv, rows_dev,
-                               key_idx, scale, out, ldo, out32);
+            if (hs != 64)  // head-major cross K/V
+                hipLaunchKernelGGL((k_attn_step<false, true>), dim3(H, n_rows), dim3(64), 0, s, q, ldq, kbase, vbase, ld_kv,
+                                   hs, rows_dev, key_idx, scale, out, ldo, out32);
+            else
+                hipLaunchKernelGGL((k_attn_step<false, false>), dim3(H, n_rows), dim3(64), 0, s, q, ldq, kbase, vbase, ld_kv,
+                                   hs, rows_dev, key_idx, scale, out, ldo, out32);
         }
     }
     if (any_tiled) {
         if (max_keys > DA_MAX_KEYS) throw std::runtime_error("attn_decoder: too many keys");
         hipLaunchKernelGGL(k_attn_decoder, dim3((H + 3) / 4, n_rows), dim3(256), 0, s, q, ldq, kbase, vbase, ld_kv,
-                           rows_dev, key_idx, H, scale, out, ldo, out32);
+                           hs, rows_dev, key_idx, H, scale, out, ldo, out32);
     }
 }
 

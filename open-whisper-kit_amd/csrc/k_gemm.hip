@@ -55,11 +55,14 @@ __device__ __forceinline__ void epi_store(const EpiParams & p, int r, int c, flo
     } else if constexpr (MODE == EPI_KV_CROSS) {
         const int d = p.d;
         const int clip = r / p.T, t = r - clip * p.T;
-        const size_t row = (size_t) (p.slot_map ? p.slot_map[clip] : clip) * p.T + t;
+        // head-major cache [slot][head][t][64]: one (row, head) of a decode step streams its
+        // keys (and values) as one contiguous run
+        const size_t base = (size_t) (p.slot_map ? p.slot_map[clip] : clip) * p.T * d + (size_t) t * 64;
         if (c < d) {
-            p.out16b[row * d + c] = (_Float16) (acc * p.scale);
+            p.out16b[base + (size_t) (c >> 6) * p.T * 64 + (c & 63)] = (_Float16) (acc * p.scale);
         } else {
-            p.out16c[row * d + (c - d)] = (_Float16) (acc + p.bias2[c - d]);
+            const int cv = c - d;
+            p.out16c[base + (size_t) (cv >> 6) * p.T * 64 + (cv & 63)] = (_Float16) (acc + p.bias2[cv]);
         }
     } else if constexpr (MODE == EPI_QKV_DEC) {
         const int d = p.d;

@@ -21,8 +21,7 @@ __device__ __forceinline__ double wave_sum_d(double v) {
 // ----------------------------------------------------------------------------------
 constexpr int LN_V4 = 8;  // float4 per lane held in registers -> d <= 2048
 
-// LayerNorm of one row held in registers (lane owns float4 groups lane + 64 j); shared by
-// k_layernorm_f16 and k_resid_layernorm so both produce identical bits
+// LayerNorm of one row held in registers (lane owns float4 groups lane + 64 j)
 __device__ __forceinline__ void ln_row_regs(const float4 (&xv)[LN_V4], int lane, int d, const float * __restrict__ w,
                                             const float * __restrict__ b, float eps, _Float16 * __restrict__ o,
                                             float * __restrict__ o32) {
@@ -86,20 +85,35 @@ __global__ __launch_bounds__(256) void k_layernorm_f16(const float * __restrict_
 // Finishes an EPI_PARTIAL decode-row GEMM: sums its k splits in order (row-major partial
 // rows [ks][M][N], k_gemm.hip), adds bias and the residual (out = resid + (acc + bias),
 // whisper.cpp's ggml_add(mul_mat + b, inpL)), writes the new residual row, then LayerNorms it
-// for the next matmul.
+// for the next matmul. One 256-thread block per row (a decode pass has <= 32 rows, so the
+// row's partial loads are spread over 4 waves instead of one); the LayerNorm statistics are
+// the same double sums as ln_row_regs (exact for a row of f32 values; the variance sum
+// differs from the one-wave order only below double precision).
+constexpr int RL_V4 = 2;  // float4 per thread -> N <= 2048
+
+__device__ __forceinline__ double block_sum_d(double v, double * red) {
+    v = wave_sum_d(v);
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) red[w] = v;
+    __syncthreads();
+    const double t = (red[0] + red[1]) + (red[2] + red[3]);
+    __syncthreads();
+    return t;
+}
+
 __global__ __launch_bounds__(256) void k_resid_layernorm(int M, int N, int KS, const float * __restrict__ part,
                                                          const float * __restrict__ bias, float * __restrict__ x,
                                                          const float * __restrict__ w, const float * __restrict__ b,
                                                          float eps, _Float16 * __restrict__ xn, int ldo) {
-    const int lane = threadIdx.x & 63;
-    const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (row >= M) return;
+    __shared__ double red[4];
+    const int t = threadIdx.x;
+    const int row = blockIdx.x;
     const int n4 = N >> 2;
     float4 * xr = (float4 *) (x + (size_t) row * N);
-    float4 xv[LN_V4];
+    float4 xv[RL_V4];
 #pragma unroll
-    for (int j = 0; j < LN_V4; ++j) {
-        const int i = lane + 64 * j;
+    for (int j = 0; j < RL_V4; ++j) {
+        const int i = t + 256 * j;
         float4 r = float4{0.f, 0.f, 0.f, 0.f};
         if (i < n4) {
             float4 a = ((const float4 *) (part + (size_t) row * N))[i];
@@ -117,15 +131,45 @@ __global__ __launch_bounds__(256) void k_resid_layernorm(int M, int N, int KS, c
         }
         xv[j] = r;
     }
-    if (w) ln_row_regs(xv, lane, N, w, b, eps, xn + (size_t) row * ldo, nullptr);
+    if (!w) return;
+    double s = 0.0;
+#pragma unroll
+    for (int j = 0; j < RL_V4; ++j)
+        s += ((double) xv[j].x + (double) xv[j].y) + ((double) xv[j].z + (double) xv[j].w);
+    s = block_sum_d(s, red);
+    const float mean = (float) s / (float) N;
+    double v = 0.0;
+#pragma unroll
+    for (int j = 0; j < RL_V4; ++j) {
+        if (t + 256 * j < n4) {
+            const float tx = xv[j].x - mean, ty = xv[j].y - mean, tz = xv[j].z - mean, tw = xv[j].w - mean;
+            v += ((double) (tx * tx) + (double) (ty * ty)) + ((double) (tz * tz) + (double) (tw * tw));
+        }
+    }
+    v = block_sum_d(v, red);
+    const float var = (float) (v / (double) N);
+    const float scale = 1.0f / sqrtf(var + eps);
+    _Float16 * o = xn + (size_t) row * ldo;
+#pragma unroll
+    for (int j = 0; j < RL_V4; ++j) {
+        const int i = t + 256 * j;
+        if (i < n4) {
+            const float4 ww = ((const float4 *) w)[i], bb = ((const float4 *) b)[i];
+            half4 h;
+            h[0] = (_Float16) ((xv[j].x - mean) * scale * ww.x + bb.x);
+            h[1] = (_Float16) ((xv[j].y - mean) * scale * ww.y + bb.y);
+            h[2] = (_Float16) ((xv[j].z - mean) * scale * ww.z + bb.z);
+            h[3] = (_Float16) ((xv[j].w - mean) * scale * ww.w + bb.w);
+            *(half4 *) (o + 4 * i) = h;
+        }
+    }
 }
 
 void resid_layernorm(hipStream_t s, int M, int N, int ks, const float * part, const float * bias, float * x,
                      const float * lnw, const float * lnb, float eps, _Float16 * xn, int ldo) {
     if (M <= 0) return;
-    if (M > 32 || N % 16 != 0 || N > 4 * 64 * LN_V4) throw std::runtime_error("resid_layernorm: unsupported shape");
-    hipLaunchKernelGGL(k_resid_layernorm, dim3((M + 3) / 4), dim3(256), 0, s, M, N, ks, part, bias, x, lnw, lnb, eps,
-                       xn, ldo);
+    if (M > 32 || N % 16 != 0 || N > 4 * 256 * RL_V4) throw std::runtime_error("resid_layernorm: unsupported shape");
+    hipLaunchKernelGGL(k_resid_layernorm, dim3(M), dim3(256), 0, s, M, N, ks, part, bias, x, lnw, lnb, eps, xn, ldo);
 }
 
 void layernorm_f16(hipStream_t s, const float * x, int rows, int d, const float * w, const float * b, float eps,

@@ -165,13 +165,16 @@ struct AttnRow {
     int n_zero_pad;     // trailing all-zero keys (cross attention padding)
     int mode;           // 0 = one_chunk (F16 accumulator), 1 = tiled (F32 accumulator), 2 = soft_max (no FA)
 };
+// ld_kv: elements between consecutive keys; hs: elements between consecutive heads (64 for
+// the interleaved [cell][d] self-attention cache, n_keys * 64 for the head-major cross K/V)
 void attn_decoder(hipStream_t s, const _Float16 * q, int ldq, const _Float16 * kbase, const _Float16 * vbase,
-                  int ld_kv, const AttnRow * rows_dev, int n_rows, const int * key_idx, int H, float scale,
-                  int max_keys, _Float16 * out, int ldo, bool any_one_chunk, bool any_tiled, float * out32 = nullptr);
+                  int ld_kv, int hs, const AttnRow * rows_dev, int n_rows, const int * key_idx, int H, float scale,
+                  int max_keys, _Float16 * out, int ldo, bool any_one_chunk, bool any_tiled, float * out32 = nullptr,
+                  bool oc_listed = true);  // false: every one_chunk row is a contiguous cell run
 // rows with mode 2 (flash_attn = false contexts): soft_max attention, F16 probabilities;
 // optional DTW capture of alignment-head probabilities cap[a][key][row] (amap: head -> a or -1)
 void attn_decoder_softmax(hipStream_t s, const _Float16 * q, int ldq, const _Float16 * kbase, const _Float16 * vbase,
-                          int ld_kv, const AttnRow * rows_dev, int n_rows, const int * key_idx, int H, float scale,
+                          int ld_kv, int hs, const AttnRow * rows_dev, int n_rows, const int * key_idx, int H, float scale,
                           int max_keys, _Float16 * out, int ldo, const int * amap, float * cap, int cap_rows,
                           float * out32 = nullptr);
 int attn_max_listed_keys();  // per-row limit of the one_chunk kernel's key list

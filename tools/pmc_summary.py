@@ -34,4 +34,5 @@ def main(d, counter):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else "FETCH_SIZE")
+    for c in (sys.argv[2] if len(sys.argv) > 2 else "FETCH_SIZE").split(","):
+        main(sys.argv[1], c)
