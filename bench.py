@@ -46,7 +46,7 @@ CLIP_SAMPLES = 480000     # 30 s at 16 kHz
 MFMA_CLASSES = {"gemm_enc", "gemm_cross", "gemm_conv", "gemm_dec_big", "gemm_logits_big", "attn_encoder"}
 MAX_TOKENS = 219          # completion at i >= max_tokens -> 220 tokens per clip
 # kernel symbol of each single-kernel class (for the PMC traffic lookup)
-CLASS_KERNEL = {"attn_cross": "k_attn_stepILb0", "attn_self": "k_attn_stepILb1", "attn_encoder": "k_attn_encoder"}
+CLASS_KERNEL = {"attn_cross": "k_attn_stepILb0ELb1", "attn_self": "k_attn_stepILb0ELb0", "attn_encoder": "k_attn_encoder"}
 PMC_SUMMARY = os.path.join(ROOT, "profiles", "pmc_fetch_summary.txt")
 
 
