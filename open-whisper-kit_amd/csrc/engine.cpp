@@ -178,7 +178,7 @@ void Engine::download_mel(int slot, float * host) const {
 static double gemm_flops(double M, double N, double K) { return 2.0 * M * N * K; }
 
 void Engine::linear(const char * cls, int mode, int M, int N, int K, const _Float16 * A16, const float * A32, int lda,
-                    const _Float16 * W, const Q5W & q, const EpiParams & ep, const _Float16 * Wt, bool dec) {
+                    const _Float16 * W, const Q5W & q, const EpiParams & ep, const _Float16 * Wt, bool dec, bool a_q8) {
     if (!q) {
         ProfScope ps(prof, stream, cls, gemm_flops(M, N, K), 2.0 * ((double) M * K + (double) N * K));
         if (dec) gemm(stream, mode, M, N, K, A16, lda, W, K, ep, &gws_, Wt);
@@ -186,8 +186,9 @@ void Engine::linear(const char * cls, int mode, int M, int N, int K, const _Floa
         return;
     }
     // the reference rounds each activation row to Q8_0 (x86 quantize_row_q8_0) before the
-    // q5_0 x q8_0 dot; bytes: Q5_0 weights at 22 B per 32 + the int8 activations
-    {
+    // q5_0 x q8_0 dot; bytes: Q5_0 weights at 22 B per 32 + the int8 activations. a_q8: the
+    // producer (LayerNorm, one_chunk attention) already wrote q8a_ / q8d_
+    if (!a_q8) {
         ProfScope ps(prof, stream, "quantize_q8");
         quantize_q8(stream, A32, A16, lda, M, K, q8a_.as<int8_t>(), q8d_.as<float>());
     }
@@ -223,7 +224,6 @@ void Engine::encode(const std::vector<int> & slots, const std::vector<int> & off
         e_enc_.alloc((size_t) M * d * 2);
         e_enc32_.alloc((size_t) M * d * 4);
         if (m->q5) {
-            e_xn32_.alloc((size_t) M * d * 4);
             e_ao32_.alloc((size_t) M * d * 4);
             q8a_.alloc(std::max(q8a_.bytes, (size_t) M * 4 * d));
             q8d_.alloc(std::max(q8d_.bytes, (size_t) M * 4 * d / 32 * 4));
@@ -278,7 +278,7 @@ void Engine::encode(const std::vector<int> & slots, const std::vector<int> & off
         {
             ProfScope ps(prof, stream, "layernorm");
             layernorm_f16(stream, e_x_.as<float>(), M, d, L.attn_ln_w, L.attn_ln_b, hp.eps, e_xn_.as<_Float16>(), d,
-                          nullptr, m->q5 ? e_xn32_.as<float>() : nullptr);
+                          nullptr, nullptr, q8a(), q8d());
         }
         {
             EpiParams ep;
@@ -290,7 +290,8 @@ void Engine::encode(const std::vector<int> & slots, const std::vector<int> & off
             ep.d = d;
             ep.T = T;
             ep.Tpad = Tpad;
-            linear("gemm_enc", EPI_QKV_ENC, M, 3 * d, d, e_xn_.as<_Float16>(), e_xn32_.as<float>(), d, L.w_qkv, L.q_qkv, ep);
+            linear("gemm_enc", EPI_QKV_ENC, M, 3 * d, d, e_xn_.as<_Float16>(), nullptr, d, L.w_qkv, L.q_qkv, ep, nullptr,
+                   false, m->q5);
         }
         {
             // 4*T*Tpad_kv*d flops (QK^T and PV over the 1536 reference keys)
@@ -314,7 +315,7 @@ void Engine::encode(const std::vector<int> & slots, const std::vector<int> & off
         {
             ProfScope ps(prof, stream, "layernorm");
             layernorm_f16(stream, e_x_.as<float>(), M, d, L.mlp_ln_w, L.mlp_ln_b, hp.eps, e_xn_.as<_Float16>(), d,
-                          nullptr, m->q5 ? e_xn32_.as<float>() : nullptr);
+                          nullptr, nullptr, q8a(), q8d());
         }
         {
             EpiParams ep;
@@ -322,8 +323,8 @@ void Engine::encode(const std::vector<int> & slots, const std::vector<int> & off
             ep.gelu_tab = m->gelu_tab;
             ep.out16 = e_h_.as<_Float16>();
             ep.ldo = 4 * d;
-            linear("gemm_enc", EPI_GELU_F16, M, 4 * d, d, e_xn_.as<_Float16>(), e_xn32_.as<float>(), d, L.w_mlp0, L.q_mlp0,
-                   ep);
+            linear("gemm_enc", EPI_GELU_F16, M, 4 * d, d, e_xn_.as<_Float16>(), nullptr, d, L.w_mlp0, L.q_mlp0, ep,
+                   nullptr, false, m->q5);
         }
         {
             EpiParams ep;
@@ -338,7 +339,7 @@ void Engine::encode(const std::vector<int> & slots, const std::vector<int> & off
     {
         ProfScope ps(prof, stream, "layernorm");
         layernorm_f16(stream, e_x_.as<float>(), M, d, m->e_ln_w, m->e_ln_b, hp.eps, e_enc_.as<_Float16>(), d, nullptr,
-                      e_enc32_.as<float>());
+                      e_enc32_.as<float>(), q8a(), q8d());
     }
     last_enc_n_ = n;
 
@@ -355,8 +356,9 @@ void Engine::encode(const std::vector<int> & slots, const std::vector<int> & off
         ep.d = d;
         ep.T = T;
         ep.slot_map = e_slotmap_.as<int>();
-        linear("gemm_cross", EPI_KV_CROSS, M, 2 * d, d, e_enc_.as<_Float16>(), m->q5 ? e_enc32_.as<float>() : nullptr, d,
-               L.cw_kv, L.q_ckv, ep);
+        // Q5_0: the final LayerNorm wrote the encoder output's Q8_0 rows once for all layers
+        linear("gemm_cross", EPI_KV_CROSS, M, 2 * d, d, e_enc_.as<_Float16>(), nullptr, d, L.cw_kv, L.q_ckv, ep, nullptr,
+               false, m->q5);
     }
 }
 
@@ -459,9 +461,7 @@ void Engine::decode(const std::vector<DecodeRow> & rows, const std::vector<int> 
             d_h_.alloc((size_t) C * 4 * d * 2);
             d_xl_.alloc((size_t) C * d * 2);
             if (m->q5) {
-                d_xn32_.alloc((size_t) C * d * 4);
                 d_ao32_.alloc((size_t) C * d * 4);
-                d_xl32_.alloc((size_t) C * d * 4);
                 q8a_.alloc(std::max(q8a_.bytes, (size_t) C * 4 * d));
                 q8d_.alloc(std::max(q8d_.bytes, (size_t) C * 4 * d / 32 * 4));
             }
@@ -582,13 +582,18 @@ void Engine::launch_decode(const DecShape & sh) {
 
     const bool q5 = m->q5;
     // A32: the f32 activation a Q5_0 GEMM quantizes (null: the f16 A is exact, e.g. GELU output)
+    // a_q8: the A operand's Q8_0 rows are already in q8a_ / q8d_ (Q5_0 models; written by the
+    // producing LayerNorm or one_chunk attention kernel)
     auto G = [&](const char * cls, int mode, int N, int K, const _Float16 * A, const float * A32, const _Float16 * W,
-                 const _Float16 * Wt, const Q5W & q, const EpiParams & ep, int Mr) {
+                 const _Float16 * Wt, const Q5W & q, const EpiParams & ep, int Mr, bool a_q8 = false) {
         (void) cls;
-        linear(Mr <= 64 ? "gemm_dec" : "gemm_dec_big", mode, Mr, N, K, A, A32, K, W, q, ep, Wt, true);
+        linear(Mr <= 64 ? "gemm_dec" : "gemm_dec_big", mode, Mr, N, K, A, A32, K, W, q, ep, Wt, true, a_q8);
     };
-    float * xn32 = q5 ? d_xn32_.as<float>() : nullptr;
     float * ao32 = q5 ? d_ao32_.as<float>() : nullptr;
+    // Q5_0: attention passes whose rows all take the one_chunk kernel emit the Q8_0 rows
+    // themselves; otherwise their f32 output is quantized by the GEMM call
+    const bool fq_self = q5 && self_oc && !self_tl && !sh.self_sm;
+    const bool fq_cross = q5 && cross_oc && !cross_tl && !sh.cross_sm;
 
     {
         ProfScope ps(prof, stream, "embed");
@@ -612,17 +617,18 @@ void Engine::launch_decode(const DecShape & sh) {
                         d_xn_.as<_Float16>(), d);
     };
     auto resid_full = [&](const _Float16 * A, const float * A32, const _Float16 * W, const _Float16 * Wt,
-                          const Q5W & q, int K, const float * bias) {
+                          const Q5W & q, int K, const float * bias, bool a_q8 = false) {
         EpiParams ep;
         ep.bias = bias;
         ep.resid = d_x_.as<float>();
         ep.out32 = d_x_.as<float>();
         ep.ldo = d;
-        G("resid", EPI_RESID_F32, d, K, A, A32, W, Wt, q, ep, R);
+        G("resid", EPI_RESID_F32, d, K, A, A32, W, Wt, q, ep, R, a_q8);
     };
     auto ln = [&](const float * w, const float * b) {
         ProfScope ps(prof, stream, "layernorm");
-        layernorm_f16(stream, d_x_.as<float>(), R, d, w, b, hp.eps, d_xn_.as<_Float16>(), d, nullptr, xn32);
+        layernorm_f16(stream, d_x_.as<float>(), R, d, w, b, hp.eps, d_xn_.as<_Float16>(), d, nullptr, nullptr, q8a(),
+                      q8d());
     };
     for (int l = 0; l < hp.n_text_layer; ++l) {
         const DecLayerW & L = m->dec[l];
@@ -640,13 +646,14 @@ void Engine::launch_decode(const DecShape & sh) {
             ep.out16c = Vl;
             ep.d = d;
             ep.row_off = d_rowoff;
-            G("qkv", EPI_QKV_DEC, 3 * d, d, d_xn_.as<_Float16>(), xn32, L.w_qkv, L.t_qkv, L.q_qkv, ep, R);
+            G("qkv", EPI_QKV_DEC, 3 * d, d, d_xn_.as<_Float16>(), nullptr, L.w_qkv, L.t_qkv, L.q_qkv, ep, R, q5);
         }
         {
             ProfScope ps(prof, stream, "attn_self");
             // one_chunk rows all on contiguous cell runs: the list-free kernel (see k_attn_step)
             attn_decoder(stream, d_q_.as<_Float16>(), d, Kl, Vl, d, 64, d_rs, R, d_keys, H, 1.0f, max_keys,
-                         d_ao_.as<_Float16>(), d, self_oc, self_tl, ao32, sh.self_list);
+                         d_ao_.as<_Float16>(), d, self_oc, self_tl, fq_self ? nullptr : ao32, sh.self_list,
+                         fq_self ? q8a() : nullptr, fq_self ? q8d() : nullptr);
             if (sh.self_sm)  // masked soft_max with scale 1 (Q, K pre-scaled; whisper.cpp:2614-2628)
                 attn_decoder_softmax(stream, d_q_.as<_Float16>(), d, Kl, Vl, d, 64, d_rs, R, d_keys, H, 1.0f, max_keys,
                                      d_ao_.as<_Float16>(), d, nullptr, nullptr, 0, ao32);
@@ -654,7 +661,7 @@ void Engine::launch_decode(const DecShape & sh) {
         if (fused) {
             resid_ln(d_ao_.as<_Float16>(), L.w_o, L.t_o, d, L.b_o, L.cross_ln_w, L.cross_ln_b);
         } else {
-            resid_full(d_ao_.as<_Float16>(), ao32, L.w_o, L.t_o, L.q_o, d, L.b_o);
+            resid_full(d_ao_.as<_Float16>(), ao32, L.w_o, L.t_o, L.q_o, d, L.b_o, fq_self);
             ln(L.cross_ln_w, L.cross_ln_b);
         }
         {
@@ -662,14 +669,15 @@ void Engine::launch_decode(const DecShape & sh) {
             ep.bias = L.cb_q;
             ep.out16 = d_q_.as<_Float16>();
             ep.ldo = d;
-            G("cq", EPI_F16, d, d, d_xn_.as<_Float16>(), xn32, L.cw_q, L.t_cq, L.q_cq, ep, R);
+            G("cq", EPI_F16, d, d, d_xn_.as<_Float16>(), nullptr, L.cw_q, L.t_cq, L.q_cq, ep, R, q5);
         }
         {
             // bytes: cross K and V of each row's clip (the HBM-bound part of a decode step)
             ProfScope ps(prof, stream, "attn_cross", 4.0 * R * (double) n_ctx_pad * d, 2.0 * 2.0 * R * (double) T * d);
             attn_decoder(stream, d_q_.as<_Float16>(), d, cross_k_.as<_Float16>() + l * cross_stride,
                          cross_v_.as<_Float16>() + l * cross_stride, 64, T * 64, d_rc, R, nullptr, H,
-                         kq_scale, T, d_ao_.as<_Float16>(), d, cross_oc, cross_tl, ao32);
+                         kq_scale, T, d_ao_.as<_Float16>(), d, cross_oc, cross_tl, fq_cross ? nullptr : ao32, true,
+                         fq_cross ? q8a() : nullptr, fq_cross ? q8d() : nullptr);
             if (sh.cross_sm)  // soft_max_ext(KQ, nullptr, KQscale) over n_audio_ctx keys (whisper.cpp:2697-2738)
                 attn_decoder_softmax(stream, d_q_.as<_Float16>(), d, cross_k_.as<_Float16>() + l * cross_stride,
                                      cross_v_.as<_Float16>() + l * cross_stride, 64, T * 64, d_rc, R, nullptr, H, kq_scale, T,
@@ -679,7 +687,7 @@ void Engine::launch_decode(const DecShape & sh) {
         if (fused) {
             resid_ln(d_ao_.as<_Float16>(), L.cw_o, L.t_co, d, L.cb_o, L.mlp_ln_w, L.mlp_ln_b);
         } else {
-            resid_full(d_ao_.as<_Float16>(), ao32, L.cw_o, L.t_co, L.q_co, d, L.cb_o);
+            resid_full(d_ao_.as<_Float16>(), ao32, L.cw_o, L.t_co, L.q_co, d, L.cb_o, fq_cross);
             ln(L.mlp_ln_w, L.mlp_ln_b);
         }
         {
@@ -688,7 +696,7 @@ void Engine::launch_decode(const DecShape & sh) {
             ep.gelu_tab = m->gelu_tab;
             ep.out16 = d_h_.as<_Float16>();
             ep.ldo = 4 * d;
-            G("mlp0", EPI_GELU_F16, 4 * d, d, d_xn_.as<_Float16>(), xn32, L.w_mlp0, L.t_mlp0, L.q_mlp0, ep, R);
+            G("mlp0", EPI_GELU_F16, 4 * d, d, d_xn_.as<_Float16>(), nullptr, L.w_mlp0, L.t_mlp0, L.q_mlp0, ep, R, q5);
         }
         if (fused) {
             const bool last = l + 1 == hp.n_text_layer;
@@ -703,13 +711,13 @@ void Engine::launch_decode(const DecShape & sh) {
         {
             ProfScope ps(prof, stream, "layernorm");
             layernorm_f16(stream, d_x_.as<float>(), n_logit_rows, d, m->d_ln_w, m->d_ln_b, hp.eps, d_xl_.as<_Float16>(),
-                          d, d_lsel, q5 ? d_xl32_.as<float>() : nullptr);
+                          d, d_lsel, nullptr, q8a(), q8d());
         }
         EpiParams ep;
         ep.out32 = logits_.as<float>();
         ep.ldo = nv;
         linear(n_logit_rows <= 64 ? "gemm_logits" : "gemm_logits_big", EPI_F32, n_logit_rows, nv, d,
-               d_xl_.as<_Float16>(), q5 ? d_xl32_.as<float>() : nullptr, d, m->d_te, m->q_te, ep, m->d_te_t, true);
+               d_xl_.as<_Float16>(), nullptr, d, m->d_te, m->q_te, ep, m->d_te_t, true, q5);
     }
 }
 

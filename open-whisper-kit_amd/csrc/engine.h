@@ -168,8 +168,12 @@ private:
     // Q5_0 models: f32 activations feeding the quantized GEMMs and their Q8_0 copy
     void linear(const char * cls, int mode, int M, int N, int K, const _Float16 * A16, const float * A32, int lda,
                 const _Float16 * W, const Q5W & q, const EpiParams & ep, const _Float16 * Wt = nullptr,
-                bool dec = false);
+                bool dec = false,
+                bool a_q8 = false);
     DevBuf q8a_, q8d_;
+    // Q5_0 models: the Q8_0 activation buffers producers write for the next linear (else null)
+    int8_t * q8a() { return m->q5 ? q8a_.as<int8_t>() : nullptr; }
+    float * q8d() { return m->q5 ? q8d_.as<float>() : nullptr; }
     DevBuf e_xn32_, e_ao32_, d_xn32_, d_ao32_, d_xl32_;
 
     DevBuf amap_, cap_;  // DTW: head map [L][H], captured probabilities [n_ah][T][cap_rows_]

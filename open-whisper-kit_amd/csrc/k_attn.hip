@@ -395,7 +395,8 @@ __global__ __launch_bounds__(64) void k_attn_step(const _Float16 * __restrict__ 
                                                   const _Float16 * __restrict__ kb, const _Float16 * __restrict__ vb,
                                                   int ld_kv, int hs, const AttnRow * __restrict__ rows,
                                                   const int * __restrict__ key_idx, float scale,
-                                                  _Float16 * __restrict__ out, int ldo, float * __restrict__ out32) {
+                                                  _Float16 * __restrict__ out, int ldo, float * __restrict__ out32,
+                                                  int8_t * __restrict__ q8, float * __restrict__ q8d) {
     // NOTE: any ordinary LDS store in this kernel (s_list below) makes the compiler drain
     // every in-flight global_load_lds (s_waitcnt vmcnt(0)) before the ring reads of each
     // chunk; the host therefore launches LIST = true only for passes with a listed row
@@ -406,9 +407,23 @@ __global__ __launch_bounds__(64) void k_attn_step(const _Float16 * __restrict__ 
     if (job.mode != 0) return;  // tiled (F32) rows: k_attn_decoder
     const int h = blockIdx.x;
     const int n = job.n_keys;
+    // the output (f32 or f16) and, for a Q5_0 consumer, its Q8_0 rounding (two 32-lane blocks;
+    // x86 quantize_row_q8_0 as k_quantize_q8)
+    auto emit = [&](float y) {
+        const size_t o = (size_t) job.q_row * ldo + h * 64 + lane;
+        if (out32) out32[o] = y;
+        else out[o] = (_Float16) y;
+        if (q8) {
+            float m = fabsf(y);
+#pragma unroll
+            for (int sh = 16; sh > 0; sh >>= 1) m = fmaxf(m, __shfl_xor(m, sh, 32));
+            const float id = m != 0.0f ? 127.f / m : 0.0f;
+            q8[o] = (int8_t) rintf(y * id);
+            if ((lane & 31) == 0) q8d[o >> 5] = (float) (_Float16) (m / 127.f);
+        }
+    };
     if (n <= 0) {
-        if (out32) out32[(size_t) job.q_row * ldo + h * 64 + lane] = 0.0f;
-        else out[(size_t) job.q_row * ldo + h * 64 + lane] = (_Float16) 0.0f;
+        emit(0.0f);
         return;
     }
     // a listed row whose cells are not one contiguous run (the host passes contiguous runs
@@ -552,8 +567,7 @@ __global__ __launch_bounds__(64) void k_attn_step(const _Float16 * __restrict__ 
         }
     }
     const float S_inv = S == 0.0f ? 0.0f : 1.0f / S;
-    if (out32) out32[(size_t) job.q_row * ldo + h * 64 + lane] = (float) acc * S_inv;
-    else out[(size_t) job.q_row * ldo + h * 64 + lane] = (_Float16) ((float) acc * S_inv);
+    emit((float) acc * S_inv);
 }
 
 // ----------------------------------------------------------------------------------
@@ -776,20 +790,21 @@ int attn_max_tiled_keys() { return DA_MAX_KEYS; }
 
 void attn_decoder(hipStream_t s, const _Float16 * q, int ldq, const _Float16 * kbase, const _Float16 * vbase, int ld_kv,
                   int hs, const AttnRow * rows_dev, int n_rows, const int * key_idx, int H, float scale, int max_keys,
-                  _Float16 * out, int ldo, bool any_one_chunk, bool any_tiled, float * out32, bool oc_listed) {
+                  _Float16 * out, int ldo, bool any_one_chunk, bool any_tiled, float * out32, bool oc_listed,
+                  int8_t * q8, float * q8d) {
     if (n_rows <= 0) return;
     if (any_one_chunk) {
         if (key_idx && oc_listed) {
             if (max_keys > AS_MAX_LIST) throw std::runtime_error("attn_decoder: too many listed keys");
             hipLaunchKernelGGL((k_attn_step<true, false>), dim3(H, n_rows), dim3(64), 0, s, q, ldq, kbase, vbase, ld_kv, hs,
-                               rows_dev, key_idx, scale, out, ldo, out32);
+                               rows_dev, key_idx, scale, out, ldo, out32, q8, q8d);
         } else {
             if (hs != 64)  // head-major cross K/V
                 hipLaunchKernelGGL((k_attn_step<false, true>), dim3(H, n_rows), dim3(64), 0, s, q, ldq, kbase, vbase, ld_kv,
-                                   hs, rows_dev, key_idx, scale, out, ldo, out32);
+                                   hs, rows_dev, key_idx, scale, out, ldo, out32, q8, q8d);
             else
                 hipLaunchKernelGGL((k_attn_step<false, false>), dim3(H, n_rows), dim3(64), 0, s, q, ldq, kbase, vbase, ld_kv,
-                                   hs, rows_dev, key_idx, scale, out, ldo, out32);
+                                   hs, rows_dev, key_idx, scale, out, ldo, out32, q8, q8d);
         }
     }
     if (any_tiled) {

@@ -576,6 +576,105 @@ __global__ __launch_bounds__(512) void k_gemm_q5_skinny(int M, int N, int K, con
     }
 }
 
+// decode rows (M <= 32): one 16-column tile per block, wave w takes J consecutive K blocks
+// and issues ALL its weight (packed Q5_0) and activation (int8) loads before the first
+// MFMA -- like k_gemm_rows, a launch is one memory round trip. The activation scales of the
+// whole A (M x K/32 floats) are staged in LDS; every K block's exact integer dot
+// (v_mfma_i32_16x16x32_i8) is scaled by d_a * d_w into the f32 accumulator; wave partial
+// tiles are summed in fixed wave order. K up to GQ_MAXW * J * 32 (5120 at J = 10).
+constexpr int GQ_MAXW = 16;
+constexpr int GQ_J = 10;
+constexpr int GQ_MAX_SCALES = 32 * 160;  // M x K/32 activation scales in LDS
+// M * nb <= 32 * nb and blockDim = 64 * ceil(nb / GQ_J) -> at most 32 * GQ_J / 64 + 1 per thread
+constexpr int GQ_DA_PER_THREAD = 32 * GQ_J / 64 + 1;
+
+template <int MODE, int MT>
+__global__ __launch_bounds__(GQ_MAXW * 64) void k_gemm_q5_rows(int M, int N, int K, const int8_t * __restrict__ qa,
+                                                               const float * __restrict__ da, Q5W w, EpiParams ep) {
+    __shared__ floatx4 red[GQ_MAXW][MT][64];
+    __shared__ float sda[GQ_MAX_SCALES];
+    const int tid = threadIdx.x, lane = tid & 63, nw = blockDim.x >> 6;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: branch-free k range
+    const int n0 = blockIdx.x * 16;
+    const int nb = K >> 5;
+    const int kb0 = wave * GQ_J;
+    const int nj = max(0, min(GQ_J, nb - kb0));
+    const int g = lane >> 4;
+    const int c16 = lane & 15;
+    uint64_t raw[GQ_J];
+    uint32_t qh[GQ_J];
+    _Float16 dw[GQ_J];
+    long a[MT][GQ_J];
+    // the tile's blocks are contiguous 352 B records (Q5W::tiled): coalesced loads. Blocks
+    // past this wave's range load a valid record and a zero activation (adds exact zeros).
+    const uint8_t * tb = w.tiled + (size_t) blockIdx.x * nb * Q5_TILE_BYTES;
+#pragma unroll
+    for (int j = 0; j < GQ_J; ++j) {
+        const int kb = min(kb0 + j, nb - 1);
+        const uint8_t * rec = tb + (size_t) kb * Q5_TILE_BYTES;
+        raw[j] = *(const uint64_t *) (rec + c16 * 16 + (g & 1) * 8);
+        qh[j] = *(const uint32_t *) (rec + 256 + c16 * 4);
+        dw[j] = *(const _Float16 *) (rec + 320 + c16 * 2);
+#pragma unroll
+        for (int i = 0; i < MT; ++i) {
+            const int ra = min(i * 16 + c16, M - 1);
+            const long t = *(const long *) (qa + (size_t) ra * K + kb * 32 + 8 * g);
+            a[i][j] = j < nj ? t : 0L;
+        }
+    }
+    // activation scales (at most GQ_DA_PER_THREAD per thread: M <= 32, nw = ceil(nb / J)) to
+    // LDS; every load of the launch is issued before the first wait (one round trip)
+    float dv[GQ_DA_PER_THREAD];
+#pragma unroll
+    for (int u = 0; u < GQ_DA_PER_THREAD; ++u) {
+        const int i = tid + u * blockDim.x;
+        dv[u] = i < M * nb ? da[i] : 0.0f;
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int u = 0; u < GQ_DA_PER_THREAD; ++u) {
+        const int i = tid + u * blockDim.x;
+        if (i < M * nb) sda[i] = dv[u];
+    }
+    __syncthreads();
+    floatx4 acc[MT];
+#pragma unroll
+    for (int i = 0; i < MT; ++i) acc[i] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < GQ_J; ++j) {
+        const int kb = min(kb0 + j, nb - 1);
+        uint64_t v = (g < 2 ? raw[j] : (raw[j] >> 4)) & 0x0F0F0F0F0F0F0F0FULL;
+        const uint32_t h8 = (qh[j] >> (8 * g)) & 0xFFu;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v |= (uint64_t) ((h8 >> e) & 1u) << (8 * e + 4);
+        v = ((v | 0x8080808080808080ULL) - 0x1010101010101010ULL) ^ 0x8080808080808080ULL;
+        const float dwf = (float) dw[j];
+#pragma unroll
+        for (int i = 0; i < MT; ++i) {
+            const intx4 z = {0, 0, 0, 0};
+            const intx4 iv = __builtin_amdgcn_mfma_i32_16x16x32_i8(a[i][j], (long) v, z, 0, 0, 0);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int r = min(i * 16 + 4 * g + e, M - 1);
+                acc[i][e] += (float) iv[e] * (sda[r * nb + kb] * dwf);
+            }
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < MT; ++i) red[wave][i][lane] = acc[i];
+    __syncthreads();
+    for (int o = tid; o < MT * 256; o += blockDim.x) {
+        const int r = o >> 4, cc = o & 15;
+        const int i = r >> 4, rr = r & 15;
+        const int ln = 16 * (rr >> 2) + cc, e = rr & 3;
+        const float * rp = (const float *) &red[0][i][ln] + e;
+        float sum = rp[0];
+        for (int ww = 1; ww < nw; ++ww) sum += rp[ww * MT * 64 * 4];
+        const int c = n0 + cc;
+        if (r < M && c < N) epi_store<MODE>(ep, r, c, sum);
+    }
+}
+
 // tiles: 64 x 64 per block, 4 waves of 32 x 32; per 32-wide K block the int8 operands are
 // staged in LDS (the Q5 weights expanded to int8 on the way), one MFMA per 16 x 16 tile,
 // then the per-block scale d_a * d_w folds the integer dot into the f32 accumulator
@@ -646,13 +745,40 @@ __global__ __launch_bounds__(256) void k_gemm_q5_big(int M, int N, int K, const 
 template <int MODE> struct LaunchQ5 {
     static void run(hipStream_t s, int M, int N, int K, const int8_t * qa, const float * da, const Q5W & w,
                     const EpiParams & ep) {
-        if (M <= 64)
+        const int nb = K / 32;
+        if (M <= 32 && w.tiled && nb <= GQ_MAXW * GQ_J && M * nb <= GQ_MAX_SCALES) {
+            const int nw = (nb + GQ_J - 1) / GQ_J;
+            if (M <= 16)
+                hipLaunchKernelGGL((k_gemm_q5_rows<MODE, 1>), dim3((N + 15) / 16), dim3(nw * 64), 0, s, M, N, K, qa, da,
+                                   w, ep);
+            else
+                hipLaunchKernelGGL((k_gemm_q5_rows<MODE, 2>), dim3((N + 15) / 16), dim3(nw * 64), 0, s, M, N, K, qa, da,
+                                   w, ep);
+        } else if (M <= 64)
             hipLaunchKernelGGL(k_gemm_q5_skinny<MODE>, dim3((N + 15) / 16), dim3(512), 0, s, M, N, K, qa, da, w, ep);
         else
             hipLaunchKernelGGL(k_gemm_q5_big<MODE>, dim3(((M + 63) / 64) * ((N + 63) / 64)), dim3(256), 0, s, M, N, K,
                                qa, da, w, ep);
     }
 };
+
+size_t q5_tiled_bytes(int N, int K) { return (size_t) ((N + 15) / 16) * (K / 32) * Q5_TILE_BYTES; }
+
+void q5_tile_host(const uint8_t * qs, const uint32_t * qh, const uint16_t * d, int N, int K, uint8_t * out) {
+    const int nb = K / 32, nt = (N + 15) / 16;
+    memset(out, 0, q5_tiled_bytes(N, K));
+    for (int t = 0; t < nt; ++t)
+        for (int kb = 0; kb < nb; ++kb) {
+            uint8_t * o = out + ((size_t) t * nb + kb) * Q5_TILE_BYTES;
+            for (int c = 0; c < 16; ++c) {
+                const int n = t * 16 + c;
+                if (n >= N) break;
+                memcpy(o + c * 16, qs + (size_t) n * (K / 2) + kb * 16, 16);
+                memcpy(o + 256 + c * 4, &qh[(size_t) n * nb + kb], 4);
+                memcpy(o + 320 + c * 2, &d[(size_t) n * nb + kb], 2);
+            }
+        }
+}
 
 void q5_split_host(const uint8_t * blocks, int N, int K, uint8_t * qs, uint32_t * qh, uint16_t * d) {
     const int nb = K / 32;

@@ -24,7 +24,8 @@ constexpr int LN_V4 = 8;  // float4 per lane held in registers -> d <= 2048
 // LayerNorm of one row held in registers (lane owns float4 groups lane + 64 j)
 __device__ __forceinline__ void ln_row_regs(const float4 (&xv)[LN_V4], int lane, int d, const float * __restrict__ w,
                                             const float * __restrict__ b, float eps, _Float16 * __restrict__ o,
-                                            float * __restrict__ o32) {
+                                            float * __restrict__ o32, int8_t * __restrict__ q8 = nullptr,
+                                            float * __restrict__ q8d = nullptr) {
     const int n4 = d >> 2;
     double s = 0.0;
 #pragma unroll
@@ -48,9 +49,10 @@ __device__ __forceinline__ void ln_row_regs(const float4 (&xv)[LN_V4], int lane,
 #pragma unroll
     for (int j = 0; j < LN_V4; ++j) {
         const int i = lane + 64 * j;
+        if (64 * j >= n4) break;  // wave-uniform: no lane of this group is in the row
+        float4 y = float4{0.f, 0.f, 0.f, 0.f};
         if (i < n4) {
             const float4 ww = w4[i], bb = b4[i];
-            float4 y;
             y.x = (xv[j].x - mean) * scale * ww.x + bb.x;
             y.y = (xv[j].y - mean) * scale * ww.y + bb.y;
             y.z = (xv[j].z - mean) * scale * ww.z + bb.z;
@@ -60,13 +62,32 @@ __device__ __forceinline__ void ln_row_regs(const float4 (&xv)[LN_V4], int lane,
             *(half4 *) (o + 4 * i) = h;
             if (o32) *(float4 *) (o32 + 4 * i) = y;
         }
+        if (q8) {
+            // Q8_0 of the f32 output (x86 quantize_row_q8_0, as k_quantize_q8): a 32-element
+            // block is 8 consecutive float4 = 8 lanes; d % 32 == 0 keeps groups whole
+            float m = fmaxf(fmaxf(fabsf(y.x), fabsf(y.y)), fmaxf(fabsf(y.z), fabsf(y.w)));
+            m = fmaxf(m, __shfl_xor(m, 1, 8));
+            m = fmaxf(m, __shfl_xor(m, 2, 8));
+            m = fmaxf(m, __shfl_xor(m, 4, 8));
+            if (i < n4) {
+                const float id = m != 0.0f ? 127.f / m : 0.0f;
+                char4 qv;
+                qv.x = (signed char) rintf(y.x * id);
+                qv.y = (signed char) rintf(y.y * id);
+                qv.z = (signed char) rintf(y.z * id);
+                qv.w = (signed char) rintf(y.w * id);
+                *(char4 *) (q8 + 4 * i) = qv;
+                if ((lane & 7) == 0) q8d[i >> 3] = (float) (_Float16) (m / 127.f);
+            }
+        }
     }
 }
 
 __global__ __launch_bounds__(256) void k_layernorm_f16(const float * __restrict__ x, int rows, int d,
                                                        const float * __restrict__ w, const float * __restrict__ b,
                                                        float eps, _Float16 * __restrict__ out, int ldo,
-                                                       const int * __restrict__ row_idx, float * __restrict__ out32) {
+                                                       const int * __restrict__ row_idx, float * __restrict__ out32,
+                                                       int8_t * __restrict__ q8, float * __restrict__ q8d) {
     const int lane = threadIdx.x & 63;
     const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (row >= rows) return;
@@ -79,7 +100,8 @@ __global__ __launch_bounds__(256) void k_layernorm_f16(const float * __restrict_
         const int i = lane + 64 * j;
         xv[j] = i < n4 ? xr[i] : float4{0.f, 0.f, 0.f, 0.f};
     }
-    ln_row_regs(xv, lane, d, w, b, eps, out + (size_t) row * ldo, out32 ? out32 + (size_t) row * d : nullptr);
+    ln_row_regs(xv, lane, d, w, b, eps, out + (size_t) row * ldo, out32 ? out32 + (size_t) row * d : nullptr,
+                q8 ? q8 + (size_t) row * d : nullptr, q8 ? q8d + (size_t) row * (d / 32) : nullptr);
 }
 
 // Finishes an EPI_PARTIAL decode-row GEMM: sums its k splits in order (row-major partial
@@ -173,11 +195,12 @@ void resid_layernorm(hipStream_t s, int M, int N, int ks, const float * part, co
 }
 
 void layernorm_f16(hipStream_t s, const float * x, int rows, int d, const float * w, const float * b, float eps,
-                   _Float16 * out, int ldo, const int * row_idx, float * out32) {
+                   _Float16 * out, int ldo, const int * row_idx, float * out32, int8_t * q8, float * q8d) {
     if (rows <= 0) return;
     if (d % 4 != 0 || d > 4 * 64 * LN_V4 || ldo % 4 != 0) throw std::runtime_error("layernorm_f16: unsupported width");
+    if (q8 && (d % 32 != 0 || !q8d)) throw std::runtime_error("layernorm_f16: Q8_0 output needs d % 32 == 0");
     hipLaunchKernelGGL(k_layernorm_f16, dim3((rows + 3) / 4), dim3(256), 0, s, x, rows, d, w, b, eps, out, ldo,
-                       row_idx, out32);
+                       row_idx, out32, q8, q8d);
 }
 
 // token + position embedding (whisper.cpp:2515-2518: get_rows(d_te) + get_rows(d_pe))

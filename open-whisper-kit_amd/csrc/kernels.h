@@ -88,8 +88,14 @@ struct Q5W {
     const uint8_t * qs = nullptr;   // [N][K/2]: block b = 16 bytes, byte j = element j | element j+16 << 4
     const uint32_t * qh = nullptr;  // [N][K/32]: 5th bits, bit j = element j
     const _Float16 * d = nullptr;   // [N][K/32]: block scales
+    // decode-step matrices: per (16-row tile t, block kb) 352 B at (t * K/32 + kb) * 352 =
+    // qs of the 16 rows (16 x 16 B) | qh (16 x 4 B) | d (16 x 2 B); rows past N zero
+    const uint8_t * tiled = nullptr;
     explicit operator bool() const { return qs != nullptr; }
 };
+constexpr int Q5_TILE_BYTES = 352;
+size_t q5_tiled_bytes(int N, int K);
+void q5_tile_host(const uint8_t * qs, const uint32_t * qh, const uint16_t * d, int N, int K, uint8_t * out);
 // Q8_0 rows of A (f32 if A32, else f16): q [M][K] int8, dq [M][K/32] (the f16-rounded scale)
 void quantize_q8(hipStream_t s, const float * A32, const _Float16 * A16, int lda, int M, int K, int8_t * q, float * dq);
 // C[M,N] = Q8(A) . Q5(W)^T with the fused epilogue `mode` (any EpiMode except EPI_PARTIAL)
@@ -103,8 +109,11 @@ void q5_split_host(const uint8_t * blocks, int N, int K, uint8_t * qs, uint32_t 
 // ---------------------------------------------------------------------------------
 // out16[r] = f16(LN(x[r]) * w + b); mean/variance accumulated in double (ref ops.cpp:3578-3623)
 // row_idx (optional): output row i normalises input row row_idx[i]; out32 (optional) f32 copy
+// q8/q8d (optional): the f32 output rows as Q8_0 ([row][d] int8, [row][d/32] f16-rounded
+// scales), the activation rounding of a Q5_0 GEMM done in the producer
 void layernorm_f16(hipStream_t s, const float * x, int rows, int d, const float * w, const float * b,
-                   float eps, _Float16 * out, int ldo, const int * row_idx = nullptr, float * out32 = nullptr);
+                   float eps, _Float16 * out, int ldo, const int * row_idx = nullptr, float * out32 = nullptr,
+                   int8_t * q8 = nullptr, float * q8d = nullptr);
 // decoder input embedding: x[r] = f32(tok_emb[tok[r]]) + pos_emb[pos[r]]
 void embed_tokens(hipStream_t s, const _Float16 * tok_emb, const float * pos_emb, const int * tokens,
                   const int * pos, int rows, int d, float * x);
@@ -170,7 +179,8 @@ struct AttnRow {
 void attn_decoder(hipStream_t s, const _Float16 * q, int ldq, const _Float16 * kbase, const _Float16 * vbase,
                   int ld_kv, int hs, const AttnRow * rows_dev, int n_rows, const int * key_idx, int H, float scale,
                   int max_keys, _Float16 * out, int ldo, bool any_one_chunk, bool any_tiled, float * out32 = nullptr,
-                  bool oc_listed = true);  // false: every one_chunk row is a contiguous cell run
+                  bool oc_listed = true,  // false: every one_chunk row is a contiguous cell run
+                  int8_t * q8 = nullptr, float * q8d = nullptr);  // one_chunk rows: Q8_0 of the f32 output
 // rows with mode 2 (flash_attn = false contexts): soft_max attention, F16 probabilities;
 // optional DTW capture of alignment-head probabilities cap[a][key][row] (amap: head -> a or -1)
 void attn_decoder_softmax(hipStream_t s, const _Float16 * q, int ldq, const _Float16 * kbase, const _Float16 * vbase,

@@ -437,6 +437,7 @@ Model * load_model(whisper_model_loader * loader, int device, std::string & err)
     if (m->q5 && n_loaded > 0) {
         std::vector<std::vector<std::string>> groups;
         groups.push_back({"decoder.token_embedding.weight"});
+        const size_t n_dec_first = 0;  // token embedding: a decode (logits) matrix too
         for (int i = 0; i < hp.n_audio_layer; ++i) {
             const std::string p = "encoder.blocks." + std::to_string(i) + ".";
             groups.push_back({p + "attn.query.weight", p + "attn.key.weight", p + "attn.value.weight"});
@@ -450,18 +451,22 @@ Model * load_model(whisper_model_loader * loader, int device, std::string & err)
                                    "mlp.2.weight"})
                 groups.push_back({p + n});
         }
+        const size_t n_enc_groups = 1 + 4 * (size_t) hp.n_audio_layer;  // groups [1, n_enc_groups): encoder
         size_t qoff = 0;
-        struct Plan { size_t qs, qh, d; int N, K; };
+        struct Plan { size_t qs, qh, d, tiled; int N, K; };
         std::vector<Plan> plans;
-        for (const auto & gr : groups) {
+        for (size_t gi = 0; gi < groups.size(); ++gi) {
+            const auto & gr = groups[gi];
             int N = 0;
             const int K = (int) S[idx.at(gr[0])].ne[0];
             for (const auto & n : gr) N += (int) S[idx.at(n)].ne[1];
-            Plan pl{0, 0, 0, N, K};
+            Plan pl{0, 0, 0, (size_t) -1, N, K};
             auto res = [&](size_t bytes) { size_t o = qoff; qoff += (bytes + 255) & ~(size_t) 255; return o; };
             pl.qs = res((size_t) N * K / 2);
             pl.qh = res((size_t) N * (K / 32) * 4);
             pl.d = res((size_t) N * (K / 32) * 2);
+            // decode-step matrices also get the column-tiled copy the decode-row GEMM streams
+            if (gi == n_dec_first || gi >= n_enc_groups) pl.tiled = res(q5_tiled_bytes(N, K));
             plans.push_back(pl);
         }
         m->q5blob.alloc(qoff);
@@ -486,6 +491,12 @@ Model * load_model(whisper_model_loader * loader, int device, std::string & err)
             w.qs = (const uint8_t *) (qb + pl.qs);
             w.qh = (const uint32_t *) (qb + pl.qh);
             w.d = (const _Float16 *) (qb + pl.d);
+            if (pl.tiled != (size_t) -1) {
+                std::vector<uint8_t> tl(q5_tiled_bytes(pl.N, pl.K));
+                q5_tile_host(qs.data(), qh.data(), dd.data(), pl.N, pl.K, tl.data());
+                OWK_HIP_CHECK(hipMemcpy(qb + pl.tiled, tl.data(), tl.size(), hipMemcpyHostToDevice));
+                w.tiled = (const uint8_t *) (qb + pl.tiled);
+            }
             q5m[groups[gi][0]] = w;
         }
     }

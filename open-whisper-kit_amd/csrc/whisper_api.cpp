@@ -1192,6 +1192,13 @@ int owk_debug_gemm_q5(int device, int M, int N, int K, const float * a, const ui
         w.qs = dqs.as<uint8_t>();
         w.qh = dqh.as<uint32_t>();
         w.d = ddd.as<_Float16>();
+        // the tiled copy a model keeps for its decode-step matrices (decode-row GEMM path)
+        std::vector<uint8_t> tl(q5_tiled_bytes(N, K));
+        q5_tile_host(qs.data(), qh.data(), dd.data(), N, K, tl.data());
+        DevBuf dtl;
+        dtl.alloc(tl.size());
+        OWK_HIP_CHECK(hipMemcpy(dtl.ptr, tl.data(), tl.size(), hipMemcpyHostToDevice));
+        w.tiled = dtl.as<uint8_t>();
         quantize_q8(s, da.as<float>(), nullptr, K, M, K, q8.as<int8_t>(), q8d.as<float>());
         EpiParams ep;
         ep.out32 = dout.as<float>();

@@ -25,7 +25,7 @@ def q5_vals(blocks, N, K):
     hb = ((qh[..., None] >> np.arange(32)) & 1).astype(np.int32)
     return (lo | (hb << 4)) - 16, d
 
-for M, N, K in ((8, 384, 384), (40, 1536, 384), (300, 384, 1536), (1500, 1152, 384)):
+for M, N, K in ((8, 384, 384), (32, 1280, 5120), (24, 3840, 1280), (17, 5120, 1280), (40, 1536, 384), (300, 384, 1536), (1500, 1152, 384)):
     a = (rng.standard_normal((M, K)) * 0.7).astype(np.float32)
     wf = (rng.standard_normal((N, K)) / np.sqrt(K)).astype(np.float32)
     blocks = S.q5_0_blocks(wf)
