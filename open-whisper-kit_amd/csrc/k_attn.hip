@@ -704,7 +704,6 @@ __global__ __launch_bounds__(256) void k_attn_softmax(const _Float16 * __restric
     __shared__ _Float16 p16[SM_MAX_KEYS];
     __shared__ float redf[4];
     __shared__ double redd[4];
-    __shared__ floatx4 acc4[4][16];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const AttnRow job = rows[blockIdx.y];
     if (job.mode != 2) return;
@@ -715,8 +714,9 @@ __global__ __launch_bounds__(256) void k_attn_softmax(const _Float16 * __restric
     const _Float16 * vh = vb + job.kv_base + (size_t) h * hs;
     const _Float16 * qr = q + (size_t) job.q_row * ldq + h * 64;
 
-    // scores
+    // scores (lane = key; iterations unrolled so several keys' loads are in flight)
     float mx = -INFINITY;
+#pragma unroll 3
     for (int i = tid; i < n; i += 256) {
         const int cell = list ? list[i] : i;
         const half8 * kr = (const half8 *) (kh + (size_t) cell * ld_kv);
@@ -759,17 +759,33 @@ __global__ __launch_bounds__(256) void k_attn_softmax(const _Float16 * __restric
         if (a >= 0) cap[((size_t) a * n + i) * cap_rows + job.q_row] = p;
     }
     __syncthreads();
-    // P . V: wave w takes keys w, w+4, ...; lane = head dim
-    float acc = 0.0f;
-    for (int i = wave; i < n; i += 4) {
-        const int cell = list ? list[i] : i;
-        acc = fmaf((float) p16[i], (float) vh[(size_t) cell * ld_kv + lane], acc);
+    // P . V: thread t takes keys kg = t / 8, kg + 32, ... and head dims 8 (t % 8) .. +8 (one
+    // 16-byte load per key, 8 threads cover a 128-byte V row); 8 keys in flight per thread;
+    // the 32 key-group partials are summed in fixed order through LDS
+    const int kg = tid >> 3, seg = tid & 7;
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int i0 = kg; i0 < n; i0 += 32 * 8) {
+        half8 vv[8];
+        float pp[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int i = min(i0 + 32 * u, n - 1);
+            const int cell = list ? list[i] : i;
+            vv[u] = *(const half8 *) (vh + (size_t) cell * ld_kv + seg * 8);
+            pp[u] = i0 + 32 * u < n ? (float) p16[i] : 0.0f;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+#pragma unroll
+            for (int e = 0; e < 8; ++e) acc[e] = fmaf(pp[u], (float) vv[u][e], acc[e]);
     }
-    ((float *) acc4)[wave * 64 + lane] = acc;
+    float * red = sp;  // the scores are consumed: reuse as [32][64] partials
+#pragma unroll
+    for (int e = 0; e < 8; ++e) red[kg * 64 + seg * 8 + e] = acc[e];
     __syncthreads();
     if (wave == 0) {
-        const float * a4 = (const float *) acc4;
-        const float r = (a4[lane] + a4[64 + lane]) + (a4[128 + lane] + a4[192 + lane]);
+        float r = 0.0f;
+        for (int g = 0; g < 32; ++g) r += red[g * 64 + lane];
         if (out32) out32[(size_t) job.q_row * ldo + h * 64 + lane] = r;
         else out[(size_t) job.q_row * ldo + h * 64 + lane] = (_Float16) r;
     }

@@ -1,0 +1,102 @@
+"""BASELINE configs[4] on one MI355X: large-v3 transcription with DTW token timestamps plus
+streaming-SortFormer diarization of 10 minutes of audio.
+
+Workload (synthetic data and random-init weights of the real architectures, as bench.py):
+  * a seeded 10 min synthetic 16 kHz clip;
+  * transcription: large-v3 F16 with flash_attn = false (DTW needs the soft_max path, as in
+    the reference) and dtw_aheads_preset = WHISPER_AHEADS_LARGE_V3; the clip is cut into 30 s
+    chunks decoded as one owk_full_batch (the whisper_full_parallel split), greedy,
+    temperature_inc = 0, timestamps on, token timestamps on;
+  * diarization: sortformer_diarize of the whole clip (default parameters).
+Reports the wall time of each part and the real-time factor of the whole job; the reference
+CPU path (16 threads) is timed on ONE 30 s chunk of the same transcription settings.
+
+    python tools/pipeline_bench.py [--minutes 10] [--no-cpu]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
+sys.path.insert(0, os.path.join(ROOT, "open-whisper-kit_amd", "python"))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+import owk  # noqa: E402
+import owk_synth as S  # noqa: E402
+import sortformer as SF  # noqa: E402
+import sortformer_synth as SS  # noqa: E402
+
+AHEADS_LARGE_V3 = 13
+CHUNK = 30 * 16000
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--minutes", type=float, default=10.0)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--prof", action="store_true", help="per-kernel-class HIP-event timing of the ASR part (eager)")
+    args = ap.parse_args()
+    cache = os.environ.get("OWK_MODEL_CACHE", "/tmp/owk_models")
+    model = S.ensure_model("large-v3", cache_dir=cache)
+    meta = json.load(open(os.path.join(ROOT, "tests", "golden", "sf_golden.json")))
+    sf_path = os.path.join(cache, f"synth-sortformer-s{meta['seed']}.gguf")
+    if not os.path.exists(sf_path):
+        assert SS.write_model(sf_path, meta["seed"]) == meta["sha256"]
+    n = int(args.minutes * 60 * 16000)
+    pcm = S.synth_audio(n, 5)
+    chunks = [pcm[i:i + CHUNK] for i in range(0, n, CHUNK)]
+
+    owk.quiet()
+    w = owk.Whisper(model, flash_attn=False, dtw_preset=AHEADS_LARGE_V3)
+    p = w.params(0, language="en", temperature_inc=0.0, token_timestamps=True)
+    sf = SF.Sortformer(sf_path)
+    # warm-up (code objects, buffers, graphs) on one chunk
+    st = [w.new_state()]
+    w.full_batch(st, chunks[:1], p)
+    sf.diarize(pcm[:CHUNK])
+
+    states = [w.new_state() for _ in chunks]
+    if args.prof:
+        w.L.owk_prof_enable(w.ctx, 1)
+        w.L.owk_prof_reset(w.ctx)
+    t0 = time.perf_counter()
+    ret = w.full_batch(states, chunks, p)
+    t_asr = time.perf_counter() - t0
+    assert ret == 0, ret
+    if args.prof:
+        tot = {c: w.prof(c) for c in w.prof_classes()}
+        for c, v in sorted(tot.items(), key=lambda kv: -kv[1]["ms"]):
+            print(f"[prof] {c:20s} {v['ms']:10.2f} ms  launches {v['launches']:8d}", file=sys.stderr, flush=True)
+    n_tok = sum(len(s["tokens"]) for st_ in states for s in w.segments(st_))
+    n_dtw = sum(1 for st_ in states for s in w.segments(st_) for t in s["tokens"] if t[8] >= 0)
+    t0 = time.perf_counter()
+    probs = sf.diarize(pcm)
+    t_diar = time.perf_counter() - t0
+    audio_s = n / 16000
+    out = {"metric": "transcribe + DTW + diarize real-time factor (audio-s/wall-s), configs[4]",
+           "unit": "audio-s/wall-s", "value": round(audio_s / (t_asr + t_diar), 2), "audio_s": audio_s,
+           "asr_wall_s": round(t_asr, 3), "diarize_wall_s": round(t_diar, 4), "chunks": len(chunks),
+           "tokens": n_tok, "tokens_with_t_dtw": n_dtw, "diarize_frames": int(probs.shape[0]),
+           "workload": "large-v3 F16 flash_attn=false + DTW (LARGE_V3 heads), 30 s chunks in one batch, greedy; "
+                       "SortFormer offline, synthetic weights and audio"}
+    sf.close()
+    if not args.no_cpu:
+        import ref_oracle as R
+        if R.available():
+            nt = min(len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", "1000")))
+            ref = R.Ref(model, flash_attn=False, dtw_preset=AHEADS_LARGE_V3)
+            t0 = time.perf_counter()
+            r, segs = ref.full(chunks[0], n_threads=nt, language="en", temperature_inc=0.0, token_timestamps=True)
+            rw = time.perf_counter() - t0
+            ref.close()
+            out["cpu_baseline_asr"] = {"value": round(30.0 / rw, 3), "unit": "audio-s/wall-s", "cores": nt,
+                                       "kind": "reference", "sample": f"one 30 s chunk, same settings, ret={r}, "
+                                       f"{sum(len(s['tokens']) for s in segs)} tokens, wall {rw:.1f} s"}
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
