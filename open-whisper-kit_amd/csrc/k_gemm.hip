@@ -186,9 +186,25 @@ __global__ __launch_bounds__(256, 2) void k_gemm_big(int M, int N, int K, const 
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const int c = n0 + wn * 64 + j * 16 + (lane & 15);
+            const int r0 = m0 + wm * 64 + i * 16 + 4 * (lane >> 4);
+            if constexpr (MODE == EPI_QKV_ENC) {
+                // V columns go to the transposed [clip][head][dim][Tpad] image: a lane's 4 rows
+                // are 4 consecutive t of one clip (T % 4 == 0, r0 % 4 == 0): one 8-byte store
+                const int d = ep.d;
+                if (c >= 2 * d && c < N && r0 + 3 < M && ep.T % 4 == 0) {
+                    const int cc = c - 2 * d;
+                    const int clip = r0 / ep.T, t = r0 - clip * ep.T;
+                    const float bv = ep.bias2[cc];
+                    half4 hv;
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) hv[e] = (_Float16) (acc[i][j][e] + bv);
+                    *(half4 *) (ep.out16c + (((size_t) clip * (d >> 6) + (cc >> 6)) * 64 + (cc & 63)) * ep.Tpad + t) = hv;
+                    continue;
+                }
+            }
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-                const int r = m0 + wm * 64 + i * 16 + 4 * (lane >> 4) + e;
+                const int r = r0 + e;
                 if (r < M && c < N) epi_store<MODE>(ep, r, c, acc[i][j][e]);
             }
         }

@@ -268,6 +268,8 @@ __global__ __launch_bounds__(256) void k_mel(const MelJob * __restrict__ jobs, c
     }
     __shared__ double frame[400];
     __shared__ double power[201];
+    __shared__ double stw[800];  // cos / sin table in LDS: the DFT loop reads it 800 times per bin
+    for (int j = threadIdx.x; j < 800; j += blockDim.x) stw[j] = tw[j];
     const int off = f * 160;
     for (int j = threadIdx.x; j < 400; j += blockDim.x) {
         const int p = off + j;  // index into the padded signal
@@ -283,8 +285,8 @@ __global__ __launch_bounds__(256) void k_mel(const MelJob * __restrict__ jobs, c
         int idx = 0;
         for (int j = 0; j < 400; ++j) {
             const double x = frame[j];
-            re += x * tw[idx];
-            im -= x * tw[400 + idx];
+            re += x * stw[idx];
+            im -= x * stw[400 + idx];
             idx += k;
             if (idx >= 400) idx -= 400;
         }
