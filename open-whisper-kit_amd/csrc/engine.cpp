@@ -495,14 +495,16 @@ void Engine::decode(const std::vector<DecodeRow> & rows, const std::vector<int> 
         const DecodeRow & x = rows[r];
         tok[r] = x.token;
         pos[r] = x.pos;
-        rowoff[r] = ((int64_t) x.slot * kv_cells + x.cell) * d;
+        // self-attention cache [layer][slot][head][cell][64] (head-major: a (row, head) streams
+        // its cells as one contiguous run)
+        rowoff[r] = (int64_t) x.slot * kv_cells * d + (int64_t) x.cell * 64;
         rs[r] = AttnRow{r, (int) ((int64_t) x.slot * kv_cells * d), x.n_keys, x.key_off, 0, x.mode_self};
         if (x.mode_self == 0 && x.n_keys > 0) {  // one contiguous run of cells: no list needed
             const int * kl = key_list.data() + x.key_off;
             bool run = true;
             for (int i = 1; i < x.n_keys && run; ++i) run = kl[i] == kl[0] + i;
             if (run) {
-                rs[r].kv_base += kl[0] * d;
+                rs[r].kv_base += kl[0] * 64;
                 rs[r].key_list = -1;
             }
         }
@@ -646,16 +648,18 @@ void Engine::launch_decode(const DecShape & sh) {
             ep.out16c = Vl;
             ep.d = d;
             ep.row_off = d_rowoff;
+            ep.Tpad = kv_cells * 64;
             G("qkv", EPI_QKV_DEC, 3 * d, d, d_xn_.as<_Float16>(), nullptr, L.w_qkv, L.t_qkv, L.q_qkv, ep, R, q5);
         }
         {
             ProfScope ps(prof, stream, "attn_self");
             // one_chunk rows all on contiguous cell runs: the list-free kernel (see k_attn_step)
-            attn_decoder(stream, d_q_.as<_Float16>(), d, Kl, Vl, d, 64, d_rs, R, d_keys, H, 1.0f, max_keys,
+            attn_decoder(stream, d_q_.as<_Float16>(), d, Kl, Vl, 64, kv_cells * 64, d_rs, R, d_keys, H, 1.0f, max_keys,
                          d_ao_.as<_Float16>(), d, self_oc, self_tl, fq_self ? nullptr : ao32, sh.self_list,
                          fq_self ? q8a() : nullptr, fq_self ? q8d() : nullptr);
             if (sh.self_sm)  // masked soft_max with scale 1 (Q, K pre-scaled; whisper.cpp:2614-2628)
-                attn_decoder_softmax(stream, d_q_.as<_Float16>(), d, Kl, Vl, d, 64, d_rs, R, d_keys, H, 1.0f, max_keys,
+                attn_decoder_softmax(stream, d_q_.as<_Float16>(), d, Kl, Vl, 64, kv_cells * 64, d_rs, R, d_keys, H, 1.0f,
+                                     max_keys,
                                      d_ao_.as<_Float16>(), d, nullptr, nullptr, 0, ao32);
         }
         if (fused) {

@@ -145,7 +145,7 @@ private:
     DevBuf post_d_, post_out_d_;
     // slot storage
     DevBuf cross_k_, cross_v_;   // [L][cap_slots][n_audio_ctx][d]
-    DevBuf self_k_, self_v_;     // [L][cap_slots][kv_cells][d]
+    DevBuf self_k_, self_v_;     // [L][cap_slots][head][kv_cells][64] (head-major)
     std::vector<DevBuf *> mel_;  // per slot [n_mel][n_len]
     std::vector<int> mel_len_;
 

@@ -815,7 +815,7 @@ void attn_decoder(hipStream_t s, const _Float16 * q, int ldq, const _Float16 * k
             hipLaunchKernelGGL((k_attn_step<true, false>), dim3(H, n_rows), dim3(64), 0, s, q, ldq, kbase, vbase, ld_kv, hs,
                                rows_dev, key_idx, scale, out, ldo, out32, q8, q8d);
         } else {
-            if (hs != 64)  // head-major cross K/V
+            if (!key_idx)  // cross attention (no cell lists): the once-per-step K/V stream
                 hipLaunchKernelGGL((k_attn_step<false, true>), dim3(H, n_rows), dim3(64), 0, s, q, ldq, kbase, vbase, ld_kv,
                                    hs, rows_dev, key_idx, scale, out, ldo, out32, q8, q8d);
             else

@@ -69,9 +69,12 @@ __device__ __forceinline__ void epi_store(const EpiParams & p, int r, int c, flo
         if (c < d) {
             p.out16[(size_t) r * p.ldo + c] = (_Float16) ((acc + p.bias[c]) * p.scale);
         } else if (c < 2 * d) {
-            p.out16b[p.row_off[r] + (c - d)] = (_Float16) (acc * p.scale);
+            // head-major self-attention cache [slot][head][cell][64]; Tpad = cells * 64
+            const int cc = c - d;
+            p.out16b[p.row_off[r] + (size_t) (cc >> 6) * p.Tpad + (cc & 63)] = (_Float16) (acc * p.scale);
         } else {
-            p.out16c[p.row_off[r] + (c - 2 * d)] = (_Float16) (acc + p.bias2[c - 2 * d]);
+            const int cc = c - 2 * d;
+            p.out16c[p.row_off[r] + (size_t) (cc >> 6) * p.Tpad + (cc & 63)] = (_Float16) (acc + p.bias2[cc]);
         }
     } else if constexpr (MODE == EPI_F32) {
         p.out32[(size_t) r * p.ldo + c] = acc;

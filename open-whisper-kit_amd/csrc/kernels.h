@@ -45,7 +45,8 @@ struct EpiParams {
     int Tpad = 0;                   // padded key count of the transposed V (EPI_QKV_ENC)
     const float * pos = nullptr;    // EPI_CONV2 positional embedding [T][d]
     const uint16_t * gelu_tab = nullptr;  // 65536-entry f16 GELU table
-    const int64_t * row_off = nullptr;    // EPI_QKV_DEC: element offset of each row's KV cell
+    const int64_t * row_off = nullptr;    // EPI_QKV_DEC: element offset of each row's KV cell in head 0
+                                          // (head h at + h * Tpad: the cache is head-major)
     const int * slot_map = nullptr;       // EPI_KV_CROSS: clip index -> cross-KV slot (null = identity)
 };
 
