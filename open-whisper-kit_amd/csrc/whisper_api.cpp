@@ -997,12 +997,43 @@ int owk_full_batch(struct whisper_context * ctx, struct whisper_state ** states,
                    const struct owk_full_ext * ext, const float * const * samples, const int * n_samples, int n_clips) {
     std::lock_guard<std::mutex> lk(ctx->mu);
     std::vector<whisper_full_params> ps(std::max(n_clips, 1), params);
-    try {
-        return full_batch(ctx, states, ps.data(), ext, samples, n_samples, n_clips);
-    } catch (const std::exception & e) {
-        log_msg(GGML_LOG_LEVEL_ERROR, "owk_full_batch: %s\n", e.what());
-        return -6;
+    // Clip groups on concurrent streams: the clips are independent, so G groups each run the
+    // whole stage-major pipeline on their own engine (the engine of the group's first state:
+    // own HIP stream, buffers and captured decode graphs) from their own host thread. The
+    // hardware queues then interleave one group's latency-bound decode kernels (small GEMMs,
+    // LayerNorms, launch gaps) with another group's HBM-bound attention. Per-clip results do
+    // not depend on the grouping. Opt-in (OWK_STREAM_GROUPS): measured on MI355X with 32
+    // large-v3 clips, 2 groups of 16 take exactly as long as one batch of 32 and 4 groups of
+    // 8 take 2.3x as long -- the dependent-kernel boundaries do not overlap across queues.
+    int groups = 1;
+    if (const char * g = getenv("OWK_STREAM_GROUPS")) groups = atoi(g);
+    if (ctx->prof.on) groups = 1;  // per-kernel HIP events live in one shared recorder
+    groups = std::max(1, std::min(groups, n_clips));
+    if (groups == 1) {
+        try {
+            return full_batch(ctx, states, ps.data(), ext, samples, n_samples, n_clips);
+        } catch (const std::exception & e) {
+            log_msg(GGML_LOG_LEVEL_ERROR, "owk_full_batch: %s\n", e.what());
+            return -6;
+        }
     }
+    std::vector<int> ret(groups, 0);
+    std::vector<std::thread> th;
+    for (int g = 0; g < groups; ++g) {
+        const int c0 = (int) ((int64_t) n_clips * g / groups), c1 = (int) ((int64_t) n_clips * (g + 1) / groups);
+        th.emplace_back([&, g, c0, c1] {
+            try {
+                ret[g] = full_batch(ctx, states + c0, ps.data() + c0, ext, samples + c0, n_samples + c0, c1 - c0);
+            } catch (const std::exception & e) {
+                log_msg(GGML_LOG_LEVEL_ERROR, "owk_full_batch: %s\n", e.what());
+                ret[g] = -6;
+            }
+        });
+    }
+    for (auto & t : th) t.join();
+    for (int r : ret)
+        if (r != 0) return r;
+    return 0;
 }
 
 void owk_prof_enable(struct whisper_context * ctx, int enable) {
