@@ -92,7 +92,7 @@ def header_symbols(include_dir=None):
     import re
     include_dir = include_dir or os.path.normpath(os.path.join(HERE, "..", "..", "include"))
     syms = []
-    for h in ("whisper.h", "owk.h", "ggml-backend.h"):
+    for h in ("whisper.h", "owk.h", "owk_diarize.h", "ggml-backend.h"):
         txt = open(os.path.join(include_dir, h)).read()
         txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
         for m in re.finditer(r"\b((?:whisper|owk|ggml_backend)_[a-z0-9_]+)\s*\(", txt):
@@ -313,3 +313,103 @@ class Whisper:
                             no_speech_prob=L.whisper_full_get_segment_no_speech_prob_from_state(state, i),
                             tokens=toks))
         return out
+
+
+# ---------------------------------------------------------------------------------
+# speaker attribution (include/owk_diarize.h): the reference SDK's Swift
+# DiarizationAligner / RTTMParser, implemented in C++ inside libwhisper.so
+# ---------------------------------------------------------------------------------
+class OwkWord(C.Structure):
+    _fields_ = [("word", C.c_char_p), ("start", C.c_float), ("end", C.c_float), ("probability", C.c_float)]
+
+
+class OwkDseg(C.Structure):
+    _fields_ = [("speaker", C.c_char_p), ("start", C.c_float), ("end", C.c_float)]
+
+
+class OwkAlignOptions(C.Structure):
+    _fields_ = [("fill_nearest", C.c_int), ("sentence_smoothing", C.c_int), ("max_words_in_sentence", C.c_int)]
+
+
+class AlignmentFailed(ValueError):
+    """DiarizationError.alignmentFailed of the reference SDK."""
+
+
+def _diarize_protos(L):
+    vp, ip, fp, cp = C.c_void_p, C.c_int, C.POINTER(C.c_float), C.c_char_p
+    L.owk_align_default_options.restype = OwkAlignOptions
+    L.owk_align.restype = vp
+    L.owk_align.argtypes = [C.POINTER(OwkWord), ip, C.POINTER(OwkDseg), ip, OwkAlignOptions]
+    L.owk_alignment_free.argtypes = [vp]
+    L.owk_alignment_n_words.argtypes = [vp]
+    L.owk_alignment_word_speaker.argtypes = [vp, ip]
+    L.owk_alignment_word_speaker.restype = cp
+    L.owk_alignment_n_utterances.argtypes = [vp]
+    L.owk_alignment_utterance.argtypes = [vp, ip, C.POINTER(cp), C.POINTER(cp), fp, fp, C.POINTER(ip), C.POINTER(ip)]
+    L.owk_alignment_text.argtypes = [vp]
+    L.owk_alignment_text.restype = cp
+    L.owk_rttm_parse.restype = vp
+    L.owk_rttm_parse.argtypes = [cp]
+    L.owk_rttm_n_segments.argtypes = [vp]
+    L.owk_rttm_segment.argtypes = [vp, ip, C.POINTER(cp), fp, fp]
+    L.owk_rttm_free.argtypes = [vp]
+    L.owk_rttm_generate.argtypes = [C.POINTER(OwkDseg), ip, cp, C.c_char_p, ip]
+
+
+def _dec(b):
+    return None if b is None else b.decode("utf-8")
+
+
+def align(words, segments, fill_nearest=False, sentence_smoothing=True, max_words_in_sentence=50):
+    """DiarizationAligner.align: words = [(text, start, end, prob)], segments = [(speaker, start, end)].
+    Returns {"words": [(text, start, end, speaker)], "segments": [{speaker, text, start, end, words}], "text"}."""
+    L = load()
+    _diarize_protos(L)
+    W = (OwkWord * max(1, len(words)))(*[OwkWord(w[0].encode(), w[1], w[2], w[3] if len(w) > 3 else 0.0) for w in words])
+    S = (OwkDseg * max(1, len(segments)))(*[OwkDseg(s[0].encode(), s[1], s[2]) for s in segments])
+    opt = OwkAlignOptions(int(fill_nearest), int(sentence_smoothing), int(max_words_in_sentence))
+    h = L.owk_align(W, len(words), S, len(segments), opt)
+    if not h:
+        raise AlignmentFailed("maxWordsInSentence must be greater than 0")
+    try:
+        out_words = [(w[0], w[1], w[2], _dec(L.owk_alignment_word_speaker(h, i))) for i, w in enumerate(words)]
+        utts = []
+        for i in range(L.owk_alignment_n_utterances(h)):
+            spk, txt = C.c_char_p(), C.c_char_p()
+            t0, t1 = C.c_float(), C.c_float()
+            first, n = C.c_int(), C.c_int()
+            L.owk_alignment_utterance(h, i, C.byref(spk), C.byref(txt), C.byref(t0), C.byref(t1), C.byref(first),
+                                      C.byref(n))
+            utts.append({"speaker": _dec(spk.value), "text": _dec(txt.value), "start": t0.value, "end": t1.value,
+                         "words": list(range(first.value, first.value + n.value))})
+        return {"words": out_words, "segments": utts, "text": _dec(L.owk_alignment_text(h))}
+    finally:
+        L.owk_alignment_free(h)
+
+
+def rttm_parse(text):
+    """RTTMParser.parse -> [(speaker, start, end)] sorted by start."""
+    L = load()
+    _diarize_protos(L)
+    h = L.owk_rttm_parse(text.encode())
+    try:
+        out = []
+        for i in range(L.owk_rttm_n_segments(h)):
+            spk = C.c_char_p()
+            t0, t1 = C.c_float(), C.c_float()
+            L.owk_rttm_segment(h, i, C.byref(spk), C.byref(t0), C.byref(t1))
+            out.append((_dec(spk.value), t0.value, t1.value))
+        return out
+    finally:
+        L.owk_rttm_free(h)
+
+
+def rttm_generate(segments, filename):
+    """RTTMParser.generate for [(speaker, start, end)]."""
+    L = load()
+    _diarize_protos(L)
+    S = (OwkDseg * max(1, len(segments)))(*[OwkDseg(s[0].encode(), s[1], s[2]) for s in segments])
+    n = L.owk_rttm_generate(S, len(segments), filename.encode(), None, 0)
+    buf = C.create_string_buffer(n + 1)
+    L.owk_rttm_generate(S, len(segments), filename.encode(), buf, n + 1)
+    return buf.value.decode()

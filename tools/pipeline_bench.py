@@ -7,7 +7,10 @@ Workload (synthetic data and random-init weights of the real architectures, as b
     the reference) and dtw_aheads_preset = WHISPER_AHEADS_LARGE_V3; the clip is cut into 30 s
     chunks decoded as one owk_full_batch (the whisper_full_parallel split), greedy,
     temperature_inc = 0, timestamps on, token timestamps on;
-  * diarization: sortformer_diarize of the whole clip (default parameters).
+  * diarization: sortformer_diarize of the whole clip (default parameters);
+  * alignment: sortformer_to_rttm -> RTTM parse -> DiarizationAligner.align of every token
+    (the Swift SDK's WordTiming per token, WhisperContext.swift:126-139, chunk offsets added),
+    all host C++ in libwhisper.so (include/owk_diarize.h).
 Reports the wall time of each part and the real-time factor of the whole job; the reference
 CPU path (16 threads) is timed on ONE 30 s chunk of the same transcription settings.
 
@@ -75,10 +78,26 @@ def main():
     t0 = time.perf_counter()
     probs = sf.diarize(pcm)
     t_diar = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    import ctypes as C
+    w.L.whisper_token_to_str.restype = C.c_char_p
+    w.L.whisper_token_to_str.argtypes = [C.c_void_p, C.c_int]
+    segs = owk.rttm_parse(SF.to_rttm(probs))
+    words = []
+    for ci, st_ in enumerate(states):
+        off = ci * CHUNK / 16000.0
+        for s in w.segments(st_):
+            for t in s["tokens"]:
+                txt = w.L.whisper_token_to_str(w.ctx, t[0]).decode("utf-8", "replace")
+                words.append((txt, off + t[6] / 100.0, off + t[7] / 100.0, t[2]))
+    aligned = owk.align(words, segs)
+    t_align = time.perf_counter() - t0
     audio_s = n / 16000
-    out = {"metric": "transcribe + DTW + diarize real-time factor (audio-s/wall-s), configs[4]",
-           "unit": "audio-s/wall-s", "value": round(audio_s / (t_asr + t_diar), 2), "audio_s": audio_s,
-           "asr_wall_s": round(t_asr, 3), "diarize_wall_s": round(t_diar, 4), "chunks": len(chunks),
+    out = {"metric": "transcribe + DTW + diarize + align real-time factor (audio-s/wall-s), configs[4]",
+           "unit": "audio-s/wall-s", "value": round(audio_s / (t_asr + t_diar + t_align), 2), "audio_s": audio_s,
+           "asr_wall_s": round(t_asr, 3), "diarize_wall_s": round(t_diar, 4), "align_wall_s": round(t_align, 4),
+           "rttm_segments": len(segs), "aligned_words": len(aligned["words"]),
+           "utterances": len(aligned["segments"]), "chunks": len(chunks),
            "tokens": n_tok, "tokens_with_t_dtw": n_dtw, "diarize_frames": int(probs.shape[0]),
            "workload": "large-v3 F16 flash_attn=false + DTW (LARGE_V3 heads), 30 s chunks in one batch, greedy; "
                        "SortFormer offline, synthetic weights and audio"}
