@@ -34,6 +34,17 @@ WHISPER_API int owk_full_batch(struct whisper_context * ctx, struct whisper_stat
                                struct whisper_full_params params, const struct owk_full_ext * ext,
                                const float * const * samples, const int * n_samples, int n_clips);
 
+/* Silero VAD over n_streams independent streams in one device pass (all chunks encoded
+ * together, one LSTM workgroup per stream, each stream from a zero state): probs_out[s]
+ * receives ceil(n_samples[s] / 512) speech probabilities, the values
+ * whisper_vad_detect_speech would give for that stream alone. Returns 0 on success. */
+WHISPER_API int owk_vad_detect_batch(struct whisper_vad_context * vctx, const float * const * samples,
+                                     const int * n_samples, int n_streams, float * const * probs_out);
+/* test hook (host only): whisper_vad_segments_from_probs on a caller's probabilities;
+ * writes [start_cs, end_cs] pairs (up to cap) and returns the segment count */
+WHISPER_API int owk_vad_segments_raw(const float * probs, int n_probs, int n_window, struct whisper_vad_params params,
+                                     int64_t * out_cs, int cap);
+
 /* per-kernel-class device timing with HIP events recorded on the engine stream */
 WHISPER_API void owk_prof_enable(struct whisper_context * ctx, int enable);
 WHISPER_API void owk_prof_reset(struct whisper_context * ctx);

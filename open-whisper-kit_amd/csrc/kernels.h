@@ -225,4 +225,25 @@ void nosp_probs(hipStream_t s, const float * row0, int n_vocab, const int2 * req
 void process_logits(hipStream_t s, float * logits, int n_vocab, const LogitJob * jobs_dev, int n_jobs,
                     const VocabInfo & vi, TokenOut * out_dev, float * logprobs_out, float * probs_out);
 
+// Silero VAD (k_vad.hip). Weights as the kernels read them: F16 conv weights transposed
+// to [(ic * K + k)][OC] (im2col row order), W_ih transposed to [128][512], W_hh row-major.
+struct VadWeights {
+    const _Float16 * stft_T;    // [256][258]
+    const _Float16 * enc_T[4];  // [(ic*3 + k)][OC]
+    const float * enc_b[4];
+    const float * ih_T;         // [128][512]
+    const float * b_ih;
+    const float * w_hh;         // [512][128]
+    const float * b_hh;
+    const _Float16 * wf;        // [128]
+    const float * bf;           // [1]
+};
+// chunks of n_streams streams; chunk g reads pcm[pcm_off[s] + 512 * chunk_index[g] ...] of
+// stream s = chunk_stream[g] (zero past pcm_len[s]); stream s owns chunks
+// [stream_first[s], stream_first[s] + stream_n[s]) and LSTM state state[s][h(128) | c(128)]
+void launch_vad(const VadWeights & w, const float * pcm, const int64_t * pcm_off, const int * pcm_len,
+                const int * chunk_stream, const int * chunk_index, int n_chunks, const int * stream_first,
+                const int * stream_n, int n_streams, float * ig, float * hist, float * state, float * probs,
+                hipStream_t stream);
+
 } // namespace owk

@@ -72,6 +72,11 @@ struct whisper_state {
     // DTW alignment heads (dtw_token_timestamps): [layer][head] -> global index or -1
     std::vector<int> dtw_amap;
     int dtw_n_ah = 0;
+    // whisper_full's VAD pre-pass (ref whisper.cpp:923-932, 6643-6826): the state's own VAD
+    // context and the processed -> original centisecond table the segment getters apply
+    whisper_vad_context * vad_context = nullptr;
+    bool has_vad_segments = false;
+    std::vector<std::pair<int64_t, int64_t>> vad_map;
 };
 
 struct whisper_context {
@@ -107,6 +112,10 @@ void dtw_timestamps(whisper_context * ctx, whisper_state * st, int i_segment, in
                     int medfilt, const std::vector<float> & cap, int n_ah, int n_audio_ctx, int n_tok, int sot_len);
 // configure a state's engine for its context (attention mode, alignment heads)
 void configure_engine(const whisper_context * ctx, whisper_state * st);
+// Silero VAD (vad.cpp)
+bool vad_filter(whisper_context * ctx, whisper_state * state, const whisper_full_params & params, const float * samples,
+                int n_samples, std::vector<float> & filtered);
+int64_t vad_map_time(int64_t t, const std::vector<std::pair<int64_t, int64_t>> & map);
 int full_batch(whisper_context * ctx, whisper_state ** states, const whisper_full_params * params,
                const owk_full_ext * ext, const float * const * samples, const int * n_samples, int n_clips);
 } // namespace owk

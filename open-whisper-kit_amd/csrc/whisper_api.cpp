@@ -169,25 +169,6 @@ struct whisper_context_params * whisper_context_default_params_by_ref(void) {
     return new whisper_context_params(whisper_context_default_params());
 }
 
-struct whisper_vad_params whisper_vad_default_params(void) {
-    // ref whisper.cpp:4438-4449
-    whisper_vad_params r{};
-    r.threshold = 0.5f;
-    r.min_speech_duration_ms = 250;
-    r.min_silence_duration_ms = 100;
-    r.max_speech_duration_s = FLT_MAX;
-    r.speech_pad_ms = 30;
-    r.samples_overlap = 0.1f;
-    return r;
-}
-
-struct whisper_vad_context_params whisper_vad_default_context_params(void) {
-    whisper_vad_context_params r{};
-    r.n_threads = 4;
-    r.use_gpu = false;
-    r.gpu_device = 0;
-    return r;
-}
 
 struct whisper_full_params whisper_full_default_params(enum whisper_sampling_strategy strategy) {
     whisper_full_params r{};
@@ -385,7 +366,10 @@ int whisper_ctx_init_openvino_encoder_with_state(struct whisper_context *, struc
 }
 int whisper_ctx_init_openvino_encoder(struct whisper_context *, const char *, const char *, const char *) { return 1; }
 
-void whisper_free_state(struct whisper_state * state) { delete state; }
+void whisper_free_state(struct whisper_state * state) {
+    if (state && state->vad_context) whisper_vad_free(state->vad_context);  // ref 3838-3841
+    delete state;
+}
 
 void whisper_free(struct whisper_context * ctx) {
     if (!ctx) return;
@@ -754,7 +738,21 @@ int whisper_full_with_state(struct whisper_context * ctx, struct whisper_state *
     }
 }
 
+// ref 7778-7799: the VAD pre-pass belongs to whisper_full (not whisper_full_with_state)
 int whisper_full(struct whisper_context * ctx, struct whisper_full_params params, const float * samples, int n_samples) {
+    std::vector<float> vad_samples;
+    if (params.vad) {
+        if (!vad_filter(ctx, ctx->state, params, samples, n_samples, vad_samples)) {
+            log_msg(GGML_LOG_LEVEL_ERROR, "whisper_full: failed to compute VAD\n");
+            return -1;
+        }
+        if (vad_samples.empty()) {
+            ctx->state->result_all.clear();
+            return 0;
+        }
+        samples = vad_samples.data();
+        n_samples = (int) vad_samples.size();
+    }
     return whisper_full_with_state(ctx, ctx->state, params, samples, n_samples);
 }
 
@@ -763,9 +761,15 @@ int whisper_full(struct whisper_context * ctx, struct whisper_full_params params
 int whisper_full_parallel(struct whisper_context * ctx, struct whisper_full_params params, const float * samples,
                           int n_samples, int n_processors) {
     if (n_processors == 1) return whisper_full(ctx, params, samples, n_samples);
+    std::vector<float> vad_samples;  // ref 7812-7824
     if (params.vad) {
-        log_msg(GGML_LOG_LEVEL_ERROR, "whisper_full_parallel: VAD is not supported by this engine build\n");
-        return -1;
+        if (!vad_filter(ctx, ctx->state, params, samples, n_samples, vad_samples)) {
+            log_msg(GGML_LOG_LEVEL_ERROR, "whisper_full_parallel: failed to compute VAD\n");
+            return -1;
+        }
+        if (vad_samples.empty()) return 0;
+        samples = vad_samples.data();
+        n_samples = (int) vad_samples.size();
     }
     const int offset_samples = (WHISPER_SAMPLE_RATE * params.offset_ms) / 1000;
     const int per = (n_samples - offset_samples) / n_processors;
@@ -833,10 +837,20 @@ int whisper_full_n_segments_from_state(struct whisper_state * state) { return (i
 int whisper_full_n_segments(struct whisper_context * ctx) { return (int) ctx->state->result_all.size(); }
 int whisper_full_lang_id_from_state(struct whisper_state * state) { return state->lang_id; }
 int whisper_full_lang_id(struct whisper_context * ctx) { return ctx->state->lang_id; }
-int64_t whisper_full_get_segment_t0_from_state(struct whisper_state * state, int i) { return state->result_all[i].t0; }
-int64_t whisper_full_get_segment_t1_from_state(struct whisper_state * state, int i) { return state->result_all[i].t1; }
-int64_t whisper_full_get_segment_t0(struct whisper_context * ctx, int i) { return ctx->state->result_all[i].t0; }
-int64_t whisper_full_get_segment_t1(struct whisper_context * ctx, int i) { return ctx->state->result_all[i].t1; }
+// segment times in the original audio when whisper_full ran the VAD pre-pass (ref 7986-8025)
+int64_t whisper_full_get_segment_t0_from_state(struct whisper_state * state, int i) {
+    if (!state->has_vad_segments || state->vad_map.empty()) return state->result_all[i].t0;
+    return vad_map_time(state->result_all[i].t0, state->vad_map);
+}
+int64_t whisper_full_get_segment_t1_from_state(struct whisper_state * state, int i) {
+    if (!state->has_vad_segments || state->vad_map.empty()) return state->result_all[i].t1;
+    int64_t t1 = vad_map_time(state->result_all[i].t1, state->vad_map);
+    const int64_t t0 = whisper_full_get_segment_t0_from_state(state, i);
+    if (t1 - t0 < 10) t1 = t0 + 10;
+    return t1;
+}
+int64_t whisper_full_get_segment_t0(struct whisper_context * ctx, int i) { return whisper_full_get_segment_t0_from_state(ctx->state, i); }
+int64_t whisper_full_get_segment_t1(struct whisper_context * ctx, int i) { return whisper_full_get_segment_t1_from_state(ctx->state, i); }
 bool whisper_full_get_segment_speaker_turn_next_from_state(struct whisper_state * state, int i) {
     return state->result_all[i].speaker_turn_next;
 }
@@ -873,36 +887,6 @@ float whisper_full_get_segment_no_speech_prob(struct whisper_context * ctx, int 
 float whisper_full_get_segment_no_speech_prob_from_state(struct whisper_state * state, int i) {
     return state->result_all[i].no_speech_prob;
 }
-
-// ---------------------------------------------------------------------------------
-// VAD: not part of this engine build (SURVEY 2.1 N9, next-row candidate)
-// ---------------------------------------------------------------------------------
-struct whisper_vad_context * whisper_vad_init_from_file_with_params(const char *, struct whisper_vad_context_params) {
-    log_msg(GGML_LOG_LEVEL_ERROR, "whisper_vad_init: Silero VAD is not available in this engine build\n");
-    return nullptr;
-}
-struct whisper_vad_context * whisper_vad_init_with_params(struct whisper_model_loader * loader, struct whisper_vad_context_params) {
-    if (loader && loader->close) loader->close(loader->context);
-    log_msg(GGML_LOG_LEVEL_ERROR, "whisper_vad_init: Silero VAD is not available in this engine build\n");
-    return nullptr;
-}
-bool whisper_vad_detect_speech(struct whisper_vad_context *, const float *, int) { return false; }
-bool whisper_vad_detect_speech_stateful(struct whisper_vad_context *, const float *, int) { return false; }
-void whisper_vad_reset_state(struct whisper_vad_context *) {}
-int whisper_vad_n_probs(struct whisper_vad_context *) { return 0; }
-float * whisper_vad_probs(struct whisper_vad_context *) { return nullptr; }
-struct whisper_vad_segments * whisper_vad_segments_from_probs(struct whisper_vad_context *, struct whisper_vad_params) {
-    return nullptr;
-}
-struct whisper_vad_segments * whisper_vad_segments_from_samples(struct whisper_vad_context *, struct whisper_vad_params,
-                                                                 const float *, int) {
-    return nullptr;
-}
-int whisper_vad_segments_n_segments(struct whisper_vad_segments *) { return 0; }
-float whisper_vad_segments_get_segment_t0(struct whisper_vad_segments *, int) { return 0.0f; }
-float whisper_vad_segments_get_segment_t1(struct whisper_vad_segments *, int) { return 0.0f; }
-void whisper_vad_free_segments(struct whisper_vad_segments *) {}
-void whisper_vad_free(struct whisper_vad_context *) {}
 
 // ---------------------------------------------------------------------------------
 // microbenchmarks (ref 8107-8375: memcpy and ggml_mul_mat GFLOPS) on the device

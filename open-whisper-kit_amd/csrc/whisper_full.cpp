@@ -820,10 +820,8 @@ int full_batch(whisper_context * ctx, whisper_state ** states, const whisper_ful
                const owk_full_ext * ext, const float * const * samples, const int * n_samples, int n_clips) {
     if (n_clips <= 0) return 0;
     const whisper_full_params & params = params_v[0];
-    if (params.vad) {
-        log_msg(GGML_LOG_LEVEL_ERROR, "whisper_full: VAD is not supported by this engine build\n");
-        return -1;
-    }
+    // params.vad is whisper_full's pre-pass (whisper_api.cpp); like the reference's
+    // whisper_full_with_state, the per-state path ignores it
     if (params.n_grammar_rules > 0) {
         log_msg(GGML_LOG_LEVEL_ERROR, "whisper_full: grammar-constrained decoding is not supported by this engine build\n");
         return -1;

@@ -40,6 +40,10 @@ class VadParams(C.Structure):
                 ("max_speech_duration_s", C.c_float), ("speech_pad_ms", C.c_int), ("samples_overlap", C.c_float)]
 
 
+class VadContextParams(C.Structure):  # whisper.h:682-686
+    _fields_ = [("n_threads", C.c_int), ("use_gpu", C.c_bool), ("gpu_device", C.c_int)]
+
+
 class _Greedy(C.Structure):
     _fields_ = [("best_of", C.c_int)]
 
@@ -192,6 +196,30 @@ def load(path: str | None = None) -> C.CDLL:
     L.owk_debug_gelu_table.restype = C.POINTER(C.c_uint16)
     u16p = C.POINTER(C.c_uint16)
     L.owk_debug_gemm.argtypes = [ip, ip, ip, ip, u16p, u16p, fp]
+    # Silero VAD (whisper.h:678-732, owk.h)
+    L.whisper_vad_default_params.restype = VadParams
+    L.whisper_vad_default_context_params.restype = VadContextParams
+    L.whisper_vad_init_from_file_with_params.restype = vp
+    L.whisper_vad_init_from_file_with_params.argtypes = [C.c_char_p, VadContextParams]
+    for n in ("whisper_vad_detect_speech", "whisper_vad_detect_speech_stateful"):
+        getattr(L, n).restype = C.c_bool
+        getattr(L, n).argtypes = [vp, fp, ip]
+    L.whisper_vad_reset_state.argtypes = [vp]
+    L.whisper_vad_n_probs.argtypes = [vp]
+    L.whisper_vad_probs.restype = fp
+    L.whisper_vad_probs.argtypes = [vp]
+    L.whisper_vad_segments_from_probs.restype = vp
+    L.whisper_vad_segments_from_probs.argtypes = [vp, VadParams]
+    L.whisper_vad_segments_from_samples.restype = vp
+    L.whisper_vad_segments_from_samples.argtypes = [vp, VadParams, fp, ip]
+    L.whisper_vad_segments_n_segments.argtypes = [vp]
+    for n in ("whisper_vad_segments_get_segment_t0", "whisper_vad_segments_get_segment_t1"):
+        getattr(L, n).restype = C.c_float
+        getattr(L, n).argtypes = [vp, ip]
+    L.whisper_vad_free_segments.argtypes = [vp]
+    L.whisper_vad_free.argtypes = [vp]
+    L.owk_vad_detect_batch.argtypes = [vp, C.POINTER(fp), C.POINTER(ip), ip, C.POINTER(fp)]
+    L.owk_vad_segments_raw.argtypes = [fp, ip, ip, VadParams, C.POINTER(C.c_int64), ip]
     _lib = L
     return L
 

@@ -202,6 +202,11 @@ int ref_decode(void * vctx, const int * tokens, int n_tokens, int n_past, int n_
 
 float * ref_logits(void * vctx) { return whisper_get_logits((whisper_context *) vctx); }
 
+// whisper_full's VAD pre-pass (whisper.cpp:7785-7796, 6643-6826): a non-null path turns it
+// on for the following ref_full calls with whisper_vad_default_params()
+static std::string g_vad_path;
+void ref_set_vad(const char * path) { g_vad_path = path ? path : ""; }
+
 int ref_full(void * vctx, const float * pcm, int n, const ref_full_cfg * cfg) {
     auto * ctx = (whisper_context *) vctx;
     auto p = whisper_full_default_params(cfg->strategy == 1 ? WHISPER_SAMPLING_BEAM_SEARCH
@@ -231,6 +236,10 @@ int ref_full(void * vctx, const float * pcm, int n, const ref_full_cfg * cfg) {
         g_rec_suppress_eot = cfg->suppress_eot != 0;
         g_rec_trace_only = cfg->record_topk == 2;
         p.logits_filter_callback = ref_record_cb;
+    }
+    if (!g_vad_path.empty()) {
+        p.vad = true;
+        p.vad_model_path = g_vad_path.c_str();
     }
     return whisper_full(ctx, p, pcm, n);
 }

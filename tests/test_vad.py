@@ -1,0 +1,246 @@
+"""Silero VAD: whisper_vad_* C ABI and whisper_full's VAD pre-pass.
+
+Fixtures: tests/golden/vad_golden.{json,npz}, made by tests/golden/make_golden_vad.py
+running the REFERENCE (ref/src/whisper.cpp:4345-5496, 6643-6826, 7947-8025 compiled into
+oracle/_ref) on the reference's own real-weight Silero v6.2.0 test model
+(tests/golden/silero-v6.2.0-ggml.bin, copied from ref/models/for-tests-silero-v6.2.0-ggml.bin).
+The reference's own test (ref/tests/test-vad.cpp:30-39) asserts 344 probabilities and
+4 segments for samples/jfk.wav; both are checked here too.
+
+Tolerances: speech probabilities |diff| <= 1e-3 (f32 sums in another order, plus the
+F16 roundings of the conv inputs they can flip: the numpy restatement sits at 1.6e-4 of
+the reference); segment boundaries (integer centiseconds) identical; whisper_full tokens
+and segment times identical.
+"""
+import ctypes as C
+import json
+import os
+
+import numpy as np
+import pytest
+
+import owk
+import vad_np as V
+from make_golden_vad import PARAM_VARIANTS, vad_clips
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+VAD_MODEL = os.path.join(GOLDEN, "silero-v6.2.0-ggml.bin")
+PROB_ATOL = 1e-3
+
+
+@pytest.fixture(scope="module")
+def vg():
+    return json.load(open(os.path.join(GOLDEN, "vad_golden.json"))), np.load(os.path.join(GOLDEN, "vad_golden.npz"))
+
+
+@pytest.fixture(scope="module")
+def clips():
+    return vad_clips()
+
+
+def _params(L, **kw):
+    p = L.whisper_vad_default_params()
+    for k, v in kw.items():
+        setattr(p, k, v)
+    return p
+
+
+# ------------------------------------------------------------------ CPU: oracle + host logic
+def test_reference_known_answers(vg):
+    """ref/tests/test-vad.cpp:30-39 on the committed fixture."""
+    meta, arr = vg
+    assert arr["probs/jfk"].shape == (344,)
+    assert len(meta["segments"]["jfk/default"]) == 4
+
+
+def test_oracle_probs_pinned(vg, clips):
+    meta, arr = vg
+    v = V.Vad(VAD_MODEL)
+    for name in ("jfk", "short", "silence"):
+        np.testing.assert_allclose(v.detect(clips[name]), arr[f"probs/{name}"], atol=PROB_ATOL, rtol=0)
+    jfk = clips["jfk"]
+    sp = meta["stateful_splits"]
+    v.reset()
+    got = np.concatenate([v.detect(jfk[sp[i]:sp[i + 1]], reset=False) for i in range(len(sp) - 1)])
+    np.testing.assert_allclose(got, arr["probs/jfk_stateful"], atol=PROB_ATOL, rtol=0)
+
+
+def test_oracle_segments_pinned(vg):
+    meta, arr = vg
+    for key, want in meta["segments"].items():
+        clip, var = key.split("/")
+        got = V.segments_from_probs(arr[f"probs/{clip}"], **PARAM_VARIANTS[var])
+        assert [list(map(float, s)) for s in got] == want, key
+
+
+def _segments_raw(L, probs, **kw):
+    probs = np.ascontiguousarray(probs, np.float32)
+    out = np.zeros(2 * 4096, np.int64)
+    n = L.owk_vad_segments_raw(owk.fptr(probs), len(probs), 512, _params(L, **kw),
+                               out.ctypes.data_as(C.POINTER(C.c_int64)), 4096)
+    return [(int(out[2 * i]), int(out[2 * i + 1])) for i in range(n)]
+
+
+def test_segments_host_code_matches_reference(vg):
+    """the product's C++ segments_from_probs (csrc/vad.cpp) on the reference's probabilities"""
+    L = owk.load()
+    meta, arr = vg
+    for key, want in meta["segments"].items():
+        clip, var = key.split("/")
+        got = _segments_raw(L, arr[f"probs/{clip}"], **PARAM_VARIANTS[var])
+        assert [list(map(float, s)) for s in got] == want, key
+
+
+def test_segments_host_code_random_differential():
+    """randomized: C++ host logic vs the Python restatement on blocky random probabilities"""
+    L = owk.load()
+    rng = np.random.default_rng(3)
+    for trial in range(200):
+        n = int(rng.integers(0, 900))
+        runs = np.repeat(rng.uniform(0, 1, size=max(1, n // 6 + 1)), rng.integers(1, 30, size=max(1, n // 6 + 1)))[:n]
+        probs = np.clip(runs + 0.1 * rng.standard_normal(len(runs)), 0, 1).astype(np.float32)
+        kw = dict(threshold=float(rng.choice([0.2, 0.5, 0.7])), min_speech_duration_ms=int(rng.choice([0, 250, 600])),
+                  min_silence_duration_ms=int(rng.choice([0, 100, 400])),
+                  max_speech_duration_s=float(rng.choice([0.5, 2.0, 3.4028235e38])),
+                  speech_pad_ms=int(rng.choice([0, 30, 150])))
+        assert _segments_raw(L, probs, **kw) == V.segments_from_probs(probs, **kw), (trial, kw)
+
+
+def test_default_params_match_reference():
+    """ref/tests/test-vad.cpp:12-23 and whisper.cpp:4429-4449"""
+    L = owk.load()
+    p = L.whisper_vad_default_params()
+    assert p.threshold == np.float32(0.5) and p.min_speech_duration_ms == 250
+    assert p.min_silence_duration_ms == 100 and p.samples_overlap == np.float32(0.1) and p.speech_pad_ms == 30
+    c = L.whisper_vad_default_context_params()
+    assert c.n_threads == 4 and not c.use_gpu and c.gpu_device == 0
+
+
+# ------------------------------------------------------------------ GPU
+@pytest.fixture(scope="module")
+def vctx():
+    L = owk.load()
+    assert L.owk_device_ok(0) == 1, "no gfx950 device / HIP code object not loadable"
+    owk.quiet()
+    v = L.whisper_vad_init_from_file_with_params(VAD_MODEL.encode(), L.whisper_vad_default_context_params())
+    assert v, "whisper_vad_init_from_file_with_params failed"
+    yield L, v
+    L.whisper_vad_free(v)
+
+
+def _probs(L, v):
+    n = L.whisper_vad_n_probs(v)
+    return np.ctypeslib.as_array(L.whisper_vad_probs(v), (n,)).copy() if n else np.zeros(0, np.float32)
+
+
+def _segs(L, s):
+    out = [[L.whisper_vad_segments_get_segment_t0(s, i), L.whisper_vad_segments_get_segment_t1(s, i)]
+           for i in range(L.whisper_vad_segments_n_segments(s))]
+    L.whisper_vad_free_segments(s)
+    return out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("clip", ["jfk", "composite", "silence", "short"])
+def test_gpu_probs_and_segments(vctx, vg, clips, clip):
+    L, v = vctx
+    meta, arr = vg
+    pcm = np.ascontiguousarray(clips[clip], np.float32)
+    assert L.whisper_vad_detect_speech(v, owk.fptr(pcm), len(pcm))
+    got = _probs(L, v)
+    want = arr[f"probs/{clip}"]
+    assert got.shape == want.shape
+    np.testing.assert_allclose(got, want, atol=PROB_ATOL, rtol=0)
+    for key, segs in meta["segments"].items():
+        c, var = key.split("/")
+        if c == clip:
+            assert _segs(L, L.whisper_vad_segments_from_probs(v, _params(L, **PARAM_VARIANTS[var]))) == segs, key
+
+
+@pytest.mark.gpu
+def test_gpu_stateful_and_reset(vctx, vg, clips):
+    L, v = vctx
+    meta, arr = vg
+    jfk = clips["jfk"]
+    sp = meta["stateful_splits"]
+    L.whisper_vad_reset_state(v)
+    parts = []
+    for i in range(len(sp) - 1):
+        piece = np.ascontiguousarray(jfk[sp[i]:sp[i + 1]])
+        assert L.whisper_vad_detect_speech_stateful(v, owk.fptr(piece), len(piece))
+        parts.append(_probs(L, v))
+    np.testing.assert_allclose(np.concatenate(parts), arr["probs/jfk_stateful"], atol=PROB_ATOL, rtol=0)
+    # a stateless call after stateful ones starts from zero state again
+    pcm = np.ascontiguousarray(jfk)
+    assert L.whisper_vad_detect_speech(v, owk.fptr(pcm), len(pcm))
+    np.testing.assert_allclose(_probs(L, v), arr["probs/jfk"], atol=PROB_ATOL, rtol=0)
+    # segments_from_samples = detect + segments_from_probs; empty input -> 0 probs
+    assert _segs(L, L.whisper_vad_segments_from_samples(v, L.whisper_vad_default_params(), owk.fptr(pcm), len(pcm))) \
+        == meta["segments"]["jfk/default"]
+    assert L.whisper_vad_detect_speech(v, owk.fptr(pcm), 0) and L.whisper_vad_n_probs(v) == 0
+
+
+@pytest.mark.gpu
+def test_gpu_batch_equals_single_streams(vctx, vg, clips):
+    """owk_vad_detect_batch: many streams in one pass = each stream alone (bit-identical)"""
+    L, v = vctx
+    meta, arr = vg
+    rng = np.random.default_rng(9)
+    streams = [clips["jfk"], clips["composite"], clips["short"], clips["silence"]]
+    streams += [clips["composite"][int(rng.integers(0, 300000)):][:int(rng.integers(1, 200000))] for _ in range(12)]
+    streams = [np.ascontiguousarray(s, np.float32) for s in streams]
+    outs = [np.zeros((len(s) + 511) // 512, np.float32) for s in streams]
+    n = len(streams)
+    ret = L.owk_vad_detect_batch(v, (C.POINTER(C.c_float) * n)(*[owk.fptr(s) for s in streams]),
+                                 (C.c_int * n)(*[len(s) for s in streams]), n,
+                                 (C.POINTER(C.c_float) * n)(*[owk.fptr(o) for o in outs]))
+    assert ret == 0
+    for s, o in zip(streams, outs):
+        assert L.whisper_vad_detect_speech(v, owk.fptr(s), len(s))
+        np.testing.assert_array_equal(o, _probs(L, v))
+    np.testing.assert_allclose(outs[0], arr["probs/jfk"], atol=PROB_ATOL, rtol=0)
+
+
+_EOT = {}
+
+
+@C.CFUNCTYPE(None, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.POINTER(C.c_float), C.c_void_p)
+def _suppress_eot(ctx, state, tokens, n_tokens, logits, ud):
+    logits[_EOT["id"]] = -np.inf
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("clip", ["jfk", "composite"])
+@pytest.mark.parametrize("cfg", ["greedy", "fixed"])
+def test_gpu_whisper_full_with_vad(vctx, vg, model_path, clips, clip, cfg):
+    """whisper_full(params.vad = true) on the synthetic tiny.en model: filtered audio, decode,
+    and segment times mapped back to the original audio (ref 6643-6826, 7947-8025)"""
+    meta, _ = vg
+    want = meta["full"][f"{clip}/{cfg}"]
+    w = owk.Whisper(model_path("tiny.en"))
+    try:
+        L = w.L
+        kw = dict(temperature_inc=0.0, language="en")
+        if cfg == "fixed":
+            kw["max_tokens"] = 20
+        p = w.params(0, **kw)
+        p.vad = True
+        p.vad_model_path = VAD_MODEL.encode()
+        if cfg == "fixed":
+            _EOT["id"] = L.whisper_token_eot(w.ctx)
+            p.logits_filter_callback = C.cast(_suppress_eot, C.c_void_p)
+        pcm = np.ascontiguousarray(clips[clip], np.float32)
+        ret = L.whisper_full(w.ctx, p, owk.fptr(pcm), len(pcm))
+        assert ret == want["ret"]
+        L.whisper_full_get_segment_t0.restype = C.c_int64
+        L.whisper_full_get_segment_t1.restype = C.c_int64
+        L.whisper_full_get_segment_t0.argtypes = [C.c_void_p, C.c_int]
+        L.whisper_full_get_segment_t1.argtypes = [C.c_void_p, C.c_int]
+        L.whisper_full_get_token_id.argtypes = [C.c_void_p, C.c_int, C.c_int]
+        L.whisper_full_n_tokens.argtypes = [C.c_void_p, C.c_int]
+        got = [{"t0": L.whisper_full_get_segment_t0(w.ctx, i), "t1": L.whisper_full_get_segment_t1(w.ctx, i),
+                "tokens": [L.whisper_full_get_token_id(w.ctx, i, j) for j in range(L.whisper_full_n_tokens(w.ctx, i))]}
+               for i in range(L.whisper_full_n_segments(w.ctx))]
+        assert got == want["segments"]
+    finally:
+        w.close() if hasattr(w, "close") else None
