@@ -36,6 +36,15 @@ __device__ __forceinline__ float r16(float x) { return (float) (_Float16) x; }
 
 __device__ __forceinline__ float sigm(float x) { return 1.0f / (1.0f + expf(-x)); }
 
+// Workgroup barrier that orders LDS only. __syncthreads() also drains the wave's global
+// loads/stores (vmcnt) at every step; the LSTM recurrence shares nothing but LDS, so its
+// prefetches and history stores stay in flight across the barrier.
+__device__ __forceinline__ void lds_barrier() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
 // conv1d over VAD_CH chunks: in [ch][IC][Lin] (already F16-rounded), wT [(ic*K + k)][OC] f16,
 // out [ch][OC][Lout] = relu(conv + bias); thread per output channel, im2col (ic, k) order.
 template <int IC, int OC, int K, int LIN, int LOUT, int S, int P>
@@ -184,32 +193,48 @@ __global__ void __launch_bounds__(VAD_G) vad_lstm_kernel(
         c = hst[VAD_H + r];
     }
     __syncthreads();
-    float igv = n > 0 ? ig[(size_t) first * VAD_G + r] : 0.0f;
-    for (int t = 0; t < n; ++t) {
-        const float cur_ig = igv;
-        if (t + 1 < n) igv = ig[(size_t) (first + t + 1) * VAD_G + r];  // in flight across the step
-        float a0 = 0.0f, a1 = 0.0f, a2 = 0.0f, a3 = 0.0f;
+    // ig rows prefetched one block of VAD_PF steps ahead: the only global-memory wait of
+    // the recurrence is at block boundaries
+    constexpr int VAD_PF = 8;
+    float buf[VAD_PF];
 #pragma unroll
-        for (int j = 0; j < VAD_H; j += 4) {
-            const float4 h4 = *(const float4 *) &hs[j];
-            a0 = __builtin_fmaf(wr[j], h4.x, a0);
-            a1 = __builtin_fmaf(wr[j + 1], h4.y, a1);
-            a2 = __builtin_fmaf(wr[j + 2], h4.z, a2);
-            a3 = __builtin_fmaf(wr[j + 3], h4.w, a3);
+    for (int k = 0; k < VAD_PF; ++k) buf[k] = k < n ? ig[(size_t) (first + k) * VAD_G + r] : 0.0f;
+    for (int tb = 0; tb < n; tb += VAD_PF) {
+        float nxt[VAD_PF];
+#pragma unroll
+        for (int k = 0; k < VAD_PF; ++k) {
+            const int tt = tb + VAD_PF + k;
+            nxt[k] = tt < n ? ig[(size_t) (first + tt) * VAD_G + r] : 0.0f;
         }
-        const float hid = ((a0 + a1) + (a2 + a3)) + bh;
-        const float pre = cur_ig + hid;  // inp_gate + hid_gate (ref 4582)
-        gs[r] = (r >= 2 * VAD_H && r < 3 * VAD_H) ? tanhf(pre) : sigm(pre);
-        __syncthreads();
-        if (r < VAD_H) {
-            const float fc = gs[VAD_H + r] * c;
-            const float ig_ = gs[r] * gs[2 * VAD_H + r];
-            c = fc + ig_;
-            const float h = gs[3 * VAD_H + r] * tanhf(c);
-            hs[r] = h;
-            hist[(size_t) (first + t) * VAD_H + r] = h;
+#pragma unroll
+        for (int k = 0; k < VAD_PF; ++k) {
+            const int t = tb + k;
+            if (t >= n) break;
+            float a0 = 0.0f, a1 = 0.0f, a2 = 0.0f, a3 = 0.0f;
+#pragma unroll
+            for (int j = 0; j < VAD_H; j += 4) {
+                const float4 h4 = *(const float4 *) &hs[j];
+                a0 = __builtin_fmaf(wr[j], h4.x, a0);
+                a1 = __builtin_fmaf(wr[j + 1], h4.y, a1);
+                a2 = __builtin_fmaf(wr[j + 2], h4.z, a2);
+                a3 = __builtin_fmaf(wr[j + 3], h4.w, a3);
+            }
+            const float hid = ((a0 + a1) + (a2 + a3)) + bh;
+            const float pre = buf[k] + hid;  // inp_gate + hid_gate (ref 4582)
+            gs[r] = (r >= 2 * VAD_H && r < 3 * VAD_H) ? tanhf(pre) : sigm(pre);
+            lds_barrier();
+            if (r < VAD_H) {
+                const float fc = gs[VAD_H + r] * c;
+                const float ig_ = gs[r] * gs[2 * VAD_H + r];
+                c = fc + ig_;
+                const float h = gs[3 * VAD_H + r] * tanhf(c);
+                hs[r] = h;
+                hist[(size_t) (first + t) * VAD_H + r] = h;
+            }
+            lds_barrier();
         }
-        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < VAD_PF; ++k) buf[k] = nxt[k];
     }
     if (r < VAD_H) {
         hst[r] = hs[r];
