@@ -8,6 +8,7 @@
 // std::nth_element, silence profile, feed/flush mel buffering) runs on the host exactly as
 // the reference does, since its tie order is part of the result.
 #include "sortformer.h"
+#include "owk_sortformer.h"
 
 #include "sf_kernels.h"
 
@@ -448,20 +449,30 @@ void ensure_pos(sortformer_context * ctx, int T) {
     ctx->pos_n = n_pos;
 }
 
+// independent sequences stacked along the rows of one buffer: (first row, length). Row-wise
+// layers (GEMMs, LayerNorms) run once over all rows -- one weight read for every stream --;
+// attention and the depthwise conv run per sequence.
+typedef std::vector<std::pair<int, int>> Segs;
+
 // conformer layers 0..last over x (device f32 [T][d], already xscaled). Returns the buffer
 // holding the output (f32) and fills ctx->s_xn with its f16 copy.
-float * run_conformer(sortformer_context * ctx, float * x, int T, int last) {
+float * run_conformer(sortformer_context * ctx, float * x, const Segs & segs, int last) {
+    int T = 0, Tmax = 0;
+    for (const auto & sg : segs) {
+        T += sg.second;
+        Tmax = std::max(Tmax, sg.second);
+    }
     const int d = ctx->d_model;
     hipStream_t s = ctx->stream;
     float * y = grow<float>(ctx->s_y, (size_t) T * d);
     _Float16 * xn = grow<_Float16>(ctx->s_xn, (size_t) T * d);
     _Float16 * hbuf = grow<_Float16>(ctx->s_h, (size_t) T * 4 * d);
     float * qkv = grow<float>(ctx->s_qkv, (size_t) T * 3 * d);
-    float * P = grow<float>(ctx->s_P, (size_t) (2 * T - 1) * d);
+    float * P = grow<float>(ctx->s_P, (size_t) (2 * Tmax - 1) * d);
     _Float16 * ao = grow<_Float16>(ctx->s_ao, (size_t) T * d);
     float * cv = grow<float>(ctx->s_cv, (size_t) T * 2 * d);
     _Float16 * g = grow<_Float16>(ctx->s_g, (size_t) T * d);
-    ensure_pos(ctx, T);
+    ensure_pos(ctx, Tmax);
     const float eps = 1e-5f;
     for (int il = 0; il <= last; ++il) {
         const ConfLayer & L = ctx->conf[il];
@@ -484,9 +495,12 @@ float * run_conformer(sortformer_context * ctx, float * x, int T, int last) {
             gemm(s, EPI_BIAS_F32, T, 3 * d, d, xn, d, ctx->h(L.qkv), d, e);
             EpiParams ep;
             ep.out32 = P; ep.ldo = d;
-            gemm(s, EPI_F32, 2 * T - 1, d, d, ctx->pos16.as<_Float16>(), d, ctx->h(L.pos), d, ep);
-            sf::attention(s, CONF_DH, true, qkv, 3 * d, d, 2 * d, T, CONF_H, ctx->f(L.pbu), ctx->f(L.pbv), P,
-                          1.0f / sqrtf((float) CONF_DH), ao);
+            gemm(s, EPI_F32, 2 * Tmax - 1, d, d, ctx->pos16.as<_Float16>(), d, ctx->h(L.pos), d, ep);
+            // positions Tb-1 .. -(Tb-1) of a shorter sequence are rows Tmax-Tb .. of the table
+            for (const auto & sg : segs)
+                sf::attention(s, CONF_DH, true, qkv + (size_t) sg.first * 3 * d, 3 * d, d, 2 * d, sg.second, CONF_H,
+                              ctx->f(L.pbu), ctx->f(L.pbv), P + (size_t) (Tmax - sg.second) * d,
+                              1.0f / sqrtf((float) CONF_DH), ao + (size_t) sg.first * d);
             EpiParams eo;
             eo.bias = ctx->f(L.out_b); eo.resid = x; eo.out32 = x; eo.ldo = d;
             gemm(s, EPI_RESID_F32, T, d, d, ao, d, ctx->h(L.out), d, eo);
@@ -497,7 +511,9 @@ float * run_conformer(sortformer_context * ctx, float * x, int T, int last) {
             EpiParams e;
             e.bias = ctx->f(L.pw1_b); e.out32 = cv; e.ldo = 2 * d;
             gemm(s, EPI_BIAS_F32, T, 2 * d, d, xn, d, ctx->h(L.pw1), d, e);
-            sf::glu_dwconv(s, cv, T, d, ctx->f(L.dw), CONF_K, ctx->f(L.dw_b), g);
+            for (const auto & sg : segs)
+                sf::glu_dwconv(s, cv + (size_t) sg.first * 2 * d, sg.second, d, ctx->f(L.dw), CONF_K, ctx->f(L.dw_b),
+                               g + (size_t) sg.first * d);
             EpiParams eo;
             eo.bias = ctx->f(L.pw2_b); eo.resid = x; eo.out32 = x; eo.ldo = d;
             gemm(s, EPI_RESID_F32, T, d, d, g, d, ctx->h(L.pw2), d, eo);
@@ -515,6 +531,7 @@ float * run_conformer(sortformer_context * ctx, float * x, int T, int last) {
     }
     return x;
 }
+float * run_conformer(sortformer_context * ctx, float * x, int T, int last) { return run_conformer(ctx, x, Segs{{0, T}}, last); }
 
 // projection 512 -> 192 from the f16 copy in s_xn -> s_t32 (f32) + s_t16 (f16)
 void run_projection(sortformer_context * ctx, const _Float16 * x16, int T) {
@@ -526,7 +543,9 @@ void run_projection(sortformer_context * ctx, const _Float16 * x16, int T) {
 }
 
 // transformer layers 0..last over s_t32 / s_t16 (in place) (ref:1467-1520)
-void run_transformer(sortformer_context * ctx, int T, int last) {
+void run_transformer(sortformer_context * ctx, const Segs & segs, int last) {
+    int T = 0;
+    for (const auto & sg : segs) T += sg.second;
     hipStream_t s = ctx->stream;
     float * x32 = ctx->s_t32.as<float>();
     _Float16 * x16 = ctx->s_t16.as<_Float16>();
@@ -540,8 +559,9 @@ void run_transformer(sortformer_context * ctx, int T, int last) {
         EpiParams e;
         e.bias = ctx->f(L.qkv_b); e.out32 = qkv; e.ldo = 3 * TF_D;
         gemm(s, EPI_BIAS_F32, T, 3 * TF_D, TF_D, x16, TF_D, ctx->h(L.qkv), TF_D, e);
-        sf::attention(s, TF_DH, false, qkv, 3 * TF_D, TF_D, 2 * TF_D, T, TF_H, nullptr, nullptr, nullptr,
-                      1.0f / sqrtf((float) TF_DH), ao);
+        for (const auto & sg : segs)
+            sf::attention(s, TF_DH, false, qkv + (size_t) sg.first * 3 * TF_D, 3 * TF_D, TF_D, 2 * TF_D, sg.second, TF_H,
+                          nullptr, nullptr, nullptr, 1.0f / sqrtf((float) TF_DH), ao + (size_t) sg.first * TF_D);
         EpiParams eo;
         eo.bias = ctx->f(L.out_b); eo.resid = x32; eo.out32 = y; eo.ldo = TF_D;
         gemm(s, EPI_RESID_F32, T, TF_D, TF_D, ao, TF_D, ctx->h(L.out), TF_D, eo);
@@ -555,6 +575,8 @@ void run_transformer(sortformer_context * ctx, int T, int last) {
         layernorm_f16(s, y, T, TF_D, ctx->f(L.ln2_w), ctx->f(L.ln2_b), eps, x16, TF_D, nullptr, x32);
     }
 }
+
+void run_transformer(sortformer_context * ctx, int T, int last) { run_transformer(ctx, Segs{{0, T}}, last); }
 
 // prediction head over s_t32 -> s_pred [T][4] (ref:1597-1612)
 float * run_prediction(sortformer_context * ctx, int T) {
@@ -574,17 +596,21 @@ float * run_prediction(sortformer_context * ctx, int T) {
 
 // the full head (sortformer_compute_streaming_prediction, ref:1924-2224) of a device input
 // x [T][d] (f32, not yet xscaled; overwritten) -> host preds [T][4]
-void run_head(sortformer_context * ctx, int T, std::vector<float> & preds) {
+void run_head(sortformer_context * ctx, const Segs & segs, std::vector<float> & preds) {
+    int T = 0;
+    for (const auto & sg : segs) T += sg.second;
     float * x = ctx->s_x.as<float>();
     sf::scale(ctx->stream, x, (size_t) T * ctx->d_model, sqrtf((float) ctx->d_model), x);
-    run_conformer(ctx, x, T, ctx->n_conf - 1);
+    run_conformer(ctx, x, segs, ctx->n_conf - 1);
     run_projection(ctx, ctx->s_xn.as<_Float16>(), T);
-    run_transformer(ctx, T, ctx->n_trans - 1);
+    run_transformer(ctx, segs, ctx->n_trans - 1);
     float * p = run_prediction(ctx, T);
     preds.resize((size_t) T * N_SPK);
     OWK_HIP_CHECK(hipMemcpyAsync(preds.data(), p, preds.size() * 4, hipMemcpyDeviceToHost, ctx->stream));
     OWK_HIP_CHECK(hipStreamSynchronize(ctx->stream));
 }
+
+void run_head(sortformer_context * ctx, int T, std::vector<float> & preds) { run_head(ctx, Segs{{0, T}}, preds); }
 
 // ---------------------------------------------------------------------------------
 // streaming bookkeeping (host, ref:1729-1920)
@@ -697,30 +723,62 @@ int validate(const StreamConfig & c) {  // ref:2226-2265
 // on [spkcache | fifo | chunk], append the chunk's predictions to `out`, and (update) advance
 // the FIFO / speaker cache (ref:2349-2548; flush passes update = false, ref:3161-3249).
 // Returns frames appended, or -1 (flush: chunk_len_used <= 0 stops the loop -> -2).
-int process_chunk(sortformer_context * ctx, const StreamConfig & cfg, StreamState & st, const float * mel, int ld,
-                  int c0, int n, int left_offset, int right_offset, bool update, std::vector<float> & out) {
-    const int d = ctx->d_model, sub = ctx->subsampling;
-    const int lc = (int) round((double) left_offset / sub);
-    const int rc = (int) ceil((double) right_offset / sub);
-    const int Tc = run_preenc(ctx, mel, ld, c0, n);
-    const int used = Tc - lc - rc;
-    if (!update && used <= 0) return -2;
-    std::vector<float> chunk((size_t) Tc * d);
-    OWK_HIP_CHECK(hipMemcpyAsync(chunk.data(), ctx->s_pre.ptr, chunk.size() * 4, hipMemcpyDeviceToHost, ctx->stream));
-    OWK_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+// one chunk of one stream: rows of its head input and the host copy of its pre-encoder output
+struct ChunkWork {
+    int Tc = 0, lc = 0, rc = 0, used = 0, T_total = 0;
+    std::vector<float> chunk;
+};
 
-    const int T_total = st.spkcache_len + st.fifo_len + Tc;
-    float * x = grow<float>(ctx->s_x, (size_t) T_total * d);
+int chunk_rows(const sortformer_context * ctx, int n) { return conv_out(conv_out(conv_out(n))); }
+
+// pre-encoder of mel frames [c0, c0 + n), then the head input [spkcache | fifo | chunk] written
+// to x_dst (device rows, T_total of them)
+void prep_chunk(sortformer_context * ctx, StreamState & st, const float * mel, int ld, int c0, int n, int left_offset,
+                int right_offset, float * x_dst, ChunkWork & w) {
+    const int d = ctx->d_model, sub = ctx->subsampling;
+    w.lc = (int) round((double) left_offset / sub);
+    w.rc = (int) ceil((double) right_offset / sub);
+    w.Tc = run_preenc(ctx, mel, ld, c0, n);
+    w.used = w.Tc - w.lc - w.rc;
+    w.chunk.resize((size_t) w.Tc * d);
+    OWK_HIP_CHECK(hipMemcpyAsync(w.chunk.data(), ctx->s_pre.ptr, w.chunk.size() * 4, hipMemcpyDeviceToHost, ctx->stream));
+    w.T_total = st.spkcache_len + st.fifo_len + w.Tc;
+    float * x = x_dst;
     if (st.spkcache_len > 0)
         OWK_HIP_CHECK(hipMemcpyAsync(x, st.spkcache.data(), (size_t) st.spkcache_len * d * 4, hipMemcpyHostToDevice, ctx->stream));
     if (st.fifo_len > 0)
         OWK_HIP_CHECK(hipMemcpyAsync(x + (size_t) st.spkcache_len * d, st.fifo.data(), (size_t) st.fifo_len * d * 4,
                                      hipMemcpyHostToDevice, ctx->stream));
-    OWK_HIP_CHECK(hipMemcpyAsync(x + (size_t) (st.spkcache_len + st.fifo_len) * d, ctx->s_pre.ptr, (size_t) Tc * d * 4,
+    OWK_HIP_CHECK(hipMemcpyAsync(x + (size_t) (st.spkcache_len + st.fifo_len) * d, ctx->s_pre.ptr, (size_t) w.Tc * d * 4,
                                  hipMemcpyDeviceToDevice, ctx->stream));
-    std::vector<float> pred;
-    run_head(ctx, T_total, pred);
+    // the host copies read st's vectors and fill w.chunk: complete before they change
+    OWK_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+}
 
+int post_chunk(const sortformer_context * ctx, const StreamConfig & cfg, StreamState & st, ChunkWork & w,
+               const std::vector<float> & pred, bool update, std::vector<float> & out);
+
+int process_chunk(sortformer_context * ctx, const StreamConfig & cfg, StreamState & st, const float * mel, int ld,
+                  int c0, int n, int left_offset, int right_offset, bool update, std::vector<float> & out) {
+    const int d = ctx->d_model;
+    const int Tc = chunk_rows(ctx, n);
+    const int lc = (int) round((double) left_offset / ctx->subsampling);
+    const int rc = (int) ceil((double) right_offset / ctx->subsampling);
+    if (!update && Tc - lc - rc <= 0) return -2;
+    ChunkWork w;
+    float * x = grow<float>(ctx->s_x, (size_t) (st.spkcache_len + st.fifo_len + Tc) * d);
+    prep_chunk(ctx, st, mel, ld, c0, n, left_offset, right_offset, x, w);
+    std::vector<float> pred;
+    run_head(ctx, w.T_total, pred);
+    return post_chunk(ctx, cfg, st, w, pred, update, out);
+}
+
+// output rows and the FIFO / speaker-cache update of one chunk from its head predictions
+int post_chunk(const sortformer_context * ctx, const StreamConfig & cfg, StreamState & st, ChunkWork & w,
+               const std::vector<float> & pred, bool update, std::vector<float> & out) {
+    const int d = ctx->d_model;
+    const int lc = w.lc, used = w.used;
+    const std::vector<float> & chunk = w.chunk;
     const int ps = st.spkcache_len + st.fifo_len + lc;
     if (used > 0) out.insert(out.end(), pred.begin() + (size_t) ps * N_SPK, pred.begin() + (size_t) (ps + used) * N_SPK);
     if (!update) return std::max(used, 0);
@@ -1137,68 +1195,177 @@ struct sortformer_stream_state * sortformer_stream_init_with_params(struct sortf
     return s;
 }
 
+}  // extern "C"
+
+namespace {
+
+// the mel half of a feed (ref:2776-2890): overlap + new samples -> mel with fresh zero
+// padding (the reference's feed-boundary quirk), appended to the buffered frames; the
+// chunks [c0, c0 + n) with their context offsets that are complete
+struct FeedPlan {
+    std::vector<float> cm;  // [n_mels][tot]
+    int tot = 0, stt = 0;
+    struct Chunk {
+        int c0, n, lo, ro;
+    };
+    std::vector<Chunk> chunks;
+};
+
+FeedPlan feed_plan(sortformer_stream_state * sst, const float * audio_samples, int n_samples) {
+    sortformer_context * ctx = sst->ctx;
+    FeedPlan fp;
+    const int64_t before = sst->total_samples_fed;
+    sst->total_samples_fed += n_samples;
+    const int n_mels = ctx->n_mels, sub = ctx->subsampling;
+    std::vector<float> audio(sst->audio_overlap);
+    audio.insert(audio.end(), audio_samples, audio_samples + n_samples);
+    const int total_len = (int) audio.size();
+    const MelDims md = run_mel(ctx, audio.data(), total_len);
+    std::vector<float> mel((size_t) n_mels * md.n_frames_out);
+    OWK_HIP_CHECK(hipMemcpyAsync(mel.data(), ctx->s_mel.ptr, mel.size() * 4, hipMemcpyDeviceToHost, ctx->stream));
+    OWK_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    const int ov = ctx->n_fft - ctx->hop;
+    if (total_len > ov) sst->audio_overlap.assign(audio.end() - ov, audio.end());
+    else sst->audio_overlap = audio;
+    int new_frames = (int) (sst->total_samples_fed / ctx->hop) - (int) (std::max<int64_t>(before, 0) / ctx->hop);
+    new_frames = std::max(0, std::min(new_frames, md.seq_len));
+    const int skip = md.seq_len - new_frames;
+    const int tot = sst->mel_buffer_frames + new_frames;
+    fp.tot = tot;
+    fp.cm.resize((size_t) n_mels * tot);
+    for (int m = 0; m < n_mels; ++m) {
+        if (sst->mel_buffer_frames)
+            memcpy(&fp.cm[(size_t) m * tot], &sst->mel_buffer[(size_t) m * sst->mel_buffer_frames], (size_t) sst->mel_buffer_frames * 4);
+        if (new_frames)
+            memcpy(&fp.cm[(size_t) m * tot + sst->mel_buffer_frames], &mel[(size_t) m * md.n_frames_out + skip], (size_t) new_frames * 4);
+    }
+    int stt = 0;
+    const int min_chunk = sst->cfg.chunk_len * sub + sst->cfg.chunk_right_context * sub;
+    while (tot > 0 && stt < tot) {
+        if (tot - stt < min_chunk) break;
+        const int end = std::min(stt + sst->cfg.chunk_len * sub, tot);
+        const int lo = std::min(sst->cfg.chunk_left_context * sub, stt);
+        const int ro = std::min(sst->cfg.chunk_right_context * sub, tot - end);
+        fp.chunks.push_back({stt - lo, end + ro - (stt - lo), lo, ro});
+        stt = end;
+    }
+    fp.stt = stt;
+    return fp;
+}
+
+// keep the incomplete tail frames, hand out the predictions (ref:3090-3112)
+int feed_finish(sortformer_stream_state * sst, const FeedPlan & fp, const std::vector<float> & out, float * probs_out,
+                int probs_out_max) {
+    const int n_mels = sst->ctx->n_mels, tot = fp.tot, stt = fp.stt;
+    const int rem = tot - stt;
+    if (rem > 0) {
+        std::vector<float> mb((size_t) n_mels * rem);
+        for (int m = 0; m < n_mels; ++m) memcpy(&mb[(size_t) m * rem], &fp.cm[(size_t) m * tot + stt], (size_t) rem * 4);
+        sst->mel_buffer = std::move(mb);
+        sst->mel_buffer_frames = rem;
+    } else {
+        sst->mel_buffer.clear();
+        sst->mel_buffer_frames = 0;
+    }
+    const int n_out = std::min((int) (out.size() / N_SPK), probs_out_max);
+    if (n_out > 0) memcpy(probs_out, out.data(), (size_t) n_out * N_SPK * 4);
+    sst->total_frames_output += n_out;
+    return n_out;
+}
+
+} // namespace
+
+extern "C" {
+
 int sortformer_stream_feed(struct sortformer_stream_state * sst, const float * audio_samples, int n_samples,
                            float * probs_out, int probs_out_max) {  // ref:2776-3113
     if (!sst || !audio_samples || n_samples <= 0 || !probs_out || probs_out_max <= 0) return -1;
     sortformer_context * ctx = sst->ctx;
     try {
         dev_guard(ctx);
-        const int64_t before = sst->total_samples_fed;
-        sst->total_samples_fed += n_samples;
-        const int n_mels = ctx->n_mels, sub = ctx->subsampling;
-        // overlap + new samples -> mel with fresh zero padding (the reference's feed-boundary quirk)
-        std::vector<float> audio(sst->audio_overlap);
-        audio.insert(audio.end(), audio_samples, audio_samples + n_samples);
-        const int total_len = (int) audio.size();
-        const MelDims md = run_mel(ctx, audio.data(), total_len);
-        std::vector<float> mel((size_t) n_mels * md.n_frames_out);
-        OWK_HIP_CHECK(hipMemcpyAsync(mel.data(), ctx->s_mel.ptr, mel.size() * 4, hipMemcpyDeviceToHost, ctx->stream));
-        OWK_HIP_CHECK(hipStreamSynchronize(ctx->stream));
-        const int ov = ctx->n_fft - ctx->hop;
-        if (total_len > ov) sst->audio_overlap.assign(audio.end() - ov, audio.end());
-        else sst->audio_overlap = audio;
-        int new_frames = (int) (sst->total_samples_fed / ctx->hop) - (int) (std::max<int64_t>(before, 0) / ctx->hop);
-        new_frames = std::max(0, std::min(new_frames, md.seq_len));
-        const int skip = md.seq_len - new_frames;
-        const int tot = sst->mel_buffer_frames + new_frames;
-        std::vector<float> cm((size_t) n_mels * tot);
-        for (int m = 0; m < n_mels; ++m) {
-            if (sst->mel_buffer_frames)
-                memcpy(&cm[(size_t) m * tot], &sst->mel_buffer[(size_t) m * sst->mel_buffer_frames], (size_t) sst->mel_buffer_frames * 4);
-            if (new_frames)
-                memcpy(&cm[(size_t) m * tot + sst->mel_buffer_frames], &mel[(size_t) m * md.n_frames_out + skip], (size_t) new_frames * 4);
-        }
+        FeedPlan fp = feed_plan(sst, audio_samples, n_samples);
         std::vector<float> out;
-        int stt = 0;
-        const int min_chunk = sst->cfg.chunk_len * sub + sst->cfg.chunk_right_context * sub;
-        if (tot > 0) {
-            float * dm = grow<float>(ctx->s_mel, cm.size());
-            OWK_HIP_CHECK(hipMemcpyAsync(dm, cm.data(), cm.size() * 4, hipMemcpyHostToDevice, ctx->stream));
-            while (stt < tot) {
-                if (tot - stt < min_chunk) break;
-                const int end = std::min(stt + sst->cfg.chunk_len * sub, tot);
-                const int lo = std::min(sst->cfg.chunk_left_context * sub, stt);
-                const int ro = std::min(sst->cfg.chunk_right_context * sub, tot - end);
-                process_chunk(ctx, sst->cfg, sst->st, dm, tot, stt - lo, end + ro - (stt - lo), lo, ro, true, out);
-                stt = end;
-            }
+        if (!fp.chunks.empty()) {
+            float * dm = grow<float>(ctx->s_mel, fp.cm.size());
+            OWK_HIP_CHECK(hipMemcpyAsync(dm, fp.cm.data(), fp.cm.size() * 4, hipMemcpyHostToDevice, ctx->stream));
+            for (const auto & c : fp.chunks)
+                process_chunk(ctx, sst->cfg, sst->st, dm, fp.tot, c.c0, c.n, c.lo, c.ro, true, out);
         }
-        const int rem = tot - stt;
-        if (rem > 0) {
-            std::vector<float> mb((size_t) n_mels * rem);
-            for (int m = 0; m < n_mels; ++m) memcpy(&mb[(size_t) m * rem], &cm[(size_t) m * tot + stt], (size_t) rem * 4);
-            sst->mel_buffer = std::move(mb);
-            sst->mel_buffer_frames = rem;
-        } else {
-            sst->mel_buffer.clear();
-            sst->mel_buffer_frames = 0;
-        }
-        const int n_out = std::min((int) (out.size() / N_SPK), probs_out_max);
-        if (n_out > 0) memcpy(probs_out, out.data(), (size_t) n_out * N_SPK * 4);
-        sst->total_frames_output += n_out;
-        return n_out;
+        return feed_finish(sst, fp, out, probs_out, probs_out_max);
     } catch (const std::exception & e) {
         fprintf(stderr, "sortformer_stream_feed: %s\n", e.what());
+        return -1;
+    }
+}
+
+// Many live streams of one context fed together (owk.h): their chunks are processed in
+// rounds -- round r holds the r-th pending chunk of every stream -- and each round is ONE
+// head pass over the stacked [spkcache | fifo | chunk] rows of all its streams. Per stream
+// the chunk order, the AOSC bookkeeping and the outputs are those of sortformer_stream_feed.
+int owk_sortformer_stream_feed_batch(struct sortformer_stream_state ** ssts, const float * const * samples,
+                                     const int * n_samples, int n_streams, float * const * probs_out,
+                                     const int * probs_out_max, int * n_out) {
+    if (!ssts || n_streams <= 0 || !samples || !n_samples || !probs_out || !probs_out_max || !n_out) return -1;
+    sortformer_context * ctx = ssts[0]->ctx;
+    for (int i = 0; i < n_streams; ++i) {
+        if (!ssts[i] || ssts[i]->ctx != ctx || !samples[i] || n_samples[i] <= 0 || !probs_out[i] || probs_out_max[i] <= 0)
+            return -1;
+        for (int j = 0; j < i; ++j)
+            if (ssts[j] == ssts[i]) return -1;  // a stream's chunks are sequential: once per batch
+    }
+    try {
+        dev_guard(ctx);
+        const int d = ctx->d_model;
+        std::vector<FeedPlan> plans(n_streams);
+        size_t mel_tot = 0;
+        std::vector<size_t> mel_off(n_streams);
+        size_t rounds = 0;
+        for (int i = 0; i < n_streams; ++i) {
+            plans[i] = feed_plan(ssts[i], samples[i], n_samples[i]);
+            mel_off[i] = mel_tot;
+            mel_tot += plans[i].cm.size();
+            rounds = std::max(rounds, plans[i].chunks.size());
+        }
+        DevBuf dmel;
+        dmel.alloc(std::max<size_t>(mel_tot, 1) * 4);
+        for (int i = 0; i < n_streams; ++i)
+            if (!plans[i].cm.empty())
+                OWK_HIP_CHECK(hipMemcpyAsync(dmel.as<float>() + mel_off[i], plans[i].cm.data(), plans[i].cm.size() * 4,
+                                             hipMemcpyHostToDevice, ctx->stream));
+        std::vector<std::vector<float>> outs(n_streams);
+        for (size_t r = 0; r < rounds; ++r) {
+            std::vector<int> who;
+            Segs segs;
+            int rows = 0;
+            for (int i = 0; i < n_streams; ++i) {
+                if (r >= plans[i].chunks.size()) continue;
+                const StreamState & st = ssts[i]->st;
+                const int T = st.spkcache_len + st.fifo_len + chunk_rows(ctx, plans[i].chunks[r].n);
+                who.push_back(i);
+                segs.push_back({rows, T});
+                rows += T;
+            }
+            float * x = grow<float>(ctx->s_x, (size_t) rows * d);
+            std::vector<ChunkWork> works(who.size());
+            for (size_t k = 0; k < who.size(); ++k) {
+                const int i = who[k];
+                const auto & c = plans[i].chunks[r];
+                prep_chunk(ctx, ssts[i]->st, dmel.as<float>() + mel_off[i], plans[i].tot, c.c0, c.n, c.lo, c.ro,
+                           x + (size_t) segs[k].first * d, works[k]);
+            }
+            std::vector<float> pred_all;
+            run_head(ctx, segs, pred_all);
+            for (size_t k = 0; k < who.size(); ++k) {
+                const int i = who[k];
+                std::vector<float> pred(pred_all.begin() + (size_t) segs[k].first * N_SPK,
+                                        pred_all.begin() + (size_t) (segs[k].first + segs[k].second) * N_SPK);
+                post_chunk(ctx, ssts[i]->cfg, ssts[i]->st, works[k], pred, true, outs[i]);
+            }
+        }
+        for (int i = 0; i < n_streams; ++i) n_out[i] = feed_finish(ssts[i], plans[i], outs[i], probs_out[i], probs_out_max[i]);
+        return 0;
+    } catch (const std::exception & e) {
+        fprintf(stderr, "owk_sortformer_stream_feed_batch: %s\n", e.what());
         return -1;
     }
 }

@@ -58,6 +58,9 @@ def load(path: str | None = None) -> C.CDLL:
     L.sortformer_diarize.argtypes = [vp, fp, ip, fp, ip]
     L.sortformer_to_rttm.argtypes = [fp, ip, C.c_float, ip, C.c_char_p, C.c_char_p, ip]
     L.sortformer_stream_preset_params.restype = StreamParams
+    if hasattr(L, "owk_sortformer_stream_feed_batch"):  # include/owk_sortformer.h
+        L.owk_sortformer_stream_feed_batch.argtypes = [C.POINTER(vp), C.POINTER(fp), C.POINTER(ip), ip, C.POINTER(fp),
+                                                       C.POINTER(ip), C.POINTER(ip)]
     L.sortformer_stream_preset_params.argtypes = [ip]
     L.sortformer_stream_init.restype = vp
     L.sortformer_stream_init.argtypes = [vp, ip]
@@ -227,3 +230,22 @@ class Stream:
             self.close()
         except Exception:
             pass
+
+
+def feed_batch(streams, pcms):
+    """owk_sortformer_stream_feed_batch: feed pcms[i] to streams[i] (one context) in one call;
+    returns the per-stream [n_out, 4] outputs."""
+    n = len(streams)
+    L = streams[0].sf.L
+    arrs = [np.ascontiguousarray(p, np.float32) for p in pcms]
+    outs = [np.zeros((len(a) // 1280 + 64, 4), np.float32) for a in arrs]
+    n_out = (C.c_int * n)()
+    ret = L.owk_sortformer_stream_feed_batch((C.c_void_p * n)(*[s.st for s in streams]),
+                                             (C.POINTER(C.c_float) * n)(*[_fp(a) for a in arrs]),
+                                             (C.c_int * n)(*[len(a) for a in arrs]), n,
+                                             (C.POINTER(C.c_float) * n)(*[_fp(o) for o in outs]),
+                                             (C.c_int * n)(*[o.shape[0] for o in outs]), n_out)
+    if ret != 0:
+        raise RuntimeError("owk_sortformer_stream_feed_batch failed")
+    return [o[:k] for o, k in zip(outs, n_out)]
+

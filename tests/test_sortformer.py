@@ -270,3 +270,53 @@ def test_stream(sf, sfg, test60, name):
         assert np.array_equal(st.feed(test60[pos:pos + n]), outs[i])
         pos += n
     st.close()
+
+
+@pytest.mark.gpu
+def test_stream_feed_batch(sf, sfg, test60):
+    """owk_sortformer_stream_feed_batch: the three golden stream
+    configurations plus ragged copies fed as ONE batch per round of blocks. Every stream
+    reproduces the reference's golden outputs within the noise floor, its per-feed frame
+    counts exactly, and the same stream fed alone within the same noise floor (the stacked
+    GEMMs sum in another order than a lone stream's split-K ones; AOSC amplifies it)."""
+    import sortformer as SF
+
+    meta, A = sfg
+    names = list(STREAMS) + list(STREAMS)
+    streams = [sf.stream(STREAMS[nm][0]) for nm in names]
+    solo = [sf.stream(STREAMS[nm][0]) for nm in names]
+    pos = [0] * len(names)
+    outs = [[] for _ in names]
+    counts = [[] for _ in names]
+    solo_outs = [[] for _ in names]
+    i = 0
+    while any(p < len(test60) for p in pos):
+        act, pcms = [], []
+        for k, nm in enumerate(names):
+            blocks = STREAMS[nm][1]
+            if pos[k] >= len(test60):
+                continue
+            b = blocks[i % len(blocks)] if k < len(STREAMS) else blocks[(i + 1) % len(blocks)]
+            n = min(b, len(test60) - pos[k])
+            act.append(k)
+            pcms.append(test60[pos[k]:pos[k] + n])
+            pos[k] += n
+        for k, o in zip(act, SF.feed_batch([streams[k] for k in act], pcms)):
+            outs[k].append(o)
+            counts[k].append(o.shape[0])
+        for k, pcm in zip(act, pcms):
+            solo_outs[k].append(solo[k].feed(pcm))
+        i += 1
+    for k, nm in enumerate(names):
+        fl = streams[k].flush()
+        outs[k].append(fl)
+        counts[k].append(fl.shape[0])
+        solo_outs[k].append(solo[k].flush())
+        got = np.concatenate(outs[k])
+        within_floor(meta, f"stream/{nm}", got, np.concatenate(solo_outs[k]))
+        if k < len(STREAMS):
+            assert counts[k] == meta["results"][f"stream_counts/{nm}"]
+            within_floor(meta, f"stream/{nm}", got, A[f"stream/{nm}"])
+    for st in streams + solo:
+        st.close()
+
