@@ -542,6 +542,12 @@ __device__ __forceinline__ long q5_group(const uint8_t * qs_blk, uint32_t qh, in
     return (long) v;
 }
 
+// group g (8 int8) of K block kb of weight row n, Q5_0 (unpacked) or Q8_0 (as stored)
+__device__ __forceinline__ long wq_group(const Q5W & w, int n, int kb, int g, int K, int nb) {
+    if (w.q8) return *(const long *) (w.qs + (size_t) n * K + kb * 32 + 8 * g);
+    return q5_group(w.qs + (size_t) n * (K / 2) + kb * 16, w.qh[(size_t) n * nb + kb], g);
+}
+
 // skinny: M <= 64 rows; one 16-column tile per block, 8 waves split the K blocks, partial
 // tiles reduced through LDS in fixed wave order
 template <int MODE>
@@ -559,7 +565,7 @@ __global__ __launch_bounds__(512) void k_gemm_q5_skinny(int M, int N, int K, con
 #pragma unroll
     for (int i = 0; i < 4; ++i) acc[i] = floatx4{0.f, 0.f, 0.f, 0.f};
     for (int kb = kb0; kb < kb1; ++kb) {
-        const long b = q5_group(w.qs + (size_t) n * (K / 2) + kb * 16, w.qh[(size_t) n * nb + kb], g);
+        const long b = wq_group(w, n, kb, g, K, nb);
         const float dw = (float) w.d[(size_t) n * nb + kb];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
@@ -626,14 +632,22 @@ __global__ __launch_bounds__(GQ_MAXW * 64) void k_gemm_q5_rows(int M, int N, int
     long a[MT][GQ_J];
     // the tile's blocks are contiguous 352 B records (Q5W::tiled): coalesced loads. Blocks
     // past this wave's range load a valid record and a zero activation (adds exact zeros).
-    const uint8_t * tb = w.tiled + (size_t) blockIdx.x * nb * Q5_TILE_BYTES;
+    const bool q8 = w.q8;
+    const int tbytes = q8 ? Q8_TILE_BYTES : Q5_TILE_BYTES;
+    const uint8_t * tb = w.tiled + (size_t) blockIdx.x * nb * tbytes;
 #pragma unroll
     for (int j = 0; j < GQ_J; ++j) {
         const int kb = min(kb0 + j, nb - 1);
-        const uint8_t * rec = tb + (size_t) kb * Q5_TILE_BYTES;
-        raw[j] = *(const uint64_t *) (rec + c16 * 16 + (g & 1) * 8);
-        qh[j] = *(const uint32_t *) (rec + 256 + c16 * 4);
-        dw[j] = *(const _Float16 *) (rec + 320 + c16 * 2);
+        const uint8_t * rec = tb + (size_t) kb * tbytes;
+        if (q8) {
+            raw[j] = *(const uint64_t *) (rec + c16 * 32 + g * 8);
+            qh[j] = 0;
+            dw[j] = *(const _Float16 *) (rec + 512 + c16 * 2);
+        } else {
+            raw[j] = *(const uint64_t *) (rec + c16 * 16 + (g & 1) * 8);
+            qh[j] = *(const uint32_t *) (rec + 256 + c16 * 4);
+            dw[j] = *(const _Float16 *) (rec + 320 + c16 * 2);
+        }
 #pragma unroll
         for (int i = 0; i < MT; ++i) {
             const int ra = min(i * 16 + c16, M - 1);
@@ -662,11 +676,14 @@ __global__ __launch_bounds__(GQ_MAXW * 64) void k_gemm_q5_rows(int M, int N, int
 #pragma unroll
     for (int j = 0; j < GQ_J; ++j) {
         const int kb = min(kb0 + j, nb - 1);
-        uint64_t v = (g < 2 ? raw[j] : (raw[j] >> 4)) & 0x0F0F0F0F0F0F0F0FULL;
-        const uint32_t h8 = (qh[j] >> (8 * g)) & 0xFFu;
+        uint64_t v = raw[j];
+        if (!q8) {
+            v = (g < 2 ? raw[j] : (raw[j] >> 4)) & 0x0F0F0F0F0F0F0F0FULL;
+            const uint32_t h8 = (qh[j] >> (8 * g)) & 0xFFu;
 #pragma unroll
-        for (int e = 0; e < 8; ++e) v |= (uint64_t) ((h8 >> e) & 1u) << (8 * e + 4);
-        v = ((v | 0x8080808080808080ULL) - 0x1010101010101010ULL) ^ 0x8080808080808080ULL;
+            for (int e = 0; e < 8; ++e) v |= (uint64_t) ((h8 >> e) & 1u) << (8 * e + 4);
+            v = ((v | 0x8080808080808080ULL) - 0x1010101010101010ULL) ^ 0x8080808080808080ULL;
+        }
         const float dwf = (float) dw[j];
 #pragma unroll
         for (int i = 0; i < MT; ++i) {
@@ -718,7 +735,7 @@ __global__ __launch_bounds__(256) void k_gemm_q5_big(int M, int N, int K, const 
     const int ra = min(m0 + srow, M - 1), rb = min(n0 + srow, N - 1);
     auto stage = [&](int buf, int kb) {
         *(long *) &sA[buf][srow][sq * 8] = *(const long *) (qa + (size_t) ra * K + kb * 32 + sq * 8);
-        *(long *) &sB[buf][srow][sq * 8] = q5_group(w.qs + (size_t) rb * (K / 2) + kb * 16, w.qh[(size_t) rb * nb + kb], sq);
+        *(long *) &sB[buf][srow][sq * 8] = wq_group(w, rb, kb, sq, K, nb);
         if (sq == 0) {
             sdA[buf][srow] = da[(size_t) ra * nb + kb];
             sdB[buf][srow] = (float) w.d[(size_t) rb * nb + kb];
@@ -797,6 +814,32 @@ void q5_tile_host(const uint8_t * qs, const uint32_t * qh, const uint16_t * d, i
                 memcpy(o + 320 + c * 2, &d[(size_t) n * nb + kb], 2);
             }
         }
+}
+
+size_t q8_tiled_bytes(int N, int K) { return (size_t) ((N + 15) / 16) * (K / 32) * Q8_TILE_BYTES; }
+
+void q8_tile_host(const int8_t * qs, const uint16_t * d, int N, int K, uint8_t * out) {
+    const int nb = K / 32, nt = (N + 15) / 16;
+    memset(out, 0, q8_tiled_bytes(N, K));
+    for (int t = 0; t < nt; ++t)
+        for (int kb = 0; kb < nb; ++kb) {
+            uint8_t * o = out + ((size_t) t * nb + kb) * Q8_TILE_BYTES;
+            for (int c = 0; c < 16; ++c) {
+                const int n = t * 16 + c;
+                if (n >= N) break;
+                memcpy(o + c * 32, qs + (size_t) n * K + kb * 32, 32);
+                memcpy(o + 512 + c * 2, &d[(size_t) n * nb + kb], 2);
+            }
+        }
+}
+
+void q8_split_host(const uint8_t * blocks, int N, int K, int8_t * qs, uint16_t * d) {
+    const int nb = K / 32;
+    for (size_t i = 0; i < (size_t) N * nb; ++i) {
+        const uint8_t * b = blocks + i * 34;  // block_q8_0: d (f16), qs[32]
+        memcpy(&d[i], b, 2);
+        memcpy(qs + i * 32, b + 2, 32);
+    }
 }
 
 void q5_split_host(const uint8_t * blocks, int N, int K, uint8_t * qs, uint32_t * qh, uint16_t * d) {

@@ -238,10 +238,27 @@ __global__ void k_embed_q5(const uint8_t * __restrict__ qs, const uint32_t * __r
     }
 }
 
+__global__ void k_embed_q8(const int8_t * __restrict__ qs, const _Float16 * __restrict__ dd,
+                           const float * __restrict__ pe, const int * __restrict__ tok, const int * __restrict__ pos,
+                           int rows, int d, float * __restrict__ x) {
+    const int r = blockIdx.x;
+    if (r >= rows) return;
+    const size_t row = (size_t) tok[r];
+    const int nb = d / 32;
+    const float * p = pe + (size_t) pos[r] * d;
+    for (int i = threadIdx.x; i < d; i += blockDim.x) {
+        const float v = (float) qs[row * d + i] * (float) dd[row * nb + (i >> 5)];  // dequantize_row_q8_0
+        x[(size_t) r * d + i] = v + p[i];
+    }
+}
+
 void embed_tokens_q5(hipStream_t s, const Q5W & te, const float * pe, const int * tok, const int * pos, int rows, int d,
                      float * x) {
     if (rows <= 0) return;
-    hipLaunchKernelGGL(k_embed_q5, dim3(rows), dim3(256), 0, s, te.qs, te.qh, te.d, pe, tok, pos, rows, d, x);
+    if (te.q8)
+        hipLaunchKernelGGL(k_embed_q8, dim3(rows), dim3(256), 0, s, (const int8_t *) te.qs, te.d, pe, tok, pos, rows, d, x);
+    else
+        hipLaunchKernelGGL(k_embed_q5, dim3(rows), dim3(256), 0, s, te.qs, te.qh, te.d, pe, tok, pos, rows, d, x);
 }
 
 // ----------------------------------------------------------------------------------

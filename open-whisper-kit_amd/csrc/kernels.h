@@ -92,9 +92,17 @@ struct Q5W {
     // decode-step matrices: per (16-row tile t, block kb) 352 B at (t * K/32 + kb) * 352 =
     // qs of the 16 rows (16 x 16 B) | qh (16 x 4 B) | d (16 x 2 B); rows past N zero
     const uint8_t * tiled = nullptr;
+    // Q8_0 matrices (MOSTLY_Q8_0 models) share the pipeline: qs = [N][K] int8, qh unused,
+    // tiled records of 16 rows x 32 int8 | 16 x d (544 B)
+    bool q8 = false;
     explicit operator bool() const { return qs != nullptr; }
 };
 constexpr int Q5_TILE_BYTES = 352;
+constexpr int Q8_TILE_BYTES = 544;
+size_t q8_tiled_bytes(int N, int K);
+void q8_tile_host(const int8_t * qs, const uint16_t * d, int N, int K, uint8_t * out);
+// block_q8_0 rows (d f16, qs[32]) -> qs [N][K], d [N][K/32]
+void q8_split_host(const uint8_t * blocks, int N, int K, int8_t * qs, uint16_t * d);
 size_t q5_tiled_bytes(int N, int K);
 void q5_tile_host(const uint8_t * qs, const uint32_t * qh, const uint16_t * d, int N, int K, uint8_t * out);
 // Q8_0 rows of A (f32 if A32, else f16): q [M][K] int8, dq [M][K/32] (the f16-rounded scale)

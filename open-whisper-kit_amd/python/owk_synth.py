@@ -213,7 +213,28 @@ def q5_0_blocks(x: np.ndarray) -> bytes:
     return out.tobytes()
 
 
-def quantize_q5_0(src: str, dst: str) -> str:
+def q8_0_blocks(x: np.ndarray) -> bytes:
+    """block_q8_0 rows of f32 values: quantize_row_q8_0_ref (ref ggml/src/ggml-quants.c:199-222):
+    d = amax / 127 (stored f16), q = roundf(x * (1/d)) (round half away from zero)."""
+    b = x.astype(np.float32).reshape(-1, 32)
+    amax = np.abs(b).max(axis=1)
+    d = (amax / np.float32(127.0)).astype(np.float32)
+    idv = np.where(d != 0, np.float32(1.0) / np.where(d != 0, d, np.float32(1.0)), np.float32(0.0)).astype(np.float32)
+    x0 = (b * idv[:, None]).astype(np.float32)
+    q = (np.sign(x0) * np.floor(np.abs(x0) + np.float32(0.5))).astype(np.int8)
+    out = np.zeros((b.shape[0], 34), np.uint8)
+    out[:, 0:2] = d.astype("<f2").view(np.uint8).reshape(-1, 2)
+    out[:, 2:34] = q.view(np.uint8)
+    return out.tobytes()
+
+
+def quantize_q8_0(src: str, dst: str) -> str:
+    """Q8_0 copy of an F16 ggml-bin model as whisper-quantize writes it (same tensor rule as
+    quantize_q5_0; ttype 8, ftype 2007 = GGML_QNT_VERSION 2 * 1000 + MOSTLY_Q8_0 7)."""
+    return quantize_q5_0(src, dst, kind="q8_0")
+
+
+def quantize_q5_0(src: str, dst: str, kind: str = "q5_0") -> str:
     """Q5_0 copy of an F16 ggml-bin model, as whisper-quantize writes it
     (/root/reference examples/quantize/quantize.cpp:159-168, examples/common-ggml.cpp:97-230):
     every 2-D tensor except the positional embeddings becomes Q5_0 (ttype 6), ftype becomes
@@ -235,7 +256,7 @@ def quantize_q5_0(src: str, dst: str) -> str:
             h.update(b)
         w(take(4))
         hp = list(struct.unpack("<11i", take(44)))
-        hp[10] = 2000 + 8
+        hp[10] = 2000 + (8 if kind == "q5_0" else 7)
         w(struct.pack("<11i", *hp))
         n_mel, n_fft = struct.unpack("<ii", take(8))
         w(struct.pack("<ii", n_mel, n_fft))
@@ -254,12 +275,12 @@ def quantize_q5_0(src: str, dst: str) -> str:
             nel = int(np.prod(ne))
             data = take(nel * (2 if ttype == 1 else 4))
             quant = n_dims == 2 and name.decode() not in skip
-            w(struct.pack("<iii", n_dims, name_len, 6 if quant else ttype))
+            w(struct.pack("<iii", n_dims, name_len, (6 if kind == "q5_0" else 8) if quant else ttype))
             w(struct.pack("<%di" % n_dims, *ne))
             w(name)
             if quant:
                 x = np.frombuffer(data, "<f2" if ttype == 1 else "<f4").astype(np.float32)
-                w(q5_0_blocks(x))
+                w(q5_0_blocks(x) if kind == "q5_0" else q8_0_blocks(x))
             else:
                 w(data)
     os.replace(tmp, dst)
@@ -270,15 +291,15 @@ def ensure_model(model: str, seed: int = 1234, cache_dir: str | None = None) -> 
     """Path to a cached synthetic model (generated on first use)."""
     cache_dir = cache_dir or os.environ.get("OWK_MODEL_CACHE", "/tmp/owk_models")
     os.makedirs(cache_dir, exist_ok=True)
-    q5 = model.endswith("-q5_0")
-    base = model[:-5] if q5 else model
+    kind = next((k for k in ("q5_0", "q8_0") if model.endswith("-" + k)), None)
+    base = model[:-5] if kind else model
     path = os.path.join(cache_dir, f"synth-{base}-s{seed}.bin")
     if not os.path.exists(path):
         write_model(path, base, seed)
-    if q5:
-        qpath = os.path.join(cache_dir, f"synth-{base}-q5_0-s{seed}.bin")
+    if kind:
+        qpath = os.path.join(cache_dir, f"synth-{base}-{kind}-s{seed}.bin")
         if not os.path.exists(qpath):
-            quantize_q5_0(path, qpath)
+            quantize_q5_0(path, qpath, kind=kind)
         return qpath
     return path
 

@@ -14,7 +14,8 @@ perturbed by 1e-7 relative noise (below the f32 ulp of most samples); tests/test
 bounds the GPU error by 2x that floor, and decoded sequences may part only where the two
 tokens are within 2x the logit floor of each other.
 
-Usage (in a container that has /root/reference):  python tests/golden/make_golden_q5.py
+Usage (in a container that has /root/reference):  python tests/golden/make_golden_q5.py [q8_0]
+(q8_0: the same fixtures for Q8_0 files, owk_synth.quantize_q8_0 -> q8_golden.{json,npz})
 """
 import json
 import os
@@ -33,6 +34,8 @@ OUT = os.path.dirname(os.path.abspath(__file__))
 SEED = 1234
 MODELS = ["tiny.en", "l3-mini"]
 TF_TOKENS = 48
+KIND = sys.argv[1] if len(sys.argv) > 1 else "q5_0"
+assert KIND in ("q5_0", "q8_0")
 
 
 def main():
@@ -44,8 +47,9 @@ def main():
     for model in MODELS:
         src = os.path.join(cache, f"synth-{model}-s{SEED}.bin")
         S.write_model(src, model, SEED)
-        path = os.path.join(cache, f"synth-{model}-q5_0-s{SEED}.bin")
-        meta["models"][model] = {"sha256": S.quantize_q5_0(src, path)}
+        path = os.path.join(cache, f"synth-{model}-{KIND}-s{SEED}.bin")
+        quant = S.quantize_q5_0 if KIND == "q5_0" else S.quantize_q8_0
+        meta["models"][model] = {"sha256": quant(src, path)}
         ref = R.Ref(path)
         multilingual = S.MODELS[model][0] >= 51865
         for cname, pcm in audio.items():
@@ -114,8 +118,10 @@ def main():
                 meta["results"][f"{key}/noise_floor/agree/{cfg}"] = min(agree)
             print(model, cname, "floors", meta["results"][key + "/noise_floor/enc_rows"], dl, flush=True)
         ref.close()
-    np.savez_compressed(os.path.join(OUT, "q5_golden.npz"), **arrays)
-    with open(os.path.join(OUT, "q5_golden.json"), "w") as f:
+    stem = "q5_golden" if KIND == "q5_0" else "q8_golden"
+    meta["kind"] = KIND
+    np.savez_compressed(os.path.join(OUT, stem + ".npz"), **arrays)
+    with open(os.path.join(OUT, stem + ".json"), "w") as f:
         json.dump(meta, f, indent=0)
 
 

@@ -1,4 +1,6 @@
-"""Q5_0 models (ftype 2008).
+"""Q5_0 and Q8_0 models (ftype 2008 / 2007).
+Every test runs for both kinds: q5_golden.* (Q5_0) and q8_golden.* (Q8_0), made by
+tests/golden/make_golden_q5.py [q8_0] from the reference on the same synthetic weights.
 
 CPU: owk_synth.quantize_q5_0 (restatement of whisper-quantize) writes byte-identical files to
 the reference quantizer compiled from its own sources (oracle/_ref/whisper-quantize).
@@ -25,9 +27,15 @@ GOLDEN = os.path.join(ROOT, "tests", "golden")
 QUANT = os.path.join(ROOT, "oracle", "_ref", "whisper-quantize")
 
 
-@pytest.fixture(scope="module")
-def q5g():
-    return json.load(open(os.path.join(GOLDEN, "q5_golden.json"))), np.load(os.path.join(GOLDEN, "q5_golden.npz"))
+KINDS = {"q5_0": ("q5_golden", 8), "q8_0": ("q8_golden", 7)}  # fixture stem, GGML_FTYPE_MOSTLY_*
+
+
+@pytest.fixture(scope="module", params=list(KINDS))
+def q5g(request):
+    stem = KINDS[request.param][0]
+    meta = json.load(open(os.path.join(GOLDEN, stem + ".json")))
+    meta["kind"] = request.param
+    return meta, np.load(os.path.join(GOLDEN, stem + ".npz"))
 
 
 def q5_model(model, meta):
@@ -36,11 +44,12 @@ def q5_model(model, meta):
     cache = os.environ.get("OWK_MODEL_CACHE", "/tmp/owk_models")
     os.makedirs(cache, exist_ok=True)
     src = S.ensure_model(model, meta["seed"], cache)
-    path = os.path.join(cache, f"synth-{model}-q5_0-s{meta['seed']}.bin")
+    kind = meta["kind"]
+    path = os.path.join(cache, f"synth-{model}-{kind}-s{meta['seed']}.bin")
     sha_file = path + ".sha256"
     want = meta["models"][model]["sha256"]
     if not (os.path.exists(path) and os.path.exists(sha_file) and open(sha_file).read().strip() == want):
-        assert S.quantize_q5_0(src, path) == want
+        assert (S.quantize_q5_0 if kind == "q5_0" else S.quantize_q8_0)(src, path) == want
         with open(sha_file, "w") as f:
             f.write(want)
     return path
@@ -53,20 +62,23 @@ def test_quantizer_matches_reference(q5g, tmp_path):
 
     meta, _ = q5g
     src = S.ensure_model("tiny.en", meta["seed"])
-    out = str(tmp_path / "ref_q5.bin")
-    subprocess.run([QUANT, src, out, "q5_0"], check=True, capture_output=True)
+    kind = meta["kind"]
+    out = str(tmp_path / f"ref_{kind}.bin")
+    subprocess.run([QUANT, src, out, kind], check=True, capture_output=True)
     ref = hashlib.sha256(open(out, "rb").read()).hexdigest()
     assert ref == meta["models"]["tiny.en"]["sha256"]
-    assert S.quantize_q5_0(src, str(tmp_path / "py_q5.bin")) == ref
+    quant = S.quantize_q5_0 if kind == "q5_0" else S.quantize_q8_0
+    assert quant(src, str(tmp_path / f"py_{kind}.bin")) == ref
 
 
 _ctx = {}
 
 
 def wq5(model, meta):
-    if model not in _ctx:
-        _ctx[model] = owk.Whisper(q5_model(model, meta))
-    return _ctx[model]
+    key = (meta["kind"], model)
+    if key not in _ctx:
+        _ctx[key] = owk.Whisper(q5_model(model, meta))
+    return _ctx[key]
 
 
 @pytest.mark.gpu
@@ -77,7 +89,7 @@ def test_q5_encoder_and_logits(q5g, clips, model, clip):
     owk.quiet()
     w = wq5(model, meta)
     L = w.L
-    assert L.whisper_model_ftype(w.ctx) == 8
+    assert L.whisper_model_ftype(w.ctx) == KINDS[meta["kind"]][1]
     st = w.new_state()
     pcm = clips[clip]
     key = f"{model}/{clip}"
@@ -137,7 +149,7 @@ def test_q5_whisper_full(q5g, clips, model, clip, cfg):
         rp = np.array([t[2] for t in r[:agree]])
         np.testing.assert_allclose(gp, rp, atol=fl)
     else:
-        _compare(got, want["segments"], f"q5/{model}/{clip}/{cfg}", p_atol=fl, tie=fl)
+        _compare(got, want["segments"], f"{meta['kind']}/{model}/{clip}/{cfg}", p_atol=fl, tie=fl)
 
 
 @pytest.mark.gpu
