@@ -186,13 +186,13 @@ void Engine::linear(const char * cls, int mode, int M, int N, int K, const _Floa
         return;
     }
     // the reference rounds each activation row to Q8_0 (x86 quantize_row_q8_0) before the
-    // q5_0 x q8_0 dot; bytes: Q5_0 weights at 22 B per 32 + the int8 activations. a_q8: the
+    // q5_0 (q8_0) x q8_0 dot; bytes: Q5_0 (Q8_0) weights at 22 (34) B per 32 + the int8 activations. a_q8: the
     // producer (LayerNorm, one_chunk attention) already wrote q8a_ / q8d_
     if (!a_q8) {
         ProfScope ps(prof, stream, "quantize_q8");
         quantize_q8(stream, A32, A16, lda, M, K, q8a_.as<int8_t>(), q8d_.as<float>());
     }
-    ProfScope ps(prof, stream, cls, gemm_flops(M, N, K), (double) N * K * 22.0 / 32.0 + (double) M * K);
+    ProfScope ps(prof, stream, cls, gemm_flops(M, N, K), (double) N * K * (q.q8 ? 34.0 : 22.0) / 32.0 + (double) M * K);
     gemm_q5(stream, mode, M, N, K, q8a_.as<int8_t>(), q8d_.as<float>(), q, ep);
 }
 

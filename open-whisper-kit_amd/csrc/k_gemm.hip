@@ -613,7 +613,7 @@ constexpr int GQ_MAX_SCALES = 32 * 160;  // M x K/32 activation scales in LDS
 // M * nb <= 32 * nb and blockDim = 64 * ceil(nb / GQ_J) -> at most 32 * GQ_J / 64 + 1 per thread
 constexpr int GQ_DA_PER_THREAD = 32 * GQ_J / 64 + 1;
 
-template <int MODE, int MT>
+template <int MODE, int MT, bool Q8>
 __global__ __launch_bounds__(GQ_MAXW * 64) void k_gemm_q5_rows(int M, int N, int K, const int8_t * __restrict__ qa,
                                                                const float * __restrict__ da, Q5W w, EpiParams ep) {
     __shared__ floatx4 red[GQ_MAXW][MT][64];
@@ -632,14 +632,14 @@ __global__ __launch_bounds__(GQ_MAXW * 64) void k_gemm_q5_rows(int M, int N, int
     long a[MT][GQ_J];
     // the tile's blocks are contiguous 352 B records (Q5W::tiled): coalesced loads. Blocks
     // past this wave's range load a valid record and a zero activation (adds exact zeros).
-    const bool q8 = w.q8;
-    const int tbytes = q8 ? Q8_TILE_BYTES : Q5_TILE_BYTES;
+    constexpr bool q8 = Q8;  // Q8_0 records (compile time: the load phase stays branch-free)
+    constexpr int tbytes = Q8 ? Q8_TILE_BYTES : Q5_TILE_BYTES;
     const uint8_t * tb = w.tiled + (size_t) blockIdx.x * nb * tbytes;
 #pragma unroll
     for (int j = 0; j < GQ_J; ++j) {
         const int kb = min(kb0 + j, nb - 1);
         const uint8_t * rec = tb + (size_t) kb * tbytes;
-        if (q8) {
+        if constexpr (q8) {
             raw[j] = *(const uint64_t *) (rec + c16 * 32 + g * 8);
             qh[j] = 0;
             dw[j] = *(const _Float16 *) (rec + 512 + c16 * 2);
@@ -677,7 +677,7 @@ __global__ __launch_bounds__(GQ_MAXW * 64) void k_gemm_q5_rows(int M, int N, int
     for (int j = 0; j < GQ_J; ++j) {
         const int kb = min(kb0 + j, nb - 1);
         uint64_t v = raw[j];
-        if (!q8) {
+        if constexpr (!q8) {
             v = (g < 2 ? raw[j] : (raw[j] >> 4)) & 0x0F0F0F0F0F0F0F0FULL;
             const uint32_t h8 = (qh[j] >> (8 * g)) & 0xFFu;
 #pragma unroll
@@ -784,12 +784,15 @@ template <int MODE> struct LaunchQ5 {
         const int nb = K / 32;
         if (M <= 32 && w.tiled && nb <= GQ_MAXW * GQ_J && M * nb <= GQ_MAX_SCALES) {
             const int nw = (nb + GQ_J - 1) / GQ_J;
-            if (M <= 16)
-                hipLaunchKernelGGL((k_gemm_q5_rows<MODE, 1>), dim3((N + 15) / 16), dim3(nw * 64), 0, s, M, N, K, qa, da,
-                                   w, ep);
+            const dim3 grid((N + 15) / 16), block(nw * 64);
+            if (M <= 16 && w.q8)
+                hipLaunchKernelGGL((k_gemm_q5_rows<MODE, 1, true>), grid, block, 0, s, M, N, K, qa, da, w, ep);
+            else if (M <= 16)
+                hipLaunchKernelGGL((k_gemm_q5_rows<MODE, 1, false>), grid, block, 0, s, M, N, K, qa, da, w, ep);
+            else if (w.q8)
+                hipLaunchKernelGGL((k_gemm_q5_rows<MODE, 2, true>), grid, block, 0, s, M, N, K, qa, da, w, ep);
             else
-                hipLaunchKernelGGL((k_gemm_q5_rows<MODE, 2>), dim3((N + 15) / 16), dim3(nw * 64), 0, s, M, N, K, qa, da,
-                                   w, ep);
+                hipLaunchKernelGGL((k_gemm_q5_rows<MODE, 2, false>), grid, block, 0, s, M, N, K, qa, da, w, ep);
         } else if (M <= 64)
             hipLaunchKernelGGL(k_gemm_q5_skinny<MODE>, dim3((N + 15) / 16), dim3(512), 0, s, M, N, K, qa, da, w, ep);
         else
