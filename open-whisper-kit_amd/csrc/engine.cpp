@@ -192,7 +192,7 @@ void Engine::linear(const char * cls, int mode, int M, int N, int K, const _Floa
         ProfScope ps(prof, stream, "quantize_q8");
         quantize_q8(stream, A32, A16, lda, M, K, q8a_.as<int8_t>(), q8d_.as<float>());
     }
-    ProfScope ps(prof, stream, cls, gemm_flops(M, N, K), (double) N * K * (q.q8 ? 34.0 : 22.0) / 32.0 + (double) M * K);
+    ProfScope ps(prof, stream, cls, gemm_flops(M, N, K), (double) N * K * (q.q8 ? 34.0 : (q.q4 ? 18.0 : 22.0)) / 32.0 + (double) M * K);
     gemm_q5(stream, mode, M, N, K, q8a_.as<int8_t>(), q8d_.as<float>(), q, ep);
 }
 

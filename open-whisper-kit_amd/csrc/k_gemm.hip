@@ -542,9 +542,16 @@ __device__ __forceinline__ long q5_group(const uint8_t * qs_blk, uint32_t qh, in
     return (long) v;
 }
 
-// group g (8 int8) of K block kb of weight row n, Q5_0 (unpacked) or Q8_0 (as stored)
+// 8 consecutive Q4_0 weights of one block as int8: the nibbles of q5_group, value - 8
+__device__ __forceinline__ uint64_t q4_unpack(uint64_t raw, int g) {
+    const uint64_t v = (g < 2 ? raw : (raw >> 4)) & 0x0F0F0F0F0F0F0F0FULL;
+    return ((v | 0x8080808080808080ULL) - 0x0808080808080808ULL) ^ 0x8080808080808080ULL;
+}
+
+// group g (8 int8) of K block kb of weight row n: Q5_0 / Q4_0 (unpacked) or Q8_0 (as stored)
 __device__ __forceinline__ long wq_group(const Q5W & w, int n, int kb, int g, int K, int nb) {
     if (w.q8) return *(const long *) (w.qs + (size_t) n * K + kb * 32 + 8 * g);
+    if (w.q4) return (long) q4_unpack(*(const uint64_t *) (w.qs + (size_t) n * (K / 2) + kb * 16 + (g & 1) * 8), g);
     return q5_group(w.qs + (size_t) n * (K / 2) + kb * 16, w.qh[(size_t) n * nb + kb], g);
 }
 
@@ -613,7 +620,7 @@ constexpr int GQ_MAX_SCALES = 32 * 160;  // M x K/32 activation scales in LDS
 // M * nb <= 32 * nb and blockDim = 64 * ceil(nb / GQ_J) -> at most 32 * GQ_J / 64 + 1 per thread
 constexpr int GQ_DA_PER_THREAD = 32 * GQ_J / 64 + 1;
 
-template <int MODE, int MT, bool Q8>
+template <int MODE, int MT, int FMT>  // FMT: 0 Q5_0, 1 Q8_0, 2 Q4_0
 __global__ __launch_bounds__(GQ_MAXW * 64) void k_gemm_q5_rows(int M, int N, int K, const int8_t * __restrict__ qa,
                                                                const float * __restrict__ da, Q5W w, EpiParams ep) {
     __shared__ floatx4 red[GQ_MAXW][MT][64];
@@ -632,8 +639,9 @@ __global__ __launch_bounds__(GQ_MAXW * 64) void k_gemm_q5_rows(int M, int N, int
     long a[MT][GQ_J];
     // the tile's blocks are contiguous 352 B records (Q5W::tiled): coalesced loads. Blocks
     // past this wave's range load a valid record and a zero activation (adds exact zeros).
-    constexpr bool q8 = Q8;  // Q8_0 records (compile time: the load phase stays branch-free)
-    constexpr int tbytes = Q8 ? Q8_TILE_BYTES : Q5_TILE_BYTES;
+    // record format at compile time: the load phase stays branch-free
+    constexpr bool q8 = FMT == 1, q4 = FMT == 2;
+    constexpr int tbytes = q8 ? Q8_TILE_BYTES : (q4 ? Q4_TILE_BYTES : Q5_TILE_BYTES);
     const uint8_t * tb = w.tiled + (size_t) blockIdx.x * nb * tbytes;
 #pragma unroll
     for (int j = 0; j < GQ_J; ++j) {
@@ -643,6 +651,10 @@ __global__ __launch_bounds__(GQ_MAXW * 64) void k_gemm_q5_rows(int M, int N, int
             raw[j] = *(const uint64_t *) (rec + c16 * 32 + g * 8);
             qh[j] = 0;
             dw[j] = *(const _Float16 *) (rec + 512 + c16 * 2);
+        } else if constexpr (q4) {
+            raw[j] = *(const uint64_t *) (rec + c16 * 16 + (g & 1) * 8);
+            qh[j] = 0;
+            dw[j] = *(const _Float16 *) (rec + 256 + c16 * 2);
         } else {
             raw[j] = *(const uint64_t *) (rec + c16 * 16 + (g & 1) * 8);
             qh[j] = *(const uint32_t *) (rec + 256 + c16 * 4);
@@ -677,7 +689,9 @@ __global__ __launch_bounds__(GQ_MAXW * 64) void k_gemm_q5_rows(int M, int N, int
     for (int j = 0; j < GQ_J; ++j) {
         const int kb = min(kb0 + j, nb - 1);
         uint64_t v = raw[j];
-        if constexpr (!q8) {
+        if constexpr (q4) {
+            v = q4_unpack(raw[j], g);
+        } else if constexpr (!q8) {
             v = (g < 2 ? raw[j] : (raw[j] >> 4)) & 0x0F0F0F0F0F0F0F0FULL;
             const uint32_t h8 = (qh[j] >> (8 * g)) & 0xFFu;
 #pragma unroll
@@ -785,14 +799,16 @@ template <int MODE> struct LaunchQ5 {
         if (M <= 32 && w.tiled && nb <= GQ_MAXW * GQ_J && M * nb <= GQ_MAX_SCALES) {
             const int nw = (nb + GQ_J - 1) / GQ_J;
             const dim3 grid((N + 15) / 16), block(nw * 64);
-            if (M <= 16 && w.q8)
-                hipLaunchKernelGGL((k_gemm_q5_rows<MODE, 1, true>), grid, block, 0, s, M, N, K, qa, da, w, ep);
-            else if (M <= 16)
-                hipLaunchKernelGGL((k_gemm_q5_rows<MODE, 1, false>), grid, block, 0, s, M, N, K, qa, da, w, ep);
-            else if (w.q8)
-                hipLaunchKernelGGL((k_gemm_q5_rows<MODE, 2, true>), grid, block, 0, s, M, N, K, qa, da, w, ep);
-            else
-                hipLaunchKernelGGL((k_gemm_q5_rows<MODE, 2, false>), grid, block, 0, s, M, N, K, qa, da, w, ep);
+            const int fmt = w.q8 ? 1 : (w.q4 ? 2 : 0);
+            if (M <= 16) {
+                if (fmt == 1) hipLaunchKernelGGL((k_gemm_q5_rows<MODE, 1, 1>), grid, block, 0, s, M, N, K, qa, da, w, ep);
+                else if (fmt == 2) hipLaunchKernelGGL((k_gemm_q5_rows<MODE, 1, 2>), grid, block, 0, s, M, N, K, qa, da, w, ep);
+                else hipLaunchKernelGGL((k_gemm_q5_rows<MODE, 1, 0>), grid, block, 0, s, M, N, K, qa, da, w, ep);
+            } else {
+                if (fmt == 1) hipLaunchKernelGGL((k_gemm_q5_rows<MODE, 2, 1>), grid, block, 0, s, M, N, K, qa, da, w, ep);
+                else if (fmt == 2) hipLaunchKernelGGL((k_gemm_q5_rows<MODE, 2, 2>), grid, block, 0, s, M, N, K, qa, da, w, ep);
+                else hipLaunchKernelGGL((k_gemm_q5_rows<MODE, 2, 0>), grid, block, 0, s, M, N, K, qa, da, w, ep);
+            }
         } else if (M <= 64)
             hipLaunchKernelGGL(k_gemm_q5_skinny<MODE>, dim3((N + 15) / 16), dim3(512), 0, s, M, N, K, qa, da, w, ep);
         else
@@ -817,6 +833,32 @@ void q5_tile_host(const uint8_t * qs, const uint32_t * qh, const uint16_t * d, i
                 memcpy(o + 320 + c * 2, &d[(size_t) n * nb + kb], 2);
             }
         }
+}
+
+size_t q4_tiled_bytes(int N, int K) { return (size_t) ((N + 15) / 16) * (K / 32) * Q4_TILE_BYTES; }
+
+void q4_tile_host(const uint8_t * qs, const uint16_t * d, int N, int K, uint8_t * out) {
+    const int nb = K / 32, nt = (N + 15) / 16;
+    memset(out, 0, q4_tiled_bytes(N, K));
+    for (int t = 0; t < nt; ++t)
+        for (int kb = 0; kb < nb; ++kb) {
+            uint8_t * o = out + ((size_t) t * nb + kb) * Q4_TILE_BYTES;
+            for (int c = 0; c < 16; ++c) {
+                const int n = t * 16 + c;
+                if (n >= N) break;
+                memcpy(o + c * 16, qs + (size_t) n * (K / 2) + kb * 16, 16);
+                memcpy(o + 256 + c * 2, &d[(size_t) n * nb + kb], 2);
+            }
+        }
+}
+
+void q4_split_host(const uint8_t * blocks, int N, int K, uint8_t * qs, uint16_t * d) {
+    const int nb = K / 32;
+    for (size_t i = 0; i < (size_t) N * nb; ++i) {
+        const uint8_t * b = blocks + i * 18;  // block_q4_0: d (f16), qs[16]
+        memcpy(&d[i], b, 2);
+        memcpy(qs + i * 16, b + 2, 16);
+    }
 }
 
 size_t q8_tiled_bytes(int N, int K) { return (size_t) ((N + 15) / 16) * (K / 32) * Q8_TILE_BYTES; }

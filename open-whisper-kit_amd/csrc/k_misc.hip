@@ -252,10 +252,29 @@ __global__ void k_embed_q8(const int8_t * __restrict__ qs, const _Float16 * __re
     }
 }
 
+__global__ void k_embed_q4(const uint8_t * __restrict__ qs, const _Float16 * __restrict__ dd,
+                           const float * __restrict__ pe, const int * __restrict__ tok, const int * __restrict__ pos,
+                           int rows, int d, float * __restrict__ x) {
+    const int r = blockIdx.x;
+    if (r >= rows) return;
+    const size_t row = (size_t) tok[r];
+    const int nb = d / 32;
+    const float * p = pe + (size_t) pos[r] * d;
+    for (int i = threadIdx.x; i < d; i += blockDim.x) {
+        const int b = i >> 5, j = i & 31;
+        const uint8_t byte = qs[row * (d / 2) + b * 16 + (j & 15)];
+        const int q = j < 16 ? (byte & 0x0F) : (byte >> 4);
+        const float v = (float) (q - 8) * (float) dd[row * nb + b];  // dequantize_row_q4_0
+        x[(size_t) r * d + i] = v + p[i];
+    }
+}
+
 void embed_tokens_q5(hipStream_t s, const Q5W & te, const float * pe, const int * tok, const int * pos, int rows, int d,
                      float * x) {
     if (rows <= 0) return;
-    if (te.q8)
+    if (te.q4)
+        hipLaunchKernelGGL(k_embed_q4, dim3(rows), dim3(256), 0, s, te.qs, te.d, pe, tok, pos, rows, d, x);
+    else if (te.q8)
         hipLaunchKernelGGL(k_embed_q8, dim3(rows), dim3(256), 0, s, (const int8_t *) te.qs, te.d, pe, tok, pos, rows, d, x);
     else
         hipLaunchKernelGGL(k_embed_q5, dim3(rows), dim3(256), 0, s, te.qs, te.qh, te.d, pe, tok, pos, rows, d, x);

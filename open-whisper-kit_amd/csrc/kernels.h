@@ -95,10 +95,18 @@ struct Q5W {
     // Q8_0 matrices (MOSTLY_Q8_0 models) share the pipeline: qs = [N][K] int8, qh unused,
     // tiled records of 16 rows x 32 int8 | 16 x d (544 B)
     bool q8 = false;
+    // Q4_0 matrices (MOSTLY_Q4_0): qs as Q5_0's nibbles (value - 8), qh unused, tiled records
+    // of 16 rows x 16 B | 16 x d (288 B)
+    bool q4 = false;
     explicit operator bool() const { return qs != nullptr; }
 };
 constexpr int Q5_TILE_BYTES = 352;
 constexpr int Q8_TILE_BYTES = 544;
+constexpr int Q4_TILE_BYTES = 288;
+size_t q4_tiled_bytes(int N, int K);
+void q4_tile_host(const uint8_t * qs, const uint16_t * d, int N, int K, uint8_t * out);
+// block_q4_0 rows (d f16, qs[16]) -> qs [N][K/2], d [N][K/32]
+void q4_split_host(const uint8_t * blocks, int N, int K, uint8_t * qs, uint16_t * d);
 size_t q8_tiled_bytes(int N, int K);
 void q8_tile_host(const int8_t * qs, const uint16_t * d, int N, int K, uint8_t * out);
 // block_q8_0 rows (d f16, qs[32]) -> qs [N][K], d [N][K/32]

@@ -219,13 +219,14 @@ Model * load_model(whisper_model_loader * loader, int device, std::string & err)
     const int qntvr = hp.ftype / 1000;
     (void) qntvr;
     hp.ftype %= 1000;
-    // GGML_FTYPE_MOSTLY_F16 (1), MOSTLY_Q8_0 (7), MOSTLY_Q5_0 (8) (ggml.h:440-450)
-    if (hp.ftype != 1 && hp.ftype != 7 && hp.ftype != 8) {
-        err = "unsupported ftype " + std::to_string(hp.ftype) + " (this engine build loads F16, Q8_0 and Q5_0 models)";
+    // GGML_FTYPE_MOSTLY_F16 (1), MOSTLY_Q4_0 (2), MOSTLY_Q8_0 (7), MOSTLY_Q5_0 (8) (ggml.h:440-450)
+    if (hp.ftype != 1 && hp.ftype != 2 && hp.ftype != 7 && hp.ftype != 8) {
+        err = "unsupported ftype " + std::to_string(hp.ftype) + " (this engine build loads F16, Q4_0, Q8_0 and Q5_0 models)";
         return nullptr;
     }
-    m->q5 = hp.ftype == 8 || hp.ftype == 7;  // quantized weights x Q8_0 activations
+    m->q5 = hp.ftype == 8 || hp.ftype == 7 || hp.ftype == 2;  // quantized weights x Q8_0 activations
     m->q8 = hp.ftype == 7;
+    m->q4 = hp.ftype == 2;
 
     // mel filters
     m->n_filters_mel = r.get<int32_t>();
@@ -308,7 +309,7 @@ Model * load_model(whisper_model_loader * loader, int device, std::string & err)
         // Q5_0 / Q8_0 models: every 2-D weight is GGML_TYPE_Q5_0 (6, 22 bytes per 32) or
         // GGML_TYPE_Q8_0 (8, 34 bytes per 32) (whisper-quantize)
         const bool want_q5 = m->q5 && sp.f16 && sp.ne.size() == 2;
-        const int qtype = m->q8 ? 8 : 6, qbytes = m->q8 ? 34 : 22;
+        const int qtype = m->q8 ? 8 : (m->q4 ? 2 : 6), qbytes = m->q8 ? 34 : (m->q4 ? 18 : 22);
         if (want_q5 ? ttype != qtype : (ttype != 0 && ttype != 1)) {
             err = "tensor '" + name + "': unsupported type " + std::to_string(ttype);
             return nullptr;
@@ -467,10 +468,11 @@ Model * load_model(whisper_model_loader * loader, int device, std::string & err)
             Plan pl{0, 0, 0, (size_t) -1, N, K};
             auto res = [&](size_t bytes) { size_t o = qoff; qoff += (bytes + 255) & ~(size_t) 255; return o; };
             pl.qs = res(m->q8 ? (size_t) N * K : (size_t) N * K / 2);
-            pl.qh = m->q8 ? 0 : res((size_t) N * (K / 32) * 4);
+            pl.qh = (m->q8 || m->q4) ? 0 : res((size_t) N * (K / 32) * 4);
             pl.d = res((size_t) N * (K / 32) * 2);
             // decode-step matrices also get the column-tiled copy the decode-row GEMM streams
-            if (gi == n_dec_first || gi >= n_enc_groups) pl.tiled = res(m->q8 ? q8_tiled_bytes(N, K) : q5_tiled_bytes(N, K));
+            if (gi == n_dec_first || gi >= n_enc_groups)
+                pl.tiled = res(m->q8 ? q8_tiled_bytes(N, K) : (m->q4 ? q4_tiled_bytes(N, K) : q5_tiled_bytes(N, K)));
             plans.push_back(pl);
         }
         m->q5blob.alloc(qoff);
@@ -500,7 +502,32 @@ Model * load_model(whisper_model_loader * loader, int device, std::string & err)
             }
             q5m[groups[gi][0]] = w;
         }
-        for (size_t gi = 0; gi < groups.size() && !m->q8; ++gi) {
+        for (size_t gi = 0; gi < groups.size() && m->q4; ++gi) {
+            const Plan & pl = plans[gi];
+            std::vector<uint8_t> qs((size_t) pl.N * pl.K / 2);
+            std::vector<uint16_t> dd((size_t) pl.N * (pl.K / 32));
+            int row = 0;
+            for (const auto & n : groups[gi]) {
+                const HostTensor & t = host(n);
+                const int rows = (int) S[idx.at(n)].ne[1];
+                q4_split_host(t.data.data(), rows, pl.K, qs.data() + (size_t) row * pl.K / 2, dd.data() + (size_t) row * (pl.K / 32));
+                row += rows;
+            }
+            OWK_HIP_CHECK(hipMemcpy(qb + pl.qs, qs.data(), qs.size(), hipMemcpyHostToDevice));
+            OWK_HIP_CHECK(hipMemcpy(qb + pl.d, dd.data(), dd.size() * 2, hipMemcpyHostToDevice));
+            Q5W w;
+            w.q4 = true;
+            w.qs = (const uint8_t *) (qb + pl.qs);
+            w.d = (const _Float16 *) (qb + pl.d);
+            if (pl.tiled != (size_t) -1) {
+                std::vector<uint8_t> tl(q4_tiled_bytes(pl.N, pl.K));
+                q4_tile_host(qs.data(), dd.data(), pl.N, pl.K, tl.data());
+                OWK_HIP_CHECK(hipMemcpy(qb + pl.tiled, tl.data(), tl.size(), hipMemcpyHostToDevice));
+                w.tiled = (const uint8_t *) (qb + pl.tiled);
+            }
+            q5m[groups[gi][0]] = w;
+        }
+        for (size_t gi = 0; gi < groups.size() && !m->q8 && !m->q4; ++gi) {
             const Plan & pl = plans[gi];
             std::vector<uint8_t> qs((size_t) pl.N * pl.K / 2);
             std::vector<uint32_t> qh((size_t) pl.N * (pl.K / 32));

@@ -213,6 +213,26 @@ def q5_0_blocks(x: np.ndarray) -> bytes:
     return out.tobytes()
 
 
+def q4_0_blocks(x: np.ndarray) -> bytes:
+    """ggml Q4_0 blocks (18 B per 32 weights), restating quantize_row_q4_0_ref
+    (/root/reference ggml/src/ggml-quants.c:36-71): d = max / -8 with max the first
+    largest-magnitude value, q = min(15, (int8)(x / d + 8.5)) (the multiply-add contracted to
+    one FMA as in q5_0_blocks), element j low nibble, j + 16 high nibble of byte j."""
+    b = np.ascontiguousarray(x, np.float32).reshape(-1, 32)
+    am = np.argmax(np.abs(b), axis=1)
+    mx = b[np.arange(len(b)), am]
+    d = (mx / np.float32(-8.0)).astype(np.float32)
+    with np.errstate(divide="ignore"):
+        idv = np.where(d != 0, np.float32(1.0) / d, np.float32(0.0)).astype(np.float32)
+    xs = (b.astype(np.float64) * idv.astype(np.float64)[:, None] + 8.5).astype(np.float32)
+    xi = np.minimum(15, np.trunc(xs).astype(np.int64).astype(np.int8).astype(np.int64) & 0xFF).astype(np.uint8)
+    qs = (xi[:, :16] & 0x0F) | ((xi[:, 16:] & 0x0F) << 4)
+    out = np.zeros((len(b), 18), np.uint8)
+    out[:, 0:2] = d.astype("<f2").view(np.uint8).reshape(-1, 2)
+    out[:, 2:18] = qs
+    return out.tobytes()
+
+
 def q8_0_blocks(x: np.ndarray) -> bytes:
     """block_q8_0 rows of f32 values: quantize_row_q8_0_ref (ref ggml/src/ggml-quants.c:199-222):
     d = amax / 127 (stored f16), q = roundf(x * (1/d)) (round half away from zero)."""
@@ -232,6 +252,14 @@ def quantize_q8_0(src: str, dst: str) -> str:
     """Q8_0 copy of an F16 ggml-bin model as whisper-quantize writes it (same tensor rule as
     quantize_q5_0; ttype 8, ftype 2007 = GGML_QNT_VERSION 2 * 1000 + MOSTLY_Q8_0 7)."""
     return quantize_q5_0(src, dst, kind="q8_0")
+
+
+def quantize_q4_0(src: str, dst: str) -> str:
+    """Q4_0 copy (ttype 2, ftype 2002 = GGML_QNT_VERSION 2 * 1000 + MOSTLY_Q4_0 2)."""
+    return quantize_q5_0(src, dst, kind="q4_0")
+
+
+_QKIND = {"q5_0": (8, 6, q5_0_blocks), "q8_0": (7, 8, q8_0_blocks), "q4_0": (2, 2, q4_0_blocks)}  # ftype, ttype
 
 
 def quantize_q5_0(src: str, dst: str, kind: str = "q5_0") -> str:
@@ -256,7 +284,7 @@ def quantize_q5_0(src: str, dst: str, kind: str = "q5_0") -> str:
             h.update(b)
         w(take(4))
         hp = list(struct.unpack("<11i", take(44)))
-        hp[10] = 2000 + (8 if kind == "q5_0" else 7)
+        hp[10] = 2000 + _QKIND[kind][0]
         w(struct.pack("<11i", *hp))
         n_mel, n_fft = struct.unpack("<ii", take(8))
         w(struct.pack("<ii", n_mel, n_fft))
@@ -275,12 +303,12 @@ def quantize_q5_0(src: str, dst: str, kind: str = "q5_0") -> str:
             nel = int(np.prod(ne))
             data = take(nel * (2 if ttype == 1 else 4))
             quant = n_dims == 2 and name.decode() not in skip
-            w(struct.pack("<iii", n_dims, name_len, (6 if kind == "q5_0" else 8) if quant else ttype))
+            w(struct.pack("<iii", n_dims, name_len, _QKIND[kind][1] if quant else ttype))
             w(struct.pack("<%di" % n_dims, *ne))
             w(name)
             if quant:
                 x = np.frombuffer(data, "<f2" if ttype == 1 else "<f4").astype(np.float32)
-                w(q5_0_blocks(x) if kind == "q5_0" else q8_0_blocks(x))
+                w(_QKIND[kind][2](x))
             else:
                 w(data)
     os.replace(tmp, dst)
@@ -291,7 +319,7 @@ def ensure_model(model: str, seed: int = 1234, cache_dir: str | None = None) -> 
     """Path to a cached synthetic model (generated on first use)."""
     cache_dir = cache_dir or os.environ.get("OWK_MODEL_CACHE", "/tmp/owk_models")
     os.makedirs(cache_dir, exist_ok=True)
-    kind = next((k for k in ("q5_0", "q8_0") if model.endswith("-" + k)), None)
+    kind = next((k for k in ("q5_0", "q8_0", "q4_0") if model.endswith("-" + k)), None)
     base = model[:-5] if kind else model
     path = os.path.join(cache_dir, f"synth-{base}-s{seed}.bin")
     if not os.path.exists(path):

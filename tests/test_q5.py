@@ -1,6 +1,6 @@
-"""Q5_0 and Q8_0 models (ftype 2008 / 2007).
-Every test runs for both kinds: q5_golden.* (Q5_0) and q8_golden.* (Q8_0), made by
-tests/golden/make_golden_q5.py [q8_0] from the reference on the same synthetic weights.
+"""Q5_0, Q8_0 and Q4_0 models (ftype 2008 / 2007 / 2002).
+Every test runs for each kind: q5_golden.*, q8_golden.*, q4_golden.*, made by
+tests/golden/make_golden_q5.py [q8_0|q4_0] from the reference on the same synthetic weights.
 
 CPU: owk_synth.quantize_q5_0 (restatement of whisper-quantize) writes byte-identical files to
 the reference quantizer compiled from its own sources (oracle/_ref/whisper-quantize).
@@ -27,7 +27,7 @@ GOLDEN = os.path.join(ROOT, "tests", "golden")
 QUANT = os.path.join(ROOT, "oracle", "_ref", "whisper-quantize")
 
 
-KINDS = {"q5_0": ("q5_golden", 8), "q8_0": ("q8_golden", 7)}  # fixture stem, GGML_FTYPE_MOSTLY_*
+KINDS = {"q5_0": ("q5_golden", 8), "q8_0": ("q8_golden", 7), "q4_0": ("q4_golden", 2)}  # fixture stem, GGML_FTYPE_MOSTLY_*
 
 
 @pytest.fixture(scope="module", params=list(KINDS))
@@ -49,7 +49,7 @@ def q5_model(model, meta):
     sha_file = path + ".sha256"
     want = meta["models"][model]["sha256"]
     if not (os.path.exists(path) and os.path.exists(sha_file) and open(sha_file).read().strip() == want):
-        assert (S.quantize_q5_0 if kind == "q5_0" else S.quantize_q8_0)(src, path) == want
+        assert S.quantize_q5_0(src, path, kind=kind) == want
         with open(sha_file, "w") as f:
             f.write(want)
     return path
@@ -67,8 +67,7 @@ def test_quantizer_matches_reference(q5g, tmp_path):
     subprocess.run([QUANT, src, out, kind], check=True, capture_output=True)
     ref = hashlib.sha256(open(out, "rb").read()).hexdigest()
     assert ref == meta["models"]["tiny.en"]["sha256"]
-    quant = S.quantize_q5_0 if kind == "q5_0" else S.quantize_q8_0
-    assert quant(src, str(tmp_path / f"py_{kind}.bin")) == ref
+    assert S.quantize_q5_0(src, str(tmp_path / f"py_{kind}.bin"), kind=kind) == ref
 
 
 _ctx = {}
