@@ -615,14 +615,15 @@ __global__ __launch_bounds__(512) void k_gemm_q5_skinny(int M, int N, int K, con
 // (v_mfma_i32_16x16x32_i8) is scaled by d_a * d_w into the f32 accumulator; wave partial
 // tiles are summed in fixed wave order. K up to GQ_MAXW * J * 32 (5120 at J = 10).
 constexpr int GQ_MAXW = 16;
-constexpr int GQ_J = 10;
+constexpr int GQ_JMAX = 10;  // K up to GQ_MAXW * GQ_JMAX * 32; short K uses 3 blocks per wave
 constexpr int GQ_MAX_SCALES = 32 * 160;  // M x K/32 activation scales in LDS
-// M * nb <= 32 * nb and blockDim = 64 * ceil(nb / GQ_J) -> at most 32 * GQ_J / 64 + 1 per thread
-constexpr int GQ_DA_PER_THREAD = 32 * GQ_J / 64 + 1;
+// activation scales per thread: M * nb <= 32 * nb over blockDim = 64 * ceil(nb / J) threads
+// -> at most 32 * J / 64 + 1
 
-template <int MODE, int MT, int FMT>  // FMT: 0 Q5_0, 1 Q8_0, 2 Q4_0
+template <int MODE, int MT, int FMT, int GQ_J>  // FMT: 0 Q5_0, 1 Q8_0, 2 Q4_0; GQ_J K blocks per wave
 __global__ __launch_bounds__(GQ_MAXW * 64) void k_gemm_q5_rows(int M, int N, int K, const int8_t * __restrict__ qa,
                                                                const float * __restrict__ da, Q5W w, EpiParams ep) {
+    constexpr int GQ_DA_PER_THREAD = 32 * GQ_J / 64 + 1;
     __shared__ floatx4 red[GQ_MAXW][MT][64];
     __shared__ float sda[GQ_MAX_SCALES];
     const int tid = threadIdx.x, lane = tid & 63, nw = blockDim.x >> 6;
@@ -796,19 +797,25 @@ template <int MODE> struct LaunchQ5 {
     static void run(hipStream_t s, int M, int N, int K, const int8_t * qa, const float * da, const Q5W & w,
                     const EpiParams & ep) {
         const int nb = K / 32;
-        if (M <= 32 && w.tiled && nb <= GQ_MAXW * GQ_J && M * nb <= GQ_MAX_SCALES) {
-            const int nw = (nb + GQ_J - 1) / GQ_J;
+        if (M <= 32 && w.tiled && nb <= GQ_MAXW * GQ_JMAX && M * nb <= GQ_MAX_SCALES) {
+            // more, shorter waves when K allows: 3 K blocks per wave up to K = 1536
+            const int J = nb <= GQ_MAXW * 3 ? 3 : GQ_JMAX;
+            const int nw = (nb + J - 1) / J;
             const dim3 grid((N + 15) / 16), block(nw * 64);
             const int fmt = w.q8 ? 1 : (w.q4 ? 2 : 0);
+#define OWK_Q_ROWS(MT_, F_, J_) hipLaunchKernelGGL((k_gemm_q5_rows<MODE, MT_, F_, J_>), grid, block, 0, s, M, N, K, qa, da, w, ep)
+#define OWK_Q_ROWS_J(MT_, F_) do { if (J == 3) OWK_Q_ROWS(MT_, F_, 3); else OWK_Q_ROWS(MT_, F_, GQ_JMAX); } while (0)
             if (M <= 16) {
-                if (fmt == 1) hipLaunchKernelGGL((k_gemm_q5_rows<MODE, 1, 1>), grid, block, 0, s, M, N, K, qa, da, w, ep);
-                else if (fmt == 2) hipLaunchKernelGGL((k_gemm_q5_rows<MODE, 1, 2>), grid, block, 0, s, M, N, K, qa, da, w, ep);
-                else hipLaunchKernelGGL((k_gemm_q5_rows<MODE, 1, 0>), grid, block, 0, s, M, N, K, qa, da, w, ep);
+                if (fmt == 1) OWK_Q_ROWS_J(1, 1);
+                else if (fmt == 2) OWK_Q_ROWS_J(1, 2);
+                else OWK_Q_ROWS_J(1, 0);
             } else {
-                if (fmt == 1) hipLaunchKernelGGL((k_gemm_q5_rows<MODE, 2, 1>), grid, block, 0, s, M, N, K, qa, da, w, ep);
-                else if (fmt == 2) hipLaunchKernelGGL((k_gemm_q5_rows<MODE, 2, 2>), grid, block, 0, s, M, N, K, qa, da, w, ep);
-                else hipLaunchKernelGGL((k_gemm_q5_rows<MODE, 2, 0>), grid, block, 0, s, M, N, K, qa, da, w, ep);
+                if (fmt == 1) OWK_Q_ROWS_J(2, 1);
+                else if (fmt == 2) OWK_Q_ROWS_J(2, 2);
+                else OWK_Q_ROWS_J(2, 0);
             }
+#undef OWK_Q_ROWS_J
+#undef OWK_Q_ROWS
         } else if (M <= 64)
             hipLaunchKernelGGL(k_gemm_q5_skinny<MODE>, dim3((N + 15) / 16), dim3(512), 0, s, M, N, K, qa, da, w, ep);
         else
