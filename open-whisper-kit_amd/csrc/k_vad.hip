@@ -32,6 +32,8 @@ constexpr int VAD_G = 4 * VAD_H;
 constexpr int VAD_CH = 4;      // chunks per encode workgroup (weights read once per 4 chunks)
 constexpr int VAD_THREADS = 256;
 
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
 __device__ __forceinline__ float r16(float x) { return (float) (_Float16) x; }
 
 __device__ __forceinline__ float sigm(float x) { return 1.0f / (1.0f + expf(-x)); }
@@ -210,16 +212,15 @@ __global__ void __launch_bounds__(VAD_G) vad_lstm_kernel(
         for (int k = 0; k < VAD_PF; ++k) {
             const int t = tb + k;
             if (t >= n) break;
-            float a0 = 0.0f, a1 = 0.0f, a2 = 0.0f, a3 = 0.0f;
+            // packed FMAs (v_pk_fma_f32): two of the four partial sums per instruction
+            f32x2 a01 = {0.0f, 0.0f}, a23 = {0.0f, 0.0f};
 #pragma unroll
             for (int j = 0; j < VAD_H; j += 4) {
                 const float4 h4 = *(const float4 *) &hs[j];
-                a0 = __builtin_fmaf(wr[j], h4.x, a0);
-                a1 = __builtin_fmaf(wr[j + 1], h4.y, a1);
-                a2 = __builtin_fmaf(wr[j + 2], h4.z, a2);
-                a3 = __builtin_fmaf(wr[j + 3], h4.w, a3);
+                a01 = __builtin_elementwise_fma(f32x2{wr[j], wr[j + 1]}, f32x2{h4.x, h4.y}, a01);
+                a23 = __builtin_elementwise_fma(f32x2{wr[j + 2], wr[j + 3]}, f32x2{h4.z, h4.w}, a23);
             }
-            const float hid = ((a0 + a1) + (a2 + a3)) + bh;
+            const float hid = ((a01.x + a01.y) + (a23.x + a23.y)) + bh;
             const float pre = buf[k] + hid;  // inp_gate + hid_gate (ref 4582)
             gs[r] = (r >= 2 * VAD_H && r < 3 * VAD_H) ? tanhf(pre) : sigm(pre);
             lds_barrier();
