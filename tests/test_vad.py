@@ -244,3 +244,18 @@ def test_gpu_whisper_full_with_vad(vctx, vg, model_path, clips, clip, cfg):
         assert got == want["segments"]
     finally:
         w.close() if hasattr(w, "close") else None
+
+
+def test_init_rejects_bad_files(tmp_path):
+    """loader errors return NULL before any device work (ref 4761-4790, 5004-5034)"""
+    L = owk.load()
+    owk.quiet()
+    cp = L.whisper_vad_default_context_params()
+    assert not L.whisper_vad_init_from_file_with_params(str(tmp_path / "missing.bin").encode(), cp)
+    raw = open(VAD_MODEL, "rb").read()
+    bad_magic = tmp_path / "magic.bin"
+    bad_magic.write_bytes(b"XXXX" + raw[4:])
+    assert not L.whisper_vad_init_from_file_with_params(str(bad_magic).encode(), cp)
+    truncated = tmp_path / "trunc.bin"
+    truncated.write_bytes(raw[: len(raw) // 2])
+    assert not L.whisper_vad_init_from_file_with_params(str(truncated).encode(), cp)
