@@ -259,3 +259,32 @@ def test_init_rejects_bad_files(tmp_path):
     truncated = tmp_path / "trunc.bin"
     truncated.write_bytes(raw[: len(raw) // 2])
     assert not L.whisper_vad_init_from_file_with_params(str(truncated).encode(), cp)
+
+
+@pytest.mark.gpu
+def test_gpu_whisper_full_parallel_with_vad(vctx, model_path, clips):
+    """whisper_full_parallel(params.vad, 2 processors) (ref 7801-7929 with the VAD pre-pass
+    of 7812-7824): succeeds, and every segment time maps back inside the original audio in
+    order (no reference fixture covers the split-chunk merge: parity unpinned here)."""
+    w = owk.Whisper(model_path("tiny.en"))
+    try:
+        L = w.L
+        p = w.params(0, temperature_inc=0.0, language="en")
+        p.vad = True
+        p.vad_model_path = VAD_MODEL.encode()
+        pcm = np.ascontiguousarray(clips["composite"], np.float32)
+        assert L.whisper_full_parallel(w.ctx, p, owk.fptr(pcm), len(pcm), 2) == 0
+        L.whisper_full_get_segment_t0.restype = C.c_int64
+        L.whisper_full_get_segment_t1.restype = C.c_int64
+        L.whisper_full_get_segment_t0.argtypes = [C.c_void_p, C.c_int]
+        L.whisper_full_get_segment_t1.argtypes = [C.c_void_p, C.c_int]
+        n = L.whisper_full_n_segments(w.ctx)
+        assert n >= 1
+        dur_cs = len(pcm) * 100 // 16000
+        prev = -1
+        for i in range(n):
+            t0, t1 = L.whisper_full_get_segment_t0(w.ctx, i), L.whisper_full_get_segment_t1(w.ctx, i)
+            assert 0 <= t0 <= t1 <= dur_cs + 10 and t0 >= prev, (i, t0, t1)
+            prev = t0
+    finally:
+        w.close()
