@@ -751,8 +751,8 @@ void prep_chunk(sortformer_context * ctx, StreamState & st, const float * mel, i
                                      hipMemcpyHostToDevice, ctx->stream));
     OWK_HIP_CHECK(hipMemcpyAsync(x + (size_t) (st.spkcache_len + st.fifo_len) * d, ctx->s_pre.ptr, (size_t) w.Tc * d * 4,
                                  hipMemcpyDeviceToDevice, ctx->stream));
-    // the host copies read st's vectors and fill w.chunk: complete before they change
-    OWK_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    // no sync here: the copies are stream-ordered before the head pass, whose prediction
+    // read-back synchronizes the stream before post_chunk touches st or w.chunk
 }
 
 int post_chunk(const sortformer_context * ctx, const StreamConfig & cfg, StreamState & st, ChunkWork & w,
