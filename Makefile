@@ -56,7 +56,33 @@ selftest: $(SELFTEST)
 oracle:
 	$(MAKE) -C oracle/ref -j$(JOBS)
 
+# The reference's own C/C++ callers, compiled UNCHANGED from /root/reference against
+# include/ and linked to our libraries (the drop-in claim of INTEGRATION.md). Built here
+# (this container has the sources); the binaries travel to the GPU box in lib/callers/.
+REF      ?= /root/reference
+CALLERS  := $(PKG)/lib/callers
+EXCOMMON := $(REF)/examples/common.cpp $(REF)/examples/common-whisper.cpp $(REF)/examples/grammar-parser.cpp
+CALLFLAGS := -O2 -std=c++17 -w -Iinclude -I$(REF)/examples
+
+callers: $(CALLERS)/whisper-cli $(CALLERS)/whisper-bench $(CALLERS)/sortformer-diarize $(CALLERS)/test-streaming-api
+
+$(CALLERS)/whisper-cli: $(REF)/examples/cli/cli.cpp $(EXCOMMON) $(LIB) $(HDRS)
+	@mkdir -p $(CALLERS)
+	g++ $(CALLFLAGS) $< $(EXCOMMON) -o $@ -L$(PKG)/lib -lwhisper -Wl,-rpath,'$$ORIGIN/..'
+
+$(CALLERS)/whisper-bench: $(REF)/examples/bench/bench.cpp $(EXCOMMON) $(LIB) $(HDRS)
+	@mkdir -p $(CALLERS)
+	g++ $(CALLFLAGS) $< $(EXCOMMON) -o $@ -L$(PKG)/lib -lwhisper -Wl,-rpath,'$$ORIGIN/..'
+
+$(CALLERS)/sortformer-diarize: $(REF)/streaming-sortformer/src/sortformer-cli.cpp $(SFLIB) $(HDRS)
+	@mkdir -p $(CALLERS)
+	g++ $(CALLFLAGS) $< -o $@ -L$(PKG)/lib -lsortformer -Wl,-rpath,'$$ORIGIN/..'
+
+$(CALLERS)/test-streaming-api: $(REF)/streaming-sortformer/src/test-streaming-api.cpp $(SFLIB) $(HDRS)
+	@mkdir -p $(CALLERS)
+	g++ $(CALLFLAGS) $< -o $@ -L$(PKG)/lib -lsortformer -Wl,-rpath,'$$ORIGIN/..'
+
 clean:
 	rm -rf $(OBJDIR) $(PKG)/lib
 
-.PHONY: all clean oracle selftest
+.PHONY: all clean oracle selftest callers

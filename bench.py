@@ -64,6 +64,39 @@ def pmc_traffic(cls):
     return None
 
 
+# the arithmetic each weight format computes in (kernels.h)
+DTYPE = {"f16": "f16", "q5_0": "q5_0*q8_0 (int8 MFMA, f32 block scales)", "q8_0": "q8_0*q8_0 (int8 MFMA, f32 block scales)",
+         "q4_0": "q4_0*q8_0 (int8 MFMA, f32 block scales)"}
+DECODE_CLASSES = {"attn_cross", "attn_self", "gemm_dec", "layernorm", "logits_proc", "gemm_logits", "embed"}
+
+
+def model_kind(model):
+    return next((k for k in ("q5_0", "q8_0", "q4_0") if model.endswith("-" + k)), "f16")
+
+
+def phase_fractions(classes, ms_per_step):
+    """MFMA fraction over the encoder + cross-KV (+ prefill) classes, HBM fraction over
+    the decode-step classes (algorithmic bytes / their device time), whole-pipeline MFMA fraction
+    (all algorithmic FLOPs of a step / the step's wall time). From the profiled step's per-class
+    HIP-event times (one step of the same workload)."""
+    enc = [c for c in classes if c in MFMA_CLASSES]
+    dec = [c for c in classes if c in DECODE_CLASSES]
+    e_ms = sum(classes[c]["ms"] for c in enc)
+    e_fl = sum(classes[c]["flops"] for c in enc)
+    d_ms = sum(classes[c]["ms"] for c in dec)
+    d_by = sum(classes[c]["bytes"] for c in dec)
+    fl = sum(v["flops"] for v in classes.values())
+    r = lambda x: round(x, 4)
+    return {
+        "encoder_mfma": {"classes": sorted(enc), "ms": round(e_ms, 2), "tflops": r(e_fl / max(e_ms, 1e-9) / 1e9),
+                         "frac": r(e_fl / max(e_ms, 1e-9) / 1e9 / PEAK_F16_TFLOPS)},
+        "decode_hbm": {"classes": sorted(dec), "ms": round(d_ms, 2), "gbs": r(d_by / max(d_ms, 1e-9) / 1e6),
+                       "frac": r(d_by / max(d_ms, 1e-9) / 1e6 / PEAK_HBM_GBS)},
+        "pipeline_mfma": {"tflop_per_step": r(fl / 1e12), "ms_per_step": round(ms_per_step, 2),
+                          "frac": r(fl / (ms_per_step * 1e-3) / 1e12 / PEAK_F16_TFLOPS)},
+    }
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -93,26 +126,28 @@ def cpu_threads():
 
 
 def cpu_baseline(model_path, pcm):
-    """Reference ggml CPU path on one clip of the same fixed workload (bounded sample)."""
+    """Reference ggml CPU path on one clip of the same fixed workload (bounded sample).
+    Returns (baseline record, the reference's token ids for the clip)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import ref_oracle as R  # test/measurement infrastructure only
 
     if not R.available():
-        return None
+        return None, None
     nt = cpu_threads()
     ref = R.Ref(model_path)
     t0 = time.perf_counter()
     ret, segs = ref.full(pcm, n_threads=nt, language="en", no_timestamps=True, max_tokens=MAX_TOKENS,
                          suppress_eot=True, temperature_inc=0.0)
     wall = time.perf_counter() - t0
-    ntok = sum(len(s["tokens"]) for s in segs)
+    ids = [t[0] for s in segs for t in s["tokens"]]
     tm = ref.timings()
     ref.close()
     return {"value": round(len(pcm) / 16000.0 / wall, 4), "unit": "audio-s/wall-s", "cores": nt,
             "kind": "reference",
-            "sample": f"1 clip x 30 s, same model/params, {ntok} tokens, ret={ret}, wall {wall:.1f} s "
-                      f"(encode {tm['enc_ms'] / 1e3:.1f} s, decode {tm['dec_ms'] / 1e3:.1f} s), "
-                      f"ggml CPU n_threads={nt}"}
+            "sample": f"1 clip (clip 0 of the GPU batch) x 30 s, same model/params, {len(ids)} tokens, ret={ret}, "
+                      f"wall {wall:.1f} s (encode {tm['enc_ms'] / 1e3:.1f} s, decode {tm['dec_ms'] / 1e3:.1f} s), "
+                      f"ggml CPU n_threads={nt}; reference built from its sources with -march=x86-64-v4 "
+                      f"(oracle/ref/Makefile; AVX-512 F/BW/CD/DQ/VL, no VNNI/BF16 paths) rather than GGML_NATIVE"}, ids
 
 
 def clip_seeds(rank, per_gpu):
@@ -237,6 +272,7 @@ def main():
         roof["measured"] = "HIP events on the engine stream, one extra profiled step (eager launches)"
         roof["avg_launch_ms"] = round(avg_ms, 5)
         roof["launches"] = d["launches"]
+        roof["phases"] = phase_fractions(classes, 1e3 * dt / args.steps)
         if rank == 0:
             tot = sum(v["ms"] for v in classes.values())
             for c, v in sorted(classes.items(), key=lambda kv: -kv[1]["ms"]):
@@ -245,6 +281,7 @@ def main():
                     f"{v['bytes'] / max(v['ms'], 1e-9) / 1e6:8.1f} GB/s")
 
     audio_s = world * B * args.steps * CLIP_SAMPLES / 16000.0
+    kind = model_kind(args.model)
     out = {
         "metric": "real-time factor (audio-sec/wall-sec) large-v3 30s clips, 1/2/4/8 MI355X",
         "value": round(audio_s / dt, 2),
@@ -256,19 +293,29 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "f16",
+        "dtype": DTYPE[kind],
         "data": "synthetic: seeded 30 s 16 kHz clips; random-init weights of the named architecture",
-        "config": {"workload": f"{args.model} F16, {B} x 30 s clips per GPU per step, greedy "
+        "config": {"workload": f"{args.model} {kind.upper()} weights, {B} x 30 s clips per GPU per step, greedy "
                                f"(temperature_inc=0), no_timestamps, EOT suppressed, {MAX_TOKENS + 1} "
                                f"tokens/clip, audio resident in HBM",
                    "model": args.model, "clips_per_gpu": B, "global_batch": world * B,
                    "tokens_per_clip": MAX_TOKENS + 1, "parallelism": f"clip-sharded x{world} (no collectives)"},
         "roofline": roof,
         "cpu_baseline": None,
+        "parity": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
-            out["cpu_baseline"] = cpu_baseline(model_path, host[0])
+            base, ref_ids = cpu_baseline(model_path, host[0])
+            out["cpu_baseline"] = base
+            if ref_ids is not None:
+                gpu_ids = [t[0] for s in w.segments(states[0]) for t in s["tokens"]]
+                first = next((i for i, (a, b) in enumerate(zip(gpu_ids, ref_ids)) if a != b),
+                             None if len(gpu_ids) == len(ref_ids) else min(len(gpu_ids), len(ref_ids)))
+                out["parity"] = {"tokens_equal": gpu_ids == ref_ids, "clip": 0, "n_tokens": len(ref_ids),
+                                 "first_diff": first,
+                                 "against": "cpu_baseline run: the reference ggml CPU path on the same clip, "
+                                            "model and parameters"}
         except Exception as e:  # report, never hide the GPU number
             log(f"[bench] cpu baseline failed: {e}")
     if rank == 0:

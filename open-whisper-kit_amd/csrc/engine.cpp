@@ -113,6 +113,9 @@ void Engine::reserve(int slots, int cells) {
     }
     if (cells > kv_cells) {
         sync();
+        // captured decode graphs bake in the cache strides (kv_cells, cap_slots) and buffer
+        // addresses; hipMalloc may hand back the same address, so drop them on any re-layout
+        clear_graphs();
         kv_cells = cells;
         const size_t n = (size_t) hp.n_text_layer * cap_slots * kv_cells * d * 2;
         self_k_.alloc(n);
@@ -200,7 +203,7 @@ void Engine::encode(const std::vector<int> & slots, const std::vector<int> & off
     const HParams & hp = m->hp;
     const int n = (int) slots.size();
     if (n == 0) return;
-    const int T = hp.n_audio_ctx, T2 = 2 * T, d = hp.n_audio_state, H = hp.n_audio_head;
+    const int T = n_ctx(), T2 = 2 * T, d = hp.n_audio_state, H = hp.n_audio_head;
     const int Tpad = (T + 63) / 64 * 64;
     const int n_ctx_pad = (T + 255) / 256 * 256;  // GGML_PAD(n_audio_ctx, 256)
     const int n_zero_pad = n_ctx_pad - T;
@@ -217,8 +220,6 @@ void Engine::encode(const std::vector<int> & slots, const std::vector<int> & off
         e_xn_.alloc((size_t) M * d * 2);
         e_q_.alloc((size_t) M * d * 2);
         e_k_.alloc((size_t) M * d * 2);
-        e_vt_.alloc((size_t) n * H * 64 * Tpad * 2);
-        OWK_HIP_CHECK(hipMemsetAsync(e_vt_.ptr, 0, e_vt_.bytes, stream));  // padded key columns stay 0
         e_ao_.alloc((size_t) M * d * 2);
         e_h_.alloc((size_t) M * 4 * d * 2);
         e_enc_.alloc((size_t) M * d * 2);
@@ -230,6 +231,14 @@ void Engine::encode(const std::vector<int> & slots, const std::vector<int> & off
         }
     }
     e_a1_.alloc((size_t) n * T2 * kp1 * 2);
+    // transposed V [clip][head][64][Tpad]: key columns T..Tpad-1 must read as 0 (zeroed whenever
+    // the buffer or its T changes: a reduced audio_ctx re-lays it out)
+    if ((size_t) n * H * 64 * Tpad * 2 > e_vt_.bytes || vt_T_ != T) {
+        sync();
+        e_vt_.alloc(std::max(e_vt_.bytes, (size_t) n * H * 64 * Tpad * 2));
+        OWK_HIP_CHECK(hipMemsetAsync(e_vt_.ptr, 0, e_vt_.bytes, stream));
+        vt_T_ = T;
+    }
 
     std::vector<MelWindow> win(n);
     for (int i = 0; i < n; ++i) win[i] = MelWindow{mel_[slots[i]]->as<float>(), mel_len_[slots[i]], offsets[i]};
@@ -345,7 +354,7 @@ void Engine::encode(const std::vector<int> & slots, const std::vector<int> & off
 
     // cross-attention K/V for every decoder layer (whisper_build_graph_cross, ref 2272-2346)
     const float k_scale = powf(64.0f, -0.25f);
-    const size_t layer_stride = (size_t) cap_slots * T * d;
+    const size_t layer_stride = (size_t) cap_slots * hp.n_audio_ctx * d;  // capacity; slots of n_ctx() rows inside
     for (int l = 0; l < hp.n_text_layer; ++l) {
         const DecLayerW & L = m->dec[l];
         EpiParams ep;
@@ -365,17 +374,17 @@ void Engine::encode(const std::vector<int> & slots, const std::vector<int> & off
 void Engine::download_enc(int index, float * host) const {
     const HParams & hp = m->hp;
     OWK_HIP_CHECK(hipStreamSynchronize(stream));
-    const size_t n = (size_t) hp.n_audio_ctx * hp.n_audio_state;
+    const size_t n = (size_t) n_ctx() * hp.n_audio_state;
     OWK_HIP_CHECK(hipMemcpy(host, e_enc32_.as<float>() + index * n, n * 4, hipMemcpyDeviceToHost));
 }
 
 void Engine::download_cross(int slot, int layer, uint16_t * kh, uint16_t * vh) const {
     const HParams & hp = m->hp;
     OWK_HIP_CHECK(hipStreamSynchronize(stream));
-    const size_t per = (size_t) hp.n_audio_ctx * hp.n_text_state;
-    const size_t o = ((size_t) layer * cap_slots + slot) * per;
+    const int T = n_ctx(), d = hp.n_text_state, H = d / 64;
+    const size_t per = (size_t) T * d;
+    const size_t o = (size_t) layer * cap_slots * hp.n_audio_ctx * d + (size_t) slot * per;
     // device layout is head-major [head][t][64]; the caller gets the reference's [t][d]
-    const int T = hp.n_audio_ctx, d = hp.n_text_state, H = d / 64;
     std::vector<uint16_t> tk(per), tv(per);
     OWK_HIP_CHECK(hipMemcpy(tk.data(), cross_k_.as<_Float16>() + o, per * 2, hipMemcpyDeviceToHost));
     OWK_HIP_CHECK(hipMemcpy(tv.data(), cross_v_.as<_Float16>() + o, per * 2, hipMemcpyDeviceToHost));
@@ -429,7 +438,7 @@ void Engine::set_alignment_heads(const std::vector<int> & amap, int n_aheads) {
 }
 
 void Engine::download_capture(int row0, int n, std::vector<float> & out) const {
-    const int T = m->hp.n_audio_ctx;
+    const int T = n_ctx();
     if (!cap_.ptr || row0 < 0 || row0 + n > cap_rows_) throw std::runtime_error("download_capture: no such rows");
     std::vector<float> all((size_t) n_ah_ * T * cap_rows_);
     OWK_HIP_CHECK(hipMemcpyAsync(all.data(), cap_.ptr, all.size() * 4, hipMemcpyDeviceToHost, stream));
@@ -444,7 +453,7 @@ void Engine::decode(const std::vector<DecodeRow> & rows, const std::vector<int> 
     const HParams & hp = m->hp;
     const int R = (int) rows.size();
     if (R == 0) return;
-    const int d = hp.n_text_state, T = hp.n_audio_ctx;
+    const int d = hp.n_text_state, T = n_ctx();
     const int n_ctx_pad = (T + 255) / 256 * 256;
     const int nv = hp.n_vocab;
 
@@ -468,6 +477,7 @@ void Engine::decode(const std::vector<DecodeRow> & rows, const std::vector<int> 
             logits_.alloc((size_t) C * nv * 4);
         }
         dec_keys_cap_ = std::max(nk, std::max(dec_keys_cap_ * 2, 4096));
+        clear_graphs();  // staging offsets and row buffers change: no captured graph stays valid
         stage_layout(dec_rows_cap_, dec_keys_cap_);
         stg_.alloc(st_bytes_);
         d_stg_.alloc(st_bytes_);
@@ -542,7 +552,7 @@ void Engine::decode(const std::vector<DecodeRow> & rows, const std::vector<int> 
     const uint64_t key = (uint64_t) R | ((uint64_t) n_logit_rows << 20) | ((uint64_t) sh.self_oc << 40) |
                          ((uint64_t) sh.self_tl << 41) | ((uint64_t) sh.cross_oc << 42) | ((uint64_t) sh.cross_tl << 43) |
                          ((uint64_t) sh.self_sm << 44) | ((uint64_t) sh.cross_sm << 45) |
-                         ((uint64_t) sh.self_list << 46);
+                         ((uint64_t) sh.self_list << 46) | ((uint64_t) T << 48);  // T: head stride baked in
     auto it = graphs_.find(key);
     if (it == graphs_.end()) {
         if (graphs_.size() >= 64) clear_graphs();
@@ -568,7 +578,7 @@ void Engine::decode(const std::vector<DecodeRow> & rows, const std::vector<int> 
 void Engine::launch_decode(const DecShape & sh) {
     const HParams & hp = m->hp;
     const int R = sh.R, n_logit_rows = sh.n_logit;
-    const int d = hp.n_text_state, H = hp.n_text_head, T = hp.n_audio_ctx;
+    const int d = hp.n_text_state, H = hp.n_text_head, T = n_ctx();
     const int n_ctx_pad = (T + 255) / 256 * 256;
     const int nv = hp.n_vocab;
     char * dv = d_stg_.as<char>();
@@ -604,7 +614,7 @@ void Engine::launch_decode(const DecShape & sh) {
     }
     const float kq_scale = powf(64.0f, -0.25f);
     const size_t self_stride = (size_t) cap_slots * kv_cells * d;
-    const size_t cross_stride = (size_t) cap_slots * T * d;
+    const size_t cross_stride = (size_t) cap_slots * hp.n_audio_ctx * d;  // per layer (capacity)
     // R <= 32 rows: the residual matmuls (attn.out, cross_attn.out, mlp.2) emit partial tiles
     // that one fused kernel finishes together with the following LayerNorm (3 launches
     // fewer per layer); larger passes use the full-epilogue GEMMs and separate LayerNorms

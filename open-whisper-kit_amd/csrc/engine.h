@@ -88,6 +88,11 @@ public:
     // whisper_context_params.flash_attn: false selects the reference's soft_max attention
     // (encoder and decoder) -- the numerics DTW timestamps are defined with
     bool flash_attn = true;
+    // whisper_full_params.audio_ctx of the current call (state->exp_n_audio_ctx, ref whisper.cpp:921,
+    // 6986): 0 = the model's n_audio_ctx. The encoder runs over n_ctx() positions (2 * n_ctx() mel
+    // frames), cross K/V hold n_ctx() rows per slot and decoder cross-attention attends over them.
+    int audio_ctx = 0;
+    int n_ctx() const { return audio_ctx > 0 && audio_ctx < m->hp.n_audio_ctx ? audio_ctx : m->hp.n_audio_ctx; }
 
     void reserve(int slots, int cells);
 
@@ -154,6 +159,7 @@ private:
     DevBuf e_win_, e_slotmap_;
     int enc_rows_cap_ = 0;
     int last_enc_n_ = 0;
+    int vt_T_ = 0;  // n_ctx() the transposed-V buffer was zeroed for
 
     // decoder workspace
     DevBuf d_x_, d_xn_, d_q_, d_ao_, d_h_, d_xl_;

@@ -62,6 +62,9 @@ struct whisper_state {
     std::vector<owk::Segment> result_all;
     std::vector<whisper_token> prompt_past0, prompt_past1;
     int lang_id = 0;
+    // whisper_full_params.audio_ctx of the last whisper_full (ref exp_n_audio_ctx, whisper.cpp:921):
+    // the staged whisper_encode / whisper_decode calls keep using it, as in the reference
+    int exp_n_audio_ctx = 0;
     owk::Decoder decoders[owk::MAX_DECODERS];
     float no_speech_prob = 0.0f;
     std::vector<float> energy;

@@ -459,11 +459,13 @@ std::vector<whisper_vad_segment> vad_segments(const float * probs, int n_probs, 
 // processed -> original time table of the state
 bool vad_filter(whisper_context * ctx, whisper_state * state, const whisper_full_params & params, const float * samples,
                 int n_samples, std::vector<float> & filtered) {
-    (void) ctx;
     state->vad_map.clear();
     state->has_vad_segments = false;
     if (!state->vad_context) {
-        state->vad_context = whisper_vad_init_from_file_with_params(params.vad_model_path, whisper_vad_default_context_params());
+        // the pre-pass runs on the whisper context's GPU (one process per GPU: never device 0 by default)
+        whisper_vad_context_params vp = whisper_vad_default_context_params();
+        vp.gpu_device = ctx->model->device;
+        state->vad_context = whisper_vad_init_from_file_with_params(params.vad_model_path, vp);
         if (!state->vad_context) {
             log_msg(GGML_LOG_LEVEL_ERROR, "whisper_vad: failed to initialize VAD context\n");
             return false;

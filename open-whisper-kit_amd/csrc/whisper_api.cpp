@@ -439,6 +439,7 @@ int whisper_encode_with_state(struct whisper_context * ctx, struct whisper_state
     try {
         OWK_HIP_CHECK(hipSetDevice(ctx->model->device));
         Engine & e = eng_of(ctx, st);
+        e.audio_ctx = st->exp_n_audio_ctx;
         const int64_t t0 = time_us();
         e.encode({0}, {offset});
         e.sync();
@@ -461,6 +462,7 @@ int whisper_decode_with_state(struct whisper_context * ctx, struct whisper_state
     try {
         OWK_HIP_CHECK(hipSetDevice(ctx->model->device));
         Engine & e = eng_of(ctx, st);
+        e.audio_ctx = st->exp_n_audio_ctx;
         // whisper_batch_prep_legacy + seq_rm (ref 511-523, 3935-3946)
         std::vector<CallToken> toks(n_tokens);
         for (int i = 0; i < n_tokens; ++i) toks[i] = CallToken{tokens[i], n_past + i, 0, i == n_tokens - 1};
@@ -783,7 +785,10 @@ int whisper_full_parallel(struct whisper_context * ctx, struct whisper_full_para
     ns[0] = offset_samples + per;
     for (int i = 1; i < n_processors; ++i) {
         states[i] = whisper_init_state(ctx);
-        if (!states[i]) return -1;
+        if (!states[i]) {
+            for (int j = 1; j < i; ++j) whisper_free_state(states[j]);
+            return -1;
+        }
         const int start = offset_samples + i * per;
         ns[i] = (i == n_processors - 1) ? n_samples - start : per;
         ptr[i] = samples + start;
@@ -1081,7 +1086,7 @@ int owk_debug_mel(struct whisper_state * st, float * out, int cap) {
 }
 
 int owk_debug_enc(struct whisper_context * ctx, struct whisper_state * st, int index, float * out, int cap) {
-    const int n = ctx->model->hp.n_audio_ctx * ctx->model->hp.n_audio_state;
+    const int n = (st->eng ? st->eng->n_ctx() : ctx->model->hp.n_audio_ctx) * ctx->model->hp.n_audio_state;
     if (!st->eng) return -1;
     if (out) {
         if (cap < n) return -1;
@@ -1092,7 +1097,7 @@ int owk_debug_enc(struct whisper_context * ctx, struct whisper_state * st, int i
 
 int owk_debug_cross(struct whisper_context * ctx, struct whisper_state * st, int slot, int layer, uint16_t * k, uint16_t * v) {
     if (!st->eng) return -1;
-    const int n = ctx->model->hp.n_audio_ctx * ctx->model->hp.n_text_state;
+    const int n = st->eng->n_ctx() * ctx->model->hp.n_text_state;
     if (k && v) st->eng->download_cross(slot, layer, k, v);
     return n;
 }

@@ -374,11 +374,7 @@ struct Clip {
             fail(-5);
             return;
         }
-        if (p.audio_ctx != 0 && p.audio_ctx != hp().n_audio_ctx) {
-            log_msg(GGML_LOG_LEVEL_ERROR, "whisper_full_with_state: reduced audio_ctx is not supported by this engine\n");
-            fail(-5);
-            return;
-        }
+        st->exp_n_audio_ctx = p.audio_ctx;  // ref 6986 (the engine runs the batch at this n_ctx)
         prompt_init = {vocab().sot};
         if (vocab().is_multilingual()) {
             const int lid = whisper_lang_id(p.language);
@@ -774,7 +770,7 @@ struct Clip {
     // captured alignment-head attention of the DTW call: [head][n_audio_ctx][rows]
     void on_dtw(const std::vector<float> & cap, int n_ah) {
         const int n_frames = std::min(std::min(WHISPER_CHUNK_SIZE * 100, dtw_seek_delta), seek_end - seek);
-        dtw_timestamps(ctx, st, dtw_seg0, dtw_nseg, seek, n_frames, 7, cap, n_ah, hp().n_audio_ctx, (int) rows.size(),
+        dtw_timestamps(ctx, st, dtw_seg0, dtw_nseg, seek, n_frames, 7, cap, n_ah, st->exp_n_audio_ctx > 0 ? st->exp_n_audio_ctx : hp().n_audio_ctx, (int) rows.size(),
                        dtw_sot_len);
         if (p.new_segment_callback) {  // the reference's loop bounds, verbatim (ref 7750-7754)
             for (int seg = (int) st->result_all.size() - dtw_nseg; seg < dtw_nseg; seg++)
@@ -840,6 +836,13 @@ int full_batch(whisper_context * ctx, whisper_state ** states, const whisper_ful
     const int base_cells = (M.hp.n_text_ctx + 255) / 256 * 256;
     const int cells = base_cells * (n_dec_max > 1 ? n_dec_max + 2 : 1);
     eng.reserve(n_clips, std::max(cells, eng.kv_cells));
+    // audio_ctx (ref whisper.cpp:6981-6986): one encoder width per batched call
+    for (int c = 1; c < n_clips; ++c)
+        if (params_v[c].audio_ctx != params.audio_ctx) {
+            log_msg(GGML_LOG_LEVEL_ERROR, "whisper_full: clips of one batch must share audio_ctx\n");
+            return -5;
+        }
+    eng.audio_ctx = params.audio_ctx > 0 && params.audio_ctx <= M.hp.n_audio_ctx ? params.audio_ctx : 0;
 
     std::vector<Clip> clips(n_clips);
     for (int c = 0; c < n_clips; ++c) {

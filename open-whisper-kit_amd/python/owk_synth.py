@@ -19,6 +19,7 @@ from __future__ import annotations
 
 import gzip
 import hashlib
+import json
 import os
 import struct
 
@@ -315,19 +316,53 @@ def quantize_q5_0(src: str, dst: str, kind: str = "q5_0") -> str:
     return h.hexdigest()
 
 
+def _stamp_path(path: str) -> str:
+    return path + ".stamp"
+
+
+def _cached_ok(path: str) -> bool:
+    """A cache file is reused only if the stamp written after its generation completed exists
+    and records the file's current size (a file left by a killed or concurrent writer is not)."""
+    try:
+        with open(_stamp_path(path)) as f:
+            st = json.load(f)
+        return os.path.getsize(path) == st["size"]
+    except (OSError, ValueError, KeyError):
+        return False
+
+
+def _stamp(path: str, sha: str) -> None:
+    with open(_stamp_path(path) + ".tmp", "w") as f:
+        json.dump({"size": os.path.getsize(path), "sha256": sha}, f)
+    os.replace(_stamp_path(path) + ".tmp", _stamp_path(path))
+
+
+def file_sha256(path: str) -> str:
+    """SHA-256 of a model file (from its generation stamp when valid, else computed)."""
+    if _cached_ok(path):
+        with open(_stamp_path(path)) as f:
+            return json.load(f)["sha256"]
+    h = hashlib.sha256()
+    with open(path, "rb") as f:
+        for b in iter(lambda: f.read(1 << 24), b""):
+            h.update(b)
+    return h.hexdigest()
+
+
 def ensure_model(model: str, seed: int = 1234, cache_dir: str | None = None) -> str:
-    """Path to a cached synthetic model (generated on first use)."""
+    """Path to a cached synthetic model (generated on first use; regenerated when its
+    generation stamp is missing or does not match the file)."""
     cache_dir = cache_dir or os.environ.get("OWK_MODEL_CACHE", "/tmp/owk_models")
     os.makedirs(cache_dir, exist_ok=True)
-    kind = next((k for k in ("q5_0", "q8_0", "q4_0") if model.endswith("-" + k)), None)
+    kind = next((k for k in ("q5_0", "q8_0", "q4_0", "q4_1", "q5_1") if model.endswith("-" + k)), None)
     base = model[:-5] if kind else model
     path = os.path.join(cache_dir, f"synth-{base}-s{seed}.bin")
-    if not os.path.exists(path):
-        write_model(path, base, seed)
+    if not _cached_ok(path):
+        _stamp(path, write_model(path, base, seed))
     if kind:
         qpath = os.path.join(cache_dir, f"synth-{base}-{kind}-s{seed}.bin")
-        if not os.path.exists(qpath):
-            quantize_q5_0(path, qpath, kind=kind)
+        if not _cached_ok(qpath):
+            _stamp(qpath, quantize_q5_0(path, qpath, kind=kind))
         return qpath
     return path
 

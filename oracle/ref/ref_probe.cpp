@@ -32,6 +32,8 @@ struct ref_full_cfg {
     int   suppress_nst;
     float length_penalty;
     int   record_topk;      // record + truncate logits to a top-K set (see ref_record_cb)
+    int   audio_ctx;        // whisper_full_params.audio_ctx (0 = n_audio_ctx; whisper.cpp:6986)
+    int   n_processors;     // > 1: whisper_full_parallel (whisper.cpp:7801-7929)
 };
 
 // ---------------------------------------------------------------------------------
@@ -227,6 +229,7 @@ int ref_full(void * vctx, const float * pcm, int n, const ref_full_cfg * cfg) {
     p.suppress_nst     = cfg->suppress_nst != 0;
     p.length_penalty   = cfg->length_penalty;
     if (cfg->language) p.language = cfg->language;
+    p.audio_ctx        = cfg->audio_ctx;
     if (cfg->suppress_eot) p.logits_filter_callback = ref_suppress_eot_cb;
     // every golden run starts from a freshly initialised state's sampler (whisper.cpp:3470):
     // decoders[0].rng otherwise carries the draws of earlier runs on this context
@@ -241,6 +244,7 @@ int ref_full(void * vctx, const float * pcm, int n, const ref_full_cfg * cfg) {
         p.vad = true;
         p.vad_model_path = g_vad_path.c_str();
     }
+    if (cfg->n_processors > 1) return whisper_full_parallel(ctx, p, pcm, n, cfg->n_processors);
     return whisper_full(ctx, p, pcm, n);
 }
 

@@ -21,7 +21,7 @@ class RefFullCfg(C.Structure):
                 ("max_tokens", C.c_int), ("suppress_eot", C.c_int), ("token_timestamps", C.c_int),
                 ("no_context", C.c_int), ("single_segment", C.c_int), ("language", C.c_char_p),
                 ("suppress_nst", C.c_int), ("length_penalty", C.c_float),
-                ("record_topk", C.c_int)]
+                ("record_topk", C.c_int), ("audio_ctx", C.c_int), ("n_processors", C.c_int)]
 
 
 class RefTokenData(C.Structure):
@@ -136,11 +136,12 @@ class Ref:
 
     def full(self, pcm, strategy=0, n_threads=8, best_of=5, beam_size=5, temperature=0.0, temperature_inc=0.2,
              no_timestamps=False, max_tokens=0, suppress_eot=False, token_timestamps=False, no_context=True,
-             single_segment=False, language="en", suppress_nst=False, length_penalty=-1.0, record_topk=False):
+             single_segment=False, language="en", suppress_nst=False, length_penalty=-1.0, record_topk=False,
+             audio_ctx=0, n_processors=1):
         cfg = RefFullCfg(strategy, n_threads, best_of, beam_size, temperature, temperature_inc, int(no_timestamps),
                          max_tokens, int(suppress_eot), int(token_timestamps), int(no_context), int(single_segment),
                          language.encode() if language else None, int(suppress_nst), length_penalty,
-                         int(record_topk))
+                         int(record_topk), int(audio_ctx), int(n_processors))
         pcm = np.ascontiguousarray(pcm, np.float32)
         ret = self.L.ref_full(self.ctx, fptr(pcm), len(pcm), C.byref(cfg))
         return ret, self.segments(dtw=self.dtw)

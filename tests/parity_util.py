@@ -1,0 +1,156 @@
+"""Shared GPU-vs-reference comparison rules (test infrastructure).
+
+Token-level comparison of whisper_full results (`compare_segments`) and the measured logit error
+that bounds a legitimate numerical near-tie (`LogitError`).
+
+Near-ties. The engine's logits differ from the reference's by re-associated f32 sums (bounded by
+the measured error eps of the same model and clip: prefill + teacher-forced step-1 logits against
+the reference's, `LogitError.of`). When the two runs first pick different tokens g (GPU) and r
+(reference), r >= g in the reference's logits and g >= r in the GPU's, so the two tokens' logits
+are within 2 eps of each other; their log-probabilities (each run's own normaliser, also within
+eps) within 3 eps. A divergence is accepted only if |logprob_g - logprob_r| <= TIE_FACTOR * eps
+(4 eps: one eps of margin for the error growing over later decode steps); everything decided
+before it must match exactly and every case must compare a minimum number of tokens.
+"""
+import ctypes as C
+
+import numpy as np
+
+LOGIT_RTOL = 1e-3      # logits |diff| <= LOGIT_RTOL * max|logit| (north star: 1e-3)
+TIE_FACTOR = 4.0       # near-tie threshold = TIE_FACTOR * measured max |logit diff|
+MIN_COMPARED = 16      # every case compares at least min(MIN_COMPARED, reference tokens) tokens
+
+
+def flat_tokens(segs):
+    return [(si, t) for si, s in enumerate(segs) for t in s["tokens"]]
+
+
+def compare_segments(got, want, key, tie, exact=False, p_atol=2e-3, min_compared=MIN_COMPARED, log=print):
+    """Token ids, segment bounds, text, token timestamps identical to the reference's `want`.
+
+    Compared up to the first step where the runs pick different tokens whose log-probabilities
+    are within `tie` (exact=True: no divergence allowed). Returns the number of tokens compared
+    identical; asserts it is at least min(min_compared, reference tokens)."""
+    fg, fw = flat_tokens(got), flat_tokens(want)
+    n_cmp, margin = len(fw), None
+    for i, ((sg, g), (sw, r)) in enumerate(zip(fg, fw)):
+        if g[0] != r[0]:
+            margin = abs(g[3] - r[3])
+            assert not exact and margin <= tie, (
+                f"{key}: token {i} is {g[0]} vs reference {r[0]} (logprob {g[3]:.5f} vs {r[3]:.5f}, "
+                f"margin {margin:.2e} > near-tie bound {tie:.2e})")
+            n_cmp = i
+            n_done = min(sg, sw)  # finished segments before the divergence must agree completely
+            got, want = got[:n_done], want[:n_done]
+            break
+    else:
+        assert len(fg) == len(fw), f"{key}: {len(fg)} tokens vs reference {len(fw)}"
+    assert len(got) == len(want), f"{key}: {len(got)} segments vs reference {len(want)}"
+    for g, r in zip(got, want):
+        assert [t[0] for t in g["tokens"]] == [t[0] for t in r["tokens"]], f"{key}: token ids differ"
+        assert (g["t0"], g["t1"]) == (r["t0"], r["t1"]), f"{key}: segment bounds differ"
+        assert g["text"] == r["text"]
+        gp = np.array([t[2] for t in g["tokens"]])
+        rp = np.array([t[2] for t in r["tokens"]])
+        np.testing.assert_allclose(gp, rp, atol=p_atol)
+        assert [(t[6], t[7]) for t in g["tokens"]] == [(t[6], t[7]) for t in r["tokens"]], \
+            f"{key}: token timestamps differ"
+    note = "" if margin is None else f" (parted at a near-tie, margin {margin:.2e} <= {tie:.2e})"
+    log(f"[parity] {key}: {n_cmp}/{len(fw)} tokens compared identical{note}")
+    assert n_cmp >= min(min_compared, len(fw)), \
+        f"{key}: only {n_cmp} of {len(fw)} tokens compared before a near-tie (minimum {min_compared})"
+    return n_cmp
+
+
+class LogitError:
+    """Measured max |logit - reference| of a (context, model, clip): prefill + teacher-forced
+    step-1 top-64 logits of the golden set, through the staged C API on a fresh state."""
+
+    _cache = {}
+
+    @classmethod
+    def of(cls, w, meta, arr, key):
+        ck = (id(w), key)
+        if ck not in cls._cache:
+            cls._cache[ck] = cls.measure(w, meta, arr, key)
+        return cls._cache[ck]
+
+    @staticmethod
+    def measure(w, meta, arr, key, pcm=None):
+        import owk
+
+        L = w.L
+        st = w.new_state()
+        if pcm is None:
+            raise ValueError("pcm required on first measurement")
+        assert L.whisper_pcm_to_mel_with_state(w.ctx, st, owk.fptr(pcm), len(pcm), 1) == 0
+        assert L.whisper_encode_with_state(w.ctx, st, 0, 1) == 0
+        prompt = meta["results"][key + "/prefill_prompt"]
+        toks = (C.c_int32 * len(prompt))(*prompt)
+        assert L.whisper_decode_with_state(w.ctx, st, toks, len(prompt), 0, 1) == 0
+        lg = np.ctypeslib.as_array(L.whisper_get_logits_from_state(st), shape=(len(prompt) * w.n_vocab,))
+        lg = lg[(len(prompt) - 1) * w.n_vocab:].copy()
+        e1 = float(np.abs(lg[arr[key + "/prefill_top_idx"]] - arr[key + "/prefill_top_val"]).max())
+        one = (C.c_int32 * 1)(meta["results"][key + "/step1_token"])
+        assert L.whisper_decode_with_state(w.ctx, st, one, 1, len(prompt), 1) == 0
+        lg2 = np.ctypeslib.as_array(L.whisper_get_logits_from_state(st), shape=(w.n_vocab,)).copy()
+        e2 = float(np.abs(lg2[arr[key + "/step1_top_idx"]] - arr[key + "/step1_top_val"]).max())
+        L.whisper_free_state(st)
+        return max(e1, e2)
+
+    @classmethod
+    def tie(cls, w, meta, arr, key, pcm):
+        ck = (id(w), key)
+        if ck not in cls._cache:
+            cls._cache[ck] = cls.measure(w, meta, arr, key, pcm)
+        return TIE_FACTOR * cls._cache[ck]
+
+
+class Forcer:
+    """logits_filter_callback that teacher-forces a greedy decode onto the reference's token
+    sequence: `windows` is one token list per 30 s window (each followed by <|endoftext|>); every
+    logit but the forced token's is set to -inf (whisper.cpp:6254 is where the reference's own
+    callback point sits). A call with no decoded tokens yet starts the next window (greedy,
+    temperature_inc = 0: one call per step). Used to compare what is computed FROM a token sequence
+    (DTW timestamps) independently of a near-tie parting of the free runs."""
+
+    def __init__(self, windows, eot, n_vocab, token_data_type):
+        self.windows, self.eot, self.n_vocab = [list(w) for w in windows], eot, n_vocab
+        self.calls = 0
+        self.window = -1
+        TD = C.POINTER(token_data_type)
+        proto = C.CFUNCTYPE(None, C.c_void_p, C.c_void_p, TD, C.c_int, C.POINTER(C.c_float), C.c_void_p)
+        self.cfunc = proto(self._cb)
+
+    def _cb(self, ctx, state, tokens, n_tokens, logits, user):
+        self.calls += 1
+        if n_tokens == 0:
+            self.window += 1
+        lg = np.ctypeslib.as_array(logits, shape=(self.n_vocab,))
+        win = self.windows[self.window] if 0 <= self.window < len(self.windows) else []
+        t = win[n_tokens] if n_tokens < len(win) else self.eot
+        v = float(lg[t]) if np.isfinite(lg[t]) else 0.0
+        lg[:] = -np.inf
+        lg[t] = v
+
+
+def check_cross_rows(w, st, arr, key, layer, name, n_rows=16):
+    """The engine's cross-attention K/V cache rows 0..n_rows-1 of `layer` (slot 0, [t][d] f16 via
+    owk_debug_cross) against the reference's kv_cross rows (whisper_build_graph_cross,
+    whisper.cpp:2272-2346: K pre-scaled by 64^-0.25, V + bias). Same bar as the encoder output
+    they are computed from (|diff| max < 2e-2 and mean < 1e-3, relative to max|ref| when > 1)."""
+    L = w.L
+    n = L.owk_debug_cross(w.ctx, st, 0, layer, None, None)
+    k = np.zeros(n, np.uint16)
+    v = np.zeros(n, np.uint16)
+    P = lambda a: a.ctypes.data_as(C.POINTER(C.c_uint16))
+    assert L.owk_debug_cross(w.ctx, st, 0, layer, P(k), P(v)) == n
+    out = {}
+    for t, got in (("k", k), ("v", v)):
+        ref = arr[f"{key}/cross_{t}_{name}"].view(np.float16).astype(np.float32)
+        g = got[: ref.size].view(np.float16).astype(np.float32)
+        scale = max(1.0, float(np.abs(ref).max()))
+        err = np.abs(g - ref)
+        assert err.max() < 2e-2 * scale and err.mean() < 1e-3 * scale, (key, t, name, err.max(), err.mean(), scale)
+        out[t] = float(err.max())
+    return out

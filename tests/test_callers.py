@@ -1,0 +1,121 @@
+"""The reference's own C/C++ callers link UNCHANGED against include/ and our libraries.
+
+CPU: ref examples/cli/cli.cpp, examples/bench/bench.cpp (+ common.cpp, common-whisper.cpp,
+grammar-parser.cpp; SURVEY 8(b) build note), streaming-sortformer/src/sortformer-cli.cpp and
+test-streaming-api.cpp compile from /root/reference against include/, link libwhisper.so /
+libsortformer.so, and exit with the reference's init-error codes on a missing model
+(ref cli.cpp:1040-1043 -> 3, bench.cpp:76-79 -> 2, sortformer-cli.cpp:237-240 -> 1,
+test-streaming-api.cpp:45-48 -> 1). Skipped only where /root/reference is absent (GPU box).
+
+GPU: BASELINE configs[0] -- the unchanged whisper-cli (built by `make callers`, shipped in
+open-whisper-kit_amd/lib/callers/) transcribes samples/jfk.wav with the synthetic tiny.en, CLI
+defaults (beam 5 + best-of 5, temperature fallback) and `-nf`; its full JSON output (segments,
+offsets, text, token ids, token t0/t1) equals the reference whisper-cli's
+(tests/golden/make_golden_cli.py), token p within 1e-3. whisper-bench, sortformer-diarize and
+test-streaming-api run to completion on the GPU.
+"""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
+REF = "/root/reference"
+LIB = os.path.join(ROOT, "open-whisper-kit_amd", "lib")
+CALLERS = os.path.join(LIB, "callers")
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+sys.path.insert(0, GOLDEN)
+
+EXCOMMON = [f"{REF}/examples/common.cpp", f"{REF}/examples/common-whisper.cpp", f"{REF}/examples/grammar-parser.cpp"]
+PROGRAMS = {
+    # name: (sources, library, expected exit code on a missing model, argv)
+    "whisper-cli": ([f"{REF}/examples/cli/cli.cpp"] + EXCOMMON, "whisper", 3,
+                    ["-m", "/nonexistent", "-f", os.path.join(GOLDEN, "jfk.wav")]),
+    "whisper-bench": ([f"{REF}/examples/bench/bench.cpp"] + EXCOMMON, "whisper", 2, ["-m", "/nonexistent"]),
+    "sortformer-diarize": ([f"{REF}/streaming-sortformer/src/sortformer-cli.cpp"], "sortformer", 1,
+                           ["-m", "/nonexistent", "-f", "x.wav"]),
+    "test-streaming-api": ([f"{REF}/streaming-sortformer/src/test-streaming-api.cpp"], "sortformer", 1,
+                           ["-m", "/nonexistent", "-f", "x.wav"]),
+}
+
+
+@pytest.mark.skipif(not os.path.isdir(f"{REF}/examples/cli"), reason="reference sources not present")
+def test_reference_callers_build_unchanged(tmp_path):
+    procs = {}
+    for name, (srcs, lib, _, _) in PROGRAMS.items():
+        exe = tmp_path / name
+        cmd = ["g++", "-O0", "-std=c++17", "-w", f"-I{ROOT}/include", f"-I{REF}/examples", *srcs, "-o", str(exe),
+               f"-L{LIB}", f"-l{lib}", f"-Wl,-rpath,{LIB}"]
+        procs[name] = subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    for name, p in procs.items():
+        out, _ = p.communicate(timeout=300)
+        assert p.returncode == 0, f"{name} does not build against include/:\n{out[-3000:]}"
+    for name, (_, _, want, argv) in PROGRAMS.items():
+        r = subprocess.run([str(tmp_path / name), *argv], capture_output=True, text=True, timeout=60, cwd=tmp_path)
+        assert r.returncode == want, (name, r.returncode, r.stderr[-2000:])
+
+
+def _caller(name):
+    exe = os.path.join(CALLERS, name)
+    if not os.path.exists(exe):
+        raise RuntimeError(f"{exe} missing: run `make callers` (needs /root/reference) before shipping the tree")
+    return exe
+
+
+def _cli_json(model_path, extra, tmp_path):
+    from make_golden_cli import run_cli
+
+    return run_cli(_caller("whisper-cli"), model_path, os.path.join(GOLDEN, "jfk.wav"), extra, str(tmp_path))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["default", "nofallback"])
+def test_whisper_cli_configs0(case, model_path, tmp_path):
+    g = json.load(open(os.path.join(GOLDEN, "cli_golden.json")))
+    assert g["model"] == "tiny.en"
+    path = model_path("tiny.en")
+    want = g["cases"][case]
+    code, doc = _cli_json(path, want["args"], tmp_path)
+    assert code == want["exit"] and doc is not None
+    got_segs, ref_segs = doc["transcription"], want["json"]["transcription"]
+    n_tok = sum(len(s["tokens"]) for s in ref_segs)
+    print(f"[cli {case}] {len(ref_segs)} segments, {n_tok} tokens compared")
+    assert n_tok > 0
+    assert [(s["offsets"], s["text"]) for s in got_segs] == [(s["offsets"], s["text"]) for s in ref_segs]
+    for gs, rs in zip(got_segs, ref_segs):
+        assert [(t["id"], t["text"], t["offsets"]) for t in gs["tokens"]] == \
+               [(t["id"], t["text"], t["offsets"]) for t in rs["tokens"]]
+        assert max(abs(a["p"] - b["p"]) for a, b in zip(gs["tokens"], rs["tokens"])) <= 1e-3
+    assert doc["result"] == want["json"]["result"]
+
+
+@pytest.mark.gpu
+def test_whisper_bench_runs(model_path):
+    r = subprocess.run([_caller("whisper-bench"), "-m", model_path("tiny.en"), "-w", "0", "-t", "1"],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "encode time" in r.stderr
+
+
+@pytest.mark.gpu
+def test_sortformer_callers_run(tmp_path):
+    import json as _json
+
+    import sortformer_synth as SS
+
+    sfm = _json.load(open(os.path.join(GOLDEN, "sf_golden.json")))
+    cache = os.environ.get("OWK_MODEL_CACHE", "/tmp/owk_models")
+    gguf = os.path.join(cache, f"synth-sortformer-s{sfm['seed']}.gguf")
+    assert SS.write_model(gguf, sfm["seed"]) == sfm["sha256"]
+    wav = os.path.join(GOLDEN, "sf_test60.wav")
+    rttm = tmp_path / "out.rttm"
+    r = subprocess.run([_caller("sortformer-diarize"), "-m", gguf, "-f", wav, "-o", str(rttm)],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = rttm.read_text().splitlines()
+    assert lines and all(ln.startswith("SPEAKER ") for ln in lines)
+    r = subprocess.run([_caller("test-streaming-api"), "-m", gguf, "-f", wav, "-o", str(tmp_path / "s.rttm"),
+                        "--preset", "2s"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]

@@ -18,12 +18,12 @@ import numpy as np
 import pytest
 
 import owk
+from parity_util import LOGIT_RTOL, MIN_COMPARED, LogitError, check_cross_rows, compare_segments
 from recording import Injector
 
 pytestmark = pytest.mark.gpu
 
 MODELS = ["tiny.en", "base.en", "tiny", "l3-mini"]
-LOGIT_RTOL = 1e-3  # of the largest |logit| in the compared set
 
 
 @pytest.fixture(scope="module")
@@ -95,6 +95,8 @@ def test_encoder_and_prefill_logits(lib, golden, model_path, clips, model, clip)
     assert err.max() < 2e-2 and err.mean() < 1e-3, (err.max(), err.mean())
     rs = np.stack([enc.sum(axis=1, dtype=np.float64), (enc.astype(np.float64) ** 2).sum(axis=1)], axis=1)
     np.testing.assert_allclose(rs, arr[key + "/enc_rowstats"], rtol=5e-3, atol=0.5)
+    # layer-0 cross-attention K/V rows as the decoder will read them
+    check_cross_rows(w, st, arr, key, 0, "l0")
 
     prompt = meta["results"][key + "/prefill_prompt"]
     toks = (C.c_int32 * len(prompt))(*prompt)
@@ -137,45 +139,19 @@ CONFIGS = {
 
 
 STOCHASTIC = ("greedy_fallback", "beam5", "sampled")  # see tests/golden/recording.py
-TIE_LOGIT = 0.025  # two tokens closer than this in log-probability are a numerical near-tie
 
 
-def _flat(segs):
-    return [(si, t) for si, s in enumerate(segs) for t in s["tokens"]]
+def _compare(got, want, key, exact=False, p_atol=2e-3, tie=None, min_compared=MIN_COMPARED):
+    """parity_util.compare_segments with the near-tie bound given explicitly (tie) or, for
+    injected configs, none (exact=True)."""
+    return compare_segments(got, want, key, tie=0.0 if tie is None else tie, exact=exact, p_atol=p_atol,
+                            min_compared=min_compared)
 
 
-def _compare(got, want, key, exact=False, p_atol=2e-3, tie=TIE_LOGIT):
-    """Token ids, segment bounds, text and token timestamps identical to the reference.
-
-    Deterministic configs (exact=False) are compared up to the first step where the two
-    runs pick different tokens whose log-probabilities are within TIE_LOGIT of each
-    other: the f32 reordering noise of the logits (<= 1e-3 x max|logit|) cannot order
-    such a pair, and the trajectories legitimately part there. Any other difference
-    fails. Injected stochastic configs (exact=True) must match completely.
-    """
-    fg, fw = _flat(got), _flat(want)
-    for i, ((sg, g), (sw, r)) in enumerate(zip(fg, fw)):
-        if g[0] != r[0]:
-            gap = abs(g[3] - r[3])
-            assert not exact and gap < tie, (
-                f"{key}: token {i} is {g[0]} vs reference {r[0]} (logprob {g[3]:.5f} vs {r[3]:.5f})")
-            # finished segments before the divergence must agree completely
-            n_done = min(sg, sw)
-            got, want = got[:n_done], want[:n_done]
-            break
-    else:
-        assert len(fg) == len(fw), f"{key}: {len(fg)} tokens vs reference {len(fw)}"
-    assert len(got) == len(want), f"{key}: {len(got)} segments vs reference {len(want)}"
-    for g, r in zip(got, want):
-        assert [t[0] for t in g["tokens"]] == [t[0] for t in r["tokens"]], f"{key}: token ids differ"
-        assert (g["t0"], g["t1"]) == (r["t0"], r["t1"]), f"{key}: segment bounds differ"
-        assert g["text"] == r["text"]
-        gp = np.array([t[2] for t in g["tokens"]])
-        rp = np.array([t[2] for t in r["tokens"]])
-        np.testing.assert_allclose(gp, rp, atol=p_atol)
-        gt = [(t[6], t[7]) for t in g["tokens"]]
-        rt = [(t[6], t[7]) for t in r["tokens"]]
-        assert gt == rt, f"{key}: token timestamps differ"
+def _tie(w, golden, model, clip, clips):
+    """Near-tie bound of (model, clip): TIE_FACTOR x the measured max logit error (parity_util)."""
+    meta, arr = golden
+    return LogitError.tie(w, meta, arr, f"{model}/{clip}", clips[clip])
 
 
 @pytest.mark.parametrize("model", MODELS)
@@ -207,7 +183,31 @@ def test_whisper_full(lib, golden, model_path, clips, model, clip, cfg):
         assert inj.calls > 0 and inj.misses == 0, (inj.calls, inj.misses)
         _compare(w.segments(st), want["segments"], key, exact=True, p_atol=1e-5)
     else:
-        _compare(w.segments(st), want["segments"], key)
+        _compare(w.segments(st), want["segments"], key, tie=_tie(w, golden, model, clip, clips))
+
+
+def test_greedy_then_beam_on_one_state(lib, golden, model_path, clips):
+    """One state decodes greedy, then beam search (its KV cache grows to n_decoders + 2 sets of
+    cells, ref whisper.cpp:7157-7175), then greedy again: captured decode graphs must be rebuilt
+    on every re-layout (never replayed with stale strides) and each result equals the reference."""
+    meta, arr = golden
+    model, clip = "tiny.en", "jfk"
+    w = whisper(model_path, model)
+    st = w.new_state()
+    tie = _tie(w, golden, model, clip, clips)
+    for cfg in ("greedy", "beam5", "greedy"):
+        key = f"{model}/{clip}/full/{cfg}"
+        p, _ = _cfg_params(w, CONFIGS[cfg])
+        inj = None
+        if cfg in STOCHASTIC:
+            inj = Injector(arr, key, w.n_vocab, owk.TokenData)
+            p.logits_filter_callback = C.cast(inj.cfunc, C.c_void_p)
+        assert w.full(st, clips[clip], p) == meta["results"][key]["ret"]
+        if inj is not None:
+            assert inj.calls > 0 and inj.misses == 0
+            _compare(w.segments(st), meta["results"][key]["segments"], f"state-reuse/{cfg}", exact=True, p_atol=1e-5)
+        else:
+            _compare(w.segments(st), meta["results"][key]["segments"], f"state-reuse/{cfg}", tie=tie)
 
 
 def test_batch_matches_single(lib, golden, model_path, clips):
@@ -220,7 +220,8 @@ def test_batch_matches_single(lib, golden, model_path, clips):
     p, _ = _cfg_params(w, CONFIGS["greedy"])
     assert w.full_batch(states, [clips[n] for n in names], p) == 0
     for st, n in zip(states, names):
-        _compare(w.segments(st), meta["results"][f"{model}/{n}/full/greedy"]["segments"], f"batch/{n}")
+        _compare(w.segments(st), meta["results"][f"{model}/{n}/full/greedy"]["segments"], f"batch/{n}",
+                 tie=_tie(w, golden, model, n, clips))
 
 
 def test_auto_language(lib, golden, model_path, clips):
@@ -231,4 +232,5 @@ def test_auto_language(lib, golden, model_path, clips):
         p = w.params(0, language="auto", temperature_inc=0.0)
         assert w.full(st, clips["jfk"], p) == 0
         assert lib.whisper_full_lang_id_from_state(st) == meta["results"][f"{model}/jfk/lang_detect"][0]
-        _compare(w.segments(st), meta["results"][f"{model}/jfk/full/auto_lang"]["segments"], f"{model}/auto")
+        _compare(w.segments(st), meta["results"][f"{model}/jfk/full/auto_lang"]["segments"], f"{model}/auto",
+                 tie=_tie(w, golden, model, "jfk", clips))

@@ -148,7 +148,9 @@ def test_q5_whisper_full(q5g, clips, model, clip, cfg):
         rp = np.array([t[2] for t in r[:agree]])
         np.testing.assert_allclose(gp, rp, atol=fl)
     else:
-        _compare(got, want["segments"], f"{meta['kind']}/{model}/{clip}/{cfg}", p_atol=fl, tie=fl)
+        # quantized: the reference itself parts from its own trajectory after `floor` tokens, so
+        # no minimum count beyond the floor (checked above) applies here
+        _compare(got, want["segments"], f"{meta['kind']}/{model}/{clip}/{cfg}", p_atol=fl, tie=fl, min_compared=0)
 
 
 @pytest.mark.gpu
