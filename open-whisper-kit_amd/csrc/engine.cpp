@@ -167,10 +167,13 @@ void Engine::compute_mel(const std::vector<int> & slots, const std::vector<const
 }
 
 void Engine::set_mel(int slot, const float * host, int n_len, int n_mel) {
+    // n_len = 0 is legal (ref whisper_set_mel_with_state copies nothing; the encoder window is
+    // then all zeros -- examples/bench/bench.cpp:84 does exactly this)
+    if (n_len < 0 || (n_len > 0 && !host)) throw std::runtime_error("set_mel: no data");
     DevBuf * b = mel_[slot];
-    b->alloc((size_t) n_mel * n_len * 4);
+    b->alloc(std::max<size_t>((size_t) n_mel * n_len * 4, 4));
     mel_len_[slot] = n_len;
-    OWK_HIP_CHECK(hipMemcpy(b->ptr, host, (size_t) n_mel * n_len * 4, hipMemcpyHostToDevice));
+    if (n_len > 0) OWK_HIP_CHECK(hipMemcpy(b->ptr, host, (size_t) n_mel * n_len * 4, hipMemcpyHostToDevice));
 }
 
 void Engine::download_mel(int slot, float * host) const {
@@ -424,7 +427,7 @@ uint64_t Engine::buffers_signature() const {
     uint64_t h = 1469598103934665603ull;
     for (const void * p : {d_x_.ptr, d_xn_.ptr, d_q_.ptr, d_ao_.ptr, d_h_.ptr, d_xl_.ptr, logits_.ptr, d_stg_.ptr,
                            q8a_.ptr, q8d_.ptr, d_xn32_.ptr, d_ao32_.ptr, d_xl32_.ptr,
-                           self_k_.ptr, self_v_.ptr, cross_k_.ptr, cross_v_.ptr, gws_part_.ptr})
+                           self_k_.ptr, self_v_.ptr, cross_k_.ptr, cross_v_.ptr, gws_part_.ptr, ln_stats_.ptr})
         h = (h ^ (uint64_t) (uintptr_t) p) * 1099511628211ull;
     return h;
 }
@@ -465,6 +468,7 @@ void Engine::decode(const std::vector<DecodeRow> & rows, const std::vector<int> 
             const int C = dec_rows_cap_;
             d_x_.alloc((size_t) C * d * 4);
             d_xn_.alloc((size_t) C * d * 2);
+            ln_stats_.alloc((size_t) (d / 16) * std::min(C, 32) * 16);
             d_q_.alloc((size_t) C * d * 2);
             d_ao_.alloc((size_t) C * d * 2);
             d_h_.alloc((size_t) C * 4 * d * 2);
@@ -615,18 +619,37 @@ void Engine::launch_decode(const DecShape & sh) {
     const float kq_scale = powf(64.0f, -0.25f);
     const size_t self_stride = (size_t) cap_slots * kv_cells * d;
     const size_t cross_stride = (size_t) cap_slots * hp.n_audio_ctx * d;  // per layer (capacity)
-    // R <= 32 rows: the residual matmuls (attn.out, cross_attn.out, mlp.2) emit partial tiles
-    // that one fused kernel finishes together with the following LayerNorm (3 launches
-    // fewer per layer); larger passes use the full-epilogue GEMMs and separate LayerNorms
+    // R <= 32 rows (F16 weights): no LayerNorm launches inside the decoder. The residual matmuls
+    // (attn.out, cross_attn.out, mlp.2) add bias + residual in their epilogue and leave per
+    // (16-column tile, row) statistics of the updated row; the next matmul (self Q/K/V, cross Q,
+    // mlp.0 -- every LayerNorm of the decoder feeds exactly one) normalises its A operand from them
+    // (AlnParams). Larger passes use the full-epilogue GEMMs and separate LayerNorms.
     const bool fused = R <= 32 && !q5;
-    float * part = gws_.partial;
-    auto resid_ln = [&](const _Float16 * A, const _Float16 * W, const _Float16 * Wt, int K, const float * bias,
-                        const float * lnw, const float * lnb) {
+    double * lnst = (double *) ln_stats_.ptr;
+    auto resid_stats = [&](const _Float16 * A, const _Float16 * Wt, int K, const float * bias) {
         EpiParams ep;
-        G("part", EPI_PARTIAL, d, K, A, nullptr, W, Wt, Q5W(), ep, R);
-        ProfScope ps(prof, stream, "layernorm");
-        resid_layernorm(stream, R, d, gemm_partial_splits(K), part, bias, d_x_.as<float>(), lnw, lnb, hp.eps,
-                        d_xn_.as<_Float16>(), d);
+        ep.bias = bias;
+        ep.resid = d_x_.as<float>();
+        ep.out32 = d_x_.as<float>();
+        ep.ldo = d;
+        ep.stats = lnst;
+        ProfScope ps(prof, stream, "gemm_dec", 2.0 * R * (double) d * K, 2.0 * ((double) R * K + (double) d * K));
+        gemm(stream, EPI_RESID_STATS, R, d, K, A, K, nullptr, K, ep, &gws_, Wt);
+    };
+    auto aln_of = [&](const float * w, const float * b) {
+        AlnParams a;
+        a.x = d_x_.as<float>();
+        a.ldx = d;
+        a.stats = lnst;
+        a.ntiles = d / 16;
+        a.w = w;
+        a.b = b;
+        a.eps = hp.eps;
+        return a;
+    };
+    auto G_ln = [&](int mode, int N, const _Float16 * Wt, const EpiParams & ep, const AlnParams & aln) {
+        ProfScope ps(prof, stream, "gemm_dec", 2.0 * R * (double) N * d, 2.0 * ((double) R * d + (double) N * d));
+        gemm_rows_ln(stream, mode, R, N, d, aln, Wt, ep, &gws_);
     };
     auto resid_full = [&](const _Float16 * A, const float * A32, const _Float16 * W, const _Float16 * Wt,
                           const Q5W & q, int K, const float * bias, bool a_q8 = false) {
@@ -646,6 +669,7 @@ void Engine::launch_decode(const DecShape & sh) {
         const DecLayerW & L = m->dec[l];
         _Float16 * Kl = self_k_.as<_Float16>() + l * self_stride;
         _Float16 * Vl = self_v_.as<_Float16>() + l * self_stride;
+        // layer 0 of a fused pass: the embeddings have no statistics yet -> one LayerNorm launch
         if (!fused || l == 0) ln(L.attn_ln_w, L.attn_ln_b);
         {
             EpiParams ep;
@@ -659,7 +683,8 @@ void Engine::launch_decode(const DecShape & sh) {
             ep.d = d;
             ep.row_off = d_rowoff;
             ep.Tpad = kv_cells * 64;
-            G("qkv", EPI_QKV_DEC, 3 * d, d, d_xn_.as<_Float16>(), nullptr, L.w_qkv, L.t_qkv, L.q_qkv, ep, R, q5);
+            if (fused && l > 0) G_ln(EPI_QKV_DEC, 3 * d, L.t_qkv, ep, aln_of(L.attn_ln_w, L.attn_ln_b));
+            else G("qkv", EPI_QKV_DEC, 3 * d, d, d_xn_.as<_Float16>(), nullptr, L.w_qkv, L.t_qkv, L.q_qkv, ep, R, q5);
         }
         {
             ProfScope ps(prof, stream, "attn_self");
@@ -673,7 +698,7 @@ void Engine::launch_decode(const DecShape & sh) {
                                      d_ao_.as<_Float16>(), d, nullptr, nullptr, 0, ao32);
         }
         if (fused) {
-            resid_ln(d_ao_.as<_Float16>(), L.w_o, L.t_o, d, L.b_o, L.cross_ln_w, L.cross_ln_b);
+            resid_stats(d_ao_.as<_Float16>(), L.t_o, d, L.b_o);
         } else {
             resid_full(d_ao_.as<_Float16>(), ao32, L.w_o, L.t_o, L.q_o, d, L.b_o, fq_self);
             ln(L.cross_ln_w, L.cross_ln_b);
@@ -683,7 +708,8 @@ void Engine::launch_decode(const DecShape & sh) {
             ep.bias = L.cb_q;
             ep.out16 = d_q_.as<_Float16>();
             ep.ldo = d;
-            G("cq", EPI_F16, d, d, d_xn_.as<_Float16>(), nullptr, L.cw_q, L.t_cq, L.q_cq, ep, R, q5);
+            if (fused) G_ln(EPI_F16, d, L.t_cq, ep, aln_of(L.cross_ln_w, L.cross_ln_b));
+            else G("cq", EPI_F16, d, d, d_xn_.as<_Float16>(), nullptr, L.cw_q, L.t_cq, L.q_cq, ep, R, q5);
         }
         {
             // bytes: cross K and V of each row's clip (the HBM-bound part of a decode step)
@@ -699,7 +725,7 @@ void Engine::launch_decode(const DecShape & sh) {
                                      sh.capture ? cap_.as<float>() : nullptr, R, ao32);
         }
         if (fused) {
-            resid_ln(d_ao_.as<_Float16>(), L.cw_o, L.t_co, d, L.cb_o, L.mlp_ln_w, L.mlp_ln_b);
+            resid_stats(d_ao_.as<_Float16>(), L.t_co, d, L.cb_o);
         } else {
             resid_full(d_ao_.as<_Float16>(), ao32, L.cw_o, L.t_co, L.q_co, d, L.cb_o, fq_cross);
             ln(L.mlp_ln_w, L.mlp_ln_b);
@@ -710,16 +736,11 @@ void Engine::launch_decode(const DecShape & sh) {
             ep.gelu_tab = m->gelu_tab;
             ep.out16 = d_h_.as<_Float16>();
             ep.ldo = 4 * d;
-            G("mlp0", EPI_GELU_F16, 4 * d, d, d_xn_.as<_Float16>(), nullptr, L.w_mlp0, L.t_mlp0, L.q_mlp0, ep, R, q5);
+            if (fused) G_ln(EPI_GELU_F16, 4 * d, L.t_mlp0, ep, aln_of(L.mlp_ln_w, L.mlp_ln_b));
+            else G("mlp0", EPI_GELU_F16, 4 * d, d, d_xn_.as<_Float16>(), nullptr, L.w_mlp0, L.t_mlp0, L.q_mlp0, ep, R, q5);
         }
-        if (fused) {
-            const bool last = l + 1 == hp.n_text_layer;
-            const DecLayerW * nx = last ? nullptr : &m->dec[l + 1];
-            resid_ln(d_h_.as<_Float16>(), L.w_mlp1, L.t_mlp1, 4 * d, L.b_mlp1, nx ? nx->attn_ln_w : nullptr,
-                     nx ? nx->attn_ln_b : nullptr);
-        } else {
-            resid_full(d_h_.as<_Float16>(), nullptr, L.w_mlp1, L.t_mlp1, L.q_mlp1, 4 * d, L.b_mlp1);
-        }
+        if (fused) resid_stats(d_h_.as<_Float16>(), L.t_mlp1, 4 * d, L.b_mlp1);
+        else resid_full(d_h_.as<_Float16>(), nullptr, L.w_mlp1, L.t_mlp1, L.q_mlp1, 4 * d, L.b_mlp1);
     }
     if (n_logit_rows > 0) {
         {

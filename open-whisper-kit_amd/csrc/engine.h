@@ -187,6 +187,7 @@ private:
 
     DevBuf mel_jobs_, pcm_tmp_;
     DevBuf gws_part_;  // split-K workspace of the decode-row GEMMs
+    DevBuf ln_stats_;  // [d/16][rows] {sum, M2} of the residual GEMMs (EPI_RESID_STATS) for the next LayerNorm
     GemmWs gws_;
 };
 

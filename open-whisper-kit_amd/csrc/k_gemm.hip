@@ -101,6 +101,10 @@ __device__ __forceinline__ void epi_store(const EpiParams & p, int r, int c, flo
     }
 }
 template <> __device__ __forceinline__ void epi_store<EPI_PARTIAL>(const EpiParams &, int, int, float) {}
+// EPI_RESID_STATS outside the decode-row GEMM (reduce kernel of a split launch): the residual part
+template <> __device__ __forceinline__ void epi_store<EPI_RESID_STATS>(const EpiParams & p, int r, int c, float acc) {
+    epi_store<EPI_RESID_F32>(p, r, c, acc);
+}
 
 typedef __attribute__((address_space(3))) void * lds_ptr_t;
 
@@ -193,6 +197,182 @@ __global__ __launch_bounds__(256, 2) void k_gemm_big(int M, int N, int K, const 
             if constexpr (MODE == EPI_QKV_ENC) {
                 // V columns go to the transposed [clip][head][dim][Tpad] image: a lane's 4 rows
                 // are 4 consecutive t of one clip (T % 4 == 0, r0 % 4 == 0): one 8-byte store
+                const int d = ep.d;
+                if (c >= 2 * d && c < N && r0 + 3 < M && ep.T % 4 == 0) {
+                    const int cc = c - 2 * d;
+                    const int clip = r0 / ep.T, t = r0 - clip * ep.T;
+                    const float bv = ep.bias2[cc];
+                    half4 hv;
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) hv[e] = (_Float16) (acc[i][j][e] + bv);
+                    *(half4 *) (ep.out16c + (((size_t) clip * (d >> 6) + (cc >> 6)) * 64 + (cc & 63)) * ep.Tpad + t) = hv;
+                    continue;
+                }
+            }
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int r = r0 + e;
+                if (r < M && c < N) epi_store<MODE>(ep, r, c, acc[i][j][e]);
+            }
+        }
+}
+
+// ---------------------------------------------------------------------------------
+// 256x256 block tile for the large encoder / cross-KV GEMMs (M = clips x 1500 rows).
+// 8 waves (2 in M x 4 in N), each 128x64 of the output = 8 x 4 MFMA 16x16x32 tiles
+// (128 accumulators). K advances in 32-deep steps through a 4-slot LDS ring
+// (slot = 256 x 32 f16 of A + of W = 32 KB, 128 KB in all, one block per CU):
+//   top of step j: s_waitcnt vmcnt(4) (this wave's step-j DMA landed; step j+1's 4
+//   global_load_lds stay in flight) -> s_barrier (every wave's step-j DMA landed, and
+//   every wave is done reading step j-2's slot) -> issue step j+2 into that slot ->
+//   read fragments + 32 MFMAs of step j.
+// Two K-steps stay in flight across every barrier (the "pipelining across barriers"
+// rule of the CDNA guide: counted vmcnt, raw s_barrier, one __shared__ array), so the
+// loop never drains the DMA queue. LDS image: 64-B rows (32 f16), 16-B chunk c of row r
+// stored at chunk c ^ ((r >> 2) & 3) -- the swizzle is applied to the global source
+// address of each lane (global_load_lds writes lane-linear), and the ds_read_b128 of 16
+// consecutive rows then hits 16 distinct 16-B bank groups.
+// ---------------------------------------------------------------------------------
+constexpr int G2_M = 256, G2_N = 256, G2_K = 32;
+constexpr int G2_OP = G2_M * G2_K * 2;     // 16 KB: one operand of one K-step
+constexpr int G2_SLOT = 2 * G2_OP;         // 32 KB
+
+template <int MODE, int G2_SLOTS>
+__global__ __launch_bounds__(512, 2) void k_gemm_256(int M, int N, int K, const _Float16 * __restrict__ A, int lda,
+                                                     const _Float16 * __restrict__ W, int ldw, EpiParams ep) {
+    // G2_SLOTS ring slots: G2_SLOTS - 2 K-steps stay in flight past every barrier
+    static_assert(G2_SLOTS == 4 || G2_SLOTS == 5, "ring depth");
+    constexpr int AHEAD = G2_SLOTS - 2;  // steps issued beyond the one being computed
+    __shared__ __attribute__((aligned(1024))) char smem[G2_SLOTS * G2_SLOT];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wr = wave >> 2, wc = wave & 3;
+
+    const int nbn = (N + G2_N - 1) / G2_N;
+    const int nb = gridDim.x;
+    int bid = blockIdx.x;
+    {  // XCD-aware order: a run of consecutive tiles (one A row panel) per XCD
+        const int xcd = bid & 7, q = nb >> 3, rr = nb & 7;
+        const int base = xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q;
+        bid = base + (bid >> 3);
+    }
+    const int bm = bid / nbn, bn = bid - bm * nbn;
+    const int m0 = bm * G2_M, n0 = bn * G2_N;
+
+    // staging: wave w issues row groups 2w, 2w+1 (16 rows x 64 B each) of A and of W
+    const int srow0 = wave * 32 + (lane >> 2);
+    const _Float16 * ga[2];
+    const _Float16 * gw[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int row = srow0 + i * 16;
+        const int c = (lane & 3) ^ ((row >> 2) & 3);
+        ga[i] = A + (size_t) min(m0 + row, M - 1) * lda + c * 8;
+        gw[i] = W + (size_t) min(n0 + row, N - 1) * ldw + c * 8;
+    }
+    auto stage = [&](int slot, int k0) {
+        char * sA = smem + slot * G2_SLOT + wave * 2048;
+        char * sB = sA + G2_OP;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            __builtin_amdgcn_global_load_lds((const void *) (ga[i] + k0), (lds_ptr_t) (sA + i * 1024), 16, 0, 0);
+            __builtin_amdgcn_global_load_lds((const void *) (gw[i] + k0), (lds_ptr_t) (sB + i * 1024), 16, 0, 0);
+        }
+    };
+
+    floatx4 acc[8][4];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+    // fragment addresses (byte offsets inside an operand image): row r, logical chunk g
+    const int g = lane >> 4, l16 = lane & 15;
+    int offA[8], offB[4];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const int r = wr * 128 + i * 16 + l16;
+        offA[i] = r * 64 + ((g ^ ((r >> 2) & 3)) << 4);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int r = wc * 64 + j * 16 + l16;
+        offB[j] = r * 64 + ((g ^ ((r >> 2) & 3)) << 4);
+    }
+
+    const int nk = K / G2_K;
+    // waits for step `next` while steps next+1 .. next+AHEAD-1 (those issued) stay in flight
+    auto wait_step = [&](int next) {
+        const int later = min(AHEAD - 1, nk - 1 - next);
+        if (later >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        else if (later == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    };
+    // prologue: steps 0 .. AHEAD-1 in flight, step 0 landed, step AHEAD issued, first fragments read
+#pragma unroll
+    for (int i = 0; i < AHEAD; ++i)
+        if (i < nk) stage(i, i * G2_K);
+    wait_step(0);
+    __builtin_amdgcn_s_barrier();
+    if (AHEAD < nk) stage(AHEAD, AHEAD * G2_K);
+    half8 b[4], a[2];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) b[t] = *(const half8 *) (smem + G2_OP + offB[t]);
+    a[0] = *(const half8 *) (smem + offA[0]);
+    a[1] = *(const half8 *) (smem + offA[1]);
+    // step j = 4 groups of 8 MFMAs (2 row tiles x 4 column tiles); the fragments of the next
+    // group -- across the step boundary: of step j+1, after its DMA wait + barrier -- are read
+    // before the current group's MFMAs are issued, so LDS latency hides behind them
+    int slot = 0;
+    for (int j = 0; j < nk; ++j) {
+        const char * sA = smem + slot * G2_SLOT;
+        const int nslot = slot + 1 == G2_SLOTS ? 0 : slot + 1;
+        half8 bn[4], an[2];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            if (g < 3) {
+                an[0] = *(const half8 *) (sA + offA[2 * g + 2]);
+                an[1] = *(const half8 *) (sA + offA[2 * g + 3]);
+            } else if (j + 1 < nk) {
+                // step j+1 landed for every wave (this wave: counted vmcnt; all: barrier), and
+                // every wave is done with step j-1's slot: restage it with step j+1+AHEAD
+                wait_step(j + 1);
+                __builtin_amdgcn_s_barrier();
+                if (j + 1 + AHEAD < nk) {
+                    const int fs = slot == 0 ? G2_SLOTS - 1 : slot - 1;  // (j - 1) mod G2_SLOTS
+                    stage(fs, (j + 1 + AHEAD) * G2_K);
+                }
+                const char * nA = smem + nslot * G2_SLOT;
+#pragma unroll
+                for (int t = 0; t < 4; ++t) bn[t] = *(const half8 *) (nA + G2_OP + offB[t]);
+                an[0] = *(const half8 *) (nA + offA[0]);
+                an[1] = *(const half8 *) (nA + offA[1]);
+            }
+            // keep the order: next fragments' ds_reads issued, then this group's MFMAs (the
+            // scheduler would otherwise consume each read right after issuing it)
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int t = 0; t < 4; ++t)
+                    acc[2 * g + i][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[i], b[t], acc[2 * g + i][t], 0, 0, 0);
+            __builtin_amdgcn_sched_barrier(0);
+            a[0] = an[0];
+            a[1] = an[1];
+        }
+#pragma unroll
+        for (int t = 0; t < 4; ++t) b[t] = bn[t];
+        slot = nslot;
+    }
+
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int c = n0 + wc * 64 + j * 16 + l16;
+            const int r0 = m0 + wr * 128 + i * 16 + 4 * g;
+            if constexpr (MODE == EPI_QKV_ENC) {
+                // V columns -> the transposed [clip][head][dim][Tpad] image: a lane's 4 rows are 4
+                // consecutive t of one clip (T % 4 == 0, r0 % 4 == 0): one 8-byte store
                 const int d = ep.d;
                 if (c >= 2 * d && c < N && r0 + 3 < M && ep.T % 4 == 0) {
                     const int cc = c - 2 * d;
@@ -319,20 +499,39 @@ void tile_weights(hipStream_t s, const _Float16 * W, int N, int K, _Float16 * ou
 
 size_t tiled_weight_elems(int N, int K) { return (size_t) ((N + 15) / 16) * 16 * K; }
 
-template <int MODE, int MT, int J>
+template <int MODE, int MT, int J, bool ALN>
 __global__ __launch_bounds__(GR_MAXW * 64) void k_gemm_rows(int M, int N, int K, const _Float16 * __restrict__ A,
                                                             int lda, const _Float16 * __restrict__ Wt, EpiParams ep,
-                                                            float * __restrict__ part) {
+                                                            float * __restrict__ part, AlnParams aln) {
+    // ALN: the A operand is LayerNorm(aln.x) computed here (AlnParams, kernels.h); its row
+    // statistics come from the producer's EPI_RESID_STATS partials, 4 rows per wave at most
+    constexpr int RPW = 4;
     __shared__ floatx4 red[GR_MAXW][MT][64];
+    __shared__ float s_ln[2][32];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = blockDim.x >> 6;
     const int tile = blockIdx.x, n0 = tile * 16;
     const int nsteps = K >> 5;
     const int ks0 = (blockIdx.y * nw + wave) * J;
     const int nj = max(0, min(J, nsteps - ks0));
+    const half8 z8 = {0, 0, 0, 0, 0, 0, 0, 0};
+
+    // ALN: the statistics partials first (in-order vmcnt: they can be waited for while the
+    // weight and activation loads issued after them stay in flight). Addresses are clamped and
+    // invalid entries zeroed after the load (a conditional load would make hipcc wait per load).
+    double2 stv[RPW][2];
+    if constexpr (ALN) {
+#pragma unroll
+        for (int q = 0; q < RPW; ++q)
+#pragma unroll
+            for (int hh = 0; hh < 2; ++hh) {
+                const int r = min(wave + q * nw, M - 1), t = min(lane + 64 * hh, aln.ntiles - 1);
+                stv[q][hh] = ((const double2 *) aln.stats)[(size_t) t * M + r];
+            }
+        __builtin_amdgcn_sched_barrier(0);  // issued before the weight stream
+    }
 
     // branch-free: every load is issued (k-step clamped into the matrix); operands past
     // this wave's k range are zeros so the extra MFMAs add exact zeros
-    const half8 z8 = {0, 0, 0, 0, 0, 0, 0, 0};
     const _Float16 * wp = Wt + ((size_t) tile * nsteps) * 512 + lane * 8;
     half8 b[J], a[MT][J];
 #pragma unroll
@@ -340,16 +539,95 @@ __global__ __launch_bounds__(GR_MAXW * 64) void k_gemm_rows(int M, int N, int K,
         const half8 t = *(const half8 *) (wp + (size_t) min(ks0 + j, nsteps - 1) * 512);
         b[j] = j < nj ? t : z8;
     }
-#pragma unroll
-    for (int i = 0; i < MT; ++i) {
-        const _Float16 * ap = A + (size_t) min(i * 16 + (lane & 15), M - 1) * lda + 8 * (lane >> 4);
+    float4 xa[ALN ? MT : 1][ALN ? J : 1][2], lw[ALN ? J : 1][2], lb[ALN ? J : 1][2];
+    if constexpr (ALN) {
 #pragma unroll
         for (int j = 0; j < J; ++j) {
-            const half8 t = *(const half8 *) (ap + min(ks0 + j, nsteps - 1) * 32);
-            a[i][j] = j < nj ? t : z8;
+            const int k = min(ks0 + j, nsteps - 1) * 32 + 8 * (lane >> 4);
+            lw[j][0] = *(const float4 *) (aln.w + k);
+            lw[j][1] = *(const float4 *) (aln.w + k + 4);
+            lb[j][0] = *(const float4 *) (aln.b + k);
+            lb[j][1] = *(const float4 *) (aln.b + k + 4);
+#pragma unroll
+            for (int i = 0; i < MT; ++i) {
+                const float * xp = aln.x + (size_t) min(i * 16 + (lane & 15), M - 1) * aln.ldx + k;
+                xa[i][j][0] = *(const float4 *) xp;
+                xa[i][j][1] = *(const float4 *) (xp + 4);
+            }
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < MT; ++i) {
+            const _Float16 * ap = A + (size_t) min(i * 16 + (lane & 15), M - 1) * lda + 8 * (lane >> 4);
+#pragma unroll
+            for (int j = 0; j < J; ++j) {
+                const half8 t = *(const half8 *) (ap + min(ks0 + j, nsteps - 1) * 32);
+                a[i][j] = j < nj ? t : z8;
+            }
         }
     }
     __builtin_amdgcn_sched_barrier(0);  // keep every load issued ahead of the first wait
+
+    if constexpr (ALN) {
+        // (the compiler's counted vmcnt before the first use of stv lets the weight, activation
+        // and w/b loads issued after the statistics stay in flight)
+        const int Kc = aln.ntiles * 16;  // LayerNorm width (= K)
+#pragma unroll
+        for (int q = 0; q < RPW; ++q) {
+            const int r = wave + q * nw;
+            double s1 = 0.0, m2 = 0.0;
+            double st[2] = {0.0, 0.0};
+#pragma unroll
+            for (int hh = 0; hh < 2; ++hh) {
+                const bool ok = lane + 64 * hh < aln.ntiles;
+                st[hh] = ok ? stv[q][hh].x : 0.0;
+                s1 += st[hh];
+            }
+#pragma unroll
+            for (int m = 32; m > 0; m >>= 1) s1 += __shfl_xor(s1, m, 64);
+            const float mean_f = (float) s1 / (float) Kc;  // ref: float sum / ne00
+            const double mean_d = s1 / (double) Kc;
+#pragma unroll
+            for (int hh = 0; hh < 2; ++hh) {
+                if (lane + 64 * hh < aln.ntiles) {
+                    const double dm = st[hh] / 16.0 - mean_d;
+                    m2 += stv[q][hh].y + 16.0 * dm * dm;  // Chan: combine per-tile (sum, M2)
+                }
+            }
+#pragma unroll
+            for (int m = 32; m > 0; m >>= 1) m2 += __shfl_xor(m2, m, 64);
+            const double dmf = mean_d - (double) mean_f;
+            m2 += (double) Kc * dmf * dmf;  // about the float mean, as ggml_vec_cvar_f32 centres
+            const float var = (float) (m2 / (double) Kc);
+            if (lane == 0 && r < M) {
+                s_ln[0][r] = mean_f;
+                s_ln[1][r] = 1.0f / sqrtf(var + aln.eps);
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < MT; ++i) {
+            const int r = min(i * 16 + (lane & 15), M - 1);
+            const float mean = s_ln[0][r], rstd = s_ln[1][r];
+#pragma unroll
+            for (int j = 0; j < J; ++j) {
+                half8 h;
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                    const float xv = e < 4 ? xa[i][j][0][e] : xa[i][j][1][e - 4];
+                    const float wv = e < 4 ? lw[j][0][e] : lw[j][1][e - 4];
+                    const float bv = e < 4 ? lb[j][0][e] : lb[j][1][e - 4];
+                    float v = xv - mean;  // ggml_norm: (x - mean) * scale, then ggml_mul, ggml_add
+                    v = v * rstd;
+                    v = v * wv;
+                    v = v + bv;
+                    h[e] = (_Float16) v;
+                }
+                a[i][j] = j < nj ? h : z8;
+            }
+        }
+    }
+
     floatx4 acc[MT];
 #pragma unroll
     for (int i = 0; i < MT; ++i) acc[i] = floatx4{0.f, 0.f, 0.f, 0.f};
@@ -380,7 +658,24 @@ __global__ __launch_bounds__(GR_MAXW * 64) void k_gemm_rows(int M, int N, int K,
         float sum = rp[0];
         for (int w = 1; w < nw; ++w) sum += rp[w * MT * 64 * 4];
         const int c = n0 + cc;
-        if (r < M && c < N) {
+        if constexpr (MODE == EPI_RESID_STATS) {
+            // x += acc + bias, then this tile's {sum, M2} of the updated row (16 lanes = 16 columns)
+            double dv = 0.0;
+            if (r < M && c < N) {
+                const size_t off = (size_t) r * ep.ldo + c;
+                const float v = ep.resid[off] + (sum + ep.bias[c]);
+                ep.out32[off] = v;
+                dv = v;
+            }
+            double s1 = dv;
+#pragma unroll
+            for (int m = 8; m > 0; m >>= 1) s1 += __shfl_xor(s1, m, 16);
+            const double dd = dv - s1 / 16.0;
+            double m2 = dd * dd;
+#pragma unroll
+            for (int m = 8; m > 0; m >>= 1) m2 += __shfl_xor(m2, m, 16);
+            if (cc == 0 && r < M) ((double2 *) ep.stats)[(size_t) tile * M + r] = double2{s1, m2};
+        } else if (r < M && c < N) {
             if constexpr (MODE == EPI_PARTIAL)
                 part[((size_t) blockIdx.y * M + r) * N + c] = sum;  // row-major [ks][M][N] for resid_layernorm
             else
@@ -444,6 +739,7 @@ template <template <int> class L, typename... Args> static void dispatch_mode(in
         case EPI_HALF_RESID: L<EPI_HALF_RESID>::run(args...); break;
         case EPI_RELU_F16: L<EPI_RELU_F16>::run(args...); break;
         case EPI_SIGMOID_F32: L<EPI_SIGMOID_F32>::run(args...); break;
+        case EPI_RESID_STATS: L<EPI_RESID_STATS>::run(args...); break;
         default: throw std::runtime_error("gemm: bad epilogue mode");
     }
 }
@@ -455,6 +751,17 @@ template <int MODE> struct LaunchBig {
         hipLaunchKernelGGL(k_gemm_big<MODE>, dim3(nbm * nbn), dim3(256), 0, s, M, N, K, A, lda, W, ldw, ep);
     }
 };
+static int g_gemm256 = -1;  // -1: from OWK_GEMM256 (default on); 5: the 5-slot ring
+template <int MODE> struct Launch256 {
+    static void run(hipStream_t s, int M, int N, int K, const _Float16 * A, int lda, const _Float16 * W, int ldw,
+                    const EpiParams & ep) {
+        const int nbm = (M + G2_M - 1) / G2_M, nbn = (N + G2_N - 1) / G2_N;
+        if (g_gemm256 == 5)
+            hipLaunchKernelGGL((k_gemm_256<MODE, 5>), dim3(nbm * nbn), dim3(512), 0, s, M, N, K, A, lda, W, ldw, ep);
+        else
+            hipLaunchKernelGGL((k_gemm_256<MODE, 4>), dim3(nbm * nbn), dim3(512), 0, s, M, N, K, A, lda, W, ldw, ep);
+    }
+};
 template <int MODE> struct LaunchSkinny {
     static void run(hipStream_t s, int M, int N, int K, const _Float16 * A, int lda, const _Float16 * W, int ldw,
                     const EpiParams & ep) {
@@ -463,17 +770,28 @@ template <int MODE> struct LaunchSkinny {
 };
 
 template <int MODE> struct LaunchRows {
-    template <int MT, int J>
+    template <int MT, int J, bool ALN>
     static void go(hipStream_t s, dim3 grid, int nw, int M, int N, int K, const _Float16 * A, int lda,
-                   const _Float16 * Wt, const EpiParams & ep, float * part) {
-        hipLaunchKernelGGL((k_gemm_rows<MODE, MT, J>), grid, dim3(nw * 64), 0, s, M, N, K, A, lda, Wt, ep, part);
+                   const _Float16 * Wt, const EpiParams & ep, float * part, const AlnParams & aln) {
+        hipLaunchKernelGGL((k_gemm_rows<MODE, MT, J, ALN>), grid, dim3(nw * 64), 0, s, M, N, K, A, lda, Wt, ep, part,
+                           aln);
         if (grid.y > 1 && MODE != EPI_PARTIAL)
             hipLaunchKernelGGL((k_gemm_rows_reduce<MODE, MT>), dim3(grid.x), dim3(MT * 64), 0, s, M, N, (int) grid.y,
                                part, ep);
     }
-    static void run(hipStream_t s, int M, int N, int K, const _Float16 * A, int lda, const _Float16 * Wt,
-                    const EpiParams & ep, const GemmWs * ws) {
-        const RowsPlan pl = rows_plan(K, MODE == EPI_PARTIAL);
+    template <bool ALN>
+    static void run_t(hipStream_t s, int M, int N, int K, const _Float16 * A, int lda, const _Float16 * Wt,
+                      const EpiParams & ep, const GemmWs * ws, const AlnParams & aln) {
+        RowsPlan pl = rows_plan(K, MODE == EPI_PARTIAL);
+        if (MODE == EPI_RESID_STATS) {  // whole rows of K per block (the statistics need the final sums)
+            const int nsteps = K / 32;
+            pl.J = nsteps <= 32 ? 2 : nsteps <= 64 ? 4 : nsteps <= 128 ? 8 : 10;
+            pl.KS = 1;
+            pl.nw = (nsteps + pl.J - 1) / pl.J;
+            if (pl.nw > GR_MAXW || !ep.stats) throw std::runtime_error("gemm_rows: EPI_RESID_STATS shape");
+        }
+        if (ALN && (pl.J > 4 || pl.nw * 4 < M || !aln.stats || aln.ntiles * 16 != K || aln.ntiles > 128))
+            throw std::runtime_error("gemm_rows: unsupported LayerNorm-operand shape");
         const int tiles = (N + 15) / 16;
         float * part = nullptr;
         if (pl.KS > 1 || MODE == EPI_PARTIAL) {
@@ -484,10 +802,35 @@ template <int MODE> struct LaunchRows {
         const dim3 grid(tiles, pl.KS);
         const bool one = M <= 16;
         switch (pl.J) {
-            case 2: one ? go<1, 2>(s, grid, pl.nw, M, N, K, A, lda, Wt, ep, part) : go<2, 2>(s, grid, pl.nw, M, N, K, A, lda, Wt, ep, part); break;
-            case 4: one ? go<1, 4>(s, grid, pl.nw, M, N, K, A, lda, Wt, ep, part) : go<2, 4>(s, grid, pl.nw, M, N, K, A, lda, Wt, ep, part); break;
-            default: one ? go<1, 8>(s, grid, pl.nw, M, N, K, A, lda, Wt, ep, part) : go<2, 8>(s, grid, pl.nw, M, N, K, A, lda, Wt, ep, part); break;
+            case 2: one ? go<1, 2, ALN>(s, grid, pl.nw, M, N, K, A, lda, Wt, ep, part, aln)
+                        : go<2, 2, ALN>(s, grid, pl.nw, M, N, K, A, lda, Wt, ep, part, aln); break;
+            case 4: one ? go<1, 4, ALN>(s, grid, pl.nw, M, N, K, A, lda, Wt, ep, part, aln)
+                        : go<2, 4, ALN>(s, grid, pl.nw, M, N, K, A, lda, Wt, ep, part, aln); break;
+            case 8:
+                if constexpr (!ALN) {
+                    one ? go<1, 8, false>(s, grid, pl.nw, M, N, K, A, lda, Wt, ep, part, aln)
+                        : go<2, 8, false>(s, grid, pl.nw, M, N, K, A, lda, Wt, ep, part, aln);
+                }
+                break;
+            default:
+                if constexpr (!ALN && MODE == EPI_RESID_STATS) {
+                    one ? go<1, 10, false>(s, grid, pl.nw, M, N, K, A, lda, Wt, ep, part, aln)
+                        : go<2, 10, false>(s, grid, pl.nw, M, N, K, A, lda, Wt, ep, part, aln);
+                } else {
+                    throw std::runtime_error("gemm_rows: no kernel for this plan");
+                }
+                break;
         }
+    }
+    static void run(hipStream_t s, int M, int N, int K, const _Float16 * A, int lda, const _Float16 * Wt,
+                    const EpiParams & ep, const GemmWs * ws) {
+        run_t<false>(s, M, N, K, A, lda, Wt, ep, ws, AlnParams());
+    }
+};
+template <int MODE> struct LaunchRowsLn {
+    static void run(hipStream_t s, int M, int N, int K, const AlnParams & aln, const _Float16 * Wt,
+                    const EpiParams & ep, const GemmWs * ws) {
+        LaunchRows<MODE>::template run_t<true>(s, M, N, K, nullptr, K, Wt, ep, ws, aln);
     }
 };
 
@@ -910,10 +1253,19 @@ static void check_shape(int M, int N, int K, int lda, int ldw, int kmul) {
                                  " K=" + std::to_string(K));
 }
 
+// large GEMMs (the batched encoder, cross-KV, conv) take the 256x256 ring kernel; the rest
+// (small models, SortFormer chunks) the 128x128 tile. OWK_GEMM256=0 forces the 128x128 path.
+void gemm_set_256(int on) { g_gemm256 = on; }
+static bool use_256(int M, int N, int K) {
+    if (g_gemm256 < 0) g_gemm256 = env_int("OWK_GEMM256", 1);
+    return g_gemm256 && M >= 2048 && N >= 1024 && K % G2_K == 0;
+}
+
 void gemm_f16(hipStream_t s, int mode, int M, int N, int K, const _Float16 * A, int lda, const _Float16 * W, int ldw,
               const EpiParams & ep) {
     check_shape(M, N, K, lda, ldw, GB_K);
-    dispatch_mode<LaunchBig>(mode, s, M, N, K, A, lda, W, ldw, ep);
+    if (use_256(M, N, K)) dispatch_mode<Launch256>(mode, s, M, N, K, A, lda, W, ldw, ep);
+    else dispatch_mode<LaunchBig>(mode, s, M, N, K, A, lda, W, ldw, ep);
 }
 
 void gemm_f16_skinny(hipStream_t s, int mode, int M, int N, int K, const _Float16 * A, int lda, const _Float16 * W,
@@ -936,6 +1288,18 @@ size_t gemm_ws_floats(int N, int K) {
 }
 size_t gemm_partial_floats(int N, int K) { return (size_t) rows_plan(K, true).KS * ((N + 15) / 16) * 2 * 64 * 4; }
 int gemm_partial_splits(int K) { return rows_plan(K, true).KS; }
+
+void gemm_rows_ln(hipStream_t s, int mode, int M, int N, int K, const AlnParams & aln, const _Float16 * Wt,
+                  const EpiParams & ep, const GemmWs * ws) {
+    if (!(M > 0 && M <= 32 && K % 32 == 0 && N % 16 == 0 && Wt && aln && aln.ldx >= K))
+        throw std::runtime_error("gemm_rows_ln: unsupported shape");
+    switch (mode) {
+        case EPI_F16: LaunchRowsLn<EPI_F16>::run(s, M, N, K, aln, Wt, ep, ws); break;
+        case EPI_GELU_F16: LaunchRowsLn<EPI_GELU_F16>::run(s, M, N, K, aln, Wt, ep, ws); break;
+        case EPI_QKV_DEC: LaunchRowsLn<EPI_QKV_DEC>::run(s, M, N, K, aln, Wt, ep, ws); break;
+        default: throw std::runtime_error("gemm_rows_ln: unsupported epilogue");
+    }
+}
 
 void gemm(hipStream_t s, int mode, int M, int N, int K, const _Float16 * A, int lda, const _Float16 * W, int ldw,
           const EpiParams & ep, const GemmWs * ws, const _Float16 * Wt) {

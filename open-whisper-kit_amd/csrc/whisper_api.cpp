@@ -1134,7 +1134,23 @@ int owk_debug_dtw(const float * cap, int n_ah, int n_audio_ctx, int n_tok, int s
     }
 }
 
+// uniform random f16 in [-1, 1) from a per-element hash: GEMM timings on random data (zero-filled
+// operands run 15-21 % faster through DVFS, CDNA guide 5.4 rule 25)
+__global__ static void k_fill_rand_f16(_Float16 * p, size_t n, uint32_t seed) {
+    for (size_t i = (size_t) blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t) gridDim.x * blockDim.x) {
+        uint32_t h = (uint32_t) i * 2654435761u ^ seed;
+        h ^= h >> 15; h *= 2246822519u; h ^= h >> 13; h *= 3266489917u; h ^= h >> 16;
+        p[i] = (_Float16) ((float) (h & 0xFFFF) / 32768.0f - 1.0f);
+    }
+}
+
+// mode bit 0x100: force the 128x128 large-GEMM kernel; bit 0x400: the 5-slot ring variant of the
+// 256x256 kernel; bit 0x200: random operands
 double owk_debug_gemm_bench(int device, int mode, int M, int N, int K, int iters) {
+    const bool force128 = mode & 0x100, rnd = mode & 0x200, ring5 = mode & 0x400;
+    mode &= 0xFF;
+    struct Restore { ~Restore() { gemm_set_256(1); } } restore;
+    gemm_set_256(force128 ? 0 : ring5 ? 5 : 1);
     try {
         OWK_HIP_CHECK(hipSetDevice(device));
         hipStream_t s;
@@ -1149,6 +1165,10 @@ double owk_debug_gemm_bench(int device, int mode, int M, int N, int K, int iters
         bias.alloc((size_t) N * 4);
         OWK_HIP_CHECK(hipMemset(da.ptr, 0, da.bytes));
         OWK_HIP_CHECK(hipMemset(dw.ptr, 0, dw.bytes));
+        if (rnd) {
+            hipLaunchKernelGGL(k_fill_rand_f16, dim3(4096), dim3(256), 0, s, da.as<_Float16>(), (size_t) M * K, 1u);
+            hipLaunchKernelGGL(k_fill_rand_f16, dim3(4096), dim3(256), 0, s, dw.as<_Float16>(), (size_t) N * K, 7u);
+        }
         OWK_HIP_CHECK(hipMemset(dres.ptr, 0, dres.bytes));
         OWK_HIP_CHECK(hipMemset(bias.ptr, 0, bias.bytes));
         tile_weights(s, dw.as<_Float16>(), N, K, dwt.as<_Float16>());

@@ -153,6 +153,14 @@ def load(path: str | None = None) -> C.CDLL:
     L.whisper_full_get_segment_speaker_turn_next_from_state.argtypes = [vp, ip]
     L.whisper_print_system_info.restype = C.c_char_p
     L.whisper_full_n_segments.argtypes = [vp]
+    # context-level (default state) result getters, as whisper-cli uses them
+    L.whisper_full_get_segment_t0.restype = C.c_int64
+    L.whisper_full_get_segment_t0.argtypes = [vp, ip]
+    L.whisper_full_get_segment_t1.restype = C.c_int64
+    L.whisper_full_get_segment_t1.argtypes = [vp, ip]
+    L.whisper_full_get_segment_text.restype = C.c_char_p
+    L.whisper_full_get_segment_text.argtypes = [vp, ip]
+    L.whisper_full_n_tokens.argtypes = [vp, ip]
     L.whisper_full_get_segment_t0_from_state.restype = C.c_int64
     L.whisper_full_get_segment_t0_from_state.argtypes = [vp, ip]
     L.whisper_full_get_segment_t1_from_state.restype = C.c_int64
@@ -164,6 +172,8 @@ def load(path: str | None = None) -> C.CDLL:
     L.whisper_full_n_tokens_from_state.argtypes = [vp, ip]
     L.whisper_full_get_token_data_from_state.restype = TokenData
     L.whisper_full_get_token_data_from_state.argtypes = [vp, ip, ip]
+    L.whisper_full_get_token_data.restype = TokenData
+    L.whisper_full_get_token_data.argtypes = [vp, ip, ip]
     L.whisper_pcm_to_mel_with_state.argtypes = [vp, vp, fp, ip, ip]
     L.whisper_encode_with_state.argtypes = [vp, vp, ip, ip]
     L.whisper_decode_with_state.argtypes = [vp, vp, C.POINTER(C.c_int32), ip, ip, ip]

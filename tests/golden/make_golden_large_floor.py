@@ -8,7 +8,8 @@ Also records, for every DTW fixture, the per-window token sequences of the refer
 (ref_full record_topk = 2 traces every decoder call's token prefix) so a teacher-forced GPU run can
 be driven window by window.
 
-Usage (after make_golden_large.py):  python tests/golden/make_golden_large_floor.py
+Usage (after make_golden_large.py):  python tests/golden/make_golden_large_floor.py [dtw]
+(dtw: only the window traces)
 """
 import json
 import os
@@ -28,19 +29,29 @@ OUT = os.path.dirname(os.path.abspath(__file__))
 N_PERTURB = 2
 
 
-def windows_of(ref, flat):
-    """Per-window token sequences from the traced decoder-call prefixes: a window starts where the
-    traced prefix is empty again and (ending in <|endoftext|>) emitted its longest prefix. Returns
-    None unless the windows concatenate to the reference's result tokens `flat`."""
+def windows_of(ref, flat, n_max=220):
+    """Per-window DECODED token sequences (what the decoder sampled, before segment assembly folds
+    timestamp pairs) from the traced decoder-call prefixes: a window starts where the traced prefix
+    is empty again; a window that ended on <|endoftext|> decoded exactly its longest traced prefix.
+    A window can also end on a kept token that is in no prefix: the n_text_ctx/2 - 4 = 220 step
+    limit (ref whisper.cpp:7219) or a timestamp reaching the end of the audio (7359-7441); both only
+    in the last window, whose kept token is then the last result token (an <|endoftext|> ending
+    leaves the last decoded token last). None where that cannot be told."""
     off, prefix, _, _ = ref.recorded()
-    wins = []
+    longest = []
     for i in range(len(off) - 1):
         p = prefix[off[i]:off[i + 1]].tolist()
         if not p:
-            wins.append([])
-        elif len(p) > len(wins[-1]):
-            wins[-1] = p
-    return wins if sum(wins, []) == flat else None
+            longest.append([])
+        elif len(p) > len(longest[-1]):
+            longest[-1] = p
+    for i, w in enumerate(longest[:-1]):
+        if len(w) + 1 >= n_max:
+            return None
+    last = longest[-1]
+    if len(last) + 1 >= n_max or (flat and (not last or last[-1] != flat[-1])):
+        last.append(flat[-1])
+    return longest
 
 
 def main():
@@ -48,9 +59,12 @@ def main():
     arrays = dict(np.load(os.path.join(OUT, "large_golden.npz")))
     cache = os.environ.get("OWK_MODEL_CACHE", "/tmp/owk_models")
     audio = clips()
+    dtw_only = len(sys.argv) > 1 and sys.argv[1] == "dtw"
     model = "large-v3-q5_0"
     ref = R.Ref(S.ensure_model(model, meta["seed"], cache))
     for cname, pcm in audio.items():
+        if dtw_only:
+            break
         key = f"{model}/{cname}"
         rng = np.random.default_rng(0)
         pp = (pcm * (1 + 1e-7 * rng.standard_normal(len(pcm)))).astype(np.float32)

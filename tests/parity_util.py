@@ -96,6 +96,7 @@ class LogitError:
         lg2 = np.ctypeslib.as_array(L.whisper_get_logits_from_state(st), shape=(w.n_vocab,)).copy()
         e2 = float(np.abs(lg2[arr[key + "/step1_top_idx"]] - arr[key + "/step1_top_val"]).max())
         L.whisper_free_state(st)
+        w._states.remove(st)
         return max(e1, e2)
 
     @classmethod

@@ -12,8 +12,9 @@ reference's own capture by 1e-3 relative noise moves 0.9% of the tokens by up to
 single-window jfk runs must reproduce the capture (2e-5) and every t_dtw exactly; the
 220-token synth30 windows allow <= 5% of tokens to move by <= 20 cs. The free-running decode is
 compared token by token (near-ties bounded by the measured logit error, parity_util); t_dtw is
-compared on a second run teacher-forced onto the reference's tokens (parity_util.Forcer: both
-clips are single windows), so a near-tie parting never skips the DTW check.
+compared on a second run teacher-forced onto the reference's decoded sequence (parity_util.Forcer,
+per-window sequences traced by tests/golden/make_golden_nofa_windows.py), so a near-tie parting never
+skips the DTW check.
 """
 import ctypes as C
 import json
@@ -98,7 +99,8 @@ def test_dtw_timestamps(nofa, model_path, clips, model, clip):
     _compare(w.segments(st), want["segments"], f"{model}/{clip}/dtw", tie=tie)
     # t_dtw of the reference's own token sequence: teacher-force the (single-window) decode
     r_ids = [t[0] for s in want["segments"] for t in s["tokens"]]
-    force = Forcer([r_ids], w.L.whisper_token_eot(w.ctx), w.n_vocab, owk.TokenData)
+    windows = meta["results"][f"{model}/{clip}/dtw_windows"]  # what the reference DECODED, per window
+    force = Forcer(windows, w.L.whisper_token_eot(w.ctx), w.n_vocab, owk.TokenData)
     p.logits_filter_callback = C.cast(force.cfunc, C.c_void_p)
     st = w.new_state()
     assert w.full(st, clips[clip], p) == want["ret"]
