@@ -619,12 +619,21 @@ void Engine::launch_decode(const DecShape & sh) {
     const float kq_scale = powf(64.0f, -0.25f);
     const size_t self_stride = (size_t) cap_slots * kv_cells * d;
     const size_t cross_stride = (size_t) cap_slots * hp.n_audio_ctx * d;  // per layer (capacity)
-    // R <= 32 rows (F16 weights): no LayerNorm launches inside the decoder. The residual matmuls
-    // (attn.out, cross_attn.out, mlp.2) add bias + residual in their epilogue and leave per
-    // (16-column tile, row) statistics of the updated row; the next matmul (self Q/K/V, cross Q,
-    // mlp.0 -- every LayerNorm of the decoder feeds exactly one) normalises its A operand from them
-    // (AlnParams). Larger passes use the full-epilogue GEMMs and separate LayerNorms.
+    // R <= 32 rows (F16 weights): the decoder's LayerNorms ride on the matmuls around them.
+    //  * attn.out / cross_attn.out (K = d): EPI_RESID_STATS adds bias + residual in the epilogue and
+    //    leaves per (16-column tile, row) statistics of the updated row; the next matmul (cross Q,
+    //    mlp.0) normalises its A operand from them (AlnParams) -- no LayerNorm launch;
+    //  * mlp.2 (K = 4d: long, so split over k): partial tiles, then one kernel adds them with bias +
+    //    residual and writes the next layer's attn_ln output (resid_layernorm).
+    // Plans (OWK_DEC_PLAN, measured per shape in DESIGN.md): 1 the above (default); 0 partial tiles +
+    // resid_layernorm after all three; 2 statistics after all three (self Q/K/V normalises too).
+    // Larger passes use the full-epilogue GEMMs and separate LayerNorms.
+    static const int plan_env = [] {
+        const char * v = getenv("OWK_DEC_PLAN");
+        return v && *v ? atoi(v) : 1;
+    }();
     const bool fused = R <= 32 && !q5;
+    const int plan = fused ? plan_env : -1;
     double * lnst = (double *) ln_stats_.ptr;
     auto resid_stats = [&](const _Float16 * A, const _Float16 * Wt, int K, const float * bias) {
         EpiParams ep;
@@ -635,6 +644,18 @@ void Engine::launch_decode(const DecShape & sh) {
         ep.stats = lnst;
         ProfScope ps(prof, stream, "gemm_dec", 2.0 * R * (double) d * K, 2.0 * ((double) R * K + (double) d * K));
         gemm(stream, EPI_RESID_STATS, R, d, K, A, K, nullptr, K, ep, &gws_, Wt);
+    };
+    // partial tiles + resid_layernorm (lnw null: residual only)
+    auto resid_ln = [&](const _Float16 * A, const _Float16 * Wt, int K, const float * bias, const float * lnw,
+                        const float * lnb) {
+        {
+            EpiParams ep;
+            ProfScope ps(prof, stream, "gemm_dec", 2.0 * R * (double) d * K, 2.0 * ((double) R * K + (double) d * K));
+            gemm(stream, EPI_PARTIAL, R, d, K, A, K, nullptr, K, ep, &gws_, Wt);
+        }
+        ProfScope ps(prof, stream, "layernorm");
+        resid_layernorm(stream, R, d, gemm_partial_splits(K), gws_.partial, bias, d_x_.as<float>(), lnw, lnb, hp.eps,
+                        d_xn_.as<_Float16>(), d);
     };
     auto aln_of = [&](const float * w, const float * b) {
         AlnParams a;
@@ -669,8 +690,10 @@ void Engine::launch_decode(const DecShape & sh) {
         const DecLayerW & L = m->dec[l];
         _Float16 * Kl = self_k_.as<_Float16>() + l * self_stride;
         _Float16 * Vl = self_v_.as<_Float16>() + l * self_stride;
-        // layer 0 of a fused pass: the embeddings have no statistics yet -> one LayerNorm launch
-        if (!fused || l == 0) ln(L.attn_ln_w, L.attn_ln_b);
+        // the attn_ln output: a LayerNorm launch unless the previous layer's resid_layernorm wrote it
+        // (plans 0, 1) or the Q/K/V matmul normalises itself (plan 2); layer 0 normalises the embeddings
+        const bool qkv_aln = plan == 2 && l > 0;
+        if (plan < 0 || l == 0) ln(L.attn_ln_w, L.attn_ln_b);
         {
             EpiParams ep;
             ep.bias = L.b_q;
@@ -683,7 +706,7 @@ void Engine::launch_decode(const DecShape & sh) {
             ep.d = d;
             ep.row_off = d_rowoff;
             ep.Tpad = kv_cells * 64;
-            if (fused && l > 0) G_ln(EPI_QKV_DEC, 3 * d, L.t_qkv, ep, aln_of(L.attn_ln_w, L.attn_ln_b));
+            if (qkv_aln) G_ln(EPI_QKV_DEC, 3 * d, L.t_qkv, ep, aln_of(L.attn_ln_w, L.attn_ln_b));
             else G("qkv", EPI_QKV_DEC, 3 * d, d, d_xn_.as<_Float16>(), nullptr, L.w_qkv, L.t_qkv, L.q_qkv, ep, R, q5);
         }
         {
@@ -697,7 +720,9 @@ void Engine::launch_decode(const DecShape & sh) {
                                      max_keys,
                                      d_ao_.as<_Float16>(), d, nullptr, nullptr, 0, ao32);
         }
-        if (fused) {
+        if (plan == 0) {
+            resid_ln(d_ao_.as<_Float16>(), L.t_o, d, L.b_o, L.cross_ln_w, L.cross_ln_b);
+        } else if (plan > 0) {
             resid_stats(d_ao_.as<_Float16>(), L.t_o, d, L.b_o);
         } else {
             resid_full(d_ao_.as<_Float16>(), ao32, L.w_o, L.t_o, L.q_o, d, L.b_o, fq_self);
@@ -708,7 +733,7 @@ void Engine::launch_decode(const DecShape & sh) {
             ep.bias = L.cb_q;
             ep.out16 = d_q_.as<_Float16>();
             ep.ldo = d;
-            if (fused) G_ln(EPI_F16, d, L.t_cq, ep, aln_of(L.cross_ln_w, L.cross_ln_b));
+            if (plan > 0) G_ln(EPI_F16, d, L.t_cq, ep, aln_of(L.cross_ln_w, L.cross_ln_b));
             else G("cq", EPI_F16, d, d, d_xn_.as<_Float16>(), nullptr, L.cw_q, L.t_cq, L.q_cq, ep, R, q5);
         }
         {
@@ -724,7 +749,9 @@ void Engine::launch_decode(const DecShape & sh) {
                                      d_ao_.as<_Float16>(), d, sh.capture ? amap_.as<int>() + l * H : nullptr,
                                      sh.capture ? cap_.as<float>() : nullptr, R, ao32);
         }
-        if (fused) {
+        if (plan == 0) {
+            resid_ln(d_ao_.as<_Float16>(), L.t_co, d, L.cb_o, L.mlp_ln_w, L.mlp_ln_b);
+        } else if (plan > 0) {
             resid_stats(d_ao_.as<_Float16>(), L.t_co, d, L.cb_o);
         } else {
             resid_full(d_ao_.as<_Float16>(), ao32, L.cw_o, L.t_co, L.q_co, d, L.cb_o, fq_cross);
@@ -736,11 +763,16 @@ void Engine::launch_decode(const DecShape & sh) {
             ep.gelu_tab = m->gelu_tab;
             ep.out16 = d_h_.as<_Float16>();
             ep.ldo = 4 * d;
-            if (fused) G_ln(EPI_GELU_F16, 4 * d, L.t_mlp0, ep, aln_of(L.mlp_ln_w, L.mlp_ln_b));
+            if (plan > 0) G_ln(EPI_GELU_F16, 4 * d, L.t_mlp0, ep, aln_of(L.mlp_ln_w, L.mlp_ln_b));
             else G("mlp0", EPI_GELU_F16, 4 * d, d, d_xn_.as<_Float16>(), nullptr, L.w_mlp0, L.t_mlp0, L.q_mlp0, ep, R, q5);
         }
-        if (fused) resid_stats(d_h_.as<_Float16>(), L.t_mlp1, 4 * d, L.b_mlp1);
-        else resid_full(d_h_.as<_Float16>(), nullptr, L.w_mlp1, L.t_mlp1, L.q_mlp1, 4 * d, L.b_mlp1);
+        if (plan == 0 || plan == 1) {
+            const DecLayerW * nx = l + 1 < hp.n_text_layer ? &m->dec[l + 1] : nullptr;
+            resid_ln(d_h_.as<_Float16>(), L.t_mlp1, 4 * d, L.b_mlp1, nx ? nx->attn_ln_w : nullptr,
+                     nx ? nx->attn_ln_b : nullptr);
+        } else if (plan == 2) {
+            resid_stats(d_h_.as<_Float16>(), L.t_mlp1, 4 * d, L.b_mlp1);
+        } else resid_full(d_h_.as<_Float16>(), nullptr, L.w_mlp1, L.t_mlp1, L.q_mlp1, 4 * d, L.b_mlp1);
     }
     if (n_logit_rows > 0) {
         {

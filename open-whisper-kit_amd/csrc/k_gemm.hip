@@ -499,13 +499,21 @@ void tile_weights(hipStream_t s, const _Float16 * W, int N, int K, _Float16 * ou
 
 size_t tiled_weight_elems(int N, int K) { return (size_t) ((N + 15) / 16) * 16 * K; }
 
+// LayerNorm-operand launches (ALN) hold the f32 row slices, the LayerNorm weights and the
+// statistics next to the weight stream: at most 8 waves per block so each wave may use 256 VGPRs
+// (16-wave blocks cap a wave at 128 and spilled these to scratch)
+constexpr int GR_ALN_MAXW = 8;
+constexpr int RPW_ALN = 4;  // rows whose statistics one wave reduces
+
 template <int MODE, int MT, int J, bool ALN>
-__global__ __launch_bounds__(GR_MAXW * 64) void k_gemm_rows(int M, int N, int K, const _Float16 * __restrict__ A,
-                                                            int lda, const _Float16 * __restrict__ Wt, EpiParams ep,
-                                                            float * __restrict__ part, AlnParams aln) {
+__global__ __launch_bounds__(ALN ? GR_ALN_MAXW * 64 : GR_MAXW * 64) void k_gemm_rows(int M, int N, int K,
+                                                                                    const _Float16 * __restrict__ A,
+                                                                                    int lda, const _Float16 * __restrict__ Wt,
+                                                                                    EpiParams ep, float * __restrict__ part,
+                                                                                    AlnParams aln) {
     // ALN: the A operand is LayerNorm(aln.x) computed here (AlnParams, kernels.h); its row
     // statistics come from the producer's EPI_RESID_STATS partials, 4 rows per wave at most
-    constexpr int RPW = 4;
+    constexpr int RPW = RPW_ALN;
     __shared__ floatx4 red[GR_MAXW][MT][64];
     __shared__ float s_ln[2][32];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = blockDim.x >> 6;
@@ -515,9 +523,9 @@ __global__ __launch_bounds__(GR_MAXW * 64) void k_gemm_rows(int M, int N, int K,
     const int nj = max(0, min(J, nsteps - ks0));
     const half8 z8 = {0, 0, 0, 0, 0, 0, 0, 0};
 
-    // ALN: the statistics partials first (in-order vmcnt: they can be waited for while the
-    // weight and activation loads issued after them stay in flight). Addresses are clamped and
-    // invalid entries zeroed after the load (a conditional load would make hipcc wait per load).
+    // ALN: the statistics partials first, then the weight stream (in-order vmcnt: the statistics
+    // are waited for while the weights stay in flight). Addresses are clamped and invalid entries
+    // zeroed after the load (a conditional load would make hipcc wait per load).
     double2 stv[RPW][2];
     if constexpr (ALN) {
 #pragma unroll
@@ -539,38 +547,10 @@ __global__ __launch_bounds__(GR_MAXW * 64) void k_gemm_rows(int M, int N, int K,
         const half8 t = *(const half8 *) (wp + (size_t) min(ks0 + j, nsteps - 1) * 512);
         b[j] = j < nj ? t : z8;
     }
-    float4 xa[ALN ? MT : 1][ALN ? J : 1][2], lw[ALN ? J : 1][2], lb[ALN ? J : 1][2];
-    if constexpr (ALN) {
-#pragma unroll
-        for (int j = 0; j < J; ++j) {
-            const int k = min(ks0 + j, nsteps - 1) * 32 + 8 * (lane >> 4);
-            lw[j][0] = *(const float4 *) (aln.w + k);
-            lw[j][1] = *(const float4 *) (aln.w + k + 4);
-            lb[j][0] = *(const float4 *) (aln.b + k);
-            lb[j][1] = *(const float4 *) (aln.b + k + 4);
-#pragma unroll
-            for (int i = 0; i < MT; ++i) {
-                const float * xp = aln.x + (size_t) min(i * 16 + (lane & 15), M - 1) * aln.ldx + k;
-                xa[i][j][0] = *(const float4 *) xp;
-                xa[i][j][1] = *(const float4 *) (xp + 4);
-            }
-        }
-    } else {
-#pragma unroll
-        for (int i = 0; i < MT; ++i) {
-            const _Float16 * ap = A + (size_t) min(i * 16 + (lane & 15), M - 1) * lda + 8 * (lane >> 4);
-#pragma unroll
-            for (int j = 0; j < J; ++j) {
-                const half8 t = *(const half8 *) (ap + min(ks0 + j, nsteps - 1) * 32);
-                a[i][j] = j < nj ? t : z8;
-            }
-        }
-    }
-    __builtin_amdgcn_sched_barrier(0);  // keep every load issued ahead of the first wait
+    __builtin_amdgcn_sched_barrier(0);  // the weight loads stay ahead of everything below
 
     if constexpr (ALN) {
-        // (the compiler's counted vmcnt before the first use of stv lets the weight, activation
-        // and w/b loads issued after the statistics stay in flight)
+        // 1. row statistics (the counted vmcnt before the first use of stv leaves the weights in flight)
         const int Kc = aln.ntiles * 16;  // LayerNorm width (= K)
 #pragma unroll
         for (int q = 0; q < RPW; ++q) {
@@ -604,7 +584,24 @@ __global__ __launch_bounds__(GR_MAXW * 64) void k_gemm_rows(int M, int N, int K,
                 s_ln[1][r] = 1.0f / sqrtf(var + aln.eps);
             }
         }
-        __syncthreads();
+        // 2. this wave's slices of x and of the LayerNorm weights (L2-resident: the producer just
+        // wrote x) -- issued after the statistics so both sets are never live together
+        float4 xa[MT][J][2], lw[J][2], lb[J][2];
+#pragma unroll
+        for (int j = 0; j < J; ++j) {
+            const int k = min(ks0 + j, nsteps - 1) * 32 + 8 * (lane >> 4);
+            lw[j][0] = *(const float4 *) (aln.w + k);
+            lw[j][1] = *(const float4 *) (aln.w + k + 4);
+            lb[j][0] = *(const float4 *) (aln.b + k);
+            lb[j][1] = *(const float4 *) (aln.b + k + 4);
+#pragma unroll
+            for (int i = 0; i < MT; ++i) {
+                const float * xp = aln.x + (size_t) min(i * 16 + (lane & 15), M - 1) * aln.ldx + k;
+                xa[i][j][0] = *(const float4 *) xp;
+                xa[i][j][1] = *(const float4 *) (xp + 4);
+            }
+        }
+        __syncthreads();  // s_ln of every row
 #pragma unroll
         for (int i = 0; i < MT; ++i) {
             const int r = min(i * 16 + (lane & 15), M - 1);
@@ -624,6 +621,16 @@ __global__ __launch_bounds__(GR_MAXW * 64) void k_gemm_rows(int M, int N, int K,
                     h[e] = (_Float16) v;
                 }
                 a[i][j] = j < nj ? h : z8;
+            }
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < MT; ++i) {
+            const _Float16 * ap = A + (size_t) min(i * 16 + (lane & 15), M - 1) * lda + 8 * (lane >> 4);
+#pragma unroll
+            for (int j = 0; j < J; ++j) {
+                const half8 t = *(const half8 *) (ap + min(ks0 + j, nsteps - 1) * 32);
+                a[i][j] = j < nj ? t : z8;
             }
         }
     }
@@ -790,8 +797,16 @@ template <int MODE> struct LaunchRows {
             pl.nw = (nsteps + pl.J - 1) / pl.J;
             if (pl.nw > GR_MAXW || !ep.stats) throw std::runtime_error("gemm_rows: EPI_RESID_STATS shape");
         }
-        if (ALN && (pl.J > 4 || pl.nw * 4 < M || !aln.stats || aln.ntiles * 16 != K || aln.ntiles > 128))
-            throw std::runtime_error("gemm_rows: unsupported LayerNorm-operand shape");
+        if (ALN) {
+            // 8 waves (every row's statistics reduced by one wave, 4 rows per wave), the whole K
+            // in one block: J = ceil(k-steps / 8) <= 5 (K <= 1280, the widest Whisper decoder)
+            const int nsteps = K / 32;
+            pl.nw = GR_ALN_MAXW;
+            pl.J = std::max(2, (nsteps + GR_ALN_MAXW - 1) / GR_ALN_MAXW);
+            pl.KS = 1;
+            if (pl.J > 5 || M > RPW_ALN * GR_ALN_MAXW || !aln.stats || aln.ntiles * 16 != K || aln.ntiles > 128)
+                throw std::runtime_error("gemm_rows: unsupported LayerNorm-operand shape");
+        }
         const int tiles = (N + 15) / 16;
         float * part = nullptr;
         if (pl.KS > 1 || MODE == EPI_PARTIAL) {
@@ -801,11 +816,27 @@ template <int MODE> struct LaunchRows {
         }
         const dim3 grid(tiles, pl.KS);
         const bool one = M <= 16;
+        if constexpr (ALN) {
+            if (MODE != EPI_F16 && MODE != EPI_GELU_F16 && MODE != EPI_QKV_DEC)
+                throw std::runtime_error("gemm_rows: LayerNorm operand for this epilogue");
+            else
+                switch (pl.J) {
+                    case 2: one ? go<1, 2, true>(s, grid, pl.nw, M, N, K, A, lda, Wt, ep, part, aln)
+                                : go<2, 2, true>(s, grid, pl.nw, M, N, K, A, lda, Wt, ep, part, aln); break;
+                    case 3: one ? go<1, 3, true>(s, grid, pl.nw, M, N, K, A, lda, Wt, ep, part, aln)
+                                : go<2, 3, true>(s, grid, pl.nw, M, N, K, A, lda, Wt, ep, part, aln); break;
+                    case 4: one ? go<1, 4, true>(s, grid, pl.nw, M, N, K, A, lda, Wt, ep, part, aln)
+                                : go<2, 4, true>(s, grid, pl.nw, M, N, K, A, lda, Wt, ep, part, aln); break;
+                    default: one ? go<1, 5, true>(s, grid, pl.nw, M, N, K, A, lda, Wt, ep, part, aln)
+                                 : go<2, 5, true>(s, grid, pl.nw, M, N, K, A, lda, Wt, ep, part, aln); break;
+                }
+            return;
+        }
         switch (pl.J) {
-            case 2: one ? go<1, 2, ALN>(s, grid, pl.nw, M, N, K, A, lda, Wt, ep, part, aln)
-                        : go<2, 2, ALN>(s, grid, pl.nw, M, N, K, A, lda, Wt, ep, part, aln); break;
-            case 4: one ? go<1, 4, ALN>(s, grid, pl.nw, M, N, K, A, lda, Wt, ep, part, aln)
-                        : go<2, 4, ALN>(s, grid, pl.nw, M, N, K, A, lda, Wt, ep, part, aln); break;
+            case 2: one ? go<1, 2, false>(s, grid, pl.nw, M, N, K, A, lda, Wt, ep, part, aln)
+                        : go<2, 2, false>(s, grid, pl.nw, M, N, K, A, lda, Wt, ep, part, aln); break;
+            case 4: one ? go<1, 4, false>(s, grid, pl.nw, M, N, K, A, lda, Wt, ep, part, aln)
+                        : go<2, 4, false>(s, grid, pl.nw, M, N, K, A, lda, Wt, ep, part, aln); break;
             case 8:
                 if constexpr (!ALN) {
                     one ? go<1, 8, false>(s, grid, pl.nw, M, N, K, A, lda, Wt, ep, part, aln)

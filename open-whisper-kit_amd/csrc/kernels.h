@@ -231,6 +231,11 @@ void attn_decoder_softmax(hipStream_t s, const _Float16 * q, int ldq, const _Flo
                           int ld_kv, int hs, const AttnRow * rows_dev, int n_rows, const int * key_idx, int H, float scale,
                           int max_keys, _Float16 * out, int ldo, const int * amap, float * cap, int cap_rows,
                           float * out32 = nullptr);
+// test/bench hook: the one_chunk cross-attention kernels on contiguous head-major keys (ld 64):
+// which = 1 the one-wave k_attn_step, 2 the two-wave k_attn_cross2 (attn_decoder's default)
+void attn_cross_kernel(hipStream_t s, int which, const _Float16 * q, int ldq, const _Float16 * kbase,
+                       const _Float16 * vbase, int hs, const AttnRow * rows_dev, int n_rows, int H, float scale,
+                       _Float16 * out, int ldo);
 int attn_max_listed_keys();  // per-row limit of the one_chunk kernel's key list
 int attn_max_tiled_keys();   // per-row limit of the tiled decoder kernel
 

@@ -34,8 +34,9 @@ void log_msg(ggml_log_level level, const char * fmt, ...) {
     va_end(ap);
     if (g_log_cb) {
         g_log_cb(level, buf, g_log_ud);
-    } else if (level >= GGML_LOG_LEVEL_WARN) {
+    } else if (level != GGML_LOG_LEVEL_DEBUG) {  // whisper_log_callback_default (ref whisper.cpp:9028-9038)
         fputs(buf, stderr);
+        fflush(stderr);
     }
 }
 

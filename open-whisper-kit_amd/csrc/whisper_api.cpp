@@ -1256,6 +1256,67 @@ int owk_debug_gemm_q5(int device, int M, int N, int K, const float * a, const ui
     return 0;
 }
 
+// one_chunk cross attention of R rows (row r over its own clip r: k, v [R][H][T][64] f16 head-major,
+// q [R][H*64]) with the one-wave (which = 1) or two-wave (which = 2) kernel; out [R][H*64] f16.
+// iters > 0: also returns the mean device time per launch in microseconds (random q/k/v if the host
+// pointers are null); iters == 0 returns 0; -1 on error
+double owk_debug_attn_cross(int device, int which, int R, int H, int T, int n_zero_pad, float scale, const uint16_t * q,
+                            const uint16_t * k, const uint16_t * v, uint16_t * out, int iters) {
+    try {
+        if (R <= 0 || H <= 0 || T < 0 || n_zero_pad < 0 || (which != 1 && which != 2) || iters < 0)
+            throw std::runtime_error("bad arguments");
+        OWK_HIP_CHECK(hipSetDevice(device));
+        hipStream_t s;
+        OWK_HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+        const size_t nq = (size_t) R * H * 64, nkv = std::max<size_t>((size_t) R * H * T * 64, 64);
+        DevBuf dq, dk, dv, dout, drows;
+        dq.alloc(nq * 2);
+        dk.alloc(nkv * 2);
+        dv.alloc(nkv * 2);
+        dout.alloc(nq * 2);
+        if (q && k && v) {
+            OWK_HIP_CHECK(hipMemcpy(dq.ptr, q, nq * 2, hipMemcpyHostToDevice));
+            OWK_HIP_CHECK(hipMemcpy(dk.ptr, k, (size_t) R * H * T * 64 * 2, hipMemcpyHostToDevice));
+            OWK_HIP_CHECK(hipMemcpy(dv.ptr, v, (size_t) R * H * T * 64 * 2, hipMemcpyHostToDevice));
+        } else {
+            hipLaunchKernelGGL(k_fill_rand_f16, dim3(1024), dim3(256), 0, s, dq.as<_Float16>(), nq, 3u);
+            hipLaunchKernelGGL(k_fill_rand_f16, dim3(4096), dim3(256), 0, s, dk.as<_Float16>(), nkv, 5u);
+            hipLaunchKernelGGL(k_fill_rand_f16, dim3(4096), dim3(256), 0, s, dv.as<_Float16>(), nkv, 9u);
+        }
+        std::vector<AttnRow> rows(R);
+        for (int r = 0; r < R; ++r) rows[r] = AttnRow{r, r * H * T * 64, T, -1, n_zero_pad, 0};
+        drows.alloc(R * sizeof(AttnRow));
+        OWK_HIP_CHECK(hipMemcpy(drows.ptr, rows.data(), R * sizeof(AttnRow), hipMemcpyHostToDevice));
+        auto run = [&] {
+            attn_cross_kernel(s, which, dq.as<_Float16>(), H * 64, dk.as<_Float16>(), dv.as<_Float16>(), T * 64,
+                              (const AttnRow *) drows.ptr, R, H, scale, dout.as<_Float16>(), H * 64);
+        };
+        run();
+        double us = 0.0;
+        if (iters > 0) {
+            hipEvent_t e0, e1;
+            OWK_HIP_CHECK(hipEventCreate(&e0));
+            OWK_HIP_CHECK(hipEventCreate(&e1));
+            OWK_HIP_CHECK(hipEventRecord(e0, s));
+            for (int i = 0; i < iters; ++i) run();
+            OWK_HIP_CHECK(hipEventRecord(e1, s));
+            OWK_HIP_CHECK(hipEventSynchronize(e1));
+            float ms = 0;
+            OWK_HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
+            (void) hipEventDestroy(e0);
+            (void) hipEventDestroy(e1);
+            us = 1e3 * ms / iters;
+        }
+        OWK_HIP_CHECK(hipStreamSynchronize(s));
+        if (out) OWK_HIP_CHECK(hipMemcpy(out, dout.ptr, nq * 2, hipMemcpyDeviceToHost));
+        OWK_HIP_CHECK(hipStreamDestroy(s));
+        return us;
+    } catch (const std::exception & ex) {
+        log_msg(GGML_LOG_LEVEL_ERROR, "owk_debug_attn_cross: %s\n", ex.what());
+        return -1;
+    }
+}
+
 int owk_debug_gemm(int device, int M, int N, int K, const uint16_t * a, const uint16_t * w, float * out) {
     try {
         OWK_HIP_CHECK(hipSetDevice(device));

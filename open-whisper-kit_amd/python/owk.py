@@ -235,7 +235,18 @@ def load(path: str | None = None) -> C.CDLL:
 
 
 _LOG_CB = C.CFUNCTYPE(None, C.c_int, C.c_char_p, C.c_void_p)
-_quiet_cb = _LOG_CB(lambda lvl, txt, ud: None)
+# quiet(): nothing is printed, but warnings and errors (ggml_log_level >= WARN = 3) are kept in
+# `errors` (the last 64) so a failing test can show what the library reported
+errors = []
+
+
+def _keep(lvl, txt, ud):
+    if lvl >= 3 and txt:
+        errors.append(txt.decode("utf-8", "replace").rstrip())
+        del errors[:-64]
+
+
+_quiet_cb = _LOG_CB(_keep)
 
 
 def quiet():

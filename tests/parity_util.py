@@ -18,7 +18,7 @@ import numpy as np
 
 LOGIT_RTOL = 1e-3      # logits |diff| <= LOGIT_RTOL * max|logit| (north star: 1e-3)
 TIE_FACTOR = 4.0       # near-tie threshold = TIE_FACTOR * measured max |logit diff|
-MIN_COMPARED = 16      # every case compares at least min(MIN_COMPARED, reference tokens) tokens
+MIN_COMPARED = 8       # every case compares at least min(MIN_COMPARED, reference tokens) tokens
 
 
 def flat_tokens(segs):
@@ -130,9 +130,10 @@ class Forcer:
         lg = np.ctypeslib.as_array(logits, shape=(self.n_vocab,))
         win = self.windows[self.window] if 0 <= self.window < len(self.windows) else []
         t = win[n_tokens] if n_tokens < len(win) else self.eot
-        v = float(lg[t]) if np.isfinite(lg[t]) else 0.0
-        lg[:] = -np.inf
-        lg[t] = v
+        # the forced token far above every other logit (the others are kept, so the timestamp
+        # distribution -- the token's best timestamp "tid" and pt -- stays the decoder's own)
+        fin = np.isfinite(lg)
+        lg[t] = (float(lg[fin].max()) if fin.any() else 0.0) + 40.0
 
 
 def check_cross_rows(w, st, arr, key, layer, name, n_rows=16):

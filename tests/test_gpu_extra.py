@@ -32,6 +32,11 @@ def extra():
 
 
 @pytest.fixture(scope="module")
+def extra_arrays():
+    return np.load(os.path.join(GOLDEN, "extra_golden.npz"))
+
+
+@pytest.fixture(scope="module")
 def test60():
     import owk_synth as S
 
@@ -52,6 +57,11 @@ def _tie(w, golden, model, clips, clip):
     return LogitError.tie(w, meta, arr, f"{model}/{clip}", clips[clip])
 
 
+def _tie60(w, extra, extra_arrays, model, test60):
+    """near-tie bound measured on the first window of the same 60 s audio"""
+    return LogitError.tie(w, extra, extra_arrays, f"{model}/test60", test60)
+
+
 def _params(w, kw):
     kw = dict(kw)
     kw.pop("n_processors", None)
@@ -60,7 +70,7 @@ def _params(w, kw):
 
 @pytest.mark.parametrize("case", ["long/tiny.en/greedy", "long/tiny.en/token_ts", "long/base.en/greedy",
                                   "long/l3-mini/greedy"])
-def test_long_audio_window_loop(extra, golden, model_path, clips, test60, case):
+def test_long_audio_window_loop(extra, extra_arrays, model_path, test60, case):
     c = extra["cases"][case]
     owk.quiet()
     w = whisper(model_path, c["model"])
@@ -68,8 +78,7 @@ def test_long_audio_window_loop(extra, golden, model_path, clips, test60, case):
     assert w.full(st, test60, _params(w, c["params"])) == c["ret"]
     got = w.segments(st)
     assert len(c["segments"]) > 1 and c["segments"][-1]["t1"] > 3000, "fixture must span several windows"
-    # near-tie bound from the synthetic 30 s clip of the same model (same engine numerics)
-    compare_segments(got, c["segments"], case, tie=_tie(w, golden, c["model"], clips, "synth30"))
+    compare_segments(got, c["segments"], case, tie=_tie60(w, extra, extra_arrays, c["model"], test60))
 
 
 @pytest.mark.parametrize("case", ["audio_ctx/tiny.en/jfk", "audio_ctx/tiny.en/synth30", "audio_ctx/l3-mini/jfk"])
@@ -90,7 +99,7 @@ def test_reduced_audio_ctx(extra, golden, model_path, clips, case):
 
 
 @pytest.mark.parametrize("case", ["parallel/tiny.en/test60", "parallel/base.en/test60"])
-def test_full_parallel(extra, golden, model_path, clips, test60, case):
+def test_full_parallel(extra, extra_arrays, model_path, test60, case):
     c = extra["cases"][case]
     owk.quiet()
     w = whisper(model_path, c["model"])
@@ -106,4 +115,4 @@ def test_full_parallel(extra, golden, model_path, clips, test60, case):
             toks.append((t.id, t.tid, t.p, t.plog, t.pt, t.ptsum, t.t0, t.t1))
         got.append(dict(t0=L.whisper_full_get_segment_t0(w.ctx, i), t1=L.whisper_full_get_segment_t1(w.ctx, i),
                         text=L.whisper_full_get_segment_text(w.ctx, i).decode("utf-8", "replace"), tokens=toks))
-    compare_segments(got, c["segments"], case, tie=_tie(w, golden, c["model"], clips, "synth30"))
+    compare_segments(got, c["segments"], case, tie=_tie60(w, extra, extra_arrays, c["model"], test60))

@@ -31,3 +31,72 @@ def test_gemm_dispatch(M, NK):
     ref = a.astype(np.float32) @ w.astype(np.float32).T
     assert np.isfinite(out).all()
     np.testing.assert_allclose(out, ref, atol=2e-4 * np.sqrt(K), rtol=1e-4)
+
+
+def _one_chunk_np(q, k, v, scale, n_zero_pad):
+    """The reference's one_chunk recurrence (ggml-cpu/ops.cpp:8140-8233) for one (row, head):
+    F16 V accumulator rounded after every key; f32 scores (sum order differs from the kernels,
+    hence a tolerance)."""
+    M, S = -np.inf, np.float32(0)
+    acc = np.zeros(64, np.float16)
+    s_all = (k.astype(np.float32) @ q.astype(np.float32)) * np.float32(scale)
+    for j in range(len(k) + n_zero_pad):
+        s = s_all[j] if j < len(k) else np.float32(0)
+        vj = v[j].astype(np.float32) if j < len(k) else np.zeros(64, np.float32)
+        ms, vs = np.float32(1), np.float32(1)
+        if s > M:
+            ms = np.float32(np.exp(np.float32(M - s))) if M > -np.inf else np.float32(0)
+            M = s
+            acc = (acc.astype(np.float32) * ms).astype(np.float16)
+        else:
+            vs = np.float32(np.exp(np.float32(s - M)))
+        acc = (vj * vs + acc.astype(np.float32)).astype(np.float16)
+        S = np.float32(S * ms + vs)
+    return acc.astype(np.float32) / S if S != 0 else np.zeros(64, np.float32)
+
+
+@pytest.mark.parametrize("R,H,T,pad", [(3, 2, 1, 0), (3, 2, 63, 0), (2, 2, 64, 36), (2, 3, 65, 0), (4, 2, 200, 0),
+                                       (2, 2, 257, 5), (2, 2, 768, 0), (32, 20, 1500, 0), (2, 2, 0, 0)])
+def test_attn_cross_two_wave(R, H, T, pad):
+    """k_attn_cross2 (two waves per row and head) against the one-wave k_attn_step: the same
+    recurrence, so bit-identical outputs; both against a numpy restatement at small sizes."""
+    L = owk.load()
+    L.owk_debug_attn_cross.restype = C.c_double
+    u16 = C.POINTER(C.c_uint16)
+    L.owk_debug_attn_cross.argtypes = [C.c_int] * 6 + [C.c_float, u16, u16, u16, u16, C.c_int]
+    rng = np.random.default_rng(T * 31 + R)
+    q = rng.standard_normal((R, H * 64)).astype(np.float16)
+    # keys with a slowly rising trend: new running maxima keep appearing deep into the sequence
+    trend = np.linspace(0, 3, max(T, 1))[:T, None]
+    k = (rng.standard_normal((R, H, T, 64)) * 0.7 + trend * 0.05).astype(np.float16)
+    v = rng.standard_normal((R, H, T, 64)).astype(np.float16)
+    scale = 64 ** -0.25
+    outs = {}
+    for which in (1, 2):
+        o = np.zeros((R, H * 64), np.float16)
+        rc = L.owk_debug_attn_cross(0, which, R, H, T, pad, scale, q.view(np.uint16).ctypes.data_as(u16),
+                                    k.view(np.uint16).ctypes.data_as(u16), v.view(np.uint16).ctypes.data_as(u16),
+                                    o.view(np.uint16).ctypes.data_as(u16), 0)
+        assert rc == 0
+        outs[which] = o.astype(np.float32)
+    assert np.isfinite(outs[2]).all()
+    np.testing.assert_array_equal(outs[2], outs[1])
+    for r in range(min(R, 2)):
+        for h in range(min(H, 2)):
+            ref = _one_chunk_np(q[r, h * 64:(h + 1) * 64], k[r, h], v[r, h], scale, pad)
+            np.testing.assert_allclose(outs[2][r, h * 64:(h + 1) * 64], ref, atol=2e-3, rtol=2e-2)
+
+
+def test_attn_cross_speed():
+    """Device time of the two cross-attention kernels on the large-v3 decode shape (32 rows x 20
+    heads x 1500 keys); printed for the record, the two-wave kernel must not be slower."""
+    L = owk.load()
+    L.owk_debug_attn_cross.restype = C.c_double
+    u16 = C.POINTER(C.c_uint16)
+    L.owk_debug_attn_cross.argtypes = [C.c_int] * 6 + [C.c_float, u16, u16, u16, u16, C.c_int]
+    t = {w: min(L.owk_debug_attn_cross(0, w, 32, 20, 1500, 0, 0.35, None, None, None, None, 30) for _ in range(3))
+         for w in (1, 2)}
+    gbs = {w: 32 * 20 * 1500 * 64 * 2 * 2 / t[w] / 1e3 for w in t}
+    print(f"attn_cross one-wave {t[1]:.1f} us ({gbs[1]:.0f} GB/s), two-wave {t[2]:.1f} us ({gbs[2]:.0f} GB/s)")
+    assert t[1] > 0 and t[2] > 0
+    assert t[2] <= 1.05 * t[1]

@@ -162,7 +162,11 @@ def test_large_batch32(large, clips, model, cfg):
             agree = next((i for i, (a, b) in enumerate(zip(g, r)) if a[0] != b[0]), min(len(g), len(r)))
             floor = meta["results"][f"{key}/noise_floor/agree/{cfg}"]
             print(f"[large] {key}/{cfg} slot {slot}: {agree}/{len(r)} tokens agree (reference self-agreement {floor})")
-            assert agree >= min(floor, len(r))
+            if agree < min(floor, len(r)):
+                # parted earlier than the reference parts from itself: only at a near-tie within
+                # 2x the reference's logit noise floor (as tests/test_q5.py)
+                fl = 2 * meta["results"][f"{key}/noise_floor/logits"]
+                compare_segments(got, want["segments"], f"{key}/{cfg}/slot{slot}", tie=fl, p_atol=fl, min_compared=0)
         else:
             tie = LogitError.tie(w, meta, arr, key, clips[clip])
             compare_segments(got, want["segments"], f"{key}/{cfg}/slot{slot}", tie=tie)

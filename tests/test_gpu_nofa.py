@@ -97,17 +97,20 @@ def test_dtw_timestamps(nofa, model_path, clips, model, clip):
     assert w.full(st, clips[clip], p) == want["ret"]
     tie = LogitError.tie(w, meta, nofa[1], f"{model}/{clip}", clips[clip])
     _compare(w.segments(st), want["segments"], f"{model}/{clip}/dtw", tie=tie)
-    # t_dtw of the reference's own token sequence: teacher-force the (single-window) decode
-    r_ids = [t[0] for s in want["segments"] for t in s["tokens"]]
-    windows = meta["results"][f"{model}/{clip}/dtw_windows"]  # what the reference DECODED, per window
-    force = Forcer(windows, w.L.whisper_token_eot(w.ctx), w.n_vocab, owk.TokenData)
-    p.logits_filter_callback = C.cast(force.cfunc, C.c_void_p)
-    st = w.new_state()
-    assert w.full(st, clips[clip], p) == want["ret"]
     got = w.segments(st)
     g_ids = [t[0] for s in got for t in s["tokens"]]
-    assert force.calls > 0 and g_ids == r_ids, "teacher-forced decode did not reproduce the reference tokens"
-    assert [(s["t0"], s["t1"]) for s in got] == [(s["t0"], s["t1"]) for s in want["segments"]]
+    r_ids = [t[0] for s in want["segments"] for t in s["tokens"]]
+    if g_ids != r_ids:
+        # parted at a near-tie: t_dtw of the reference's own decoded sequence from a run
+        # teacher-forced onto it (per window, traced by make_golden_nofa_windows.py)
+        windows = meta["results"][f"{model}/{clip}/dtw_windows"]
+        force = Forcer(windows, w.L.whisper_token_eot(w.ctx), w.n_vocab, owk.TokenData)
+        p.logits_filter_callback = C.cast(force.cfunc, C.c_void_p)
+        st = w.new_state()
+        assert w.full(st, clips[clip], p) == want["ret"]
+        got = w.segments(st)
+        g_ids = [t[0] for s in got for t in s["tokens"]]
+        assert force.calls > 0 and g_ids == r_ids, "teacher-forced decode did not reproduce the reference tokens"
     g_dtw = [t[8] for s in got for t in s["tokens"]]
     r_dtw = [t[8] for s in want["segments"] for t in s["tokens"]]
     print(f"[dtw] {model}/{clip}: {len(r_dtw)} tokens compared")
@@ -123,7 +126,29 @@ def test_dtw_timestamps(nofa, model_path, clips, model, clip):
         ref_cap = arr[f"{model}/jfk/dtw_cap"]
         assert cap.shape == ref_cap.shape
         assert np.abs(cap - ref_cap).max() < 2e-5
-        assert not diff, f"t_dtw differs: {diff[:10]}"
+        if diff:
+            # a window with a handful of text tokens makes the DTW lattice degenerate (its path
+            # cost near-ties over hundreds of frames). Then the whole difference must come from the
+            # <= 2e-5 capture noise: the host DTW (pinned bit-exactly on the reference capture by
+            # test_dtw_cpu.py) maps the reference capture to the reference t_dtw and the GPU
+            # capture to the GPU t_dtw.
+            din = meta["results"][f"{model}/jfk/dtw_in"]
+            n_text = sum(1 for s in want["segments"] for t in s["tokens"] if t[0] < w.L.whisper_token_eot(w.ctx))
+            assert n_text < 8, f"t_dtw differs: {diff[:10]}"
+            L.owk_debug_dtw.argtypes = [C.POINTER(C.c_float), C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                        C.POINTER(C.c_int), C.c_int]
+
+            def host_dtw(c):
+                c = np.ascontiguousarray(c, np.float32)
+                out = np.zeros(4096, np.int32)
+                n = L.owk_debug_dtw(c.ctypes.data_as(C.POINTER(C.c_float)), din["n_ah"], 1500, din["n_tok"],
+                                    din["sot_len"], din["n_frames"], 7, out.ctypes.data_as(C.POINTER(C.c_int)), len(out))
+                return [2 * int(x) for x in out[:n]][:n_text]
+
+            eot = w.L.whisper_token_eot(w.ctx)
+            assert host_dtw(ref_cap) == [t[8] for s in want["segments"] for t in s["tokens"] if t[0] < eot]
+            assert host_dtw(cap) == [t[8] for s in got for t in s["tokens"] if t[0] < eot]
+            print(f"[dtw] {model}/jfk: degenerate {n_text}-token lattice, t_dtw moved by the capture noise: {diff}")
     else:
         assert all(abs(a - b) <= 20 and a >= 0 and b >= 0 for _, a, b in diff), f"t_dtw differs: {diff[:10]}"
         assert len(diff) <= 0.05 * len(r_dtw), f"t_dtw differs on {len(diff)}/{len(r_dtw)} tokens: {diff[:10]}"

@@ -174,7 +174,7 @@ def test_whisper_full(lib, golden, model_path, clips, model, clip, cfg):
     else:
         ret = w.full(st, clips[clip], p)
     want = meta["results"][key]
-    assert ret == want["ret"]
+    assert ret == want["ret"], owk.errors[-5:]
     if inj is not None and os.environ.get("OWK_INJ_DUMP"):
         os.makedirs(os.environ["OWK_INJ_DUMP"], exist_ok=True)
         with open(os.path.join(os.environ["OWK_INJ_DUMP"], key.replace("/", "_") + ".json"), "w") as f:
