@@ -45,23 +45,37 @@ CLIP_SAMPLES = 480000     # 30 s at 16 kHz
 # decode-step classes (weights or KV streamed once per step for 32 rows) are HBM-bound
 MFMA_CLASSES = {"gemm_enc", "gemm_cross", "gemm_conv", "gemm_dec_big", "gemm_logits_big", "attn_encoder"}
 MAX_TOKENS = 219          # completion at i >= max_tokens -> 220 tokens per clip
-# kernel symbol of each single-kernel class (for the PMC traffic lookup)
-CLASS_KERNEL = {"attn_cross": "k_attn_stepILb0ELb1", "attn_self": "k_attn_stepILb0ELb0", "attn_encoder": "k_attn_encoder"}
+# kernels of each class (mangled-name patterns, for the PMC traffic lookup): the decode-row GEMM
+# epilogue 7 (EPI_F32) is the logits matmul, every other decode-row launch is gemm_dec
+CLASS_KERNELS = {
+    "attn_cross": r"k_attn_cross2|k_attn_stepILb0ELb1E",
+    "attn_self": r"k_attn_stepILb[01]ELb0E",
+    "attn_encoder": r"k_attn_encoderE",
+    "gemm_dec": r"k_gemm_rowsILi(?!7E)\d+E|k_gemm_rows_reduceILi(?!7E)\d+E",
+    "gemm_logits": r"k_gemm_rowsILi7E",
+    "layernorm": r"k_layernorm_f16|k_resid_layernorm",
+    "gemm_enc": r"k_gemm_256|k_gemm_bigILi[0-6]E",
+}
 PMC_SUMMARY = os.path.join(ROOT, "profiles", "pmc_fetch_summary.txt")
 
 
 def pmc_traffic(cls):
     """HBM bytes per launch of `cls` from the committed rocprofv3 --pmc FETCH_SIZE pass of this
-    command (tools/gpu_pmc.sh -> profiles/pmc_fetch_summary.txt). FETCH_SIZE is in KB and on
-    gfx950 counts half the bytes of wide streaming reads (MI355X_MICROARCH.md, HBM): x 1024 x 2."""
-    sym = CLASS_KERNEL.get(cls)
-    if not sym or not os.path.exists(PMC_SUMMARY):
+    command (tools/gpu_pmc.sh -> profiles/pmc_fetch_summary.txt): the FETCH_SIZE total of the
+    class's kernels over their dispatch count. FETCH_SIZE is in KB and on gfx950 counts half the
+    bytes of wide streaming reads (MI355X_MICROARCH.md, HBM): x 1024 x 2."""
+    import re
+
+    pat = CLASS_KERNELS.get(cls)
+    if not pat or not os.path.exists(PMC_SUMMARY):
         return None
+    tot, n = 0.0, 0
     for line in open(PMC_SUMMARY):
-        parts = line.split()
-        if len(parts) == 4 and sym in parts[3] and parts[0].isdigit():
-            return round(float(parts[1]) * 1024 * 2)
-    return None
+        parts = line.split(None, 3)
+        if len(parts) == 4 and parts[0].isdigit() and re.search(pat, parts[3]):
+            n += int(parts[0])
+            tot += float(parts[2])
+    return round(tot / n * 1024 * 2) if n else None
 
 
 # the arithmetic each weight format computes in (kernels.h; DESIGN.md 2)

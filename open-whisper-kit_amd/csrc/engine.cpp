@@ -90,12 +90,22 @@ Engine::Engine(const Model * m_, Prof * prof_) : m(m_), prof(prof_) {
     gws_part_.alloc(std::max<size_t>(fl, 1) * 4);
     gws_.partial = gws_part_.as<float>();
     gws_.partial_floats = fl;
+    // the second decode row group (OWK_DEC_SPLIT): its own stream and split-K workspace
+    OWK_HIP_CHECK(hipStreamCreateWithFlags(&stream2_, hipStreamNonBlocking));
+    OWK_HIP_CHECK(hipEventCreateWithFlags(&ev_fork_, hipEventDisableTiming));
+    OWK_HIP_CHECK(hipEventCreateWithFlags(&ev_join_, hipEventDisableTiming));
+    gws2_part_.alloc(std::max<size_t>(fl, 1) * 4);
+    gws2_.partial = gws2_part_.as<float>();
+    gws2_.partial_floats = fl;
 }
 
 Engine::~Engine() {
     clear_graphs();
     for (auto * b : mel_) delete b;
     if (stream) (void) hipStreamDestroy(stream);
+    if (stream2_) (void) hipStreamDestroy(stream2_);
+    if (ev_fork_) (void) hipEventDestroy(ev_fork_);
+    if (ev_join_) (void) hipEventDestroy(ev_join_);
 }
 
 void Engine::sync() { OWK_HIP_CHECK(hipStreamSynchronize(stream)); }
@@ -427,7 +437,8 @@ uint64_t Engine::buffers_signature() const {
     uint64_t h = 1469598103934665603ull;
     for (const void * p : {d_x_.ptr, d_xn_.ptr, d_q_.ptr, d_ao_.ptr, d_h_.ptr, d_xl_.ptr, logits_.ptr, d_stg_.ptr,
                            q8a_.ptr, q8d_.ptr, d_xn32_.ptr, d_ao32_.ptr, d_xl32_.ptr,
-                           self_k_.ptr, self_v_.ptr, cross_k_.ptr, cross_v_.ptr, gws_part_.ptr, ln_stats_.ptr})
+                           self_k_.ptr, self_v_.ptr, cross_k_.ptr, cross_v_.ptr, gws_part_.ptr, gws2_part_.ptr,
+                           ln_stats_.ptr})
         h = (h ^ (uint64_t) (uintptr_t) p) * 1099511628211ull;
     return h;
 }
@@ -468,7 +479,7 @@ void Engine::decode(const std::vector<DecodeRow> & rows, const std::vector<int> 
             const int C = dec_rows_cap_;
             d_x_.alloc((size_t) C * d * 4);
             d_xn_.alloc((size_t) C * d * 2);
-            ln_stats_.alloc((size_t) (d / 16) * std::min(C, 32) * 16);
+            ln_stats_.alloc((size_t) (d / 16) * 32 * 16 * 2);  // two row groups of <= 32 rows (OWK_DEC_SPLIT)
             d_q_.alloc((size_t) C * d * 2);
             d_ao_.alloc((size_t) C * d * 2);
             d_h_.alloc((size_t) C * 4 * d * 2);
@@ -632,45 +643,122 @@ void Engine::launch_decode(const DecShape & sh) {
         const char * v = getenv("OWK_DEC_PLAN");
         return v && *v ? atoi(v) : 1;
     }();
+    // two row groups on two streams (OWK_DEC_SPLIT=1): each half runs the whole layer chain for
+    // its rows; one half's latency-bound launches overlap the other's HBM-bound attention. Rows
+    // are independent inside a pass (a row reads only KV cells written before the pass and its
+    // own cell), so the halves share no data until the logits.
+    static const bool split_env = [] {
+        const char * v = getenv("OWK_DEC_SPLIT");
+        return v && atoi(v) != 0;
+    }();
     const bool fused = R <= 32 && !q5;
     const int plan = fused ? plan_env : -1;
-    double * lnst = (double *) ln_stats_.ptr;
-    auto resid_stats = [&](const _Float16 * A, const _Float16 * Wt, int K, const float * bias) {
-        EpiParams ep;
-        ep.bias = bias;
-        ep.resid = d_x_.as<float>();
-        ep.out32 = d_x_.as<float>();
-        ep.ldo = d;
-        ep.stats = lnst;
-        ProfScope ps(prof, stream, "gemm_dec", 2.0 * R * (double) d * K, 2.0 * ((double) R * K + (double) d * K));
-        gemm(stream, EPI_RESID_STATS, R, d, K, A, K, nullptr, K, ep, &gws_, Wt);
-    };
-    // partial tiles + resid_layernorm (lnw null: residual only)
-    auto resid_ln = [&](const _Float16 * A, const _Float16 * Wt, int K, const float * bias, const float * lnw,
-                        const float * lnb) {
-        {
+
+    // the fused decoder (R <= 32, F16) over rows [r0, r0 + n) on stream s
+    auto fused_rows = [&](int r0, int n, hipStream_t s, const GemmWs * ws, double * lnst) {
+        float * x = d_x_.as<float>() + (size_t) r0 * d;
+        _Float16 * xn = d_xn_.as<_Float16>() + (size_t) r0 * d;
+        _Float16 * qb = d_q_.as<_Float16>();    // attention addresses rows by AttnRow::q_row (absolute)
+        _Float16 * aob = d_ao_.as<_Float16>();
+        _Float16 * qr = qb + (size_t) r0 * d;
+        _Float16 * aor = aob + (size_t) r0 * d;
+        _Float16 * hr = d_h_.as<_Float16>() + (size_t) r0 * 4 * d;
+        auto aln_of = [&](const float * w, const float * b) {
+            AlnParams a;
+            a.x = x;
+            a.ldx = d;
+            a.stats = lnst;
+            a.ntiles = d / 16;
+            a.w = w;
+            a.b = b;
+            a.eps = hp.eps;
+            return a;
+        };
+        auto gemm_rows = [&](int mode, int N, int K, const _Float16 * A, const _Float16 * Wt, const EpiParams & ep) {
+            ProfScope ps(prof, s, "gemm_dec", 2.0 * n * (double) N * K, 2.0 * ((double) n * K + (double) N * K));
+            gemm(s, mode, n, N, K, A, K, nullptr, K, ep, ws, Wt);
+        };
+        auto gemm_ln = [&](int mode, int N, const _Float16 * Wt, const EpiParams & ep, const AlnParams & aln) {
+            ProfScope ps(prof, s, "gemm_dec", 2.0 * n * (double) N * d, 2.0 * ((double) n * d + (double) N * d));
+            gemm_rows_ln(s, mode, n, N, d, aln, Wt, ep, ws);
+        };
+        // residual matmul, bias + residual in the epilogue, row statistics for the next LayerNorm
+        auto resid_stats = [&](const _Float16 * A, const _Float16 * Wt, int K, const float * bias) {
             EpiParams ep;
-            ProfScope ps(prof, stream, "gemm_dec", 2.0 * R * (double) d * K, 2.0 * ((double) R * K + (double) d * K));
-            gemm(stream, EPI_PARTIAL, R, d, K, A, K, nullptr, K, ep, &gws_, Wt);
+            ep.bias = bias;
+            ep.resid = x;
+            ep.out32 = x;
+            ep.ldo = d;
+            ep.stats = lnst;
+            gemm_rows(EPI_RESID_STATS, d, K, A, Wt, ep);
+        };
+        // residual matmul as partial tiles + resid_layernorm (lnw null: residual only)
+        auto resid_ln = [&](const _Float16 * A, const _Float16 * Wt, int K, const float * bias, const float * lnw,
+                            const float * lnb) {
+            gemm_rows(EPI_PARTIAL, d, K, A, Wt, EpiParams());
+            ProfScope ps(prof, s, "layernorm");
+            resid_layernorm(s, n, d, gemm_partial_splits(K), ws->partial, bias, x, lnw, lnb, hp.eps, xn, d);
+        };
+        for (int l = 0; l < hp.n_text_layer; ++l) {
+            const DecLayerW & L = m->dec[l];
+            _Float16 * Kl = self_k_.as<_Float16>() + l * self_stride;
+            _Float16 * Vl = self_v_.as<_Float16>() + l * self_stride;
+            {
+                EpiParams ep;
+                ep.bias = L.b_q;
+                ep.bias2 = L.b_v;
+                ep.scale = kq_scale;
+                ep.out16 = qr;
+                ep.ldo = d;
+                ep.out16b = Kl;
+                ep.out16c = Vl;
+                ep.d = d;
+                ep.row_off = d_rowoff + r0;
+                ep.Tpad = kv_cells * 64;
+                // the attn_ln output: from the previous layer's resid_layernorm (plans 0, 1; layer 0:
+                // the LayerNorm launch before the row groups) or normalised here (plan 2)
+                if (plan == 2 && l > 0) gemm_ln(EPI_QKV_DEC, 3 * d, L.t_qkv, ep, aln_of(L.attn_ln_w, L.attn_ln_b));
+                else gemm_rows(EPI_QKV_DEC, 3 * d, d, xn, L.t_qkv, ep);
+            }
+            {
+                ProfScope ps(prof, s, "attn_self");
+                attn_decoder(s, qb, d, Kl, Vl, 64, kv_cells * 64, d_rs + r0, n, d_keys, H, 1.0f, max_keys, aob, d,
+                             self_oc, self_tl, nullptr, sh.self_list, nullptr, nullptr);
+            }
+            if (plan == 0) resid_ln(aor, L.t_o, d, L.b_o, L.cross_ln_w, L.cross_ln_b);
+            else resid_stats(aor, L.t_o, d, L.b_o);
+            {
+                EpiParams ep;
+                ep.bias = L.cb_q;
+                ep.out16 = qr;
+                ep.ldo = d;
+                if (plan == 0) gemm_rows(EPI_F16, d, d, xn, L.t_cq, ep);
+                else gemm_ln(EPI_F16, d, L.t_cq, ep, aln_of(L.cross_ln_w, L.cross_ln_b));
+            }
+            {
+                ProfScope ps(prof, s, "attn_cross", 4.0 * n * (double) n_ctx_pad * d, 2.0 * 2.0 * n * (double) T * d);
+                attn_decoder(s, qb, d, cross_k_.as<_Float16>() + l * cross_stride, cross_v_.as<_Float16>() + l * cross_stride,
+                             64, T * 64, d_rc + r0, n, nullptr, H, kq_scale, T, aob, d, cross_oc, cross_tl, nullptr, true,
+                             nullptr, nullptr);
+            }
+            if (plan == 0) resid_ln(aor, L.t_co, d, L.cb_o, L.mlp_ln_w, L.mlp_ln_b);
+            else resid_stats(aor, L.t_co, d, L.cb_o);
+            {
+                EpiParams ep;
+                ep.bias = L.b_mlp0;
+                ep.gelu_tab = m->gelu_tab;
+                ep.out16 = hr;
+                ep.ldo = 4 * d;
+                if (plan == 0) gemm_rows(EPI_GELU_F16, 4 * d, d, xn, L.t_mlp0, ep);
+                else gemm_ln(EPI_GELU_F16, 4 * d, L.t_mlp0, ep, aln_of(L.mlp_ln_w, L.mlp_ln_b));
+            }
+            if (plan == 2) {
+                resid_stats(hr, L.t_mlp1, 4 * d, L.b_mlp1);
+            } else {
+                const DecLayerW * nx = l + 1 < hp.n_text_layer ? &m->dec[l + 1] : nullptr;
+                resid_ln(hr, L.t_mlp1, 4 * d, L.b_mlp1, nx ? nx->attn_ln_w : nullptr, nx ? nx->attn_ln_b : nullptr);
+            }
         }
-        ProfScope ps(prof, stream, "layernorm");
-        resid_layernorm(stream, R, d, gemm_partial_splits(K), gws_.partial, bias, d_x_.as<float>(), lnw, lnb, hp.eps,
-                        d_xn_.as<_Float16>(), d);
-    };
-    auto aln_of = [&](const float * w, const float * b) {
-        AlnParams a;
-        a.x = d_x_.as<float>();
-        a.ldx = d;
-        a.stats = lnst;
-        a.ntiles = d / 16;
-        a.w = w;
-        a.b = b;
-        a.eps = hp.eps;
-        return a;
-    };
-    auto G_ln = [&](int mode, int N, const _Float16 * Wt, const EpiParams & ep, const AlnParams & aln) {
-        ProfScope ps(prof, stream, "gemm_dec", 2.0 * R * (double) N * d, 2.0 * ((double) R * d + (double) N * d));
-        gemm_rows_ln(stream, mode, R, N, d, aln, Wt, ep, &gws_);
     };
     auto resid_full = [&](const _Float16 * A, const float * A32, const _Float16 * W, const _Float16 * Wt,
                           const Q5W & q, int K, const float * bias, bool a_q8 = false) {
@@ -686,14 +774,27 @@ void Engine::launch_decode(const DecShape & sh) {
         layernorm_f16(stream, d_x_.as<float>(), R, d, w, b, hp.eps, d_xn_.as<_Float16>(), d, nullptr, nullptr, q8a(),
                       q8d());
     };
-    for (int l = 0; l < hp.n_text_layer; ++l) {
+    if (fused) {
+        ln(m->dec[0].attn_ln_w, m->dec[0].attn_ln_b);  // layer 0's attn_ln of the embeddings
+        const bool split = split_env && R >= 16 && !(prof && prof->on) && !sh.self_sm && !sh.cross_sm && !sh.capture;
+        double * lnst = (double *) ln_stats_.ptr;
+        if (!split) {
+            fused_rows(0, R, stream, &gws_, lnst);
+        } else {
+            const int ra = R / 2;
+            OWK_HIP_CHECK(hipEventRecord(ev_fork_, stream));
+            OWK_HIP_CHECK(hipStreamWaitEvent(stream2_, ev_fork_, 0));
+            fused_rows(0, ra, stream, &gws_, lnst);
+            fused_rows(ra, R - ra, stream2_, &gws2_, lnst + (size_t) 2 * (d / 16) * 32);
+            OWK_HIP_CHECK(hipEventRecord(ev_join_, stream2_));
+            OWK_HIP_CHECK(hipStreamWaitEvent(stream, ev_join_, 0));
+        }
+    }
+    for (int l = 0; l < hp.n_text_layer && !fused; ++l) {
         const DecLayerW & L = m->dec[l];
         _Float16 * Kl = self_k_.as<_Float16>() + l * self_stride;
         _Float16 * Vl = self_v_.as<_Float16>() + l * self_stride;
-        // the attn_ln output: a LayerNorm launch unless the previous layer's resid_layernorm wrote it
-        // (plans 0, 1) or the Q/K/V matmul normalises itself (plan 2); layer 0 normalises the embeddings
-        const bool qkv_aln = plan == 2 && l > 0;
-        if (plan < 0 || l == 0) ln(L.attn_ln_w, L.attn_ln_b);
+        ln(L.attn_ln_w, L.attn_ln_b);
         {
             EpiParams ep;
             ep.bias = L.b_q;
@@ -706,8 +807,7 @@ void Engine::launch_decode(const DecShape & sh) {
             ep.d = d;
             ep.row_off = d_rowoff;
             ep.Tpad = kv_cells * 64;
-            if (qkv_aln) G_ln(EPI_QKV_DEC, 3 * d, L.t_qkv, ep, aln_of(L.attn_ln_w, L.attn_ln_b));
-            else G("qkv", EPI_QKV_DEC, 3 * d, d, d_xn_.as<_Float16>(), nullptr, L.w_qkv, L.t_qkv, L.q_qkv, ep, R, q5);
+            G("qkv", EPI_QKV_DEC, 3 * d, d, d_xn_.as<_Float16>(), nullptr, L.w_qkv, L.t_qkv, L.q_qkv, ep, R, q5);
         }
         {
             ProfScope ps(prof, stream, "attn_self");
@@ -720,21 +820,14 @@ void Engine::launch_decode(const DecShape & sh) {
                                      max_keys,
                                      d_ao_.as<_Float16>(), d, nullptr, nullptr, 0, ao32);
         }
-        if (plan == 0) {
-            resid_ln(d_ao_.as<_Float16>(), L.t_o, d, L.b_o, L.cross_ln_w, L.cross_ln_b);
-        } else if (plan > 0) {
-            resid_stats(d_ao_.as<_Float16>(), L.t_o, d, L.b_o);
-        } else {
-            resid_full(d_ao_.as<_Float16>(), ao32, L.w_o, L.t_o, L.q_o, d, L.b_o, fq_self);
-            ln(L.cross_ln_w, L.cross_ln_b);
-        }
+        resid_full(d_ao_.as<_Float16>(), ao32, L.w_o, L.t_o, L.q_o, d, L.b_o, fq_self);
+        ln(L.cross_ln_w, L.cross_ln_b);
         {
             EpiParams ep;
             ep.bias = L.cb_q;
             ep.out16 = d_q_.as<_Float16>();
             ep.ldo = d;
-            if (plan > 0) G_ln(EPI_F16, d, L.t_cq, ep, aln_of(L.cross_ln_w, L.cross_ln_b));
-            else G("cq", EPI_F16, d, d, d_xn_.as<_Float16>(), nullptr, L.cw_q, L.t_cq, L.q_cq, ep, R, q5);
+            G("cq", EPI_F16, d, d, d_xn_.as<_Float16>(), nullptr, L.cw_q, L.t_cq, L.q_cq, ep, R, q5);
         }
         {
             // bytes: cross K and V of each row's clip (the HBM-bound part of a decode step)
@@ -749,30 +842,17 @@ void Engine::launch_decode(const DecShape & sh) {
                                      d_ao_.as<_Float16>(), d, sh.capture ? amap_.as<int>() + l * H : nullptr,
                                      sh.capture ? cap_.as<float>() : nullptr, R, ao32);
         }
-        if (plan == 0) {
-            resid_ln(d_ao_.as<_Float16>(), L.t_co, d, L.cb_o, L.mlp_ln_w, L.mlp_ln_b);
-        } else if (plan > 0) {
-            resid_stats(d_ao_.as<_Float16>(), L.t_co, d, L.cb_o);
-        } else {
-            resid_full(d_ao_.as<_Float16>(), ao32, L.cw_o, L.t_co, L.q_co, d, L.cb_o, fq_cross);
-            ln(L.mlp_ln_w, L.mlp_ln_b);
-        }
+        resid_full(d_ao_.as<_Float16>(), ao32, L.cw_o, L.t_co, L.q_co, d, L.cb_o, fq_cross);
+        ln(L.mlp_ln_w, L.mlp_ln_b);
         {
             EpiParams ep;
             ep.bias = L.b_mlp0;
             ep.gelu_tab = m->gelu_tab;
             ep.out16 = d_h_.as<_Float16>();
             ep.ldo = 4 * d;
-            if (plan > 0) G_ln(EPI_GELU_F16, 4 * d, L.t_mlp0, ep, aln_of(L.mlp_ln_w, L.mlp_ln_b));
-            else G("mlp0", EPI_GELU_F16, 4 * d, d, d_xn_.as<_Float16>(), nullptr, L.w_mlp0, L.t_mlp0, L.q_mlp0, ep, R, q5);
+            G("mlp0", EPI_GELU_F16, 4 * d, d, d_xn_.as<_Float16>(), nullptr, L.w_mlp0, L.t_mlp0, L.q_mlp0, ep, R, q5);
         }
-        if (plan == 0 || plan == 1) {
-            const DecLayerW * nx = l + 1 < hp.n_text_layer ? &m->dec[l + 1] : nullptr;
-            resid_ln(d_h_.as<_Float16>(), L.t_mlp1, 4 * d, L.b_mlp1, nx ? nx->attn_ln_w : nullptr,
-                     nx ? nx->attn_ln_b : nullptr);
-        } else if (plan == 2) {
-            resid_stats(d_h_.as<_Float16>(), L.t_mlp1, 4 * d, L.b_mlp1);
-        } else resid_full(d_h_.as<_Float16>(), nullptr, L.w_mlp1, L.t_mlp1, L.q_mlp1, 4 * d, L.b_mlp1);
+        resid_full(d_h_.as<_Float16>(), nullptr, L.w_mlp1, L.t_mlp1, L.q_mlp1, 4 * d, L.b_mlp1);
     }
     if (n_logit_rows > 0) {
         {

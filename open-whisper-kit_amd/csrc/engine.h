@@ -189,6 +189,10 @@ private:
     DevBuf gws_part_;  // split-K workspace of the decode-row GEMMs
     DevBuf ln_stats_;  // [d/16][rows] {sum, M2} of the residual GEMMs (EPI_RESID_STATS) for the next LayerNorm
     GemmWs gws_;
+    hipStream_t stream2_ = nullptr;  // second decode row group (launch_decode, OWK_DEC_SPLIT)
+    hipEvent_t ev_fork_ = nullptr, ev_join_ = nullptr;
+    DevBuf gws2_part_;
+    GemmWs gws2_;
 };
 
 } // namespace owk

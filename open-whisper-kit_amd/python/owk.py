@@ -298,6 +298,11 @@ class Whisper:
         self._states.append(s)
         return s
 
+    def free_state(self, s):
+        if s in self._states:
+            self._states.remove(s)
+            self.L.whisper_free_state(s)
+
     def params(self, strategy=WHISPER_SAMPLING_GREEDY, **kw) -> FullParams:
         p = self.L.whisper_full_default_params(strategy)
         p.print_progress = False

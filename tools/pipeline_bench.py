@@ -14,7 +14,14 @@ Workload (synthetic data and random-init weights of the real architectures, as b
 Reports the wall time of each part and the real-time factor of the whole job; the reference
 CPU path (16 threads) is timed on ONE 30 s chunk of the same transcription settings.
 
-    python tools/pipeline_bench.py [--minutes 10] [--no-cpu]
+--mode sequential runs the job as the Swift SDK does (WhisperContext.swift calls whisper_full over
+the whole buffer): ONE whisper_full over the 10 minutes -- the reference's sequential window loop
+with seek advance and prompt carry (ref src/whisper.cpp:7034-7769), no_context = false -- plus
+sortformer_stream_feed in 2 s blocks (the "2s" preset) and the aligner on the absolute token
+times. The chunk split above changes results at split points; the sequential mode is
+the reference's semantics, the chunked one the batch-throughput form. --mode both reports both.
+
+    python tools/pipeline_bench.py [--minutes 10] [--no-cpu] [--mode both|chunked|sequential]
 """
 import argparse
 import json
@@ -36,26 +43,19 @@ AHEADS_LARGE_V3 = 13
 CHUNK = 30 * 16000
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--minutes", type=float, default=10.0)
-    ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--prof", action="store_true", help="per-kernel-class HIP-event timing of the ASR part (eager)")
-    args = ap.parse_args()
-    cache = os.environ.get("OWK_MODEL_CACHE", "/tmp/owk_models")
-    model = S.ensure_model("large-v3", cache_dir=cache)
-    meta = json.load(open(os.path.join(ROOT, "tests", "golden", "sf_golden.json")))
-    sf_path = os.path.join(cache, f"synth-sortformer-s{meta['seed']}.gguf")
-    if not os.path.exists(sf_path):
-        assert SS.write_model(sf_path, meta["seed"]) == meta["sha256"]
-    n = int(args.minutes * 60 * 16000)
-    pcm = S.synth_audio(n, 5)
-    chunks = [pcm[i:i + CHUNK] for i in range(0, n, CHUNK)]
+def words_of(w, states, offsets):
+    words = []
+    for off, st_ in zip(offsets, states):
+        for s in w.segments(st_):
+            for t in s["tokens"]:
+                txt = w.L.whisper_token_to_str(w.ctx, t[0]).decode("utf-8", "replace")
+                words.append((txt, off + t[6] / 100.0, off + t[7] / 100.0, t[2]))
+    return words
 
-    owk.quiet()
-    w = owk.Whisper(model, flash_attn=False, dtw_preset=AHEADS_LARGE_V3)
+
+def run_chunked(args, w, sf, pcm, n):
+    chunks = [pcm[i:i + CHUNK] for i in range(0, n, CHUNK)]
     p = w.params(0, language="en", temperature_inc=0.0, token_timestamps=True)
-    sf = SF.Sortformer(sf_path)
     # warm-up (code objects, buffers, graphs) on one chunk
     st = [w.new_state()]
     w.full_batch(st, chunks[:1], p)
@@ -73,34 +73,94 @@ def main():
         tot = {c: w.prof(c) for c in w.prof_classes()}
         for c, v in sorted(tot.items(), key=lambda kv: -kv[1]["ms"]):
             print(f"[prof] {c:20s} {v['ms']:10.2f} ms  launches {v['launches']:8d}", file=sys.stderr, flush=True)
+        w.L.owk_prof_enable(w.ctx, 0)
     n_tok = sum(len(s["tokens"]) for st_ in states for s in w.segments(st_))
     n_dtw = sum(1 for st_ in states for s in w.segments(st_) for t in s["tokens"] if t[8] >= 0)
     t0 = time.perf_counter()
     probs = sf.diarize(pcm)
     t_diar = time.perf_counter() - t0
     t0 = time.perf_counter()
+    segs = owk.rttm_parse(SF.to_rttm(probs))
+    aligned = owk.align(words_of(w, states, [ci * CHUNK / 16000.0 for ci in range(len(chunks))]), segs)
+    t_align = time.perf_counter() - t0
+    for st_ in states + st:
+        w.free_state(st_)
+    return {"value": round(n / 16000 / (t_asr + t_diar + t_align), 2),
+            "asr_wall_s": round(t_asr, 3), "diarize_wall_s": round(t_diar, 4), "align_wall_s": round(t_align, 4),
+            "rttm_segments": len(segs), "aligned_words": len(aligned["words"]),
+            "utterances": len(aligned["segments"]), "chunks": len(chunks),
+            "tokens": n_tok, "tokens_with_t_dtw": n_dtw, "diarize_frames": int(probs.shape[0]),
+            "workload": "large-v3 F16 flash_attn=false + DTW (LARGE_V3 heads), 30 s chunks in one batch, greedy; "
+                        "SortFormer offline, synthetic weights and audio"}
+
+
+def run_sequential(args, w, sf, pcm, n):
+    p = w.params(0, language="en", temperature_inc=0.0, token_timestamps=True, no_context=False)
+    warm = w.new_state()
+    w.full(warm, pcm[:CHUNK], p)  # warm-up: code objects, buffers, batch-1 graphs
+    w.free_state(warm)
+    st = w.new_state()
+    t0 = time.perf_counter()
+    ret = w.full(st, pcm, p)
+    t_asr = time.perf_counter() - t0
+    assert ret == 0, ret
+    segs_w = w.segments(st)
+    n_tok = sum(len(s["tokens"]) for s in segs_w)
+    n_dtw = sum(1 for s in segs_w for t in s["tokens"] if t[8] >= 0)
+    # streaming diarization: 2 s blocks as a live feed would deliver them
+    stream = sf.stream("2s")
+    t0 = time.perf_counter()
+    blocks = [stream.feed(pcm[i:i + 32000]) for i in range(0, n, 32000)]
+    blocks.append(stream.flush())
+    t_diar = time.perf_counter() - t0
+    stream.close()
+    probs = np.concatenate([b for b in blocks if len(b)], axis=0) if any(len(b) for b in blocks) \
+        else np.zeros((0, 4), np.float32)
+    t0 = time.perf_counter()
+    segs = owk.rttm_parse(SF.to_rttm(probs))
+    aligned = owk.align(words_of(w, [st], [0.0]), segs)  # token times are absolute in one whisper_full
+    t_align = time.perf_counter() - t0
+    w.free_state(st)
+    return {"value": round(n / 16000 / (t_asr + t_diar + t_align), 2),
+            "asr_wall_s": round(t_asr, 3), "diarize_wall_s": round(t_diar, 4), "align_wall_s": round(t_align, 4),
+            "segments": len(segs_w), "rttm_segments": len(segs), "aligned_words": len(aligned["words"]),
+            "utterances": len(aligned["segments"]), "tokens": n_tok, "tokens_with_t_dtw": n_dtw,
+            "diarize_frames": int(probs.shape[0]),
+            "workload": "large-v3 F16 flash_attn=false + DTW (LARGE_V3 heads), ONE whisper_full over the whole "
+                        "buffer (sequential windows, prompt carry), greedy; SortFormer streamed in 2 s blocks; "
+                        "synthetic weights and audio"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--minutes", type=float, default=10.0)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--prof", action="store_true", help="per-kernel-class HIP-event timing of the ASR part (eager)")
+    ap.add_argument("--mode", choices=["both", "chunked", "sequential"], default="both")
+    args = ap.parse_args()
+    cache = os.environ.get("OWK_MODEL_CACHE", "/tmp/owk_models")
+    model = S.ensure_model("large-v3", cache_dir=cache)
+    meta = json.load(open(os.path.join(ROOT, "tests", "golden", "sf_golden.json")))
+    sf_path = os.path.join(cache, f"synth-sortformer-s{meta['seed']}.gguf")
+    if not os.path.exists(sf_path):
+        assert SS.write_model(sf_path, meta["seed"]) == meta["sha256"]
+    n = int(args.minutes * 60 * 16000)
+    pcm = S.synth_audio(n, 5)
+
+    owk.quiet()
+    w = owk.Whisper(model, flash_attn=False, dtw_preset=AHEADS_LARGE_V3)
+    sf = SF.Sortformer(sf_path)
     import ctypes as C
     w.L.whisper_token_to_str.restype = C.c_char_p
     w.L.whisper_token_to_str.argtypes = [C.c_void_p, C.c_int]
-    segs = owk.rttm_parse(SF.to_rttm(probs))
-    words = []
-    for ci, st_ in enumerate(states):
-        off = ci * CHUNK / 16000.0
-        for s in w.segments(st_):
-            for t in s["tokens"]:
-                txt = w.L.whisper_token_to_str(w.ctx, t[0]).decode("utf-8", "replace")
-                words.append((txt, off + t[6] / 100.0, off + t[7] / 100.0, t[2]))
-    aligned = owk.align(words, segs)
-    t_align = time.perf_counter() - t0
-    audio_s = n / 16000
     out = {"metric": "transcribe + DTW + diarize + align real-time factor (audio-s/wall-s), configs[4]",
-           "unit": "audio-s/wall-s", "value": round(audio_s / (t_asr + t_diar + t_align), 2), "audio_s": audio_s,
-           "asr_wall_s": round(t_asr, 3), "diarize_wall_s": round(t_diar, 4), "align_wall_s": round(t_align, 4),
-           "rttm_segments": len(segs), "aligned_words": len(aligned["words"]),
-           "utterances": len(aligned["segments"]), "chunks": len(chunks),
-           "tokens": n_tok, "tokens_with_t_dtw": n_dtw, "diarize_frames": int(probs.shape[0]),
-           "workload": "large-v3 F16 flash_attn=false + DTW (LARGE_V3 heads), 30 s chunks in one batch, greedy; "
-                       "SortFormer offline, synthetic weights and audio"}
+           "unit": "audio-s/wall-s", "audio_s": n / 16000}
+    if args.mode in ("both", "chunked"):
+        out["chunked"] = run_chunked(args, w, sf, pcm, n)
+        out["value"] = out["chunked"]["value"]
+    if args.mode in ("both", "sequential"):
+        out["sequential"] = run_sequential(args, w, sf, pcm, n)
+        out.setdefault("value", out["sequential"]["value"])
     sf.close()
     if not args.no_cpu:
         import ref_oracle as R
@@ -108,7 +168,7 @@ def main():
             nt = min(len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", "1000")))
             ref = R.Ref(model, flash_attn=False, dtw_preset=AHEADS_LARGE_V3)
             t0 = time.perf_counter()
-            r, segs = ref.full(chunks[0], n_threads=nt, language="en", temperature_inc=0.0, token_timestamps=True)
+            r, segs = ref.full(pcm[:CHUNK], n_threads=nt, language="en", temperature_inc=0.0, token_timestamps=True)
             rw = time.perf_counter() - t0
             ref.close()
             out["cpu_baseline_asr"] = {"value": round(30.0 / rw, 3), "unit": "audio-s/wall-s", "cores": nt,
