@@ -80,6 +80,10 @@ WHISPER_API long owk_debug_capture(struct whisper_state * state, float * out, lo
  * w_blocks ggml block_q5_0 rows [N][K/32]; q_out / d_out (optional) receive the Q8_0 activations */
 WHISPER_API int owk_debug_gemm_q5(int device, int M, int N, int K, const float * a, const uint8_t * w_blocks, float * out,
                                   int8_t * q_out, float * d_out);
+/* the same for any block format fmt (0 Q5_0, 1 Q8_0, 2 Q4_0, 3 Q4_1, 4 Q5_1: w_blocks are ggml blocks
+ * of that type; Q4_1 / Q5_1 take Q8_1 activations); d_out receives the raw f32 activation scales */
+WHISPER_API int owk_debug_gemm_quant(int device, int fmt, int M, int N, int K, const float * a, const uint8_t * w_blocks,
+                                     float * out, int8_t * q_out, float * d_out);
 /* mode | 0x100: force the 128x128 large-GEMM kernel; | 0x400: 5-slot ring variant of the 256x256 kernel;
  * | 0x200: uniform random operands (else zeros) */
 WHISPER_API double owk_debug_gemm_bench(int device, int mode, int M, int N, int K, int iters);

@@ -201,14 +201,14 @@ void Engine::linear(const char * cls, int mode, int M, int N, int K, const _Floa
         else gemm_f16(stream, mode, M, N, K, A16, lda, W, K, ep);
         return;
     }
-    // the reference rounds each activation row to Q8_0 (x86 quantize_row_q8_0) before the
-    // q5_0 (q8_0) x q8_0 dot; bytes: Q5_0 (Q8_0) weights at 22 (34) B per 32 + the int8 activations. a_q8: the
+    // the reference rounds each activation row to Q8_0 / Q8_1 (x86 quantize_row_q8_0 / _q8_1) before
+    // the block dot; bytes: the weight blocks (18-34 B per 32) + the int8 activations. a_q8: the
     // producer (LayerNorm, one_chunk attention) already wrote q8a_ / q8d_
     if (!a_q8) {
         ProfScope ps(prof, stream, "quantize_q8");
         quantize_q8(stream, A32, A16, lda, M, K, q8a_.as<int8_t>(), q8d_.as<float>());
     }
-    ProfScope ps(prof, stream, cls, gemm_flops(M, N, K), (double) N * K * (q.q8 ? 34.0 : (q.q4 ? 18.0 : 22.0)) / 32.0 + (double) M * K);
+    ProfScope ps(prof, stream, cls, gemm_flops(M, N, K), (double) N * K * qf_block_bytes(q.fmt) / 32.0 + (double) M * K);
     gemm_q5(stream, mode, M, N, K, q8a_.as<int8_t>(), q8d_.as<float>(), q, ep);
 }
 
@@ -651,7 +651,9 @@ void Engine::launch_decode(const DecShape & sh) {
         const char * v = getenv("OWK_DEC_SPLIT");
         return v && atoi(v) != 0;
     }();
-    const bool fused = R <= 32 && !q5;
+    // soft_max rows (flash_attn = false) and DTW captures take the per-op path below (the fused
+    // chain has no soft_max attention launches)
+    const bool fused = R <= 32 && !q5 && !sh.self_sm && !sh.cross_sm && !sh.capture;
     const int plan = fused ? plan_env : -1;
 
     // the fused decoder (R <= 32, F16) over rows [r0, r0 + n) on stream s

@@ -419,7 +419,7 @@ __global__ __launch_bounds__(64) void k_attn_step(const _Float16 * __restrict__ 
             for (int sh = 16; sh > 0; sh >>= 1) m = fmaxf(m, __shfl_xor(m, sh, 32));
             const float id = m != 0.0f ? 127.f / m : 0.0f;
             q8[o] = (int8_t) rintf(y * id);
-            if ((lane & 31) == 0) q8d[o >> 5] = (float) (_Float16) (m / 127.f);
+            if ((lane & 31) == 0) q8d[o >> 5] = m / 127.f;  // raw f32 d (kernels.h QFmt)
         }
     };
     if (n <= 0) {
@@ -613,7 +613,7 @@ __global__ __launch_bounds__(128) void k_attn_cross2(const _Float16 * __restrict
             for (int sh = 16; sh > 0; sh >>= 1) m = fmaxf(m, __shfl_xor(m, sh, 32));
             const float id = m != 0.0f ? 127.f / m : 0.0f;
             q8[o] = (int8_t) rintf(y * id);
-            if ((lane & 31) == 0) q8d[o >> 5] = (float) (_Float16) (m / 127.f);
+            if ((lane & 31) == 0) q8d[o >> 5] = m / 127.f;  // raw f32 d (kernels.h QFmt)
         }
     };
     if (n <= 0) {  // block-uniform: no barrier reached by either wave
@@ -1059,11 +1059,12 @@ void attn_decoder(hipStream_t s, const _Float16 * q, int ldq, const _Float16 * k
             hipLaunchKernelGGL((k_attn_step<true, false>), dim3(H, n_rows), dim3(64), 0, s, q, ldq, kbase, vbase, ld_kv, hs,
                                rows_dev, key_idx, scale, out, ldo, out32, q8, q8d);
         } else {
-            // cross attention (no cell lists): the once-per-step K/V stream, two waves per (row, head)
-            // (OWK_XATTN=1: the one-wave kernel, for A/B measurements)
+            // cross attention (no cell lists): the once-per-step K/V stream, one wave per (row, head);
+            // OWK_XATTN=2 selects the two-wave k_attn_cross2 (experimental: tests/test_gpu_kernels.py
+            // shows it diverging from k_attn_step beyond 3 key chunks)
             static const bool one_wave = [] {
                 const char * v = getenv("OWK_XATTN");
-                return v && atoi(v) == 1;
+                return !(v && atoi(v) == 2);
             }();
             if (!key_idx && ld_kv == 64 && !one_wave)
                 hipLaunchKernelGGL(k_attn_cross2, dim3(H, n_rows), dim3(128), 0, s, q, ldq, kbase, vbase, hs, rows_dev,

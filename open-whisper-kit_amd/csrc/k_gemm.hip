@@ -886,7 +886,7 @@ __global__ __launch_bounds__(256) void k_quantize_q8(const TA * __restrict__ A, 
         const float dd = am / 127.f;
         const float id = am != 0.0f ? 127.f / am : 0.0f;
         q[(size_t) r * K + b * 32 + lane] = (int8_t) rintf(x * id);
-        if (lane == 0) dq[(size_t) r * nb + b] = (float) (_Float16) dd;
+        if (lane == 0) dq[(size_t) r * nb + b] = dd;  // raw f32 d: consumers round to f16 (kernels.h QFmt)
     }
 }
 
@@ -903,34 +903,46 @@ void quantize_q8(hipStream_t s, const float * A32, const _Float16 * A16, int lda
 
 typedef int intx4 __attribute__((ext_vector_type(4)));
 
-// 8 consecutive Q5_0 weights of one block as int8 (B/A operand of mfma_i32_16x16x32_i8):
-// group g = elements 8g..8g+7 = low (g < 2) or high nibbles of bytes 8(g&1)..+7, 5th bits
-// qh >> 8g; value - 16 by bytewise SWAR (v | 0x80) - 16 ^ 0x80
-__device__ __forceinline__ long q5_group(const uint8_t * qs_blk, uint32_t qh, int g) {
-    const uint64_t raw = *(const uint64_t *) (qs_blk + (g & 1) * 8);
-    uint64_t v = (g < 2 ? raw : (raw >> 4)) & 0x0F0F0F0F0F0F0F0FULL;
-    const uint32_t h8 = (qh >> (8 * g)) & 0xFFu;
+// 8 consecutive weights (group g = elements 8g..8g+7) of one block as int8, the B/A operand of
+// mfma_i32_16x16x32_i8. 4/5-bit formats: nibbles of bytes 8(g&1)..+7 (low for g < 2, high
+// otherwise), 5th bits qh >> 8g; the offset (Q5_0 -16, Q4_0 -8, none for the "_1" formats, whose
+// minimum enters through m) by bytewise SWAR (v | 0x80) - off ^ 0x80. Q8_0: the bytes as stored.
+template <int FMT>
+__device__ __forceinline__ uint64_t unpack_group(uint64_t raw, uint32_t qh, int g) {
+    if constexpr (FMT == QF_Q8_0) {
+        return raw;
+    } else {
+        uint64_t v = (g < 2 ? raw : (raw >> 4)) & 0x0F0F0F0F0F0F0F0FULL;
+        if constexpr (qf_has_qh(FMT)) {
+            const uint32_t h8 = (qh >> (8 * g)) & 0xFFu;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) v |= (uint64_t) ((h8 >> e) & 1u) << (8 * e + 4);
-    v = ((v | 0x8080808080808080ULL) - 0x1010101010101010ULL) ^ 0x8080808080808080ULL;
-    return (long) v;
+            for (int e = 0; e < 8; ++e) v |= (uint64_t) ((h8 >> e) & 1u) << (8 * e + 4);
+        }
+        if constexpr (FMT == QF_Q5_0) v = ((v | 0x8080808080808080ULL) - 0x1010101010101010ULL) ^ 0x8080808080808080ULL;
+        if constexpr (FMT == QF_Q4_0) v = ((v | 0x8080808080808080ULL) - 0x0808080808080808ULL) ^ 0x8080808080808080ULL;
+        return v;
+    }
 }
 
-// 8 consecutive Q4_0 weights of one block as int8: the nibbles of q5_group, value - 8
-__device__ __forceinline__ uint64_t q4_unpack(uint64_t raw, int g) {
-    const uint64_t v = (g < 2 ? raw : (raw >> 4)) & 0x0F0F0F0F0F0F0F0FULL;
-    return ((v | 0x8080808080808080ULL) - 0x0808080808080808ULL) ^ 0x8080808080808080ULL;
-}
-
-// group g (8 int8) of K block kb of weight row n: Q5_0 / Q4_0 (unpacked) or Q8_0 (as stored)
+// group g of K block kb of weight row n from the split arrays (runtime format)
 __device__ __forceinline__ long wq_group(const Q5W & w, int n, int kb, int g, int K, int nb) {
-    if (w.q8) return *(const long *) (w.qs + (size_t) n * K + kb * 32 + 8 * g);
-    if (w.q4) return (long) q4_unpack(*(const uint64_t *) (w.qs + (size_t) n * (K / 2) + kb * 16 + (g & 1) * 8), g);
-    return q5_group(w.qs + (size_t) n * (K / 2) + kb * 16, w.qh[(size_t) n * nb + kb], g);
+    const size_t bi = (size_t) n * nb + kb;
+    if (w.fmt == QF_Q8_0) return *(const long *) (w.qs + (size_t) n * K + kb * 32 + 8 * g);
+    const uint64_t raw = *(const uint64_t *) (w.qs + bi * 16 + (g & 1) * 8);
+    switch (w.fmt) {
+        case QF_Q4_0: return (long) unpack_group<QF_Q4_0>(raw, 0u, g);
+        case QF_Q4_1: return (long) unpack_group<QF_Q4_1>(raw, 0u, g);
+        case QF_Q5_1: return (long) unpack_group<QF_Q5_1>(raw, w.qh[bi], g);
+        default: return (long) unpack_group<QF_Q5_0>(raw, w.qh[bi], g);
+    }
 }
+
+// the Q8_1 block sum term of a "_1" format: f16(d_f32 * sum(q)) (quantize_row_q8_1's y.s)
+__device__ __forceinline__ float q8_1_sum(float d_raw, int isum) { return (float) (_Float16) (d_raw * (float) isum); }
 
 // skinny: M <= 64 rows; one 16-column tile per block, 8 waves split the K blocks, partial
-// tiles reduced through LDS in fixed wave order
+// tiles reduced through LDS in fixed wave order. "_1" formats: a second MFMA against an
+// all-ones operand gives every row's block sum in the accumulator layout.
 template <int MODE>
 __global__ __launch_bounds__(512) void k_gemm_q5_skinny(int M, int N, int K, const int8_t * __restrict__ qa,
                                                         const float * __restrict__ da, Q5W w, EpiParams ep) {
@@ -942,12 +954,15 @@ __global__ __launch_bounds__(512) void k_gemm_q5_skinny(int M, int N, int K, con
     const int kb0 = (wave * nb) >> 3, kb1 = ((wave + 1) * nb) >> 3;
     const int g = lane >> 4;
     const int n = min(n0 + (lane & 15), N - 1);
-    floatx4 acc[4];
+    const bool has_m = qf_has_m(w.fmt);
+    const long ones = 0x0101010101010101L;
+    floatx4 acc[4], accm[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) acc[i] = floatx4{0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < 4; ++i) acc[i] = accm[i] = floatx4{0.f, 0.f, 0.f, 0.f};
     for (int kb = kb0; kb < kb1; ++kb) {
         const long b = wq_group(w, n, kb, g, K, nb);
         const float dw = (float) w.d[(size_t) n * nb + kb];
+        const float mw = has_m ? (float) w.m[(size_t) n * nb + kb] : 0.0f;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             if (i < MT) {
@@ -955,16 +970,20 @@ __global__ __launch_bounds__(512) void k_gemm_q5_skinny(int M, int N, int K, con
                 const long a = *(const long *) (qa + (size_t) ra * K + kb * 32 + 8 * g);
                 const intx4 z = {0, 0, 0, 0};
                 const intx4 iv = __builtin_amdgcn_mfma_i32_16x16x32_i8(a, b, z, 0, 0, 0);
+                intx4 is = z;
+                if (has_m) is = __builtin_amdgcn_mfma_i32_16x16x32_i8(a, ones, z, 0, 0, 0);
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
                     const int r = min(i * 16 + 4 * g + e, M - 1);
-                    acc[i][e] += (float) iv[e] * (da[(size_t) r * nb + kb] * dw);
+                    const float dr = da[(size_t) r * nb + kb];
+                    acc[i][e] += (float) iv[e] * ((float) (_Float16) dr * dw);
+                    if (has_m) accm[i][e] += mw * q8_1_sum(dr, is[e]);
                 }
             }
         }
     }
 #pragma unroll
-    for (int i = 0; i < 4; ++i) red[wave][i][lane] = acc[i];
+    for (int i = 0; i < 4; ++i) red[wave][i][lane] = has_m ? acc[i] + accm[i] : acc[i];
     __syncthreads();
     if (tid < 256) {
         const int i = tid >> 6, ln = tid & 63;
@@ -994,10 +1013,12 @@ constexpr int GQ_MAX_SCALES = 32 * 160;  // M x K/32 activation scales in LDS
 // activation scales per thread: M * nb <= 32 * nb over blockDim = 64 * ceil(nb / J) threads
 // -> at most 32 * J / 64 + 1
 
-template <int MODE, int MT, int FMT, int GQ_J>  // FMT: 0 Q5_0, 1 Q8_0, 2 Q4_0; GQ_J K blocks per wave
+template <int MODE, int MT, int FMT, int GQ_J>  // FMT: QFmt; GQ_J K blocks per wave
 __global__ __launch_bounds__(GQ_MAXW * 64) void k_gemm_q5_rows(int M, int N, int K, const int8_t * __restrict__ qa,
                                                                const float * __restrict__ da, Q5W w, EpiParams ep) {
     constexpr int GQ_DA_PER_THREAD = 32 * GQ_J / 64 + 1;
+    constexpr bool HAS_M = qf_has_m(FMT), HAS_QH = qf_has_qh(FMT);
+    constexpr int TB = qf_tile_bytes(FMT), QSB = qf_qs_bytes(FMT);
     __shared__ floatx4 red[GQ_MAXW][MT][64];
     __shared__ float sda[GQ_MAX_SCALES];
     const int tid = threadIdx.x, lane = tid & 63, nw = blockDim.x >> 6;
@@ -1010,31 +1031,20 @@ __global__ __launch_bounds__(GQ_MAXW * 64) void k_gemm_q5_rows(int M, int N, int
     const int c16 = lane & 15;
     uint64_t raw[GQ_J];
     uint32_t qh[GQ_J];
-    _Float16 dw[GQ_J];
+    _Float16 dw[GQ_J], mw[GQ_J];
     long a[MT][GQ_J];
-    // the tile's blocks are contiguous 352 B records (Q5W::tiled): coalesced loads. Blocks
-    // past this wave's range load a valid record and a zero activation (adds exact zeros).
-    // record format at compile time: the load phase stays branch-free
-    constexpr bool q8 = FMT == 1, q4 = FMT == 2;
-    constexpr int tbytes = q8 ? Q8_TILE_BYTES : (q4 ? Q4_TILE_BYTES : Q5_TILE_BYTES);
-    const uint8_t * tb = w.tiled + (size_t) blockIdx.x * nb * tbytes;
+    // the tile's blocks are contiguous records (qf_tile_bytes): coalesced loads. Blocks past this
+    // wave's range load a valid record and a zero activation (adds exact zeros). Record format at
+    // compile time: the load phase stays branch-free.
+    const uint8_t * tb = w.tiled + (size_t) blockIdx.x * nb * TB;
 #pragma unroll
     for (int j = 0; j < GQ_J; ++j) {
         const int kb = min(kb0 + j, nb - 1);
-        const uint8_t * rec = tb + (size_t) kb * tbytes;
-        if constexpr (q8) {
-            raw[j] = *(const uint64_t *) (rec + c16 * 32 + g * 8);
-            qh[j] = 0;
-            dw[j] = *(const _Float16 *) (rec + 512 + c16 * 2);
-        } else if constexpr (q4) {
-            raw[j] = *(const uint64_t *) (rec + c16 * 16 + (g & 1) * 8);
-            qh[j] = 0;
-            dw[j] = *(const _Float16 *) (rec + 256 + c16 * 2);
-        } else {
-            raw[j] = *(const uint64_t *) (rec + c16 * 16 + (g & 1) * 8);
-            qh[j] = *(const uint32_t *) (rec + 256 + c16 * 4);
-            dw[j] = *(const _Float16 *) (rec + 320 + c16 * 2);
-        }
+        const uint8_t * rec = tb + (size_t) kb * TB;
+        raw[j] = *(const uint64_t *) (rec + c16 * QSB + (QSB == 32 ? g * 8 : (g & 1) * 8));
+        qh[j] = HAS_QH ? *(const uint32_t *) (rec + qf_tile_off_qh(FMT) + c16 * 4) : 0u;
+        dw[j] = *(const _Float16 *) (rec + qf_tile_off_d(FMT) + c16 * 2);
+        mw[j] = HAS_M ? *(const _Float16 *) (rec + qf_tile_off_m(FMT) + c16 * 2) : (_Float16) 0.0f;
 #pragma unroll
         for (int i = 0; i < MT; ++i) {
             const int ra = min(i * 16 + c16, M - 1);
@@ -1042,8 +1052,8 @@ __global__ __launch_bounds__(GQ_MAXW * 64) void k_gemm_q5_rows(int M, int N, int
             a[i][j] = j < nj ? t : 0L;
         }
     }
-    // activation scales (at most GQ_DA_PER_THREAD per thread: M <= 32, nw = ceil(nb / J)) to
-    // LDS; every load of the launch is issued before the first wait (one round trip)
+    // activation scales (raw f32 d; at most GQ_DA_PER_THREAD per thread: M <= 32, nw = ceil(nb / J))
+    // to LDS; every load of the launch is issued before the first wait (one round trip)
     float dv[GQ_DA_PER_THREAD];
 #pragma unroll
     for (int u = 0; u < GQ_DA_PER_THREAD; ++u) {
@@ -1057,36 +1067,32 @@ __global__ __launch_bounds__(GQ_MAXW * 64) void k_gemm_q5_rows(int M, int N, int
         if (i < M * nb) sda[i] = dv[u];
     }
     __syncthreads();
-    floatx4 acc[MT];
+    floatx4 acc[MT], accm[MT];
 #pragma unroll
-    for (int i = 0; i < MT; ++i) acc[i] = floatx4{0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < MT; ++i) acc[i] = accm[i] = floatx4{0.f, 0.f, 0.f, 0.f};
+    const long ones = 0x0101010101010101L;
 #pragma unroll
     for (int j = 0; j < GQ_J; ++j) {
         const int kb = min(kb0 + j, nb - 1);
-        uint64_t v = raw[j];
-        if constexpr (q4) {
-            v = q4_unpack(raw[j], g);
-        } else if constexpr (!q8) {
-            v = (g < 2 ? raw[j] : (raw[j] >> 4)) & 0x0F0F0F0F0F0F0F0FULL;
-            const uint32_t h8 = (qh[j] >> (8 * g)) & 0xFFu;
-#pragma unroll
-            for (int e = 0; e < 8; ++e) v |= (uint64_t) ((h8 >> e) & 1u) << (8 * e + 4);
-            v = ((v | 0x8080808080808080ULL) - 0x1010101010101010ULL) ^ 0x8080808080808080ULL;
-        }
+        const uint64_t v = unpack_group<FMT>(raw[j], qh[j], g);
         const float dwf = (float) dw[j];
 #pragma unroll
         for (int i = 0; i < MT; ++i) {
             const intx4 z = {0, 0, 0, 0};
             const intx4 iv = __builtin_amdgcn_mfma_i32_16x16x32_i8(a[i][j], (long) v, z, 0, 0, 0);
+            intx4 is = z;
+            if constexpr (HAS_M) is = __builtin_amdgcn_mfma_i32_16x16x32_i8(a[i][j], ones, z, 0, 0, 0);
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
                 const int r = min(i * 16 + 4 * g + e, M - 1);
-                acc[i][e] += (float) iv[e] * (sda[r * nb + kb] * dwf);
+                const float dr = sda[r * nb + kb];
+                acc[i][e] += (float) iv[e] * ((float) (_Float16) dr * dwf);
+                if constexpr (HAS_M) accm[i][e] += (float) mw[j] * q8_1_sum(dr, is[e]);
             }
         }
     }
 #pragma unroll
-    for (int i = 0; i < MT; ++i) red[wave][i][lane] = acc[i];
+    for (int i = 0; i < MT; ++i) red[wave][i][lane] = HAS_M ? acc[i] + accm[i] : acc[i];
     __syncthreads();
     for (int o = tid; o < MT * 256; o += blockDim.x) {
         const int r = o >> 4, cc = o & 15;
@@ -1107,7 +1113,7 @@ template <int MODE>
 __global__ __launch_bounds__(256) void k_gemm_q5_big(int M, int N, int K, const int8_t * __restrict__ qa,
                                                      const float * __restrict__ da, Q5W w, EpiParams ep) {
     __shared__ __attribute__((aligned(16))) int8_t sA[2][64][40], sB[2][64][40];
-    __shared__ float sdA[2][64], sdB[2][64];
+    __shared__ float sdA[2][64], sdB[2][64], sdS[2][64], sdM[2][64];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int nbn = (N + 63) / 64;
     const int bm = blockIdx.x / nbn, bn = blockIdx.x - bm * nbn;
@@ -1115,19 +1121,34 @@ __global__ __launch_bounds__(256) void k_gemm_q5_big(int M, int N, int K, const 
     const int nb = K >> 5;
     const int wm = wave >> 1, wn = wave & 1;
     const int g = lane >> 4;
-    floatx4 acc[2][2];
+    floatx4 acc[2][2], accm[2][2];
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+        for (int j = 0; j < 2; ++j) acc[i][j] = accm[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
     const int srow = tid >> 2, sq = tid & 3;  // staging: row, 8-element group
     const int ra = min(m0 + srow, M - 1), rb = min(n0 + srow, N - 1);
+    const bool has_m = qf_has_m(w.fmt);
     auto stage = [&](int buf, int kb) {
-        *(long *) &sA[buf][srow][sq * 8] = *(const long *) (qa + (size_t) ra * K + kb * 32 + sq * 8);
+        const long av = *(const long *) (qa + (size_t) ra * K + kb * 32 + sq * 8);
+        *(long *) &sA[buf][srow][sq * 8] = av;
         *(long *) &sB[buf][srow][sq * 8] = wq_group(w, rb, kb, sq, K, nb);
+        // "_1" formats: the Q8_1 block sum of the activation row (its 4 groups sit in adjacent lanes)
+        int isum = 0;
+        if (has_m) {
+            isum = __builtin_amdgcn_sdot4((int) (av & 0xFFFFFFFF), 0x01010101, 0, false);
+            isum = __builtin_amdgcn_sdot4((int) (av >> 32), 0x01010101, isum, false);
+            isum += __shfl_xor(isum, 1, 64);
+            isum += __shfl_xor(isum, 2, 64);
+        }
         if (sq == 0) {
-            sdA[buf][srow] = da[(size_t) ra * nb + kb];
+            const float dr = da[(size_t) ra * nb + kb];
+            sdA[buf][srow] = (float) (_Float16) dr;
             sdB[buf][srow] = (float) w.d[(size_t) rb * nb + kb];
+            if (has_m) {
+                sdS[buf][srow] = q8_1_sum(dr, isum);
+                sdM[buf][srow] = (float) w.m[(size_t) rb * nb + kb];
+            }
         }
     };
     stage(0, 0);
@@ -1151,6 +1172,11 @@ __global__ __launch_bounds__(256) void k_gemm_q5_big(int M, int N, int K, const 
 #pragma unroll
                 for (int e = 0; e < 4; ++e)
                     acc[i][j][e] += (float) iv[e] * (sdA[cur][wm * 32 + i * 16 + 4 * g + e] * dw);
+                if (has_m) {  // the m_w * s_a terms in their own sum (ggml's summs), added at the end
+                    const float mw = sdM[cur][wn * 32 + j * 16 + (lane & 15)];
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) accm[i][j][e] += mw * sdS[cur][wm * 32 + i * 16 + 4 * g + e];
+                }
             }
         __syncthreads();
     }
@@ -1162,7 +1188,7 @@ __global__ __launch_bounds__(256) void k_gemm_q5_big(int M, int N, int K, const 
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
                 const int r = m0 + wm * 32 + i * 16 + 4 * g + e;
-                if (r < M && c < N) epi_store<MODE>(ep, r, c, acc[i][j][e]);
+                if (r < M && c < N) epi_store<MODE>(ep, r, c, has_m ? acc[i][j][e] + accm[i][j][e] : acc[i][j][e]);
             }
         }
 }
@@ -1176,18 +1202,18 @@ template <int MODE> struct LaunchQ5 {
             const int J = nb <= GQ_MAXW * 3 ? 3 : GQ_JMAX;
             const int nw = (nb + J - 1) / J;
             const dim3 grid((N + 15) / 16), block(nw * 64);
-            const int fmt = w.q8 ? 1 : (w.q4 ? 2 : 0);
 #define OWK_Q_ROWS(MT_, F_, J_) hipLaunchKernelGGL((k_gemm_q5_rows<MODE, MT_, F_, J_>), grid, block, 0, s, M, N, K, qa, da, w, ep)
 #define OWK_Q_ROWS_J(MT_, F_) do { if (J == 3) OWK_Q_ROWS(MT_, F_, 3); else OWK_Q_ROWS(MT_, F_, GQ_JMAX); } while (0)
-            if (M <= 16) {
-                if (fmt == 1) OWK_Q_ROWS_J(1, 1);
-                else if (fmt == 2) OWK_Q_ROWS_J(1, 2);
-                else OWK_Q_ROWS_J(1, 0);
-            } else {
-                if (fmt == 1) OWK_Q_ROWS_J(2, 1);
-                else if (fmt == 2) OWK_Q_ROWS_J(2, 2);
-                else OWK_Q_ROWS_J(2, 0);
-            }
+#define OWK_Q_ROWS_F(MT_)                                                 \
+    switch (w.fmt) {                                                      \
+        case QF_Q8_0: OWK_Q_ROWS_J(MT_, QF_Q8_0); break;                  \
+        case QF_Q4_0: OWK_Q_ROWS_J(MT_, QF_Q4_0); break;                  \
+        case QF_Q4_1: OWK_Q_ROWS_J(MT_, QF_Q4_1); break;                  \
+        case QF_Q5_1: OWK_Q_ROWS_J(MT_, QF_Q5_1); break;                  \
+        default: OWK_Q_ROWS_J(MT_, QF_Q5_0); break;                       \
+    }
+            if (M <= 16) OWK_Q_ROWS_F(1) else OWK_Q_ROWS_F(2)
+#undef OWK_Q_ROWS_F
 #undef OWK_Q_ROWS_J
 #undef OWK_Q_ROWS
         } else if (M <= 64)
@@ -1198,84 +1224,61 @@ template <int MODE> struct LaunchQ5 {
     }
 };
 
-size_t q5_tiled_bytes(int N, int K) { return (size_t) ((N + 15) / 16) * (K / 32) * Q5_TILE_BYTES; }
-
-void q5_tile_host(const uint8_t * qs, const uint32_t * qh, const uint16_t * d, int N, int K, uint8_t * out) {
-    const int nb = K / 32, nt = (N + 15) / 16;
-    memset(out, 0, q5_tiled_bytes(N, K));
-    for (int t = 0; t < nt; ++t)
-        for (int kb = 0; kb < nb; ++kb) {
-            uint8_t * o = out + ((size_t) t * nb + kb) * Q5_TILE_BYTES;
-            for (int c = 0; c < 16; ++c) {
-                const int n = t * 16 + c;
-                if (n >= N) break;
-                memcpy(o + c * 16, qs + (size_t) n * (K / 2) + kb * 16, 16);
-                memcpy(o + 256 + c * 4, &qh[(size_t) n * nb + kb], 4);
-                memcpy(o + 320 + c * 2, &d[(size_t) n * nb + kb], 2);
-            }
-        }
+int qf_block_bytes(int f) {
+    switch (f) {
+        case QF_Q5_0: return 22;  // block_q5_0: d, qh[4], qs[16]
+        case QF_Q8_0: return 34;  // block_q8_0: d, qs[32]
+        case QF_Q4_0: return 18;  // block_q4_0: d, qs[16]
+        case QF_Q4_1: return 20;  // block_q4_1: d, m, qs[16]
+        case QF_Q5_1: return 24;  // block_q5_1: d, m, qh[4], qs[16]
+    }
+    throw std::runtime_error("quant: bad format");
+}
+int qf_ggml_type(int f) {
+    static const int t[] = {6, 8, 2, 3, 7};
+    if (f < 0 || f > QF_Q5_1) throw std::runtime_error("quant: bad format");
+    return t[f];
 }
 
-size_t q4_tiled_bytes(int N, int K) { return (size_t) ((N + 15) / 16) * (K / 32) * Q4_TILE_BYTES; }
+size_t quant_tiled_bytes(int fmt, int N, int K) { return (size_t) ((N + 15) / 16) * (K / 32) * qf_tile_bytes(fmt); }
 
-void q4_tile_host(const uint8_t * qs, const uint16_t * d, int N, int K, uint8_t * out) {
-    const int nb = K / 32, nt = (N + 15) / 16;
-    memset(out, 0, q4_tiled_bytes(N, K));
-    for (int t = 0; t < nt; ++t)
-        for (int kb = 0; kb < nb; ++kb) {
-            uint8_t * o = out + ((size_t) t * nb + kb) * Q4_TILE_BYTES;
-            for (int c = 0; c < 16; ++c) {
-                const int n = t * 16 + c;
-                if (n >= N) break;
-                memcpy(o + c * 16, qs + (size_t) n * (K / 2) + kb * 16, 16);
-                memcpy(o + 256 + c * 2, &d[(size_t) n * nb + kb], 2);
-            }
-        }
-}
-
-void q4_split_host(const uint8_t * blocks, int N, int K, uint8_t * qs, uint16_t * d) {
-    const int nb = K / 32;
+void quant_split_host(int fmt, const uint8_t * blocks, int N, int K, uint8_t * qs, uint32_t * qh, uint16_t * d,
+                      uint16_t * m) {
+    const int nb = K / 32, bb = qf_block_bytes(fmt), qsb = qf_qs_bytes(fmt);
     for (size_t i = 0; i < (size_t) N * nb; ++i) {
-        const uint8_t * b = blocks + i * 18;  // block_q4_0: d (f16), qs[16]
+        const uint8_t * b = blocks + i * bb;
+        int o = 0;
         memcpy(&d[i], b, 2);
-        memcpy(qs + i * 16, b + 2, 16);
+        o += 2;
+        if (qf_has_m(fmt)) {
+            memcpy(&m[i], b + o, 2);
+            o += 2;
+        }
+        if (qf_has_qh(fmt)) {
+            memcpy(&qh[i], b + o, 4);
+            o += 4;
+        }
+        memcpy(qs + i * qsb, b + o, qsb);
     }
 }
 
-size_t q8_tiled_bytes(int N, int K) { return (size_t) ((N + 15) / 16) * (K / 32) * Q8_TILE_BYTES; }
-
-void q8_tile_host(const int8_t * qs, const uint16_t * d, int N, int K, uint8_t * out) {
-    const int nb = K / 32, nt = (N + 15) / 16;
-    memset(out, 0, q8_tiled_bytes(N, K));
+void quant_tile_host(int fmt, const uint8_t * qs, const uint32_t * qh, const uint16_t * d, const uint16_t * m, int N,
+                     int K, uint8_t * out) {
+    const int nb = K / 32, nt = (N + 15) / 16, tb = qf_tile_bytes(fmt), qsb = qf_qs_bytes(fmt);
+    memset(out, 0, quant_tiled_bytes(fmt, N, K));
     for (int t = 0; t < nt; ++t)
         for (int kb = 0; kb < nb; ++kb) {
-            uint8_t * o = out + ((size_t) t * nb + kb) * Q8_TILE_BYTES;
+            uint8_t * o = out + ((size_t) t * nb + kb) * tb;
             for (int c = 0; c < 16; ++c) {
                 const int n = t * 16 + c;
                 if (n >= N) break;
-                memcpy(o + c * 32, qs + (size_t) n * K + kb * 32, 32);
-                memcpy(o + 512 + c * 2, &d[(size_t) n * nb + kb], 2);
+                const size_t bi = (size_t) n * nb + kb;
+                memcpy(o + c * qsb, qs + bi * qsb, qsb);
+                if (qf_has_qh(fmt)) memcpy(o + qf_tile_off_qh(fmt) + c * 4, &qh[bi], 4);
+                memcpy(o + qf_tile_off_d(fmt) + c * 2, &d[bi], 2);
+                if (qf_has_m(fmt)) memcpy(o + qf_tile_off_m(fmt) + c * 2, &m[bi], 2);
             }
         }
-}
-
-void q8_split_host(const uint8_t * blocks, int N, int K, int8_t * qs, uint16_t * d) {
-    const int nb = K / 32;
-    for (size_t i = 0; i < (size_t) N * nb; ++i) {
-        const uint8_t * b = blocks + i * 34;  // block_q8_0: d (f16), qs[32]
-        memcpy(&d[i], b, 2);
-        memcpy(qs + i * 32, b + 2, 32);
-    }
-}
-
-void q5_split_host(const uint8_t * blocks, int N, int K, uint8_t * qs, uint32_t * qh, uint16_t * d) {
-    const int nb = K / 32;
-    for (size_t i = 0; i < (size_t) N * nb; ++i) {
-        const uint8_t * b = blocks + i * 22;  // block_q5_0: d (f16), qh[4], qs[16]
-        memcpy(&d[i], b, 2);
-        memcpy(&qh[i], b + 2, 4);
-        memcpy(qs + i * 16, b + 6, 16);
-    }
 }
 
 static void check_shape(int M, int N, int K, int lda, int ldw, int kmul) {

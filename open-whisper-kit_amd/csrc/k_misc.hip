@@ -77,7 +77,7 @@ __device__ __forceinline__ void ln_row_regs(const float4 (&xv)[LN_V4], int lane,
                 qv.z = (signed char) rintf(y.z * id);
                 qv.w = (signed char) rintf(y.w * id);
                 *(char4 *) (q8 + 4 * i) = qv;
-                if ((lane & 7) == 0) q8d[i >> 3] = (float) (_Float16) (m / 127.f);
+                if ((lane & 7) == 0) q8d[i >> 3] = m / 127.f;  // raw f32 d (kernels.h QFmt)
             }
         }
     }
@@ -269,12 +269,36 @@ __global__ void k_embed_q4(const uint8_t * __restrict__ qs, const _Float16 * __r
     }
 }
 
+// Q4_1 / Q5_1: dequantize_row_q4_1 / _q5_1 (ref ggml/src/ggml-quants.c:327-420): y = q * d + m,
+// contracted to one FMA by the reference's gcc build
+__global__ void k_embed_q1(const uint8_t * __restrict__ qs, const uint32_t * __restrict__ qh,
+                           const _Float16 * __restrict__ dd, const _Float16 * __restrict__ mm,
+                           const float * __restrict__ pe, const int * __restrict__ tok, const int * __restrict__ pos,
+                           int rows, int d, float * __restrict__ x) {
+    const int r = blockIdx.x;
+    if (r >= rows) return;
+    const size_t row = (size_t) tok[r];
+    const int nb = d / 32;
+    const float * p = pe + (size_t) pos[r] * d;
+    for (int i = threadIdx.x; i < d; i += blockDim.x) {
+        const int b = i >> 5, j = i & 31;
+        const uint8_t byte = qs[row * (d / 2) + b * 16 + (j & 15)];
+        int q = j < 16 ? (byte & 0x0F) : (byte >> 4);
+        if (qh) q |= ((qh[row * nb + b] >> j) & 1) << 4;
+        const float v = fmaf((float) q, (float) dd[row * nb + b], (float) mm[row * nb + b]);
+        x[(size_t) r * d + i] = v + p[i];
+    }
+}
+
 void embed_tokens_q5(hipStream_t s, const Q5W & te, const float * pe, const int * tok, const int * pos, int rows, int d,
                      float * x) {
     if (rows <= 0) return;
-    if (te.q4)
+    if (te.fmt == QF_Q4_1 || te.fmt == QF_Q5_1)
+        hipLaunchKernelGGL(k_embed_q1, dim3(rows), dim3(256), 0, s, te.qs, te.fmt == QF_Q5_1 ? te.qh : nullptr, te.d,
+                           te.m, pe, tok, pos, rows, d, x);
+    else if (te.fmt == QF_Q4_0)
         hipLaunchKernelGGL(k_embed_q4, dim3(rows), dim3(256), 0, s, te.qs, te.d, pe, tok, pos, rows, d, x);
-    else if (te.q8)
+    else if (te.fmt == QF_Q8_0)
         hipLaunchKernelGGL(k_embed_q8, dim3(rows), dim3(256), 0, s, (const int8_t *) te.qs, te.d, pe, tok, pos, rows, d, x);
     else
         hipLaunchKernelGGL(k_embed_q5, dim3(rows), dim3(256), 0, s, te.qs, te.qh, te.d, pe, tok, pos, rows, d, x);

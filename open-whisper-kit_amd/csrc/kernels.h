@@ -112,49 +112,61 @@ void tile_weights(hipStream_t s, const _Float16 * W, int N, int K, _Float16 * ou
 // (ggml_vec_dot_q5_0_q8_0, quants.c:845) scaled by d_w * d_a per block. Here the dot is
 // v_mfma_i32_16x16x32_i8 per 32-block (exact integers), scaled and accumulated in f32.
 // ---------------------------------------------------------------------------------
+// Weight formats of the quantized pipeline (ggml block types; whisper-quantize ftypes):
+//   Q5_0 (ftype 8)  w = d * (q5 - 16)       x Q8_0 activations
+//   Q8_0 (ftype 7)  w = d * q8              x Q8_0
+//   Q4_0 (ftype 2)  w = d * (q4 - 8)        x Q8_0
+//   Q4_1 (ftype 3)  w = d * q4 + m          x Q8_1 (ggml_vec_dot_q4_1_q8_1, x86 quants.c:701)
+//   Q5_1 (ftype 9)  w = d * q5 + m          x Q8_1 (ggml_vec_dot_q5_1_q8_1, x86 quants.c:925)
+// A "_1" block's dot is d_w d_a sum(qw qa) + m_w s_a with s_a = f16(d_a_f32 * sum(qa)) the
+// Q8_1 block sum (quantize_row_q8_1, x86 quants.c:388): the GEMMs form it from the int8
+// activations and the UNROUNDED f32 scale, so activation producers store the raw f32
+// d = amax / 127 and every consumer rounds it to f16 itself (the stored block_q8_*.d).
+enum QFmt : int { QF_Q5_0 = 0, QF_Q8_0 = 1, QF_Q4_0 = 2, QF_Q4_1 = 3, QF_Q5_1 = 4 };
+__host__ __device__ constexpr bool qf_has_qh(int f) { return f == QF_Q5_0 || f == QF_Q5_1; }
+__host__ __device__ constexpr bool qf_has_m(int f) { return f == QF_Q4_1 || f == QF_Q5_1; }
+__host__ __device__ constexpr int qf_qs_bytes(int f) { return f == QF_Q8_0 ? 32 : 16; }  // per 32 weights
+// column-tiled decode record per (16-row tile, 32-wide K block): qs (16 x 16 or 16 x 32 B) |
+// qh (16 x 4 B, 5-bit formats) | d (16 x 2 B) | m (16 x 2 B, "_1" formats)
+__host__ __device__ constexpr int qf_tile_bytes(int f) {
+    return 16 * qf_qs_bytes(f) + (qf_has_qh(f) ? 64 : 0) + 32 + (qf_has_m(f) ? 32 : 0);
+}
+__host__ __device__ constexpr int qf_tile_off_qh(int f) { return 16 * qf_qs_bytes(f); }
+__host__ __device__ constexpr int qf_tile_off_d(int f) { return 16 * qf_qs_bytes(f) + (qf_has_qh(f) ? 64 : 0); }
+__host__ __device__ constexpr int qf_tile_off_m(int f) { return qf_tile_off_d(f) + 32; }
+int qf_block_bytes(int f);  // ggml block size (18 / 20 / 22 / 24 / 34)
+int qf_ggml_type(int f);    // GGML_TYPE_Q5_0 6, Q8_0 8, Q4_0 2, Q4_1 3, Q5_1 7
+
 struct Q5W {
     const uint8_t * qs = nullptr;   // [N][K/2]: block b = 16 bytes, byte j = element j | element j+16 << 4
-    const uint32_t * qh = nullptr;  // [N][K/32]: 5th bits, bit j = element j
+                                    // (Q8_0: [N][K] int8)
+    const uint32_t * qh = nullptr;  // [N][K/32]: 5th bits, bit j = element j (Q5_0 / Q5_1)
     const _Float16 * d = nullptr;   // [N][K/32]: block scales
-    // decode-step matrices: per (16-row tile t, block kb) 352 B at (t * K/32 + kb) * 352 =
-    // qs of the 16 rows (16 x 16 B) | qh (16 x 4 B) | d (16 x 2 B); rows past N zero
+    const _Float16 * m = nullptr;   // [N][K/32]: block minimums (Q4_1 / Q5_1)
+    // decode-step matrices: the column-tiled records (qf_tile_bytes), rows past N zero
     const uint8_t * tiled = nullptr;
-    // Q8_0 matrices (MOSTLY_Q8_0 models) share the pipeline: qs = [N][K] int8, qh unused,
-    // tiled records of 16 rows x 32 int8 | 16 x d (544 B)
-    bool q8 = false;
-    // Q4_0 matrices (MOSTLY_Q4_0): qs as Q5_0's nibbles (value - 8), qh unused, tiled records
-    // of 16 rows x 16 B | 16 x d (288 B)
-    bool q4 = false;
+    int fmt = QF_Q5_0;
     explicit operator bool() const { return qs != nullptr; }
 };
-constexpr int Q5_TILE_BYTES = 352;
-constexpr int Q8_TILE_BYTES = 544;
-constexpr int Q4_TILE_BYTES = 288;
-size_t q4_tiled_bytes(int N, int K);
-void q4_tile_host(const uint8_t * qs, const uint16_t * d, int N, int K, uint8_t * out);
-// block_q4_0 rows (d f16, qs[16]) -> qs [N][K/2], d [N][K/32]
-void q4_split_host(const uint8_t * blocks, int N, int K, uint8_t * qs, uint16_t * d);
-size_t q8_tiled_bytes(int N, int K);
-void q8_tile_host(const int8_t * qs, const uint16_t * d, int N, int K, uint8_t * out);
-// block_q8_0 rows (d f16, qs[32]) -> qs [N][K], d [N][K/32]
-void q8_split_host(const uint8_t * blocks, int N, int K, int8_t * qs, uint16_t * d);
-size_t q5_tiled_bytes(int N, int K);
-void q5_tile_host(const uint8_t * qs, const uint32_t * qh, const uint16_t * d, int N, int K, uint8_t * out);
-// Q8_0 rows of A (f32 if A32, else f16): q [M][K] int8, dq [M][K/32] (the f16-rounded scale)
+size_t quant_tiled_bytes(int fmt, int N, int K);
+// ggml block rows -> the split arrays (qh / m may be null for formats without them)
+void quant_split_host(int fmt, const uint8_t * blocks, int N, int K, uint8_t * qs, uint32_t * qh, uint16_t * d,
+                      uint16_t * m);
+void quant_tile_host(int fmt, const uint8_t * qs, const uint32_t * qh, const uint16_t * d, const uint16_t * m, int N,
+                     int K, uint8_t * out);
+// Q8_0 / Q8_1 rows of A (f32 if A32, else f16): q [M][K] int8, dq [M][K/32] (raw f32 d = amax / 127)
 void quantize_q8(hipStream_t s, const float * A32, const _Float16 * A16, int lda, int M, int K, int8_t * q, float * dq);
-// C[M,N] = Q8(A) . Q5(W)^T with the fused epilogue `mode` (any EpiMode except EPI_PARTIAL)
+// C[M,N] = Q8(A) . Q(W)^T with the fused epilogue `mode` (any EpiMode except EPI_PARTIAL)
 void gemm_q5(hipStream_t s, int mode, int M, int N, int K, const int8_t * qa, const float * da, const Q5W & w,
              const EpiParams & ep);
-// host-side split of ggml block_q5_0 rows (22 B per block) into the Q5W arrays
-void q5_split_host(const uint8_t * blocks, int N, int K, uint8_t * qs, uint32_t * qh, uint16_t * d);
 
 // ---------------------------------------------------------------------------------
 // normalisation / elementwise
 // ---------------------------------------------------------------------------------
 // out16[r] = f16(LN(x[r]) * w + b); mean/variance accumulated in double (ref ops.cpp:3578-3623)
 // row_idx (optional): output row i normalises input row row_idx[i]; out32 (optional) f32 copy
-// q8/q8d (optional): the f32 output rows as Q8_0 ([row][d] int8, [row][d/32] f16-rounded
-// scales), the activation rounding of a Q5_0 GEMM done in the producer
+// q8/q8d (optional): the f32 output rows as Q8_0 ([row][d] int8, [row][d/32] raw f32 scales),
+// the activation rounding of a quantized GEMM done in the producer
 void layernorm_f16(hipStream_t s, const float * x, int rows, int d, const float * w, const float * b,
                    float eps, _Float16 * out, int ldo, const int * row_idx = nullptr, float * out32 = nullptr,
                    int8_t * q8 = nullptr, float * q8d = nullptr);

@@ -220,14 +220,21 @@ Model * load_model(whisper_model_loader * loader, int device, std::string & err)
     const int qntvr = hp.ftype / 1000;
     (void) qntvr;
     hp.ftype %= 1000;
-    // GGML_FTYPE_MOSTLY_F16 (1), MOSTLY_Q4_0 (2), MOSTLY_Q8_0 (7), MOSTLY_Q5_0 (8) (ggml.h:440-450)
-    if (hp.ftype != 1 && hp.ftype != 2 && hp.ftype != 7 && hp.ftype != 8) {
-        err = "unsupported ftype " + std::to_string(hp.ftype) + " (this engine build loads F16, Q4_0, Q8_0 and Q5_0 models)";
-        return nullptr;
+    // GGML_FTYPE_MOSTLY_F16 (1), MOSTLY_Q4_0 (2), MOSTLY_Q4_1 (3), MOSTLY_Q8_0 (7), MOSTLY_Q5_0 (8),
+    // MOSTLY_Q5_1 (9) (ggml.h:440-450)
+    switch (hp.ftype) {
+        case 1: break;
+        case 2: m->qfmt = QF_Q4_0; break;
+        case 3: m->qfmt = QF_Q4_1; break;
+        case 7: m->qfmt = QF_Q8_0; break;
+        case 8: m->qfmt = QF_Q5_0; break;
+        case 9: m->qfmt = QF_Q5_1; break;
+        default:
+            err = "unsupported ftype " + std::to_string(hp.ftype) +
+                  " (this engine build loads F16, Q4_0, Q4_1, Q5_0, Q5_1 and Q8_0 models)";
+            return nullptr;
     }
-    m->q5 = hp.ftype == 8 || hp.ftype == 7 || hp.ftype == 2;  // quantized weights x Q8_0 activations
-    m->q8 = hp.ftype == 7;
-    m->q4 = hp.ftype == 2;
+    m->q5 = hp.ftype != 1;  // quantized weights x Q8_0 / Q8_1 activations
 
     // mel filters
     m->n_filters_mel = r.get<int32_t>();
@@ -307,10 +314,9 @@ Model * load_model(whisper_model_loader * loader, int device, std::string & err)
         for (size_t i = 0; i < sp.ne.size(); ++i)
             if (ne[i] != sp.ne[i]) { err = "tensor '" + name + "' has wrong shape in model file"; return nullptr; }
         if (nel != expect) { err = "tensor '" + name + "' has wrong size in model file"; return nullptr; }
-        // Q5_0 / Q8_0 models: every 2-D weight is GGML_TYPE_Q5_0 (6, 22 bytes per 32) or
-        // GGML_TYPE_Q8_0 (8, 34 bytes per 32) (whisper-quantize)
+        // quantized models: every 2-D weight is of the model's block type (whisper-quantize)
         const bool want_q5 = m->q5 && sp.f16 && sp.ne.size() == 2;
-        const int qtype = m->q8 ? 8 : (m->q4 ? 2 : 6), qbytes = m->q8 ? 34 : (m->q4 ? 18 : 22);
+        const int qtype = m->q5 ? qf_ggml_type(m->qfmt) : -1, qbytes = m->q5 ? qf_block_bytes(m->qfmt) : 0;
         if (want_q5 ? ttype != qtype : (ttype != 0 && ttype != 1)) {
             err = "tensor '" + name + "': unsupported type " + std::to_string(ttype);
             return nullptr;
@@ -459,98 +465,56 @@ Model * load_model(whisper_model_loader * loader, int device, std::string & err)
         }
         const size_t n_enc_groups = 1 + 4 * (size_t) hp.n_audio_layer;  // groups [1, n_enc_groups): encoder
         size_t qoff = 0;
-        struct Plan { size_t qs, qh, d, tiled; int N, K; };
+        struct Plan { size_t qs, qh, d, m, tiled; int N, K; };
         std::vector<Plan> plans;
         for (size_t gi = 0; gi < groups.size(); ++gi) {
             const auto & gr = groups[gi];
             int N = 0;
             const int K = (int) S[idx.at(gr[0])].ne[0];
             for (const auto & n : gr) N += (int) S[idx.at(n)].ne[1];
-            Plan pl{0, 0, 0, (size_t) -1, N, K};
+            Plan pl{0, 0, 0, 0, (size_t) -1, N, K};
             auto res = [&](size_t bytes) { size_t o = qoff; qoff += (bytes + 255) & ~(size_t) 255; return o; };
-            pl.qs = res(m->q8 ? (size_t) N * K : (size_t) N * K / 2);
-            pl.qh = (m->q8 || m->q4) ? 0 : res((size_t) N * (K / 32) * 4);
+            const int f = m->qfmt;
+            pl.qs = res((size_t) N * (K / 32) * qf_qs_bytes(f));
+            pl.qh = qf_has_qh(f) ? res((size_t) N * (K / 32) * 4) : 0;
             pl.d = res((size_t) N * (K / 32) * 2);
+            pl.m = qf_has_m(f) ? res((size_t) N * (K / 32) * 2) : 0;
             // decode-step matrices also get the column-tiled copy the decode-row GEMM streams
-            if (gi == n_dec_first || gi >= n_enc_groups)
-                pl.tiled = res(m->q8 ? q8_tiled_bytes(N, K) : (m->q4 ? q4_tiled_bytes(N, K) : q5_tiled_bytes(N, K)));
+            if (gi == n_dec_first || gi >= n_enc_groups) pl.tiled = res(quant_tiled_bytes(f, N, K));
             plans.push_back(pl);
         }
         m->q5blob.alloc(qoff);
         char * qb = (char *) m->q5blob.ptr;
-        for (size_t gi = 0; gi < groups.size() && m->q8; ++gi) {
+        const int f = m->qfmt;
+        for (size_t gi = 0; gi < groups.size(); ++gi) {
             const Plan & pl = plans[gi];
-            std::vector<int8_t> qs((size_t) pl.N * pl.K);
-            std::vector<uint16_t> dd((size_t) pl.N * (pl.K / 32));
-            int row = 0;
+            const size_t nbk = (size_t) pl.N * (pl.K / 32);
+            std::vector<uint8_t> qs(nbk * qf_qs_bytes(f));
+            std::vector<uint32_t> qh(qf_has_qh(f) ? nbk : 0);
+            std::vector<uint16_t> dd(nbk), mm(qf_has_m(f) ? nbk : 0);
+            size_t row = 0;
             for (const auto & n : groups[gi]) {
                 const HostTensor & t = host(n);
                 const int rows = (int) S[idx.at(n)].ne[1];
-                q8_split_host(t.data.data(), rows, pl.K, qs.data() + (size_t) row * pl.K, dd.data() + (size_t) row * (pl.K / 32));
+                const size_t b0 = row * (pl.K / 32);
+                quant_split_host(f, t.data.data(), rows, pl.K, qs.data() + b0 * qf_qs_bytes(f),
+                                 qh.empty() ? nullptr : qh.data() + b0, dd.data() + b0, mm.empty() ? nullptr : mm.data() + b0);
                 row += rows;
             }
             OWK_HIP_CHECK(hipMemcpy(qb + pl.qs, qs.data(), qs.size(), hipMemcpyHostToDevice));
             OWK_HIP_CHECK(hipMemcpy(qb + pl.d, dd.data(), dd.size() * 2, hipMemcpyHostToDevice));
+            if (!qh.empty()) OWK_HIP_CHECK(hipMemcpy(qb + pl.qh, qh.data(), qh.size() * 4, hipMemcpyHostToDevice));
+            if (!mm.empty()) OWK_HIP_CHECK(hipMemcpy(qb + pl.m, mm.data(), mm.size() * 2, hipMemcpyHostToDevice));
             Q5W w;
-            w.q8 = true;
+            w.fmt = f;
             w.qs = (const uint8_t *) (qb + pl.qs);
             w.d = (const _Float16 *) (qb + pl.d);
+            if (!qh.empty()) w.qh = (const uint32_t *) (qb + pl.qh);
+            if (!mm.empty()) w.m = (const _Float16 *) (qb + pl.m);
             if (pl.tiled != (size_t) -1) {
-                std::vector<uint8_t> tl(q8_tiled_bytes(pl.N, pl.K));
-                q8_tile_host(qs.data(), dd.data(), pl.N, pl.K, tl.data());
-                OWK_HIP_CHECK(hipMemcpy(qb + pl.tiled, tl.data(), tl.size(), hipMemcpyHostToDevice));
-                w.tiled = (const uint8_t *) (qb + pl.tiled);
-            }
-            q5m[groups[gi][0]] = w;
-        }
-        for (size_t gi = 0; gi < groups.size() && m->q4; ++gi) {
-            const Plan & pl = plans[gi];
-            std::vector<uint8_t> qs((size_t) pl.N * pl.K / 2);
-            std::vector<uint16_t> dd((size_t) pl.N * (pl.K / 32));
-            int row = 0;
-            for (const auto & n : groups[gi]) {
-                const HostTensor & t = host(n);
-                const int rows = (int) S[idx.at(n)].ne[1];
-                q4_split_host(t.data.data(), rows, pl.K, qs.data() + (size_t) row * pl.K / 2, dd.data() + (size_t) row * (pl.K / 32));
-                row += rows;
-            }
-            OWK_HIP_CHECK(hipMemcpy(qb + pl.qs, qs.data(), qs.size(), hipMemcpyHostToDevice));
-            OWK_HIP_CHECK(hipMemcpy(qb + pl.d, dd.data(), dd.size() * 2, hipMemcpyHostToDevice));
-            Q5W w;
-            w.q4 = true;
-            w.qs = (const uint8_t *) (qb + pl.qs);
-            w.d = (const _Float16 *) (qb + pl.d);
-            if (pl.tiled != (size_t) -1) {
-                std::vector<uint8_t> tl(q4_tiled_bytes(pl.N, pl.K));
-                q4_tile_host(qs.data(), dd.data(), pl.N, pl.K, tl.data());
-                OWK_HIP_CHECK(hipMemcpy(qb + pl.tiled, tl.data(), tl.size(), hipMemcpyHostToDevice));
-                w.tiled = (const uint8_t *) (qb + pl.tiled);
-            }
-            q5m[groups[gi][0]] = w;
-        }
-        for (size_t gi = 0; gi < groups.size() && !m->q8 && !m->q4; ++gi) {
-            const Plan & pl = plans[gi];
-            std::vector<uint8_t> qs((size_t) pl.N * pl.K / 2);
-            std::vector<uint32_t> qh((size_t) pl.N * (pl.K / 32));
-            std::vector<uint16_t> dd((size_t) pl.N * (pl.K / 32));
-            int row = 0;
-            for (const auto & n : groups[gi]) {
-                const HostTensor & t = host(n);
-                const int rows = (int) S[idx.at(n)].ne[1];
-                q5_split_host(t.data.data(), rows, pl.K, qs.data() + (size_t) row * pl.K / 2,
-                              qh.data() + (size_t) row * (pl.K / 32), dd.data() + (size_t) row * (pl.K / 32));
-                row += rows;
-            }
-            OWK_HIP_CHECK(hipMemcpy(qb + pl.qs, qs.data(), qs.size(), hipMemcpyHostToDevice));
-            OWK_HIP_CHECK(hipMemcpy(qb + pl.qh, qh.data(), qh.size() * 4, hipMemcpyHostToDevice));
-            OWK_HIP_CHECK(hipMemcpy(qb + pl.d, dd.data(), dd.size() * 2, hipMemcpyHostToDevice));
-            Q5W w;
-            w.qs = (const uint8_t *) (qb + pl.qs);
-            w.qh = (const uint32_t *) (qb + pl.qh);
-            w.d = (const _Float16 *) (qb + pl.d);
-            if (pl.tiled != (size_t) -1) {
-                std::vector<uint8_t> tl(q5_tiled_bytes(pl.N, pl.K));
-                q5_tile_host(qs.data(), qh.data(), dd.data(), pl.N, pl.K, tl.data());
+                std::vector<uint8_t> tl(quant_tiled_bytes(f, pl.N, pl.K));
+                quant_tile_host(f, qs.data(), qh.empty() ? nullptr : qh.data(), dd.data(), mm.empty() ? nullptr : mm.data(),
+                                pl.N, pl.K, tl.data());
                 OWK_HIP_CHECK(hipMemcpy(qb + pl.tiled, tl.data(), tl.size(), hipMemcpyHostToDevice));
                 w.tiled = (const uint8_t *) (qb + pl.tiled);
             }

@@ -83,9 +83,8 @@ struct Model {
     const float * e_pe = nullptr;        // [n_audio_ctx][d]
     const float *e_ln_w = nullptr, *e_ln_b = nullptr;
     std::vector<EncLayerW> enc;
-    bool q5 = false;                     // quantized model (MOSTLY_Q5_0 or MOSTLY_Q8_0): 2-D linears (and d_te) are Q5W
-    bool q8 = false;                     // MOSTLY_Q8_0: those Q5W hold Q8_0 blocks (Q5W::q8)
-    bool q4 = false;                     // MOSTLY_Q4_0: Q4_0 blocks (Q5W::q4)
+    bool q5 = false;                     // quantized model (MOSTLY_Q5_0/Q8_0/Q4_0/Q4_1/Q5_1): 2-D linears (and d_te) are Q5W
+    int qfmt = 0;                        // their block format (kernels.h QFmt)
     DevBuf q5blob;
     Q5W q_te;
     const _Float16 * d_te = nullptr;     // [n_vocab][d]

@@ -1205,22 +1205,25 @@ double owk_debug_gemm_bench(int device, int mode, int M, int N, int K, int iters
     }
 }
 
-int owk_debug_gemm_q5(int device, int M, int N, int K, const float * a, const uint8_t * w_blocks, float * out,
-                      int8_t * q_out, float * d_out) {
+int owk_debug_gemm_quant(int device, int fmt, int M, int N, int K, const float * a, const uint8_t * w_blocks,
+                         float * out, int8_t * q_out, float * d_out) {
     try {
+        if (fmt < QF_Q5_0 || fmt > QF_Q5_1 || K % 32) throw std::runtime_error("bad format or K");
         OWK_HIP_CHECK(hipSetDevice(device));
         hipStream_t s;
         OWK_HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
         const int nb = K / 32;
-        std::vector<uint8_t> qs((size_t) N * K / 2);
-        std::vector<uint32_t> qh((size_t) N * nb);
-        std::vector<uint16_t> dd((size_t) N * nb);
-        q5_split_host(w_blocks, N, K, qs.data(), qh.data(), dd.data());
-        DevBuf da, dqs, dqh, ddd, dout, q8, q8d;
+        const size_t nbk = (size_t) N * nb;
+        std::vector<uint8_t> qs(nbk * qf_qs_bytes(fmt));
+        std::vector<uint32_t> qh(nbk);
+        std::vector<uint16_t> dd(nbk), mm(nbk);
+        quant_split_host(fmt, w_blocks, N, K, qs.data(), qh.data(), dd.data(), mm.data());
+        DevBuf da, dqs, dqh, ddd, dmm, dout, q8, q8d;
         da.alloc((size_t) M * K * 4);
         dqs.alloc(qs.size());
         dqh.alloc(qh.size() * 4);
         ddd.alloc(dd.size() * 2);
+        dmm.alloc(mm.size() * 2);
         dout.alloc((size_t) M * N * 4);
         q8.alloc((size_t) M * K);
         q8d.alloc((size_t) M * nb * 4);
@@ -1228,13 +1231,16 @@ int owk_debug_gemm_q5(int device, int M, int N, int K, const float * a, const ui
         OWK_HIP_CHECK(hipMemcpy(dqs.ptr, qs.data(), qs.size(), hipMemcpyHostToDevice));
         OWK_HIP_CHECK(hipMemcpy(dqh.ptr, qh.data(), qh.size() * 4, hipMemcpyHostToDevice));
         OWK_HIP_CHECK(hipMemcpy(ddd.ptr, dd.data(), dd.size() * 2, hipMemcpyHostToDevice));
+        OWK_HIP_CHECK(hipMemcpy(dmm.ptr, mm.data(), mm.size() * 2, hipMemcpyHostToDevice));
         Q5W w;
+        w.fmt = fmt;
         w.qs = dqs.as<uint8_t>();
-        w.qh = dqh.as<uint32_t>();
+        w.qh = qf_has_qh(fmt) ? dqh.as<uint32_t>() : nullptr;
         w.d = ddd.as<_Float16>();
+        w.m = qf_has_m(fmt) ? dmm.as<_Float16>() : nullptr;
         // the tiled copy a model keeps for its decode-step matrices (decode-row GEMM path)
-        std::vector<uint8_t> tl(q5_tiled_bytes(N, K));
-        q5_tile_host(qs.data(), qh.data(), dd.data(), N, K, tl.data());
+        std::vector<uint8_t> tl(quant_tiled_bytes(fmt, N, K));
+        quant_tile_host(fmt, qs.data(), qh.data(), dd.data(), mm.data(), N, K, tl.data());
         DevBuf dtl;
         dtl.alloc(tl.size());
         OWK_HIP_CHECK(hipMemcpy(dtl.ptr, tl.data(), tl.size(), hipMemcpyHostToDevice));
@@ -1250,10 +1256,15 @@ int owk_debug_gemm_q5(int device, int M, int N, int K, const float * a, const ui
         if (d_out) OWK_HIP_CHECK(hipMemcpy(d_out, q8d.ptr, (size_t) M * nb * 4, hipMemcpyDeviceToHost));
         OWK_HIP_CHECK(hipStreamDestroy(s));
     } catch (const std::exception & ex) {
-        log_msg(GGML_LOG_LEVEL_ERROR, "owk_debug_gemm_q5: %s\n", ex.what());
+        log_msg(GGML_LOG_LEVEL_ERROR, "owk_debug_gemm_quant: %s\n", ex.what());
         return -1;
     }
     return 0;
+}
+
+int owk_debug_gemm_q5(int device, int M, int N, int K, const float * a, const uint8_t * w_blocks, float * out,
+                      int8_t * q_out, float * d_out) {
+    return owk_debug_gemm_quant(device, QF_Q5_0, M, N, K, a, w_blocks, out, q_out, d_out);
 }
 
 // one_chunk cross attention of R rows (row r over its own clip r: k, v [R][H][T][64] f16 head-major,

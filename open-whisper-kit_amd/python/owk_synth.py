@@ -166,7 +166,7 @@ def write_model(path: str, model: str, seed: int = 1234) -> str:
     multilingual = n_vocab >= 51865
     rng = np.random.default_rng(seed)
     h = hashlib.sha256()
-    tmp = path + ".tmp"
+    tmp = f"{path}.tmp{os.getpid()}"
     with open(tmp, "wb") as f:
         def w(b):
             f.write(b)
@@ -234,6 +234,53 @@ def q4_0_blocks(x: np.ndarray) -> bytes:
     return out.tobytes()
 
 
+def _minmax_blocks(x: np.ndarray, nbits: int):
+    """Shared part of quantize_row_q4_1_ref / quantize_row_q5_1_ref (ref ggml/src/ggml-quants.c:
+    73-108, 154-196): d = (max - min) / (2^nbits - 1), id = 1/d, x' = (x - min) * id, and
+    x' + 0.5f -- the multiply and add contracted to one FMA by gcc (as for Q5_0), so the
+    quantized value is trunc(f32(f64(x - min) * id + 0.5))."""
+    b = np.ascontiguousarray(x, np.float32).reshape(-1, 32)
+    mn = b.min(axis=1)
+    mx = b.max(axis=1)
+    d = ((mx - mn) / np.float32((1 << nbits) - 1)).astype(np.float32)
+    with np.errstate(divide="ignore"):
+        idv = np.where(d != 0, np.float32(1.0) / d, np.float32(0.0)).astype(np.float32)
+    t = (b - mn[:, None]).astype(np.float32)
+    xs = (t.astype(np.float64) * idv.astype(np.float64)[:, None] + 0.5).astype(np.float32)
+    return b, d, mn, xs
+
+
+def q4_1_blocks(x: np.ndarray) -> bytes:
+    """ggml Q4_1 blocks (20 B per 32 weights: d f16, m f16, qs[16]), restating
+    quantize_row_q4_1_ref (ref ggml/src/ggml-quants.c:73-108): q = min(15, (int8)(x' + 0.5)),
+    element j low nibble, j + 16 high nibble of byte j."""
+    b, d, mn, xs = _minmax_blocks(x, 4)
+    xi = np.minimum(15, np.trunc(xs).astype(np.int64).astype(np.int8).astype(np.int64) & 0xFF).astype(np.uint8)
+    qs = (xi[:, :16] & 0x0F) | ((xi[:, 16:] & 0x0F) << 4)
+    out = np.zeros((len(b), 20), np.uint8)
+    out[:, 0:2] = d.astype("<f2").view(np.uint8).reshape(-1, 2)
+    out[:, 2:4] = mn.astype("<f2").view(np.uint8).reshape(-1, 2)
+    out[:, 4:20] = qs
+    return out.tobytes()
+
+
+def q5_1_blocks(x: np.ndarray) -> bytes:
+    """ggml Q5_1 blocks (24 B per 32 weights: d f16, m f16, qh u32, qs[16]), restating
+    quantize_row_q5_1_ref (ref ggml/src/ggml-quants.c:154-196): q = (uint8)(x' + 0.5), 4 low
+    bits in nibbles, 5th bits in a little-endian u32."""
+    b, d, mn, xs = _minmax_blocks(x, 5)
+    xi = (np.trunc(xs).astype(np.int64) & 0xFF).astype(np.uint8)
+    qs = (xi[:, :16] & 0x0F) | ((xi[:, 16:] & 0x0F) << 4)
+    bits = ((xi >> 4) & 1).astype(np.uint32)
+    qh = (bits << np.arange(32, dtype=np.uint32)[None, :]).sum(axis=1, dtype=np.uint64).astype("<u4")
+    out = np.zeros((len(b), 24), np.uint8)
+    out[:, 0:2] = d.astype("<f2").view(np.uint8).reshape(-1, 2)
+    out[:, 2:4] = mn.astype("<f2").view(np.uint8).reshape(-1, 2)
+    out[:, 4:8] = qh.view(np.uint8).reshape(-1, 4)
+    out[:, 8:24] = qs
+    return out.tobytes()
+
+
 def q8_0_blocks(x: np.ndarray) -> bytes:
     """block_q8_0 rows of f32 values: quantize_row_q8_0_ref (ref ggml/src/ggml-quants.c:199-222):
     d = amax / 127 (stored f16), q = roundf(x * (1/d)) (round half away from zero)."""
@@ -260,7 +307,18 @@ def quantize_q4_0(src: str, dst: str) -> str:
     return quantize_q5_0(src, dst, kind="q4_0")
 
 
-_QKIND = {"q5_0": (8, 6, q5_0_blocks), "q8_0": (7, 8, q8_0_blocks), "q4_0": (2, 2, q4_0_blocks)}  # ftype, ttype
+def quantize_q4_1(src: str, dst: str) -> str:
+    """Q4_1 copy (ttype 3, ftype 2003 = GGML_QNT_VERSION 2 * 1000 + MOSTLY_Q4_1 3)."""
+    return quantize_q5_0(src, dst, kind="q4_1")
+
+
+def quantize_q5_1(src: str, dst: str) -> str:
+    """Q5_1 copy (ttype 7, ftype 2009 = GGML_QNT_VERSION 2 * 1000 + MOSTLY_Q5_1 9)."""
+    return quantize_q5_0(src, dst, kind="q5_1")
+
+
+_QKIND = {"q5_0": (8, 6, q5_0_blocks), "q8_0": (7, 8, q8_0_blocks), "q4_0": (2, 2, q4_0_blocks),
+          "q4_1": (3, 3, q4_1_blocks), "q5_1": (9, 7, q5_1_blocks)}  # ftype, ttype
 
 
 def quantize_q5_0(src: str, dst: str, kind: str = "q5_0") -> str:
@@ -278,7 +336,7 @@ def quantize_q5_0(src: str, dst: str, kind: str = "q5_0") -> str:
         off += n
         return v
     h = hashlib.sha256()
-    tmp = dst + ".tmp"
+    tmp = f"{dst}.tmp{os.getpid()}"
     with open(tmp, "wb") as f:
         def w(b):
             f.write(b)
@@ -332,9 +390,9 @@ def _cached_ok(path: str) -> bool:
 
 
 def _stamp(path: str, sha: str) -> None:
-    with open(_stamp_path(path) + ".tmp", "w") as f:
+    with open(_stamp_path(path) + f".tmp{os.getpid()}", "w") as f:
         json.dump({"size": os.path.getsize(path), "sha256": sha}, f)
-    os.replace(_stamp_path(path) + ".tmp", _stamp_path(path))
+    os.replace(_stamp_path(path) + f".tmp{os.getpid()}", _stamp_path(path))
 
 
 def file_sha256(path: str) -> str:

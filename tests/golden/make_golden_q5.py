@@ -15,7 +15,7 @@ bounds the GPU error by 2x that floor, and decoded sequences may part only where
 tokens are within 2x the logit floor of each other.
 
 Usage (in a container that has /root/reference):  python tests/golden/make_golden_q5.py [q8_0]
-(q8_0 / q4_0: the same fixtures for Q8_0 / Q4_0 files -> q8_golden.* / q4_golden.*)
+(q8_0 / q4_0 / q4_1 / q5_1: the same fixtures for those files -> q8_ / q4_ / q41_ / q51_golden.*)
 """
 import json
 import os
@@ -35,7 +35,7 @@ SEED = 1234
 MODELS = ["tiny.en", "l3-mini"]
 TF_TOKENS = 48
 KIND = sys.argv[1] if len(sys.argv) > 1 else "q5_0"
-assert KIND in ("q5_0", "q8_0", "q4_0")
+assert KIND in ("q5_0", "q8_0", "q4_0", "q4_1", "q5_1")
 
 
 def main():
@@ -48,7 +48,7 @@ def main():
         src = os.path.join(cache, f"synth-{model}-s{SEED}.bin")
         S.write_model(src, model, SEED)
         path = os.path.join(cache, f"synth-{model}-{KIND}-s{SEED}.bin")
-        quant = {"q5_0": S.quantize_q5_0, "q8_0": S.quantize_q8_0, "q4_0": S.quantize_q4_0}[KIND]
+        quant = lambda s, d: S.quantize_q5_0(s, d, kind=KIND)
         meta["models"][model] = {"sha256": quant(src, path)}
         ref = R.Ref(path)
         multilingual = S.MODELS[model][0] >= 51865
@@ -118,7 +118,7 @@ def main():
                 meta["results"][f"{key}/noise_floor/agree/{cfg}"] = min(agree)
             print(model, cname, "floors", meta["results"][key + "/noise_floor/enc_rows"], dl, flush=True)
         ref.close()
-    stem = KIND[:2] + "_golden"
+    stem = {"q4_1": "q41", "q5_1": "q51"}.get(KIND, KIND[:2]) + "_golden"
     meta["kind"] = KIND
     np.savez_compressed(os.path.join(OUT, stem + ".npz"), **arrays)
     with open(os.path.join(OUT, stem + ".json"), "w") as f:

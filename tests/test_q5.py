@@ -1,6 +1,7 @@
-"""Q5_0, Q8_0 and Q4_0 models (ftype 2008 / 2007 / 2002).
-Every test runs for each kind: q5_golden.*, q8_golden.*, q4_golden.*, made by
-tests/golden/make_golden_q5.py [q8_0|q4_0] from the reference on the same synthetic weights.
+"""Q5_0, Q8_0, Q4_0, Q4_1 and Q5_1 models (ftype 2008 / 2007 / 2002 / 2003 / 2009; SURVEY rows A1 /
+A15, 8(f) row 4). Every test runs for each kind: q5_golden.*, q8_golden.*, q4_golden.*, q41_golden.*,
+q51_golden.*, made by tests/golden/make_golden_q5.py [q8_0|q4_0|q4_1|q5_1] from the reference on the
+same synthetic weights. Q4_1 / Q5_1 take Q8_1 activations (the block-sum term m_w * s_a).
 
 CPU: owk_synth.quantize_q5_0 (restatement of whisper-quantize) writes byte-identical files to
 the reference quantizer compiled from its own sources (oracle/_ref/whisper-quantize).
@@ -27,7 +28,10 @@ GOLDEN = os.path.join(ROOT, "tests", "golden")
 QUANT = os.path.join(ROOT, "oracle", "_ref", "whisper-quantize")
 
 
-KINDS = {"q5_0": ("q5_golden", 8), "q8_0": ("q8_golden", 7), "q4_0": ("q4_golden", 2)}  # fixture stem, GGML_FTYPE_MOSTLY_*
+KINDS = {"q5_0": ("q5_golden", 8), "q8_0": ("q8_golden", 7), "q4_0": ("q4_golden", 2), "q4_1": ("q41_golden", 3),
+         "q5_1": ("q51_golden", 9)}  # fixture stem, GGML_FTYPE_MOSTLY_*
+# owk_debug_gemm_quant format ids (kernels.h QFmt) and the ggml block type / size of each kind
+QFMT = {"q5_0": (0, 6, 22), "q8_0": (1, 8, 34), "q4_0": (2, 2, 18), "q4_1": (3, 3, 20), "q5_1": (4, 7, 24)}
 
 
 @pytest.fixture(scope="module", params=list(KINDS))
@@ -176,3 +180,42 @@ def test_q5_teacher_forced(q5g, clips, model, clip):
         assert L.whisper_decode_with_state(w.ctx, st, one, 1, i, 1) == 0
         lg = np.ctypeslib.as_array(L.whisper_get_logits_from_state(st), shape=(w.n_vocab,))
         np.testing.assert_allclose(lg[idx[i]], val[i], atol=tol, rtol=0, err_msg=f"{key} step {i}")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", list(QFMT))
+@pytest.mark.parametrize("M,N,K", [(1, 384, 384), (17, 1280, 1280), (32, 5120, 1280), (32, 1280, 5120), (40, 1536, 384),
+                                   (300, 384, 1536)])
+def test_quant_gemm_vs_reference(kind, M, N, K):
+    """The engine's quantize + quantized GEMM (decode-row kernel for M <= 32, skinny for M <= 64, tiled
+    above) against the reference's own ggml_mul_mat on the same ggml blocks and f32 activations
+    (oracle/_ref/libwhisper_ref.so ref_mul_mat: the x86 quantize_row_q8_0 / _q8_1 + vec_dot path).
+    Integer block dots are exact on both sides; only the f32 summation order differs."""
+    import sys
+    import owk_synth as S
+
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import ref_oracle as R
+
+    if not R.available():
+        pytest.skip("reference oracle not built")
+    L = owk.load()
+    fmt, wtype, bb = QFMT[kind]
+    L.owk_debug_gemm_quant.argtypes = [C.c_int] * 5 + [C.POINTER(C.c_float), C.c_void_p, C.POINTER(C.c_float),
+                                                       C.c_void_p, C.c_void_p]
+    rng = np.random.default_rng(M * 7 + N + K)
+    a = (rng.standard_normal((M, K)) * 0.7).astype(np.float32)
+    wf = (rng.standard_normal((N, K)) / np.sqrt(K) + 0.02).astype(np.float32)
+    blocks = S._QKIND[kind][2](wf)
+    assert len(blocks) == N * K // 32 * bb
+    out = np.zeros((M, N), np.float32)
+    assert L.owk_debug_gemm_quant(0, fmt, M, N, K, a.ctypes.data_as(C.POINTER(C.c_float)), blocks,
+                                  out.ctypes.data_as(C.POINTER(C.c_float)), None, None) == 0
+    RL = R.lib()
+    RL.ref_mul_mat.argtypes = [C.c_int, C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_float), C.c_int,
+                               C.POINTER(C.c_float), C.c_int]
+    ref = np.zeros((M, N), np.float32)
+    assert RL.ref_mul_mat(wtype, blocks, N, K, a.ctypes.data_as(C.POINTER(C.c_float)), M,
+                          ref.ctypes.data_as(C.POINTER(C.c_float)), 4) == 0
+    err = np.abs(out - ref).max() / np.abs(ref).max()
+    assert err < 2e-6, (kind, M, N, K, err)

@@ -37,5 +37,5 @@ for M, N, K in ((8, 384, 384), (32, 1280, 5120), (24, 3840, 1280), (17, 5120, 12
     wq, wd = q5_vals(blocks, N, K)
     isum = np.einsum("mbk,nbk->mnb", qr.reshape(M, -1, 32).astype(np.int64), wq.astype(np.int64))
     ref = (isum.astype(np.float64) * (dr[:, None, :].astype(np.float64) * wd[None, :, :].astype(np.float64))).sum(-1)
-    print(M, N, K, "q8 equal", np.array_equal(q, qr), "d equal", np.array_equal(dq, dr),
+    print(M, N, K, "q8 equal", np.array_equal(q, qr), "d equal", np.array_equal(dq.astype(np.float16).astype(np.float32), dr),
           "gemm max rel", float(np.abs(out - ref).max() / np.abs(ref).max()))
