@@ -636,12 +636,14 @@ void Engine::launch_decode(const DecShape & sh) {
     //    mlp.0) normalises its A operand from them (AlnParams) -- no LayerNorm launch;
     //  * mlp.2 (K = 4d: long, so split over k): partial tiles, then one kernel adds them with bias +
     //    residual and writes the next layer's attn_ln output (resid_layernorm).
-    // Plans (OWK_DEC_PLAN, measured per shape in DESIGN.md): 1 the above (default); 0 partial tiles +
-    // resid_layernorm after all three; 2 statistics after all three (self Q/K/V normalises too).
-    // Larger passes use the full-epilogue GEMMs and separate LayerNorms.
+    // Plans (OWK_DEC_PLAN): 0 (default) partial tiles + resid_layernorm after all three residual
+    // matmuls; 1 the above (LayerNorm-operand GEMMs for cross Q and mlp.0); 2 statistics after all
+    // three (self Q/K/V normalises too). Measured on large-v3 x 32 clips (profiles/r02e_ab.txt): RTF
+    // 923 / 846 / 806 -- the LayerNorm-operand GEMMs (12 and 23 us) cost more than the LayerNorm
+    // launches they replace. Larger passes use the full-epilogue GEMMs and separate LayerNorms.
     static const int plan_env = [] {
         const char * v = getenv("OWK_DEC_PLAN");
-        return v && *v ? atoi(v) : 1;
+        return v && *v ? atoi(v) : 0;
     }();
     // two row groups on two streams (OWK_DEC_SPLIT=1): each half runs the whole layer chain for
     // its rows; one half's latency-bound launches overlap the other's HBM-bound attention. Rows

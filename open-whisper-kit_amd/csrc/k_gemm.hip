@@ -937,8 +937,15 @@ __device__ __forceinline__ long wq_group(const Q5W & w, int n, int kb, int g, in
     }
 }
 
-// the Q8_1 block sum term of a "_1" format: f16(d_f32 * sum(q)) (quantize_row_q8_1's y.s)
-__device__ __forceinline__ float q8_1_sum(float d_raw, int isum) { return (float) (_Float16) (d_raw * (float) isum); }
+// the Q8_1 block sum term of a "_1" format: f16(d_f32 * sum(q)) (quantize_row_q8_1's y.s). The f32
+// product is rounded first (the reference's two roundings): the empty asm keeps hipcc from folding
+// multiply and conversion into one v_mad_mixlo_f16, whose single rounding of the exact product
+// breaks f16 ties the other way (measured: 2 of 14 400 block sums)
+__device__ __forceinline__ float q8_1_sum(float d_raw, int isum) {
+    float p = d_raw * (float) isum;
+    asm volatile("" : "+v"(p));
+    return (float) (_Float16) p;
+}
 
 // skinny: M <= 64 rows; one 16-column tile per block, 8 waves split the K blocks, partial
 // tiles reduced through LDS in fixed wave order. "_1" formats: a second MFMA against an
@@ -1136,8 +1143,8 @@ __global__ __launch_bounds__(256) void k_gemm_q5_big(int M, int N, int K, const 
         // "_1" formats: the Q8_1 block sum of the activation row (its 4 groups sit in adjacent lanes)
         int isum = 0;
         if (has_m) {
-            isum = __builtin_amdgcn_sdot4((int) (av & 0xFFFFFFFF), 0x01010101, 0, false);
-            isum = __builtin_amdgcn_sdot4((int) (av >> 32), 0x01010101, isum, false);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) isum += (int) (int8_t) (uint8_t) ((uint64_t) av >> (8 * e));
             isum += __shfl_xor(isum, 1, 64);
             isum += __shfl_xor(isum, 2, 64);
         }

@@ -14,7 +14,7 @@ for v in "$@"; do
   ( IFS=','; for e in $envs; do [ -n "$e" ] && export "$e"; done
     timeout -k 10 400 python bench.py --steps 2 --warmup 1 --no-cpu-baseline \
       > gpurun_out/$TAG/bench_$name.json 2> gpurun_out/$TAG/bench_$name.err ) || { echo "bench $name failed"; tail -20 gpurun_out/$TAG/bench_$name.err; exit 1; }
-  echo "$name: $(python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(d['value'], d['ms_per_step'], (d.get("parity") or {}).get("tokens_equal"))" gpurun_out/$TAG/bench_$name.json)"
+  echo "$name: $(python3 tools/bench_line.py gpurun_out/$TAG/bench_$name.json)"
 done
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/$TAG/prof -o run -- \
