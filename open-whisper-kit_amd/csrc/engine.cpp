@@ -86,7 +86,7 @@ Engine::Engine(const Model * m_, Prof * prof_) : m(m_), prof(prof_) {
     size_t fl = 0;
     for (int N : {3 * d, d, 4 * d, nv})
         for (int K : {d, 4 * d}) fl = std::max(fl, gemm_ws_floats(N, K));
-    for (int K : {d, 4 * d}) fl = std::max(fl, gemm_partial_floats(d, K));
+    for (int K : {d, 4 * d}) fl = std::max(fl, std::max(gemm_partial_floats(d, K), q5_partial_floats(d, K)));
     gws_part_.alloc(std::max<size_t>(fl, 1) * 4);
     gws_.partial = gws_part_.as<float>();
     gws_.partial_floats = fl;
@@ -794,7 +794,76 @@ void Engine::launch_decode(const DecShape & sh) {
             OWK_HIP_CHECK(hipStreamWaitEvent(stream, ev_join_, 0));
         }
     }
-    for (int l = 0; l < hp.n_text_layer && !fused; ++l) {
+    // quantized decode passes of <= 32 rows (the bench's greedy steps): the residual matmuls (attn.out,
+    // cross_attn.out, mlp.2) write split-K partial tiles and resid_layernorm adds them to the residual
+    // stream with bias and emits the next LayerNorm as f16 AND as Q8_0 rows (the next GEMM's operand):
+    // one launch where a full-epilogue GEMM plus a LayerNorm launch were
+    const bool q5p = q5 && R <= 32 && !sh.self_sm && !sh.cross_sm && !sh.capture;
+    auto resid_q5p = [&](const _Float16 * A16, const float * A32, const Q5W & q, int K, const float * bias,
+                         const float * lnw, const float * lnb, bool a_q8) {
+        EpiParams ep;
+        ep.out32 = gws_.partial;
+        if (gws_.partial_floats < q5_partial_floats(d, K)) throw std::runtime_error("decode: partial workspace");
+        linear("gemm_dec", EPI_PARTIAL, R, d, K, A16, A32, K, nullptr, q, ep, nullptr, true, a_q8);
+        ProfScope ps(prof, stream, "layernorm");
+        resid_layernorm(stream, R, d, q5_partial_splits(K), gws_.partial, bias, d_x_.as<float>(), lnw, lnb, hp.eps,
+                        d_xn_.as<_Float16>(), d, lnw ? q8a() : nullptr, lnw ? q8d() : nullptr);
+    };
+    if (q5p) ln(m->dec[0].attn_ln_w, m->dec[0].attn_ln_b);  // layer 0's attn_ln (with its Q8_0 rows)
+    for (int l = 0; l < hp.n_text_layer && q5p; ++l) {
+        const DecLayerW & L = m->dec[l];
+        const DecLayerW * nx = l + 1 < hp.n_text_layer ? &m->dec[l + 1] : nullptr;
+        _Float16 * Kl = self_k_.as<_Float16>() + l * self_stride;
+        _Float16 * Vl = self_v_.as<_Float16>() + l * self_stride;
+        {
+            EpiParams ep;
+            ep.bias = L.b_q;
+            ep.bias2 = L.b_v;
+            ep.scale = kq_scale;
+            ep.out16 = d_q_.as<_Float16>();
+            ep.ldo = d;
+            ep.out16b = Kl;
+            ep.out16c = Vl;
+            ep.d = d;
+            ep.row_off = d_rowoff;
+            ep.Tpad = kv_cells * 64;
+            G("qkv", EPI_QKV_DEC, 3 * d, d, d_xn_.as<_Float16>(), nullptr, L.w_qkv, L.t_qkv, L.q_qkv, ep, R, true);
+        }
+        {
+            ProfScope ps(prof, stream, "attn_self");
+            attn_decoder(stream, d_q_.as<_Float16>(), d, Kl, Vl, 64, kv_cells * 64, d_rs, R, d_keys, H, 1.0f, max_keys,
+                         d_ao_.as<_Float16>(), d, self_oc, self_tl, fq_self ? nullptr : ao32, sh.self_list,
+                         fq_self ? q8a() : nullptr, fq_self ? q8d() : nullptr);
+        }
+        resid_q5p(d_ao_.as<_Float16>(), ao32, L.q_o, d, L.b_o, L.cross_ln_w, L.cross_ln_b, fq_self);
+        {
+            EpiParams ep;
+            ep.bias = L.cb_q;
+            ep.out16 = d_q_.as<_Float16>();
+            ep.ldo = d;
+            G("cq", EPI_F16, d, d, d_xn_.as<_Float16>(), nullptr, L.cw_q, L.t_cq, L.q_cq, ep, R, true);
+        }
+        {
+            ProfScope ps(prof, stream, "attn_cross", 4.0 * R * (double) n_ctx_pad * d, 2.0 * 2.0 * R * (double) T * d);
+            attn_decoder(stream, d_q_.as<_Float16>(), d, cross_k_.as<_Float16>() + l * cross_stride,
+                         cross_v_.as<_Float16>() + l * cross_stride, 64, T * 64, d_rc, R, nullptr, H,
+                         kq_scale, T, d_ao_.as<_Float16>(), d, cross_oc, cross_tl, fq_cross ? nullptr : ao32, true,
+                         fq_cross ? q8a() : nullptr, fq_cross ? q8d() : nullptr);
+        }
+        resid_q5p(d_ao_.as<_Float16>(), ao32, L.q_co, d, L.cb_o, L.mlp_ln_w, L.mlp_ln_b, fq_cross);
+        {
+            EpiParams ep;
+            ep.bias = L.b_mlp0;
+            ep.gelu_tab = m->gelu_tab;
+            ep.out16 = d_h_.as<_Float16>();
+            ep.ldo = 4 * d;
+            G("mlp0", EPI_GELU_F16, 4 * d, d, d_xn_.as<_Float16>(), nullptr, L.w_mlp0, L.t_mlp0, L.q_mlp0, ep, R, true);
+        }
+        // GELU outputs are F16 table values: exact as the f32 tensor the reference quantizes
+        resid_q5p(d_h_.as<_Float16>(), nullptr, L.q_mlp1, 4 * d, L.b_mlp1, nx ? nx->attn_ln_w : nullptr,
+                  nx ? nx->attn_ln_b : nullptr, false);
+    }
+    for (int l = 0; l < hp.n_text_layer && !fused && !q5p; ++l) {
         const DecLayerW & L = m->dec[l];
         _Float16 * Kl = self_k_.as<_Float16>() + l * self_stride;
         _Float16 * Vl = self_v_.as<_Float16>() + l * self_stride;

@@ -1032,7 +1032,10 @@ __global__ __launch_bounds__(GQ_MAXW * 64) void k_gemm_q5_rows(int M, int N, int
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: branch-free k range
     const int n0 = blockIdx.x * 16;
     const int nb = K >> 5;
-    const int kb0 = wave * GQ_J;
+    // split-K (gridDim.y > 1, EPI_PARTIAL): block y covers K blocks [kblo, kblo + nbl)
+    const int kblo = blockIdx.y * nw * GQ_J;
+    const int nbl = min(nw * GQ_J, nb - kblo);
+    const int kb0 = kblo + wave * GQ_J;
     const int nj = max(0, min(GQ_J, nb - kb0));
     const int g = lane >> 4;
     const int c16 = lane & 15;
@@ -1059,19 +1062,21 @@ __global__ __launch_bounds__(GQ_MAXW * 64) void k_gemm_q5_rows(int M, int N, int
             a[i][j] = j < nj ? t : 0L;
         }
     }
-    // activation scales (raw f32 d; at most GQ_DA_PER_THREAD per thread: M <= 32, nw = ceil(nb / J))
-    // to LDS; every load of the launch is issued before the first wait (one round trip)
+    // activation scales of this block's K range (raw f32 d; at most GQ_DA_PER_THREAD per thread:
+    // M <= 32, nbl <= nw * J) to LDS as [row][kb - kblo]; every load of the launch is issued before
+    // the first wait (one round trip)
     float dv[GQ_DA_PER_THREAD];
 #pragma unroll
     for (int u = 0; u < GQ_DA_PER_THREAD; ++u) {
         const int i = tid + u * blockDim.x;
-        dv[u] = i < M * nb ? da[i] : 0.0f;
+        const int r = i / nbl;
+        dv[u] = i < M * nbl ? da[(size_t) r * nb + kblo + (i - r * nbl)] : 0.0f;
     }
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int u = 0; u < GQ_DA_PER_THREAD; ++u) {
         const int i = tid + u * blockDim.x;
-        if (i < M * nb) sda[i] = dv[u];
+        if (i < M * nbl) sda[i] = dv[u];
     }
     __syncthreads();
     floatx4 acc[MT], accm[MT];
@@ -1092,7 +1097,7 @@ __global__ __launch_bounds__(GQ_MAXW * 64) void k_gemm_q5_rows(int M, int N, int
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
                 const int r = min(i * 16 + 4 * g + e, M - 1);
-                const float dr = sda[r * nb + kb];
+                const float dr = sda[r * nbl + (kb - kblo)];
                 acc[i][e] += (float) iv[e] * ((float) (_Float16) dr * dwf);
                 if constexpr (HAS_M) accm[i][e] += (float) mw[j] * q8_1_sum(dr, is[e]);
             }
@@ -1109,7 +1114,12 @@ __global__ __launch_bounds__(GQ_MAXW * 64) void k_gemm_q5_rows(int M, int N, int
         float sum = rp[0];
         for (int ww = 1; ww < nw; ++ww) sum += rp[ww * MT * 64 * 4];
         const int c = n0 + cc;
-        if (r < M && c < N) epi_store<MODE>(ep, r, c, sum);
+        if (r < M && c < N) {
+            if constexpr (MODE == EPI_PARTIAL)
+                ep.out32[((size_t) blockIdx.y * M + r) * N + c] = sum;  // [ks][M][N] for resid_layernorm
+            else
+                epi_store<MODE>(ep, r, c, sum);
+        }
     }
 }
 
@@ -1200,15 +1210,25 @@ __global__ __launch_bounds__(256) void k_gemm_q5_big(int M, int N, int K, const 
         }
 }
 
+// k splits of a partial (EPI_PARTIAL) quantized decode-row GEMM: ~20-40 K blocks per split, 3 per
+// wave (K 1280: 2 splits of 7 waves; K 5120: 4 splits of 14 waves)
+int q5_partial_splits(int K) { return std::min(4, std::max(1, (K / 32 + 19) / 20)); }
+size_t q5_partial_floats(int N, int K) { return (size_t) q5_partial_splits(K) * 32 * N; }
+
 template <int MODE> struct LaunchQ5 {
     static void run(hipStream_t s, int M, int N, int K, const int8_t * qa, const float * da, const Q5W & w,
                     const EpiParams & ep) {
         const int nb = K / 32;
+        if (MODE == EPI_PARTIAL && !(M <= 32 && w.tiled)) throw std::runtime_error("gemm_q5: EPI_PARTIAL needs the decode-row path");
         if (M <= 32 && w.tiled && nb <= GQ_MAXW * GQ_JMAX && M * nb <= GQ_MAX_SCALES) {
-            // more, shorter waves when K allows: 3 K blocks per wave up to K = 1536
-            const int J = nb <= GQ_MAXW * 3 ? 3 : GQ_JMAX;
-            const int nw = (nb + J - 1) / J;
-            const dim3 grid((N + 15) / 16), block(nw * 64);
+            // more, shorter waves when K allows: 3 K blocks per wave up to K = 1536; partial launches
+            // (EPI_PARTIAL, summed by resid_layernorm) split K over gridDim.y (q5_partial_splits)
+            const int KS = MODE == EPI_PARTIAL ? q5_partial_splits(K) : 1;
+            const int J = (KS > 1 || nb <= GQ_MAXW * 3) ? 3 : GQ_JMAX;
+            const int per = (nb + KS - 1) / KS;
+            const int nw = (per + J - 1) / J;
+            if (nw > GQ_MAXW) throw std::runtime_error("gemm_q5: decode-row plan");
+            const dim3 grid((N + 15) / 16, KS), block(nw * 64);
 #define OWK_Q_ROWS(MT_, F_, J_) hipLaunchKernelGGL((k_gemm_q5_rows<MODE, MT_, F_, J_>), grid, block, 0, s, M, N, K, qa, da, w, ep)
 #define OWK_Q_ROWS_J(MT_, F_) do { if (J == 3) OWK_Q_ROWS(MT_, F_, 3); else OWK_Q_ROWS(MT_, F_, GQ_JMAX); } while (0)
 #define OWK_Q_ROWS_F(MT_)                                                 \
@@ -1320,6 +1340,11 @@ void gemm_q5(hipStream_t s, int mode, int M, int N, int K, const int8_t * qa, co
              const EpiParams & ep) {
     if (M <= 0 || N <= 0 || K <= 0 || K % 32) throw std::runtime_error("gemm_q5: unsupported shape");
     if (!w) throw std::runtime_error("gemm_q5: no Q5_0 weights");
+    if (mode == EPI_PARTIAL) {
+        if (!ep.out32) throw std::runtime_error("gemm_q5: EPI_PARTIAL needs the partial workspace in out32");
+        LaunchQ5<EPI_PARTIAL>::run(s, M, N, K, qa, da, w, ep);
+        return;
+    }
     dispatch_mode<LaunchQ5>(mode, s, M, N, K, qa, da, w, ep);
 }
 

@@ -126,7 +126,8 @@ __device__ __forceinline__ double block_sum_d(double v, double * red) {
 __global__ __launch_bounds__(256) void k_resid_layernorm(int M, int N, int KS, const float * __restrict__ part,
                                                          const float * __restrict__ bias, float * __restrict__ x,
                                                          const float * __restrict__ w, const float * __restrict__ b,
-                                                         float eps, _Float16 * __restrict__ xn, int ldo) {
+                                                         float eps, _Float16 * __restrict__ xn, int ldo,
+                                                         int8_t * __restrict__ q8, float * __restrict__ q8d) {
     __shared__ double red[4];
     const int t = threadIdx.x;
     const int row = blockIdx.x;
@@ -177,21 +178,43 @@ __global__ __launch_bounds__(256) void k_resid_layernorm(int M, int N, int KS, c
         const int i = t + 256 * j;
         if (i < n4) {
             const float4 ww = ((const float4 *) w)[i], bb = ((const float4 *) b)[i];
+            float4 y;
+            y.x = (xv[j].x - mean) * scale * ww.x + bb.x;
+            y.y = (xv[j].y - mean) * scale * ww.y + bb.y;
+            y.z = (xv[j].z - mean) * scale * ww.z + bb.z;
+            y.w = (xv[j].w - mean) * scale * ww.w + bb.w;
             half4 h;
-            h[0] = (_Float16) ((xv[j].x - mean) * scale * ww.x + bb.x);
-            h[1] = (_Float16) ((xv[j].y - mean) * scale * ww.y + bb.y);
-            h[2] = (_Float16) ((xv[j].z - mean) * scale * ww.z + bb.z);
-            h[3] = (_Float16) ((xv[j].w - mean) * scale * ww.w + bb.w);
+            h[0] = (_Float16) y.x;
+            h[1] = (_Float16) y.y;
+            h[2] = (_Float16) y.z;
+            h[3] = (_Float16) y.w;
             *(half4 *) (o + 4 * i) = h;
+            if (q8) {
+                // Q8_0 rows of the f32 LayerNorm output (quantized GEMM operand; x86 quantize_row_q8_0):
+                // a 32-block is the float4s of 8 consecutive threads (N % 32 == 0)
+                float m = fmaxf(fmaxf(fabsf(y.x), fabsf(y.y)), fmaxf(fabsf(y.z), fabsf(y.w)));
+#pragma unroll
+                for (int sh = 1; sh < 8; sh <<= 1) m = fmaxf(m, __shfl_xor(m, sh, 8));
+                const float id = m != 0.0f ? 127.f / m : 0.0f;
+                char4 qv;
+                qv.x = (signed char) rintf(y.x * id);
+                qv.y = (signed char) rintf(y.y * id);
+                qv.z = (signed char) rintf(y.z * id);
+                qv.w = (signed char) rintf(y.w * id);
+                *(char4 *) (q8 + (size_t) row * N + 4 * i) = qv;
+                if ((i & 7) == 0) q8d[(size_t) row * (N / 32) + (i >> 3)] = m / 127.f;  // raw f32 d (kernels.h QFmt)
+            }
         }
     }
 }
 
 void resid_layernorm(hipStream_t s, int M, int N, int ks, const float * part, const float * bias, float * x,
-                     const float * lnw, const float * lnb, float eps, _Float16 * xn, int ldo) {
+                     const float * lnw, const float * lnb, float eps, _Float16 * xn, int ldo, int8_t * q8, float * q8d) {
     if (M <= 0) return;
     if (M > 32 || N % 16 != 0 || N > 4 * 256 * RL_V4) throw std::runtime_error("resid_layernorm: unsupported shape");
-    hipLaunchKernelGGL(k_resid_layernorm, dim3(M), dim3(256), 0, s, M, N, ks, part, bias, x, lnw, lnb, eps, xn, ldo);
+    if (q8 && (N % 32 != 0 || !q8d)) throw std::runtime_error("resid_layernorm: Q8_0 output needs N % 32 == 0");
+    hipLaunchKernelGGL(k_resid_layernorm, dim3(M), dim3(256), 0, s, M, N, ks, part, bias, x, lnw, lnb, eps, xn, ldo,
+                       q8, q8d);
 }
 
 void layernorm_f16(hipStream_t s, const float * x, int rows, int d, const float * w, const float * b, float eps,

@@ -90,8 +90,10 @@ int gemm_partial_splits(int K);            // its k splits (rows of partial tile
 // x[r][c] += sum_ks partial + bias[c]  (the reference's mul_mat + bias + residual add), then
 // LayerNorm of the updated row -> xn (f16), unless lnw == nullptr (residual only).
 // `part` holds `ks` splits [ks][M][N] of an EPI_PARTIAL GEMM with M rows (M <= 32) and N columns.
+// q8/q8d (optional): the f32 LayerNorm output as Q8_0 rows too (a quantized model's next GEMM operand)
 void resid_layernorm(hipStream_t s, int M, int N, int ks, const float * part, const float * bias, float * x,
-                     const float * lnw, const float * lnb, float eps, _Float16 * xn, int ldo);
+                     const float * lnw, const float * lnb, float eps, _Float16 * xn, int ldo,
+                     int8_t * q8 = nullptr, float * q8d = nullptr);
 // dispatch on M: <= 32 rows decode-row GEMM (needs the tiled copy Wt), <= 64 skinny,
 // else 128x128 tiles (row-major W)
 void gemm(hipStream_t s, int mode, int M, int N, int K, const _Float16 * A, int lda,
@@ -156,9 +158,12 @@ void quant_tile_host(int fmt, const uint8_t * qs, const uint32_t * qh, const uin
                      int K, uint8_t * out);
 // Q8_0 / Q8_1 rows of A (f32 if A32, else f16): q [M][K] int8, dq [M][K/32] (raw f32 d = amax / 127)
 void quantize_q8(hipStream_t s, const float * A32, const _Float16 * A16, int lda, int M, int K, int8_t * q, float * dq);
-// C[M,N] = Q8(A) . Q(W)^T with the fused epilogue `mode` (any EpiMode except EPI_PARTIAL)
+// C[M,N] = Q8(A) . Q(W)^T with the fused epilogue `mode`; EPI_PARTIAL (M <= 32, tiled weights): raw
+// split-K partial tiles [q5_partial_splits(K)][M][N] to ep.out32, finished by resid_layernorm
 void gemm_q5(hipStream_t s, int mode, int M, int N, int K, const int8_t * qa, const float * da, const Q5W & w,
              const EpiParams & ep);
+int q5_partial_splits(int K);
+size_t q5_partial_floats(int N, int K);  // workspace floats of a partial quantized GEMM (M <= 32)
 
 // ---------------------------------------------------------------------------------
 // normalisation / elementwise
