@@ -1155,8 +1155,10 @@ double owk_debug_gemm_bench(int device, int mode, int M, int N, int K, int iters
         OWK_HIP_CHECK(hipSetDevice(device));
         hipStream_t s;
         OWK_HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
-        DevBuf da, dw, dwt, d32, d16, dres, part, bias;
+        DevBuf da, dw, dwt, d32, d16, dres, part, bias, gtab;
         da.alloc((size_t) M * K * 2);
+        gtab.alloc(65536 * 2);  // EPI_GELU_F16 timing: table contents do not matter
+        OWK_HIP_CHECK(hipMemset(gtab.ptr, 0, gtab.bytes));
         dw.alloc((size_t) N * K * 2);
         dwt.alloc(tiled_weight_elems(N, K) * 2);
         d32.alloc((size_t) M * N * 4);
@@ -1183,6 +1185,7 @@ double owk_debug_gemm_bench(int device, int mode, int M, int N, int K, int iters
         ep.out32 = d32.as<float>();
         ep.out16 = d16.as<_Float16>();
         ep.ldo = N;
+        ep.gelu_tab = gtab.as<uint16_t>();
         hipEvent_t e0, e1;
         OWK_HIP_CHECK(hipEventCreate(&e0));
         OWK_HIP_CHECK(hipEventCreate(&e1));

@@ -15,11 +15,13 @@ ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
 sys.path.insert(0, os.path.join(ROOT, "open-whisper-kit_amd", "python"))
 import owk  # noqa: E402
 
-EPI = {"f32": 7, "resid": 2, "gelu": 1}  # kernels.h EPI_* (EPI_F32 = 7, EPI_RESID_F32 = 2, EPI_GELU_F16 = 1)
+EPI = {"f32": 7, "resid": 2, "gelu": 1, "f16": 0}  # kernels.h EPI_* (EPI_F32 = 7, EPI_RESID_F32 = 2, EPI_GELU_F16 = 1)
 SHAPES = {  # name: (M, N, K, epilogue) -- large-v3 encoder at 32 clips x 1500 positions
     "qkv": (48000, 3840, 1280, "f32"),
     "o_proj": (48000, 1280, 1280, "resid"),
     "mlp0": (48000, 5120, 1280, "f32"),
+    "mlp0_gelu": (48000, 5120, 1280, "gelu"),
+    "mlp0_f16": (48000, 5120, 1280, "f16"),
     "mlp1": (48000, 1280, 5120, "resid"),
     "cross_kv": (48000, 2560, 1280, "f32"),
     "conv2": (48000, 1280, 3840, "f32"),
