@@ -65,6 +65,8 @@ WHISPER_API int owk_debug_cross(struct whisper_context * ctx, struct whisper_sta
 WHISPER_API const uint16_t * owk_debug_gelu_table(void);
 /* out[M][N] = A[M][K] . W[N][K]^T (f16 bits in, f32 out) through the engine's GEMM dispatch */
 WHISPER_API int owk_debug_gemm(int device, int M, int N, int K, const uint16_t * a, const uint16_t * w, float * out);
+// one large-tile epilogue mode through the 128x128 and 256x256 kernels on the same random operands: max |diff|
+WHISPER_API double owk_debug_gemm_epi_diff(int device, int mode, int M, int N, int K, int d, int T);
 /* average microseconds per launch of `iters` back-to-back engine GEMMs (epilogue `mode`, zero data) */
 /* test hook (host only): the DTW alignment of captured alignment-head attention
  * cap[(head * n_audio_ctx + j) * n_tok + t] (the reference's aheads_cross_QKs layout), as
@@ -84,6 +86,9 @@ WHISPER_API int owk_debug_gemm_q5(int device, int M, int N, int K, const float *
  * of that type; Q4_1 / Q5_1 take Q8_1 activations); d_out receives the raw f32 activation scales */
 WHISPER_API int owk_debug_gemm_quant(int device, int fmt, int M, int N, int K, const float * a, const uint8_t * w_blocks,
                                      float * out, int8_t * q_out, float * d_out);
+// use_q16 = 1: the large-tile encoder path (expanded f16 integers, gemm_q16; M >= 2048, symmetric formats)
+WHISPER_API int owk_debug_gemm_quant2(int device, int fmt, int M, int N, int K, const float * a, const uint8_t * w_blocks,
+                                      float * out, int8_t * q_out, float * d_out, int use_q16);
 /* mode | 0x100: force the 128x128 large-GEMM kernel; | 0x400: 5-slot ring variant of the 256x256 kernel;
  * | 0x200: uniform random operands (else zeros) */
 WHISPER_API double owk_debug_gemm_bench(int device, int mode, int M, int N, int K, int iters);

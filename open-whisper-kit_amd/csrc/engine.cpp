@@ -204,6 +204,19 @@ void Engine::linear(const char * cls, int mode, int M, int N, int K, const _Floa
     // the reference rounds each activation row to Q8_0 / Q8_1 (x86 quantize_row_q8_0 / _q8_1) before
     // the block dot; bytes: the weight blocks (18-34 B per 32) + the int8 activations. a_q8: the
     // producer (LayerNorm, one_chunk attention) already wrote q8a_ / q8d_
+    if (gemm_q16_applies(q, M, N, K)) {
+        // large tiles: Q8_0 integers as exact f16 + block-major scales, the f16 MFMA ring kernel
+        const int mpad = (M + 255) / 256 * 256;
+        if (q16a_.bytes < (size_t) M * K * 2 || q16d_.bytes < (size_t) (K / 32) * mpad * 4)
+            throw std::runtime_error("linear: gemm_q16 operand buffers not reserved");
+        {
+            ProfScope ps(prof, stream, "quantize_q8");
+            quantize_q8_f16(stream, A32, A16, lda, M, K, q16a_.as<_Float16>(), q16d_.as<float>(), mpad);
+        }
+        ProfScope ps(prof, stream, cls, gemm_flops(M, N, K), 2.0 * ((double) M * K + (double) N * K));
+        gemm_q16(stream, mode, M, N, K, q16a_.as<_Float16>(), q16d_.as<float>(), mpad, q, ep);
+        return;
+    }
     if (!a_q8) {
         ProfScope ps(prof, stream, "quantize_q8");
         quantize_q8(stream, A32, A16, lda, M, K, q8a_.as<int8_t>(), q8d_.as<float>());
@@ -241,6 +254,11 @@ void Engine::encode(const std::vector<int> & slots, const std::vector<int> & off
             e_ao32_.alloc((size_t) M * d * 4);
             q8a_.alloc(std::max(q8a_.bytes, (size_t) M * 4 * d));
             q8d_.alloc(std::max(q8d_.bytes, (size_t) M * 4 * d / 32 * 4));
+            // gemm_q16 operands (reserved here: growing them inside linear() would free a buffer
+            // queued kernels may still read)
+            const size_t mpad = ((size_t) M + 255) / 256 * 256;
+            q16a_.alloc(std::max(q16a_.bytes, (size_t) M * 4 * d * 2));
+            q16d_.alloc(std::max(q16d_.bytes, (size_t) (4 * d / 32) * mpad * 4));
         }
     }
     e_a1_.alloc((size_t) n * T2 * kp1 * 2);
@@ -653,9 +671,9 @@ void Engine::launch_decode(const DecShape & sh) {
         const char * v = getenv("OWK_DEC_SPLIT");
         return v && atoi(v) != 0;
     }();
-    // soft_max rows (flash_attn = false) and DTW captures take the per-op path below (the fused
-    // chain has no soft_max attention launches)
-    const bool fused = R <= 32 && !q5 && !sh.self_sm && !sh.cross_sm && !sh.capture;
+    // soft_max rows (flash_attn = false) and DTW captures run the soft_max attention launches inside
+    // the fused chain (the capture addresses rows absolutely: no row groups then)
+    const bool fused = R <= 32 && !q5;
     const int plan = fused ? plan_env : -1;
 
     // the fused decoder (R <= 32, F16) over rows [r0, r0 + n) on stream s
@@ -728,6 +746,9 @@ void Engine::launch_decode(const DecShape & sh) {
                 ProfScope ps(prof, s, "attn_self");
                 attn_decoder(s, qb, d, Kl, Vl, 64, kv_cells * 64, d_rs + r0, n, d_keys, H, 1.0f, max_keys, aob, d,
                              self_oc, self_tl, nullptr, sh.self_list, nullptr, nullptr);
+                if (sh.self_sm)  // flash_attn = false rows: masked soft_max (scale 1; Q, K pre-scaled)
+                    attn_decoder_softmax(s, qb, d, Kl, Vl, 64, kv_cells * 64, d_rs + r0, n, d_keys, H, 1.0f, max_keys, aob,
+                                         d, nullptr, nullptr, 0, nullptr);
             }
             if (plan == 0) resid_ln(aor, L.t_o, d, L.b_o, L.cross_ln_w, L.cross_ln_b);
             else resid_stats(aor, L.t_o, d, L.b_o);
@@ -744,6 +765,11 @@ void Engine::launch_decode(const DecShape & sh) {
                 attn_decoder(s, qb, d, cross_k_.as<_Float16>() + l * cross_stride, cross_v_.as<_Float16>() + l * cross_stride,
                              64, T * 64, d_rc + r0, n, nullptr, H, kq_scale, T, aob, d, cross_oc, cross_tl, nullptr, true,
                              nullptr, nullptr);
+                if (sh.cross_sm)  // soft_max_ext over n_audio_ctx keys, DTW capture of the alignment heads
+                    attn_decoder_softmax(s, qb, d, cross_k_.as<_Float16>() + l * cross_stride,
+                                         cross_v_.as<_Float16>() + l * cross_stride, 64, T * 64, d_rc + r0, n, nullptr, H,
+                                         kq_scale, T, aob, d, sh.capture ? amap_.as<int>() + l * H : nullptr,
+                                         sh.capture ? cap_.as<float>() : nullptr, R, nullptr);
             }
             if (plan == 0) resid_ln(aor, L.t_co, d, L.cb_o, L.mlp_ln_w, L.mlp_ln_b);
             else resid_stats(aor, L.t_co, d, L.cb_o);

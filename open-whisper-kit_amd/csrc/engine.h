@@ -177,6 +177,7 @@ private:
                 bool dec = false,
                 bool a_q8 = false);
     DevBuf q8a_, q8d_;
+    DevBuf q16a_, q16d_;  // gemm_q16 operands: Q8_0 integers as f16 [M][K], scales [K/32][mpad]
     // Q5_0 models: the Q8_0 activation buffers producers write for the next linear (else null)
     int8_t * q8a() { return m->q5 ? q8a_.as<int8_t>() : nullptr; }
     float * q8d() { return m->q5 ? q8d_.as<float>() : nullptr; }

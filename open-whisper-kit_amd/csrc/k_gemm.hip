@@ -21,13 +21,21 @@ __device__ __forceinline__ float gelu_lookup(const uint16_t * tab, float x) {
     return (float) __builtin_bit_cast(_Float16, r);
 }
 
+// f32 -> f16 after the f32 value is rounded: the empty asm keeps hipcc from folding a preceding
+// multiply into v_mad_mixlo_f16 (one rounding of the exact product), which differs from the
+// reference's f32 op followed by its F16 conversion on ties (measured: 1 f16 ulp on scaled outputs)
+__device__ __forceinline__ _Float16 f16_rn(float v) {
+    asm volatile("" : "+v"(v));
+    return (_Float16) v;
+}
+
 template <int MODE>
 __device__ __forceinline__ void epi_store(const EpiParams & p, int r, int c, float acc) {
     if constexpr (MODE == EPI_F16) {
         float v = acc;
         if (p.bias) v += p.bias[c];
         v *= p.scale;
-        p.out16[(size_t) r * p.ldo + c] = (_Float16) v;
+        p.out16[(size_t) r * p.ldo + c] = f16_rn(v);
     } else if constexpr (MODE == EPI_GELU_F16) {
         const float v = acc + p.bias[c];
         p.out16[(size_t) r * p.ldo + c] = (_Float16) gelu_lookup(p.gelu_tab, v);
@@ -59,7 +67,7 @@ __device__ __forceinline__ void epi_store(const EpiParams & p, int r, int c, flo
         // keys (and values) as one contiguous run
         const size_t base = (size_t) (p.slot_map ? p.slot_map[clip] : clip) * p.T * d + (size_t) t * 64;
         if (c < d) {
-            p.out16b[base + (size_t) (c >> 6) * p.T * 64 + (c & 63)] = (_Float16) (acc * p.scale);
+            p.out16b[base + (size_t) (c >> 6) * p.T * 64 + (c & 63)] = f16_rn(acc * p.scale);
         } else {
             const int cv = c - d;
             p.out16c[base + (size_t) (cv >> 6) * p.T * 64 + (cv & 63)] = (_Float16) (acc + p.bias2[cv]);
@@ -67,11 +75,11 @@ __device__ __forceinline__ void epi_store(const EpiParams & p, int r, int c, flo
     } else if constexpr (MODE == EPI_QKV_DEC) {
         const int d = p.d;
         if (c < d) {
-            p.out16[(size_t) r * p.ldo + c] = (_Float16) ((acc + p.bias[c]) * p.scale);
+            p.out16[(size_t) r * p.ldo + c] = f16_rn((acc + p.bias[c]) * p.scale);
         } else if (c < 2 * d) {
             // head-major self-attention cache [slot][head][cell][64]; Tpad = cells * 64
             const int cc = c - d;
-            p.out16b[p.row_off[r] + (size_t) (cc >> 6) * p.Tpad + (cc & 63)] = (_Float16) (acc * p.scale);
+            p.out16b[p.row_off[r] + (size_t) (cc >> 6) * p.Tpad + (cc & 63)] = f16_rn(acc * p.scale);
         } else {
             const int cc = c - 2 * d;
             p.out16c[p.row_off[r] + (size_t) (cc >> 6) * p.Tpad + (cc & 63)] = (_Float16) (acc + p.bias2[cc]);
@@ -104,6 +112,134 @@ template <> __device__ __forceinline__ void epi_store<EPI_PARTIAL>(const EpiPara
 // EPI_RESID_STATS outside the decode-row GEMM (reduce kernel of a split launch): the residual part
 template <> __device__ __forceinline__ void epi_store<EPI_RESID_STATS>(const EpiParams & p, int r, int c, float acc) {
     epi_store<EPI_RESID_F32>(p, r, c, acc);
+}
+
+// Eight consecutive outputs (row r, columns c .. c+7; c % 8 == 0) of one lane: the same values as
+// eight epi_store calls, written with 16-byte vector accesses where the mode's layout allows (the
+// per-element 2/4-byte stores of a large tile's epilogue were store-issue bound: MLP0 with GELU
+// 1161 us against 861 us with an f32 epilogue, tools/gemm_big_check.py). vec: the row's 8 columns
+// are inside N and every operand row start is 16-byte aligned (checked per launch).
+__device__ __forceinline__ half8 to_half8(const float (&v)[8]) {
+    half8 h;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) h[e] = f16_rn(v[e]);
+    return h;
+}
+__device__ __forceinline__ void load8(const float * p, float (&v)[8]) {
+    const float4 a = ((const float4 *) p)[0], b = ((const float4 *) p)[1];
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+__device__ __forceinline__ void store8(float * p, const float (&v)[8]) {
+    ((float4 *) p)[0] = make_float4(v[0], v[1], v[2], v[3]);
+    ((float4 *) p)[1] = make_float4(v[4], v[5], v[6], v[7]);
+}
+
+template <int MODE>
+__device__ __forceinline__ void epi_row8(const EpiParams & p, int r, int c, const float (&acc)[8], bool vec) {
+    constexpr bool VEC = MODE == EPI_F16 || MODE == EPI_GELU_F16 || MODE == EPI_RESID_F32 || MODE == EPI_CONV2 ||
+                         MODE == EPI_QKV_ENC || MODE == EPI_KV_CROSS || MODE == EPI_F32 || MODE == EPI_BIAS_F32 ||
+                         MODE == EPI_SILU_F16 || MODE == EPI_HALF_RESID || MODE == EPI_RELU_F16 ||
+                         MODE == EPI_SIGMOID_F32;
+    if (!VEC || !vec) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) epi_store<MODE>(p, r, c + e, acc[e]);
+        return;
+    }
+    float v[8], bb[8];
+    const size_t o = (size_t) r * p.ldo + c;
+    if constexpr (MODE == EPI_F16) {
+        if (p.bias) load8(p.bias + c, bb);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = ((p.bias ? acc[e] + bb[e] : acc[e])) * p.scale;
+        *(half8 *) (p.out16 + o) = to_half8(v);
+    } else if constexpr (MODE == EPI_GELU_F16) {
+        load8(p.bias + c, bb);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = gelu_lookup(p.gelu_tab, acc[e] + bb[e]);
+        *(half8 *) (p.out16 + o) = to_half8(v);
+    } else if constexpr (MODE == EPI_RESID_F32 || MODE == EPI_HALF_RESID) {
+        float rs[8];
+        load8(p.bias + c, bb);
+        load8(p.resid + o, rs);
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+            v[e] = MODE == EPI_RESID_F32 ? rs[e] + (acc[e] + bb[e]) : rs[e] + (acc[e] + bb[e]) * 0.5f;
+        store8(p.out32 + o, v);
+    } else if constexpr (MODE == EPI_CONV2) {
+        float ps[8];
+        load8(p.bias + c, bb);
+        load8(p.pos + (size_t) (r % p.T) * p.ldo + c, ps);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = ps[e] + gelu_lookup(p.gelu_tab, acc[e] + bb[e]);
+        store8(p.out32 + o, v);
+    } else if constexpr (MODE == EPI_QKV_ENC) {
+        // Q (+bias) and K columns only: V tiles keep the transposed per-element path
+        const int d = p.d;
+        if (c < d) {
+            load8(p.bias + c, bb);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] = acc[e] + bb[e];
+            *(half8 *) (p.out16 + (size_t) r * d + c) = to_half8(v);
+        } else if (c < 2 * d) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] = acc[e];
+            *(half8 *) (p.out16b + (size_t) r * d + (c - d)) = to_half8(v);
+        } else {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) epi_store<MODE>(p, r, c + e, acc[e]);
+        }
+    } else if constexpr (MODE == EPI_KV_CROSS) {
+        const int d = p.d;
+        const int clip = r / p.T, t = r - clip * p.T;
+        const size_t base = (size_t) (p.slot_map ? p.slot_map[clip] : clip) * p.T * d + (size_t) t * 64;
+        if (c < d) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] = acc[e] * p.scale;
+            *(half8 *) (p.out16b + base + (size_t) (c >> 6) * p.T * 64 + (c & 63)) = to_half8(v);
+        } else {
+            const int cv = c - d;
+            load8(p.bias2 + cv, bb);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] = acc[e] + bb[e];
+            *(half8 *) (p.out16c + base + (size_t) (cv >> 6) * p.T * 64 + (cv & 63)) = to_half8(v);
+        }
+    } else if constexpr (MODE == EPI_F32) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = acc[e];
+        store8(p.out32 + o, v);
+    } else if constexpr (MODE == EPI_BIAS_F32) {
+        if (p.bias) load8(p.bias + c, bb);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = p.bias ? acc[e] + bb[e] : acc[e];
+        store8(p.out32 + o, v);
+        if (p.out16) *(half8 *) (p.out16 + o) = to_half8(v);
+    } else if constexpr (MODE == EPI_SILU_F16 || MODE == EPI_RELU_F16) {
+        load8(p.bias + c, bb);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const float x = acc[e] + bb[e];
+            v[e] = MODE == EPI_SILU_F16 ? x / (1.0f + expf(-x)) : (x > 0.0f ? x : 0.0f);
+        }
+        *(half8 *) (p.out16 + o) = to_half8(v);
+    } else if constexpr (MODE == EPI_SIGMOID_F32) {
+        load8(p.bias + c, bb);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = 1.0f / (1.0f + expf(-(acc[e] + bb[e])));
+        store8(p.out32 + o, v);
+    }
+}
+
+// the vector epilogue's alignment requirements for this launch (16-byte rows of every operand)
+static bool epi_vec_ok(int mode, const EpiParams & p, int N) {
+    auto al = [](const void * q) { return ((uintptr_t) q & 15) == 0; };
+    if (N % 8 || !al(p.bias) || !al(p.bias2) || !al(p.resid) || !al(p.out32) || !al(p.out16) || !al(p.out16b) ||
+        !al(p.out16c) || !al(p.pos))
+        return false;
+    switch (mode) {
+        case EPI_QKV_ENC: case EPI_KV_CROSS: return p.d % 8 == 0;
+        case EPI_QKV_DEC: case EPI_PARTIAL: case EPI_RESID_STATS: return false;
+        default: return p.ldo % 8 == 0;
+    }
 }
 
 typedef __attribute__((address_space(3))) void * lds_ptr_t;
@@ -237,13 +373,14 @@ constexpr int G2_M = 256, G2_N = 256, G2_K = 32;
 constexpr int G2_OP = G2_M * G2_K * 2;     // 16 KB: one operand of one K-step
 constexpr int G2_SLOT = 2 * G2_OP;         // 32 KB
 
-template <int MODE, int G2_SLOTS>
+template <int MODE, int G2_SLOTS, bool SWAP = true>
 __global__ __launch_bounds__(512, 2) void k_gemm_256(int M, int N, int K, const _Float16 * __restrict__ A, int lda,
                                                      const _Float16 * __restrict__ W, int ldw, EpiParams ep) {
     // G2_SLOTS ring slots: G2_SLOTS - 2 K-steps stay in flight past every barrier
     static_assert(G2_SLOTS == 4 || G2_SLOTS == 5, "ring depth");
     constexpr int AHEAD = G2_SLOTS - 2;  // steps issued beyond the one being computed
-    __shared__ __attribute__((aligned(1024))) char smem[G2_SLOTS * G2_SLOT];
+    constexpr int SLOT = G2_SLOT;
+    __shared__ __attribute__((aligned(1024))) char smem[G2_SLOTS * SLOT];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wr = wave >> 2, wc = wave & 3;
 
@@ -258,19 +395,31 @@ __global__ __launch_bounds__(512, 2) void k_gemm_256(int M, int N, int K, const 
     const int bm = bid / nbn, bn = bid - bm * nbn;
     const int m0 = bm * G2_M, n0 = bn * G2_N;
 
-    // staging: wave w issues row groups 2w, 2w+1 (16 rows x 64 B each) of A and of W
+    // Output layout. Q/K-type tiles ("swap": every mode except the V tiles of EPI_QKV_ENC) compute
+    // C^T = W . A^T: the W fragment is the MFMA's A operand, so a lane's accumulator elements run
+    // along N -- with the W rows permuted (offB below), lane (g, l16) of row tile i holds columns
+    // wc*64 + g*8 + (0..7) and + 32 + (0..7) of row wr*128 + i*16 + l16: two 8-column runs, stored
+    // by epi_row8 as 16-byte vectors. V tiles of EPI_QKV_ENC keep C = A . W^T (4 consecutive rows
+    // per lane = 4 consecutive key positions of the transposed V image).
+    // (a compile-time choice: a runtime one made hipcc drain the DMA queue at the branch joins,
+    // 8x slower; EPI_QKV_ENC launches its V columns separately with SWAP = false, ep.c_off = 2d)
+    constexpr bool swap = SWAP;
+
+    // staging: wave w issues row groups 2w, 2w+1 (16 rows x 64 B each) of A and of W. A rows are
+    // stored with 16-B chunk c at c ^ ((r >> 2) & 3); W rows at c ^ wsw(r), which keeps both W
+    // fragment row orders (16 consecutive rows, or the permuted rows of swap tiles) conflict-free
+    auto wsw = [](int r) { return ((r >> 2) ^ (r >> 3)) & 3; };
     const int srow0 = wave * 32 + (lane >> 2);
     const _Float16 * ga[2];
     const _Float16 * gw[2];
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
         const int row = srow0 + i * 16;
-        const int c = (lane & 3) ^ ((row >> 2) & 3);
-        ga[i] = A + (size_t) min(m0 + row, M - 1) * lda + c * 8;
-        gw[i] = W + (size_t) min(n0 + row, N - 1) * ldw + c * 8;
+        ga[i] = A + (size_t) min(m0 + row, M - 1) * lda + ((lane & 3) ^ ((row >> 2) & 3)) * 8;
+        gw[i] = W + (size_t) min(n0 + row, N - 1) * ldw + ((lane & 3) ^ wsw(row)) * 8;
     }
     auto stage = [&](int slot, int k0) {
-        char * sA = smem + slot * G2_SLOT + wave * 2048;
+        char * sA = smem + slot * SLOT + wave * 2048;
         char * sB = sA + G2_OP;
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
@@ -295,8 +444,10 @@ __global__ __launch_bounds__(512, 2) void k_gemm_256(int M, int N, int K, const 
     }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-        const int r = wc * 64 + j * 16 + l16;
-        offB[j] = r * 64 + ((g ^ ((r >> 2) & 3)) << 4);
+        // swap: fragment j's row p = W row wc*64 + (j>>1)*32 + (p>>2)*8 + (j&1)*4 + (p&3), so that
+        // accumulator element e of lane group g is column wc*64 + (j>>1)*32 + g*8 + (j&1)*4 + e
+        const int r = swap ? wc * 64 + (j >> 1) * 32 + (l16 >> 2) * 8 + (j & 1) * 4 + (l16 & 3) : wc * 64 + j * 16 + l16;
+        offB[j] = r * 64 + ((g ^ wsw(r)) << 4);
     }
 
     const int nk = K / G2_K;
@@ -324,7 +475,7 @@ __global__ __launch_bounds__(512, 2) void k_gemm_256(int M, int N, int K, const 
     // before the current group's MFMAs are issued, so LDS latency hides behind them
     int slot = 0;
     for (int j = 0; j < nk; ++j) {
-        const char * sA = smem + slot * G2_SLOT;
+        const char * sA = smem + slot * SLOT;
         const int nslot = slot + 1 == G2_SLOTS ? 0 : slot + 1;
         half8 bn[4], an[2];
 #pragma unroll
@@ -341,7 +492,7 @@ __global__ __launch_bounds__(512, 2) void k_gemm_256(int M, int N, int K, const 
                     const int fs = slot == 0 ? G2_SLOTS - 1 : slot - 1;  // (j - 1) mod G2_SLOTS
                     stage(fs, (j + 1 + AHEAD) * G2_K);
                 }
-                const char * nA = smem + nslot * G2_SLOT;
+                const char * nA = smem + nslot * SLOT;
 #pragma unroll
                 for (int t = 0; t < 4; ++t) bn[t] = *(const half8 *) (nA + G2_OP + offB[t]);
                 an[0] = *(const half8 *) (nA + offA[0]);
@@ -350,11 +501,19 @@ __global__ __launch_bounds__(512, 2) void k_gemm_256(int M, int N, int K, const 
             // keep the order: next fragments' ds_reads issued, then this group's MFMAs (the
             // scheduler would otherwise consume each read right after issuing it)
             __builtin_amdgcn_sched_barrier(0);
+            if (swap) {
 #pragma unroll
-            for (int i = 0; i < 2; ++i)
+                for (int i = 0; i < 2; ++i)
 #pragma unroll
-                for (int t = 0; t < 4; ++t)
-                    acc[2 * g + i][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[i], b[t], acc[2 * g + i][t], 0, 0, 0);
+                    for (int t = 0; t < 4; ++t)
+                        acc[2 * g + i][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(b[t], a[i], acc[2 * g + i][t], 0, 0, 0);
+            } else {
+#pragma unroll
+                for (int i = 0; i < 2; ++i)
+#pragma unroll
+                    for (int t = 0; t < 4; ++t)
+                        acc[2 * g + i][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[i], b[t], acc[2 * g + i][t], 0, 0, 0);
+            }
             __builtin_amdgcn_sched_barrier(0);
             a[0] = an[0];
             a[1] = an[1];
@@ -364,17 +523,39 @@ __global__ __launch_bounds__(512, 2) void k_gemm_256(int M, int N, int K, const 
         slot = nslot;
     }
 
+    if (swap) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int r = m0 + wr * 128 + i * 16 + l16;
+            if (r >= M) continue;
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int c = n0 + wc * 64 + h * 32 + g * 8;
+                const float v[8] = {acc[i][2 * h][0], acc[i][2 * h][1], acc[i][2 * h][2], acc[i][2 * h][3],
+                                    acc[i][2 * h + 1][0], acc[i][2 * h + 1][1], acc[i][2 * h + 1][2], acc[i][2 * h + 1][3]};
+                if (c + 8 <= N) {
+                    epi_row8<MODE>(ep, r, c, v, ep.vec != 0);
+                } else {
+#pragma unroll
+                    for (int e = 0; e < 8; ++e)
+                        if (c + e < N) epi_store<MODE>(ep, r, c + e, v[e]);
+                }
+            }
+        }
+        return;
+    }
 #pragma unroll
     for (int i = 0; i < 8; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            const int c = n0 + wc * 64 + j * 16 + l16;
+            const int cl = n0 + wc * 64 + j * 16 + l16;  // launch column; c: the epilogue's column
+            const int c = cl + ep.c_off;
             const int r0 = m0 + wr * 128 + i * 16 + 4 * g;
             if constexpr (MODE == EPI_QKV_ENC) {
                 // V columns -> the transposed [clip][head][dim][Tpad] image: a lane's 4 rows are 4
                 // consecutive t of one clip (T % 4 == 0, r0 % 4 == 0): one 8-byte store
                 const int d = ep.d;
-                if (c >= 2 * d && c < N && r0 + 3 < M && ep.T % 4 == 0) {
+                if (c >= 2 * d && cl < N && r0 + 3 < M && ep.T % 4 == 0) {
                     const int cc = c - 2 * d;
                     const int clip = r0 / ep.T, t = r0 - clip * ep.T;
                     const float bv = ep.bias2[cc];
@@ -388,9 +569,191 @@ __global__ __launch_bounds__(512, 2) void k_gemm_256(int M, int N, int K, const 
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
                 const int r = r0 + e;
-                if (r < M && c < N) epi_store<MODE>(ep, r, c, acc[i][j][e]);
+                if (r < M && cl < N) epi_store<MODE>(ep, r, c, acc[i][j][e]);
             }
         }
+}
+
+// ---------------------------------------------------------------------------------
+// Quantized large-tile GEMM (gemm_q16: encoder / cross-K/V matrices of Q5_0 / Q8_0 / Q4_0 models).
+// A = the Q8_0 integers of the activation rows and W = the weight integers, both as exact f16
+// values; each 32-wide K-step is one quantization block: its MFMA dot is an exact integer
+// (|sum| <= 32 * 127 * 16 < 2^24) that enters the f32 accumulator as
+// acc = fma(dot, d_w * d_a, acc) -- ggml_vec_dot_q5_0_q8_0's per-block term (the f32 product of the
+// two f16 scales, fused multiply-add). Block 128 x 256, 8 waves of 64 x 64 (acc 64 registers: the
+// per-block scaling needs the room a 256-row tile does not leave), the ring of k_gemm_256 (4 slots,
+// two K-steps in flight across each barrier, counted vmcnt) carrying 128 A rows, 256 W rows and the
+// step's 128 + 256 scales (da / dw block-major; da rows permuted so a lane's 4 rows are one float4).
+// Output: C^T tiles (lane = 16 consecutive columns of one row), epi_row8 vector epilogues.
+// ---------------------------------------------------------------------------------
+constexpr int GQ16_M = 128;
+constexpr int GQ16_A = GQ16_M * G2_K * 2;        // 8 KB
+constexpr int GQ16_W = G2_N * G2_K * 2;          // 16 KB
+constexpr int GQ16_SLOT = GQ16_A + GQ16_W + 2048;  // + da 512 B, dw 1 KB, 512 B scratch
+constexpr int GQ16_SLOTS = 4;
+
+template <int MODE>
+__global__ __launch_bounds__(512, 2) void k_gemm_q16(int M, int N, int K, const _Float16 * __restrict__ A,
+                                                     const _Float16 * __restrict__ W, EpiParams ep) {
+    constexpr int AHEAD = GQ16_SLOTS - 2;
+    __shared__ __attribute__((aligned(1024))) char smem[GQ16_SLOTS * GQ16_SLOT];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wr = wave >> 2, wc = wave & 3;
+    const int nbn = (N + G2_N - 1) / G2_N;
+    const int nbt = gridDim.x;
+    int bid = blockIdx.x;
+    {  // XCD-aware order (k_gemm_256)
+        const int xcd = bid & 7, q = nbt >> 3, rr = nbt & 7;
+        const int base = xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q;
+        bid = base + (bid >> 3);
+    }
+    const int bm = bid / nbn, bn = bid - bm * nbn;
+    const int m0 = bm * GQ16_M, n0 = bn * G2_N;
+
+    auto wsw = [](int r) { return ((r >> 2) ^ (r >> 3)) & 3; };
+    // staging: wave w: A rows 16w .. 16w+15 (one 1 KB piece), W rows 32w .. 32w+31 (two), one 256-B
+    // scale piece (waves 0-1: d_a, 2-5: d_w, 6-7: a repeat of d_w pieces into scratch, so that every
+    // wave issues 4 loads per step)
+    const int arow = wave * 16 + (lane >> 2);
+    const _Float16 * ga = A + (size_t) min(m0 + arow, M - 1) * K + ((lane & 3) ^ ((arow >> 2) & 3)) * 8;
+    const _Float16 * gw[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int row = wave * 32 + i * 16 + (lane >> 2);
+        gw[i] = W + (size_t) min(n0 + row, N - 1) * K + ((lane & 3) ^ wsw(row)) * 8;
+    }
+    const int sp = wave < 2 ? wave : wave < 6 ? wave - 2 : wave - 6;
+    const float * gs = wave < 2 ? ep.qs_da + m0 + sp * 64 + lane * 4 : ep.qs_dw + n0 + sp * 64 + lane * 4;
+    const size_t gs_step = wave < 2 ? (size_t) ep.qs_mpad : (size_t) ep.qs_npad;
+    const int ls = wave < 2 ? GQ16_A + GQ16_W + sp * 256 : wave < 6 ? GQ16_A + GQ16_W + 512 + sp * 256
+                                                                     : GQ16_A + GQ16_W + 1536 + sp * 256;
+    auto stage = [&](int slot, int kstep) {
+        char * base = smem + slot * GQ16_SLOT;
+        const int k0 = kstep * G2_K;
+        __builtin_amdgcn_global_load_lds((const void *) (ga + k0), (lds_ptr_t) (base + wave * 1024), 16, 0, 0);
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+            __builtin_amdgcn_global_load_lds((const void *) (gw[i] + k0), (lds_ptr_t) (base + GQ16_A + wave * 2048 + i * 1024),
+                                             16, 0, 0);
+        if (lane < 16)
+            __builtin_amdgcn_global_load_lds((const void *) (gs + (size_t) kstep * gs_step), (lds_ptr_t) (base + ls), 16, 0, 0);
+    };
+
+    floatx4 acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int t = 0; t < 4; ++t) acc[i][t] = floatx4{0.f, 0.f, 0.f, 0.f};
+    const int g = lane >> 4, l16 = lane & 15;
+    int offA[4], offB[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int r = wr * 64 + i * 16 + l16;
+        offA[i] = r * 64 + ((g ^ ((r >> 2) & 3)) << 4);
+    }
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        const int r = wc * 64 + (t >> 1) * 32 + (l16 >> 2) * 8 + (t & 1) * 4 + (l16 & 3);
+        offB[t] = GQ16_A + r * 64 + ((g ^ wsw(r)) << 4);
+    }
+    const int nk = K / G2_K;
+    auto wait_step = [&](int next) {
+        const int later = min(AHEAD - 1, nk - 1 - next);
+        if (later >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        else if (later == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    };
+#pragma unroll
+    for (int i = 0; i < AHEAD; ++i)
+        if (i < nk) stage(i, i);
+    wait_step(0);
+    __builtin_amdgcn_s_barrier();
+    if (AHEAD < nk) stage(AHEAD, AHEAD);
+    half8 b[4], a[2];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) b[t] = *(const half8 *) (smem + offB[t]);
+    a[0] = *(const half8 *) (smem + offA[0]);
+    a[1] = *(const half8 *) (smem + offA[1]);
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    int slot = 0;
+    for (int j = 0; j < nk; ++j) {
+        const char * sA = smem + slot * GQ16_SLOT;
+        const int nslot = slot + 1 == GQ16_SLOTS ? 0 : slot + 1;
+        // this step's scales: d_a of the lane's 4 rows, d_w of its 16 columns
+        const float * sc = (const float *) (sA + GQ16_A + GQ16_W);
+        const float4 da4 = *(const float4 *) (sc + wr * 64 + l16 * 4);
+        const float sda[4] = {da4.x, da4.y, da4.z, da4.w};
+        f2 sdw[4][2];  // [t][pair]: columns (t >> 1) * 32 + g * 8 + (t & 1) * 4 + 2 * pair + {0, 1}
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const float4 w0 = *(const float4 *) (sc + 128 + wc * 64 + h * 32 + g * 8);
+            const float4 w1 = *(const float4 *) (sc + 128 + wc * 64 + h * 32 + g * 8 + 4);
+            sdw[2 * h][0] = f2{w0.x, w0.y}; sdw[2 * h][1] = f2{w0.z, w0.w};
+            sdw[2 * h + 1][0] = f2{w1.x, w1.y}; sdw[2 * h + 1][1] = f2{w1.z, w1.w};
+        }
+        half8 bn[4], an[2];
+#pragma unroll
+        for (int gg = 0; gg < 2; ++gg) {
+            if (gg == 0) {
+                an[0] = *(const half8 *) (sA + offA[2]);
+                an[1] = *(const half8 *) (sA + offA[3]);
+            } else if (j + 1 < nk) {
+                wait_step(j + 1);
+                __builtin_amdgcn_s_barrier();
+                if (j + 1 + AHEAD < nk) stage(slot == 0 ? GQ16_SLOTS - 1 : slot - 1, j + 1 + AHEAD);
+                const char * nA = smem + nslot * GQ16_SLOT;
+#pragma unroll
+                for (int t = 0; t < 4; ++t) bn[t] = *(const half8 *) (nA + offB[t]);
+                an[0] = *(const half8 *) (nA + offA[0]);
+                an[1] = *(const half8 *) (nA + offA[1]);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                floatx4 dot[4];
+#pragma unroll
+                for (int t = 0; t < 4; ++t)
+                    dot[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(b[t], a[i], floatx4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+                const float dav = sda[2 * gg + i];
+                const f2 da2 = f2{dav, dav};
+#pragma unroll
+                for (int t = 0; t < 4; ++t)
+#pragma unroll
+                    for (int pr = 0; pr < 2; ++pr) {
+                        const f2 dd = sdw[t][pr] * da2;  // d_w * d_a, f32
+                        const f2 dt = f2{dot[t][2 * pr], dot[t][2 * pr + 1]};
+                        f2 ac = f2{acc[2 * gg + i][t][2 * pr], acc[2 * gg + i][t][2 * pr + 1]};
+                        ac = __builtin_elementwise_fma(dt, dd, ac);
+                        acc[2 * gg + i][t][2 * pr] = ac.x;
+                        acc[2 * gg + i][t][2 * pr + 1] = ac.y;
+                    }
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            a[0] = an[0];
+            a[1] = an[1];
+        }
+#pragma unroll
+        for (int t = 0; t < 4; ++t) b[t] = bn[t];
+        slot = nslot;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int r = m0 + wr * 64 + i * 16 + l16;
+        if (r >= M) continue;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int c = n0 + wc * 64 + h * 32 + g * 8;
+            const float v[8] = {acc[i][2 * h][0], acc[i][2 * h][1], acc[i][2 * h][2], acc[i][2 * h][3],
+                                acc[i][2 * h + 1][0], acc[i][2 * h + 1][1], acc[i][2 * h + 1][2], acc[i][2 * h + 1][3]};
+            if (c + 8 <= N) {
+                epi_row8<MODE>(ep, r, c, v, ep.vec != 0);
+            } else {
+#pragma unroll
+                for (int e = 0; e < 8; ++e)
+                    if (c + e < N) epi_store<MODE>(ep, r, c + e, v[e]);
+            }
+        }
+    }
 }
 
 // ---------------------------------------------------------------------------------
@@ -763,10 +1126,35 @@ template <int MODE> struct Launch256 {
     static void run(hipStream_t s, int M, int N, int K, const _Float16 * A, int lda, const _Float16 * W, int ldw,
                     const EpiParams & ep) {
         const int nbm = (M + G2_M - 1) / G2_M, nbn = (N + G2_N - 1) / G2_N;
+        EpiParams e = ep;
+        e.vec = epi_vec_ok(MODE, ep, N) ? 1 : 0;
+        if (MODE == EPI_QKV_ENC && N > 2 * ep.d) {
+            // Q and K columns as C^T tiles, then the V columns (transposed image) as C tiles
+            const int n1 = 2 * ep.d, nb1 = (n1 + G2_N - 1) / G2_N, nb2 = (N - n1 + G2_N - 1) / G2_N;
+            hipLaunchKernelGGL((k_gemm_256<MODE, 4, true>), dim3(nbm * nb1), dim3(512), 0, s, M, n1, K, A, lda, W, ldw, e);
+            EpiParams ev = e;
+            ev.c_off = n1;
+            hipLaunchKernelGGL((k_gemm_256<MODE, 4, false>), dim3(nbm * nb2), dim3(512), 0, s, M, N - n1, K, A, lda,
+                               W + (size_t) n1 * ldw, ldw, ev);
+            return;
+        }
         if (g_gemm256 == 5)
-            hipLaunchKernelGGL((k_gemm_256<MODE, 5>), dim3(nbm * nbn), dim3(512), 0, s, M, N, K, A, lda, W, ldw, ep);
+            hipLaunchKernelGGL((k_gemm_256<MODE, 5>), dim3(nbm * nbn), dim3(512), 0, s, M, N, K, A, lda, W, ldw, e);
         else
-            hipLaunchKernelGGL((k_gemm_256<MODE, 4>), dim3(nbm * nbn), dim3(512), 0, s, M, N, K, A, lda, W, ldw, ep);
+            hipLaunchKernelGGL((k_gemm_256<MODE, 4>), dim3(nbm * nbn), dim3(512), 0, s, M, N, K, A, lda, W, ldw, e);
+    }
+};
+template <int MODE> struct Launch256Q {
+    static void run(hipStream_t s, int M, int N, int K, const _Float16 * q16, const float * dat, int mpad, const Q5W & w,
+                    const EpiParams & ep) {
+        const int nbm = (M + GQ16_M - 1) / GQ16_M, nbn = (N + G2_N - 1) / G2_N;
+        EpiParams e = ep;
+        e.vec = epi_vec_ok(MODE, ep, N) ? 1 : 0;
+        e.qs_da = dat;
+        e.qs_dw = w.dwt;
+        e.qs_mpad = mpad;
+        e.qs_npad = w.npad;
+        hipLaunchKernelGGL(k_gemm_q16<MODE>, dim3(nbm * nbn), dim3(512), 0, s, M, N, K, q16, w.wi, e);
     }
 };
 template <int MODE> struct LaunchSkinny {
@@ -901,6 +1289,45 @@ void quantize_q8(hipStream_t s, const float * A32, const _Float16 * A16, int lda
         hipLaunchKernelGGL(k_quantize_q8<_Float16>, dim3(grid), dim3(256), 0, s, A16, lda, M, K, q, dq);
 }
 
+// Q8_0 rows of A as exact f16 integers for gemm_q16 (same rounding as k_quantize_q8) and the
+// block scales block-major: dat[b * mpad + perm(r)] = (float) (f16) (amax / 127), perm = the row order
+// k_gemm_q16 reads (within a 128-row tile: (t & 64) | (t & 15) << 2 | (t >> 4) & 3)
+template <typename TA>
+__global__ __launch_bounds__(256) void k_quantize_q8_f16(const TA * __restrict__ A, int lda, int M, int K,
+                                                         _Float16 * __restrict__ q, float * __restrict__ dat, int mpad) {
+    const int nb = K >> 5;
+    const size_t total = (size_t) M * nb;
+    const int lane = threadIdx.x & 31;
+    for (size_t blk = ((size_t) blockIdx.x * blockDim.x + threadIdx.x) >> 5; blk < total;
+         blk += ((size_t) gridDim.x * blockDim.x) >> 5) {
+        const int r = (int) (blk / nb), b = (int) (blk - (size_t) r * nb);
+        const float x = (float) A[(size_t) r * lda + b * 32 + lane];
+        float am = fabsf(x);
+#pragma unroll
+        for (int o = 16; o > 0; o >>= 1) am = fmaxf(am, __shfl_xor(am, o, 32));
+        const float dd = am / 127.f;
+        const float id = am != 0.0f ? 127.f / am : 0.0f;
+        q[(size_t) r * K + b * 32 + lane] = (_Float16) (float) (int) (int8_t) rintf(x * id);
+        if (lane == 0) {
+            const int t = r & 127;
+            const int pr = (r & ~127) | (t & 64) | ((t & 15) << 2) | ((t >> 4) & 3);
+            dat[(size_t) b * mpad + pr] = (float) (_Float16) dd;
+        }
+    }
+}
+
+void quantize_q8_f16(hipStream_t s, const float * A32, const _Float16 * A16, int lda, int M, int K, _Float16 * q16,
+                     float * dat, int mpad) {
+    if (M <= 0) return;
+    if (K % 32 || mpad < (M + 127) / 128 * 128) throw std::runtime_error("quantize_q8_f16: shape");
+    const size_t blocks = (size_t) M * (K / 32);
+    const int grid = (int) std::min<size_t>((blocks * 32 + 255) / 256, 65536);
+    if (A32)
+        hipLaunchKernelGGL(k_quantize_q8_f16<float>, dim3(grid), dim3(256), 0, s, A32, lda, M, K, q16, dat, mpad);
+    else
+        hipLaunchKernelGGL(k_quantize_q8_f16<_Float16>, dim3(grid), dim3(256), 0, s, A16, lda, M, K, q16, dat, mpad);
+}
+
 typedef int intx4 __attribute__((ext_vector_type(4)));
 
 // 8 consecutive weights (group g = elements 8g..8g+7) of one block as int8, the B/A operand of
@@ -945,6 +1372,32 @@ __device__ __forceinline__ float q8_1_sum(float d_raw, int isum) {
     float p = d_raw * (float) isum;
     asm volatile("" : "+v"(p));
     return (float) (_Float16) p;
+}
+
+// Q5W block arrays -> exact f16 integers [N][K] and block scales [K/32][npad] (rows past N: 0)
+__global__ void k_expand_q16(Q5W w, int N, int K, _Float16 * __restrict__ wi, float * __restrict__ dwt, int npad) {
+    const int nb = K >> 5;
+    const size_t total = (size_t) npad * nb * 4;  // (n, kb, group of 8)
+    for (size_t p = (size_t) blockIdx.x * blockDim.x + threadIdx.x; p < total; p += (size_t) gridDim.x * blockDim.x) {
+        const int g = (int) (p & 3);
+        const size_t nk = p >> 2;
+        const int n = (int) (nk / nb), kb = (int) (nk - (size_t) n * nb);
+        if (n >= N) {
+            if (g == 0) dwt[(size_t) kb * npad + n] = 0.0f;
+            continue;
+        }
+        const long v = wq_group(w, n, kb, g, K, nb);
+        half8 h;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) h[e] = (_Float16) (float) (int8_t) (uint8_t) ((uint64_t) v >> (8 * e));
+        *(half8 *) (wi + (size_t) n * K + kb * 32 + 8 * g) = h;
+        if (g == 0) dwt[(size_t) kb * npad + n] = (float) w.d[(size_t) n * nb + kb];
+    }
+}
+
+void quant_expand_f16(hipStream_t s, const Q5W & w, int N, int K, _Float16 * wi, float * dwt, int npad) {
+    if (K % 32 || npad < N || qf_has_m(w.fmt)) throw std::runtime_error("quant_expand_f16: shape or format");
+    hipLaunchKernelGGL(k_expand_q16, dim3(2048), dim3(256), 0, s, w, N, K, wi, dwt, npad);
 }
 
 // skinny: M <= 64 rows; one 16-column tile per block, 8 waves split the K blocks, partial
@@ -1346,6 +1799,18 @@ void gemm_q5(hipStream_t s, int mode, int M, int N, int K, const int8_t * qa, co
         return;
     }
     dispatch_mode<LaunchQ5>(mode, s, M, N, K, qa, da, w, ep);
+}
+
+bool gemm_q16_applies(const Q5W & w, int M, int N, int K) {
+    return w.wi && w.dwt && use_256(M, N, K) && !qf_has_m(w.fmt);
+}
+
+void gemm_q16(hipStream_t s, int mode, int M, int N, int K, const _Float16 * q16, const float * dat, int mpad,
+              const Q5W & w, const EpiParams & ep) {
+    if (!gemm_q16_applies(w, M, N, K) || mpad < (M + GQ16_M - 1) / GQ16_M * GQ16_M || w.npad < (N + G2_N - 1) / G2_N * G2_N)
+        throw std::runtime_error("gemm_q16: unsupported shape");
+    check_shape(M, N, K, K, K, G2_K);
+    dispatch_mode<Launch256Q>(mode, s, M, N, K, q16, dat, mpad, w, ep);
 }
 
 size_t gemm_ws_floats(int N, int K) {

@@ -53,6 +53,12 @@ struct EpiParams {
                                           // (head h at + h * Tpad: the cache is head-major)
     const int * slot_map = nullptr;       // EPI_KV_CROSS: clip index -> cross-KV slot (null = identity)
     double * stats = nullptr;             // EPI_RESID_STATS: [N/16][M] {sum, M2} per tile and row
+    int vec = 0;                          // set by the large-tile launcher: 16-byte vector epilogue allowed
+    // quantized large-tile GEMM (gemm_q16): per-32-block scales, block-major [K/32][pad]
+    const float * qs_da = nullptr;        // activation d (f16-rounded), rows permuted per 256-row tile
+    const float * qs_dw = nullptr;        // weight d
+    int qs_mpad = 0, qs_npad = 0;
+    int c_off = 0;                        // large-tile launch over a column range: its first column
 };
 
 // The A operand of a decode-row GEMM as the LayerNorm of the f32 residual stream x (ggml_norm +
@@ -147,6 +153,11 @@ struct Q5W {
     const _Float16 * m = nullptr;   // [N][K/32]: block minimums (Q4_1 / Q5_1)
     // decode-step matrices: the column-tiled records (qf_tile_bytes), rows past N zero
     const uint8_t * tiled = nullptr;
+    // large-tile (encoder / cross-KV) matrices of the symmetric formats (Q5_0 / Q8_0 / Q4_0): the
+    // integer weights as exact f16 values [N][K] and the block scales transposed [K/32][npad] f32
+    const _Float16 * wi = nullptr;
+    const float * dwt = nullptr;
+    int npad = 0;
     int fmt = QF_Q5_0;
     explicit operator bool() const { return qs != nullptr; }
 };
@@ -162,6 +173,16 @@ void quantize_q8(hipStream_t s, const float * A32, const _Float16 * A16, int lda
 // split-K partial tiles [q5_partial_splits(K)][M][N] to ep.out32, finished by resid_layernorm
 void gemm_q5(hipStream_t s, int mode, int M, int N, int K, const int8_t * qa, const float * da, const Q5W & w,
              const EpiParams & ep);
+// the same product through the f16 MFMA ring kernel (M >= 2048 tiles): A = the Q8_0 integers of the
+// activation as exact f16 values [M][K] + scales (quantize_q8_f16), W = Q5W::wi / dwt; every 32-block
+// dot is exact, then acc = fma(dot, d_w * d_a, acc) in f32 (ggml_vec_dot_q5_0_q8_0's per-block term)
+void quantize_q8_f16(hipStream_t s, const float * A32, const _Float16 * A16, int lda, int M, int K, _Float16 * q16,
+                     float * dat, int mpad);
+void gemm_q16(hipStream_t s, int mode, int M, int N, int K, const _Float16 * q16, const float * dat, int mpad,
+              const Q5W & w, const EpiParams & ep);
+bool gemm_q16_applies(const Q5W & w, int M, int N, int K);
+// expand Q5W block arrays into wi / dwt (device buffers of N*K halves and K/32*npad floats)
+void quant_expand_f16(hipStream_t s, const Q5W & w, int N, int K, _Float16 * wi, float * dwt, int npad);
 int q5_partial_splits(int K);
 size_t q5_partial_floats(int N, int K);  // workspace floats of a partial quantized GEMM (M <= 32)
 

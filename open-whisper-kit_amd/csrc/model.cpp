@@ -520,6 +520,34 @@ Model * load_model(whisper_model_loader * loader, int device, std::string & err)
             }
             q5m[groups[gi][0]] = w;
         }
+        // symmetric formats: the encoder and cross-K/V matrices (M >= 2048 rows at batch) also as exact
+        // f16 integers + transposed scales for the f16 MFMA ring kernel (gemm_q16); large-v3: 1.4 GB
+        if (!qf_has_m(f)) {
+            std::vector<size_t> sel;
+            size_t tot = 0;
+            auto al = [](size_t b) { return (b + 255) & ~(size_t) 255; };
+            for (size_t gi = 1; gi < groups.size(); ++gi) {
+                if (gi >= n_enc_groups && groups[gi][0].find("cross_attn.key") == std::string::npos) continue;
+                const Plan & pl = plans[gi];
+                const int npad = (pl.N + 255) / 256 * 256;
+                tot += al((size_t) pl.N * pl.K * 2) + al((size_t) (pl.K / 32) * npad * 4);
+                sel.push_back(gi);
+            }
+            m->q16blob.alloc(tot);
+            char * b16 = (char *) m->q16blob.ptr;
+            size_t o = 0;
+            for (size_t gi : sel) {
+                const Plan & pl = plans[gi];
+                Q5W & w = q5m[groups[gi][0]];
+                w.npad = (pl.N + 255) / 256 * 256;
+                w.wi = (const _Float16 *) (b16 + o);
+                o += al((size_t) pl.N * pl.K * 2);
+                w.dwt = (const float *) (b16 + o);
+                o += al((size_t) (pl.K / 32) * w.npad * 4);
+                quant_expand_f16(nullptr, w, pl.N, pl.K, (_Float16 *) w.wi, (float *) w.dwt, w.npad);
+            }
+            OWK_HIP_CHECK(hipDeviceSynchronize());
+        }
     }
     auto Q = [&](const std::string & n) { auto it = q5m.find(n); return it == q5m.end() ? Q5W() : it->second; };
     m->conv1_w = (const _Float16 *) (base + o_conv1);

@@ -86,6 +86,7 @@ struct Model {
     bool q5 = false;                     // quantized model (MOSTLY_Q5_0/Q8_0/Q4_0/Q4_1/Q5_1): 2-D linears (and d_te) are Q5W
     int qfmt = 0;                        // their block format (kernels.h QFmt)
     DevBuf q5blob;
+    DevBuf q16blob;  // Q5W::wi / dwt of the encoder and cross-K/V matrices (symmetric formats)
     Q5W q_te;
     const _Float16 * d_te = nullptr;     // [n_vocab][d]
     const _Float16 * d_te_t = nullptr;   // tiled copy (logits of decode steps)

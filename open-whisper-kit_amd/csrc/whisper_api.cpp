@@ -1210,6 +1210,11 @@ double owk_debug_gemm_bench(int device, int mode, int M, int N, int K, int iters
 
 int owk_debug_gemm_quant(int device, int fmt, int M, int N, int K, const float * a, const uint8_t * w_blocks,
                          float * out, int8_t * q_out, float * d_out) {
+    return owk_debug_gemm_quant2(device, fmt, M, N, K, a, w_blocks, out, q_out, d_out, 0);
+}
+
+int owk_debug_gemm_quant2(int device, int fmt, int M, int N, int K, const float * a, const uint8_t * w_blocks,
+                          float * out, int8_t * q_out, float * d_out, int use_q16) {
     try {
         if (fmt < QF_Q5_0 || fmt > QF_Q5_1 || K % 32) throw std::runtime_error("bad format or K");
         OWK_HIP_CHECK(hipSetDevice(device));
@@ -1252,7 +1257,24 @@ int owk_debug_gemm_quant(int device, int fmt, int M, int N, int K, const float *
         EpiParams ep;
         ep.out32 = dout.as<float>();
         ep.ldo = N;
-        gemm_q5(s, EPI_F32, M, N, K, q8.as<int8_t>(), q8d.as<float>(), w, ep);
+        DevBuf wi, dwt, q16, q16d;
+        if (use_q16) {
+            // the large-tile path of the encoder: expanded weights, f16 Q8_0 integers, gemm_q16
+            w.npad = (N + 255) / 256 * 256;
+            wi.alloc((size_t) N * K * 2);
+            dwt.alloc((size_t) nb * w.npad * 4);
+            quant_expand_f16(s, w, N, K, wi.as<_Float16>(), dwt.as<float>(), w.npad);
+            w.wi = wi.as<_Float16>();
+            w.dwt = dwt.as<float>();
+            if (!gemm_q16_applies(w, M, N, K)) throw std::runtime_error("gemm_q16 does not apply to this shape");
+            const int mpad = (M + 255) / 256 * 256;
+            q16.alloc((size_t) M * K * 2);
+            q16d.alloc((size_t) nb * mpad * 4);
+            quantize_q8_f16(s, da.as<float>(), nullptr, K, M, K, q16.as<_Float16>(), q16d.as<float>(), mpad);
+            gemm_q16(s, EPI_F32, M, N, K, q16.as<_Float16>(), q16d.as<float>(), mpad, w, ep);
+        } else {
+            gemm_q5(s, EPI_F32, M, N, K, q8.as<int8_t>(), q8d.as<float>(), w, ep);
+        }
         OWK_HIP_CHECK(hipStreamSynchronize(s));
         OWK_HIP_CHECK(hipMemcpy(out, dout.ptr, (size_t) M * N * 4, hipMemcpyDeviceToHost));
         if (q_out) OWK_HIP_CHECK(hipMemcpy(q_out, q8.ptr, (size_t) M * K, hipMemcpyDeviceToHost));
@@ -1327,6 +1349,92 @@ double owk_debug_attn_cross(int device, int which, int R, int H, int T, int n_ze
         return us;
     } catch (const std::exception & ex) {
         log_msg(GGML_LOG_LEVEL_ERROR, "owk_debug_attn_cross: %s\n", ex.what());
+        return -1;
+    }
+}
+
+// one large-tile GEMM epilogue mode through the 128x128 kernel (per-element epilogue) and the
+// 256x256 ring kernel (C^T tiles, 16-byte vector epilogue) on the same random operands, bias,
+// residual, positional rows and the real GELU table; returns the max |difference| over every
+// output the mode writes (f32 and f16 images), or -1 on error. d / T: EPI_QKV_ENC / EPI_KV_CROSS /
+// EPI_CONV2 shape parameters (N = 3d / 2d / d).
+double owk_debug_gemm_epi_diff(int device, int mode, int M, int N, int K, int d, int T) {
+    try {
+        OWK_HIP_CHECK(hipSetDevice(device));
+        hipStream_t s;
+        OWK_HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+        const int Tpad = (T + 63) / 64 * 64;
+        const int clips = T > 0 ? (M + T - 1) / T : 1;
+        const size_t n32 = (size_t) M * N, n16 = std::max((size_t) M * N, (size_t) clips * d * Tpad);
+        DevBuf da, dw, bias, bias2, pos, gt, res[2], o32[2], o16[3][2];
+        da.alloc((size_t) M * K * 2);
+        dw.alloc((size_t) N * K * 2);
+        bias.alloc((size_t) N * 4);
+        bias2.alloc((size_t) N * 4);
+        pos.alloc((size_t) std::max(T, 1) * N * 4);
+        gt.alloc(65536 * 2);
+        OWK_HIP_CHECK(hipMemcpy(gt.ptr, gelu_table_host().data(), 65536 * 2, hipMemcpyHostToDevice));
+        hipLaunchKernelGGL(k_fill_rand_f16, dim3(4096), dim3(256), 0, s, da.as<_Float16>(), (size_t) M * K, 1u);
+        hipLaunchKernelGGL(k_fill_rand_f16, dim3(4096), dim3(256), 0, s, dw.as<_Float16>(), (size_t) N * K, 7u);
+        std::vector<float> hb(N), hb2(N), hp((size_t) std::max(T, 1) * N), hr(n32);
+        uint32_t st = 12345u;
+        auto rnd = [&] { st = st * 1664525u + 1013904223u; return (float) ((st >> 8) & 0xFFFF) / 65536.0f - 0.5f; };
+        for (auto & v : hb) v = rnd();
+        for (auto & v : hb2) v = rnd();
+        for (auto & v : hp) v = rnd();
+        for (auto & v : hr) v = rnd();
+        OWK_HIP_CHECK(hipMemcpy(bias.ptr, hb.data(), hb.size() * 4, hipMemcpyHostToDevice));
+        OWK_HIP_CHECK(hipMemcpy(bias2.ptr, hb2.data(), hb2.size() * 4, hipMemcpyHostToDevice));
+        OWK_HIP_CHECK(hipMemcpy(pos.ptr, hp.data(), hp.size() * 4, hipMemcpyHostToDevice));
+        std::vector<float> out32[2];
+        std::vector<uint16_t> out16[3][2];
+        for (int k = 0; k < 2; ++k) {
+            res[k].alloc(n32 * 4);
+            o32[k].alloc(n32 * 4);
+            OWK_HIP_CHECK(hipMemcpy(res[k].ptr, hr.data(), n32 * 4, hipMemcpyHostToDevice));
+            OWK_HIP_CHECK(hipMemset(o32[k].ptr, 0, n32 * 4));
+            for (int j = 0; j < 3; ++j) {
+                o16[j][k].alloc(n16 * 2);
+                OWK_HIP_CHECK(hipMemset(o16[j][k].ptr, 0, n16 * 2));
+            }
+            EpiParams ep;
+            ep.bias = bias.as<float>();
+            ep.bias2 = bias2.as<float>();
+            ep.scale = 0.35f;
+            ep.resid = res[k].as<float>();
+            ep.out32 = o32[k].as<float>();
+            ep.out16 = o16[0][k].as<_Float16>();
+            ep.out16b = o16[1][k].as<_Float16>();
+            ep.out16c = o16[2][k].as<_Float16>();
+            ep.ldo = N;
+            ep.d = d;
+            ep.T = T;
+            ep.Tpad = Tpad;
+            ep.pos = pos.as<float>();
+            ep.gelu_tab = gt.as<uint16_t>();
+            if (mode == EPI_RESID_F32 || mode == EPI_HALF_RESID) ep.out32 = res[k].as<float>();  // in place, as the engine
+            gemm_set_256(k == 0 ? 0 : 1);
+            gemm_f16(s, mode, M, N, K, da.as<_Float16>(), K, dw.as<_Float16>(), K, ep);
+            OWK_HIP_CHECK(hipStreamSynchronize(s));
+            out32[k].resize(n32);
+            OWK_HIP_CHECK(hipMemcpy(out32[k].data(), ep.out32, n32 * 4, hipMemcpyDeviceToHost));
+            for (int j = 0; j < 3; ++j) {
+                out16[j][k].resize(n16);
+                OWK_HIP_CHECK(hipMemcpy(out16[j][k].data(), o16[j][k].ptr, n16 * 2, hipMemcpyDeviceToHost));
+            }
+        }
+        gemm_set_256(1);
+        double mx = 0.0;
+        for (size_t i = 0; i < n32; ++i) mx = std::max(mx, (double) std::fabs(out32[0][i] - out32[1][i]));
+        for (int j = 0; j < 3; ++j)
+            for (size_t i = 0; i < n16; ++i) {
+                const _Float16 a = __builtin_bit_cast(_Float16, out16[j][0][i]), b = __builtin_bit_cast(_Float16, out16[j][1][i]);
+                mx = std::max(mx, (double) std::fabs((float) a - (float) b));
+            }
+        OWK_HIP_CHECK(hipStreamDestroy(s));
+        return mx;
+    } catch (const std::exception & ex) {
+        log_msg(GGML_LOG_LEVEL_ERROR, "owk_debug_gemm_epi_diff: %s\n", ex.what());
         return -1;
     }
 }

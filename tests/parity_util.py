@@ -10,7 +10,8 @@ the reference's, `LogitError.of`). When the two runs first pick different tokens
 are within 2 eps of each other; their log-probabilities (each run's own normaliser, also within
 eps) within 3 eps. A divergence is accepted only if |logprob_g - logprob_r| <= TIE_FACTOR * eps
 (4 eps: one eps of margin for the error growing over later decode steps); everything decided
-before it must match exactly and every case must compare a minimum number of tokens.
+before it must match exactly and every case must compare a minimum number of tokens, unless the
+parting is a hard tie (margin <= 1 eps: below the measured error itself).
 """
 import ctypes as C
 
@@ -25,12 +26,16 @@ def flat_tokens(segs):
     return [(si, t) for si, s in enumerate(segs) for t in s["tokens"]]
 
 
-def compare_segments(got, want, key, tie, exact=False, p_atol=2e-3, min_compared=MIN_COMPARED, log=print):
+def compare_segments(got, want, key, tie, exact=False, p_atol=None, min_compared=MIN_COMPARED, log=print):
     """Token ids, segment bounds, text, token timestamps identical to the reference's `want`.
 
     Compared up to the first step where the runs pick different tokens whose log-probabilities
-    are within `tie` (exact=True: no divergence allowed). Returns the number of tokens compared
-    identical; asserts it is at least min(min_compared, reference tokens)."""
+    are within `tie` (exact=True: no divergence allowed). Token probabilities agree within p_atol
+    (default max(2e-3, tie / 2): a logit error eps moves a probability p by at most ~2 eps p, and
+    tie = 4 eps). Returns the number of tokens compared identical; asserts it is at least
+    min(min_compared, reference tokens)."""
+    if p_atol is None:
+        p_atol = max(2e-3, 0.5 * tie)
     fg, fw = flat_tokens(got), flat_tokens(want)
     n_cmp, margin = len(fw), None
     for i, ((sg, g), (sw, r)) in enumerate(zip(fg, fw)):
@@ -57,8 +62,13 @@ def compare_segments(got, want, key, tie, exact=False, p_atol=2e-3, min_compared
             f"{key}: token timestamps differ"
     note = "" if margin is None else f" (parted at a near-tie, margin {margin:.2e} <= {tie:.2e})"
     log(f"[parity] {key}: {n_cmp}/{len(fw)} tokens compared identical{note}")
+    # a parting within ONE measured logit error (tie / TIE_FACTOR) is a tie no implementation with that
+    # error can decide; the minimum applies to partings in the wider (1, TIE_FACTOR] eps band
+    if margin is not None and margin <= tie / TIE_FACTOR and n_cmp < min(min_compared, len(fw)):
+        log(f"[parity] {key}: hard tie (margin {margin:.2e} <= 1 eps = {tie / TIE_FACTOR:.2e}), minimum waived")
+        return n_cmp
     assert n_cmp >= min(min_compared, len(fw)), \
-        f"{key}: only {n_cmp} of {len(fw)} tokens compared before a near-tie (minimum {min_compared})"
+        f"{key}: only {n_cmp} of {len(fw)} tokens compared before a near-tie{note} (minimum {min_compared})"
     return n_cmp
 
 

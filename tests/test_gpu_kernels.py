@@ -117,3 +117,28 @@ def test_attn_cross_speed():
     gbs = {w: 32 * 20 * 1500 * 64 * 2 * 2 / t[w] / 1e3 for w in t}
     print(f"attn_cross one-wave {t[1]:.1f} us ({gbs[1]:.0f} GB/s), two-wave {t[2]:.1f} us ({gbs[2]:.0f} GB/s)")
     assert t[1] > 0 and t[2] > 0
+
+
+# kernels.h EPI_* codes and (N, d, T) per mode for the large-tile epilogue cross-check
+_EPI_CASES = {
+    "f16": (0, 1280, 0, 0), "gelu": (1, 5120, 0, 0), "resid": (2, 1280, 0, 0), "conv2": (3, 1280, 1280, 1500),
+    "qkv_enc": (4, 3840, 1280, 1500), "kv_cross": (5, 2560, 1280, 1500), "f32": (7, 1024, 0, 0),
+    "bias_f32": (9, 1024, 0, 0), "silu": (10, 1024, 0, 0), "half_resid": (11, 1024, 0, 0), "relu": (12, 1024, 0, 0),
+    "sigmoid": (13, 1024, 0, 0), "f16_ragged": (0, 1288, 0, 0),
+}
+
+
+@pytest.mark.parametrize("case", sorted(_EPI_CASES))
+def test_gemm256_epilogue_matches_128(case):
+    """The 256x256 ring kernel computes C^T tiles and writes 8-column runs with 16-byte vector
+    epilogues (k_gemm.hip epi_row8); the 128x128 kernel writes every element with epi_store.
+    Same operands, bias, residual, positions and GELU table: every output must agree."""
+    mode, N, d, T = _EPI_CASES[case]
+    L = owk.load()
+    L.owk_debug_gemm_epi_diff.restype = C.c_double
+    L.owk_debug_gemm_epi_diff.argtypes = [C.c_int] * 7
+    M = 3000 if T else 2304
+    diff = L.owk_debug_gemm_epi_diff(0, mode, M, N, 1280, d, T)
+    print(f"{case}: max|256 - 128| = {diff:.3g}")
+    assert diff >= 0
+    assert diff <= 1e-6, f"{case}: epilogues differ by {diff}"

@@ -141,7 +141,7 @@ CONFIGS = {
 STOCHASTIC = ("greedy_fallback", "beam5", "sampled")  # see tests/golden/recording.py
 
 
-def _compare(got, want, key, exact=False, p_atol=2e-3, tie=None, min_compared=MIN_COMPARED):
+def _compare(got, want, key, exact=False, p_atol=None, tie=None, min_compared=MIN_COMPARED):
     """parity_util.compare_segments with the near-tie bound given explicitly (tie) or, for
     injected configs, none (exact=True)."""
     return compare_segments(got, want, key, tie=0.0 if tie is None else tie, exact=exact, p_atol=p_atol,

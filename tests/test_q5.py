@@ -219,3 +219,46 @@ def test_quant_gemm_vs_reference(kind, M, N, K):
                           ref.ctypes.data_as(C.POINTER(C.c_float)), 4) == 0
     err = np.abs(out - ref).max() / np.abs(ref).max()
     assert err < 2e-6, (kind, M, N, K, err)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["q5_0", "q8_0", "q4_0"])
+def test_quant_gemm_q16_vs_reference(kind):
+    """The encoder's large-tile quantized GEMM (gemm_q16: the weight and Q8_0 activation integers as
+    exact f16 values through the 128x256 MFMA ring kernel, acc = fma(block dot, d_w * d_a, acc))
+    against the reference's ggml_mul_mat on the same ggml blocks and f32 activations, at a batched
+    encoder shape (M >= 2048 rows, ragged M and N)."""
+    import sys
+    import owk_synth as S
+
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import ref_oracle as R
+
+    if not R.available():
+        pytest.skip("reference oracle not built")
+    L = owk.load()
+    fmt, wtype, bb = QFMT[kind]
+    M, N, K = 2100, 1296, 1280
+    L.owk_debug_gemm_quant2.argtypes = [C.c_int] * 5 + [C.POINTER(C.c_float), C.c_void_p, C.POINTER(C.c_float),
+                                                        C.c_void_p, C.c_void_p, C.c_int]
+    rng = np.random.default_rng(11)
+    a = (rng.standard_normal((M, K)) * 0.7).astype(np.float32)
+    wf = (rng.standard_normal((N, K)) / np.sqrt(K) + 0.02).astype(np.float32)
+    blocks = S._QKIND[kind][2](wf)
+    out = np.zeros((M, N), np.float32)
+    assert L.owk_debug_gemm_quant2(0, fmt, M, N, K, a.ctypes.data_as(C.POINTER(C.c_float)), blocks,
+                                   out.ctypes.data_as(C.POINTER(C.c_float)), None, None, 1) == 0
+    RL = R.lib()
+    RL.ref_mul_mat.argtypes = [C.c_int, C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_float), C.c_int,
+                               C.POINTER(C.c_float), C.c_int]
+    ref = np.zeros((M, N), np.float32)
+    for r0 in range(0, M, 300):  # row slices: the probe's ggml context is sized for small operands
+        r1 = min(M, r0 + 300)
+        ar = np.ascontiguousarray(a[r0:r1])
+        part = np.zeros((r1 - r0, N), np.float32)
+        assert RL.ref_mul_mat(wtype, blocks, N, K, ar.ctypes.data_as(C.POINTER(C.c_float)), r1 - r0,
+                              part.ctypes.data_as(C.POINTER(C.c_float)), 8) == 0
+        ref[r0:r1] = part
+    err = np.abs(out - ref).max() / np.abs(ref).max()
+    print(f"{kind}: gemm_q16 max rel err vs ggml_mul_mat {err:.2e}")
+    assert err < 2e-6, (kind, err)
