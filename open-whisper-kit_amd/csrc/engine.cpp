@@ -205,7 +205,8 @@ void Engine::linear(const char * cls, int mode, int M, int N, int K, const _Floa
     // the block dot; bytes: the weight blocks (18-34 B per 32) + the int8 activations. a_q8: the
     // producer (LayerNorm, one_chunk attention) already wrote q8a_ / q8d_
     if (gemm_q16_applies(q, M, N, K)) {
-        // large tiles: Q8_0 integers as exact f16 + block-major scales, the f16 MFMA ring kernel
+        // large tiles: Q8_0 integers as exact f16 + block-major scales, the f16 MFMA ring kernel; the
+        // rows are quantized from the f32 activation (A32) where the producer keeps one, as the reference
         const int mpad = (M + 255) / 256 * 256;
         if (q16a_.bytes < (size_t) M * K * 2 || q16d_.bytes < (size_t) (K / 32) * mpad * 4)
             throw std::runtime_error("linear: gemm_q16 operand buffers not reserved");
@@ -252,6 +253,7 @@ void Engine::encode(const std::vector<int> & slots, const std::vector<int> & off
         e_enc32_.alloc((size_t) M * d * 4);
         if (m->q5) {
             e_ao32_.alloc((size_t) M * d * 4);
+            e_xn32_.alloc((size_t) M * d * 4);  // f32 LayerNorm rows: gemm_q16 quantizes them like the reference
             q8a_.alloc(std::max(q8a_.bytes, (size_t) M * 4 * d));
             q8d_.alloc(std::max(q8d_.bytes, (size_t) M * 4 * d / 32 * 4));
             // gemm_q16 operands (reserved here: growing them inside linear() would free a buffer
@@ -318,7 +320,7 @@ void Engine::encode(const std::vector<int> & slots, const std::vector<int> & off
         {
             ProfScope ps(prof, stream, "layernorm");
             layernorm_f16(stream, e_x_.as<float>(), M, d, L.attn_ln_w, L.attn_ln_b, hp.eps, e_xn_.as<_Float16>(), d,
-                          nullptr, nullptr, q8a(), q8d());
+                          nullptr, m->q5 ? e_xn32_.as<float>() : nullptr, q8a(), q8d());
         }
         {
             EpiParams ep;
@@ -330,8 +332,8 @@ void Engine::encode(const std::vector<int> & slots, const std::vector<int> & off
             ep.d = d;
             ep.T = T;
             ep.Tpad = Tpad;
-            linear("gemm_enc", EPI_QKV_ENC, M, 3 * d, d, e_xn_.as<_Float16>(), nullptr, d, L.w_qkv, L.q_qkv, ep, nullptr,
-                   false, m->q5);
+            linear("gemm_enc", EPI_QKV_ENC, M, 3 * d, d, e_xn_.as<_Float16>(), m->q5 ? e_xn32_.as<float>() : nullptr, d,
+                   L.w_qkv, L.q_qkv, ep, nullptr, false, m->q5);
         }
         {
             // 4*T*Tpad_kv*d flops (QK^T and PV over the 1536 reference keys)
@@ -355,7 +357,7 @@ void Engine::encode(const std::vector<int> & slots, const std::vector<int> & off
         {
             ProfScope ps(prof, stream, "layernorm");
             layernorm_f16(stream, e_x_.as<float>(), M, d, L.mlp_ln_w, L.mlp_ln_b, hp.eps, e_xn_.as<_Float16>(), d,
-                          nullptr, nullptr, q8a(), q8d());
+                          nullptr, m->q5 ? e_xn32_.as<float>() : nullptr, q8a(), q8d());
         }
         {
             EpiParams ep;
@@ -363,8 +365,8 @@ void Engine::encode(const std::vector<int> & slots, const std::vector<int> & off
             ep.gelu_tab = m->gelu_tab;
             ep.out16 = e_h_.as<_Float16>();
             ep.ldo = 4 * d;
-            linear("gemm_enc", EPI_GELU_F16, M, 4 * d, d, e_xn_.as<_Float16>(), nullptr, d, L.w_mlp0, L.q_mlp0, ep,
-                   nullptr, false, m->q5);
+            linear("gemm_enc", EPI_GELU_F16, M, 4 * d, d, e_xn_.as<_Float16>(), m->q5 ? e_xn32_.as<float>() : nullptr, d,
+                   L.w_mlp0, L.q_mlp0, ep, nullptr, false, m->q5);
         }
         {
             EpiParams ep;
@@ -397,8 +399,8 @@ void Engine::encode(const std::vector<int> & slots, const std::vector<int> & off
         ep.T = T;
         ep.slot_map = e_slotmap_.as<int>();
         // Q5_0: the final LayerNorm wrote the encoder output's Q8_0 rows once for all layers
-        linear("gemm_cross", EPI_KV_CROSS, M, 2 * d, d, e_enc_.as<_Float16>(), nullptr, d, L.cw_kv, L.q_ckv, ep, nullptr,
-               false, m->q5);
+        linear("gemm_cross", EPI_KV_CROSS, M, 2 * d, d, e_enc_.as<_Float16>(), m->q5 ? e_enc32_.as<float>() : nullptr, d,
+               L.cw_kv, L.q_ckv, ep, nullptr, false, m->q5);
     }
 }
 

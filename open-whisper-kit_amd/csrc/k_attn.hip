@@ -70,7 +70,12 @@ __global__ __launch_bounds__(256, 2) void k_attn_encoder(const _Float16 * __rest
     floatx4 o[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) o[i] = floatx4{0.f, 0.f, 0.f, 0.f};
-    float m = -INFINITY;  // running max of this lane's query (uniform over the 4 lanes of a query)
+    // the online softmax runs in base 2: scores scaled by scale * log2(e), exponentials by the
+    // native v_exp_f32 (2 instructions where the accurate expf took ~10: this loop is VALU-bound
+    // beside its 16 MFMAs per tile). Mathematically the same softmax; the roundings move by ~1e-6
+    // relative against the reference's f32 tiled path (parity bars: tests/test_gpu_parity.py)
+    const float scale2 = scale * 1.44269504088896341f;
+    float m = -INFINITY;  // running max (base-2 units) of this lane's query (uniform over its 4 lanes)
     float lsum = 0.0f;    // partial row sum over this lane's keys
 
     const int ntiles = (T + FA_KT - 1) / FA_KT;
@@ -100,7 +105,7 @@ __global__ __launch_bounds__(256, 2) void k_attn_encoder(const _Float16 * __rest
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
                 const int key = kt * FA_KT + t * 16 + 4 * g + e;
-                float v = sc[t][e] * scale;
+                float v = sc[t][e] * scale2;
                 if (key >= T) v = -INFINITY;
                 sc[t][e] = v;
                 tmax = fmaxf(tmax, v);
@@ -108,7 +113,7 @@ __global__ __launch_bounds__(256, 2) void k_attn_encoder(const _Float16 * __rest
         tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
         tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
         const float mnew = fmaxf(m, tmax);
-        const float alpha = expf(m - mnew);  // m = -inf on the first tile -> 0
+        const float alpha = __builtin_amdgcn_exp2f(m - mnew);  // m = -inf on the first tile -> 0
         m = mnew;
         float ps = 0.0f;
         half8 pb[2];
@@ -116,7 +121,7 @@ __global__ __launch_bounds__(256, 2) void k_attn_encoder(const _Float16 * __rest
         for (int t = 0; t < 4; ++t)
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-                const float p = expf(sc[t][e] - mnew);
+                const float p = __builtin_amdgcn_exp2f(sc[t][e] - mnew);
                 ps += p;
                 pb[t >> 1][(t & 1) * 4 + e] = (_Float16) p;
             }
@@ -151,8 +156,8 @@ __global__ __launch_bounds__(256, 2) void k_attn_encoder(const _Float16 * __rest
     lsum += __shfl_xor(lsum, 32, 64);
     if (n_zero_pad > 0) {
         const float mnew = fmaxf(m, 0.0f);
-        const float alpha = expf(m - mnew);
-        lsum = lsum * alpha + (float) n_zero_pad * expf(0.0f - mnew);
+        const float alpha = __builtin_amdgcn_exp2f(m - mnew);
+        lsum = lsum * alpha + (float) n_zero_pad * __builtin_amdgcn_exp2f(0.0f - mnew);
 #pragma unroll
         for (int i = 0; i < 4; ++i) o[i] *= alpha;
     }
