@@ -86,7 +86,8 @@ WHISPER_API int owk_debug_gemm_q5(int device, int M, int N, int K, const float *
  * of that type; Q4_1 / Q5_1 take Q8_1 activations); d_out receives the raw f32 activation scales */
 WHISPER_API int owk_debug_gemm_quant(int device, int fmt, int M, int N, int K, const float * a, const uint8_t * w_blocks,
                                      float * out, int8_t * q_out, float * d_out);
-// use_q16 = 1: the large-tile encoder path (expanded f16 integers, gemm_q16; M >= 2048, symmetric formats)
+// use_q16 = 1: the large-tile encoder path (expanded f16 integers, gemm_q16; M >= 2048, symmetric formats);
+// 2: the decode-row path on f16 activation rows quantized inside the GEMM (M <= 32; out = the summed split-K partials)
 WHISPER_API int owk_debug_gemm_quant2(int device, int fmt, int M, int N, int K, const float * a, const uint8_t * w_blocks,
                                       float * out, int8_t * q_out, float * d_out, int use_q16);
 /* mode | 0x100: force the 128x128 large-GEMM kernel; | 0x400: 5-slot ring variant of the 256x256 kernel;

@@ -832,7 +832,19 @@ void Engine::launch_decode(const DecShape & sh) {
         EpiParams ep;
         ep.out32 = gws_.partial;
         if (gws_.partial_floats < q5_partial_floats(d, K)) throw std::runtime_error("decode: partial workspace");
-        linear("gemm_dec", EPI_PARTIAL, R, d, K, A16, A32, K, nullptr, q, ep, nullptr, true, a_q8);
+        static const bool a16_env = [] {
+            const char * e = getenv("OWK_Q5_A16");
+            return e && atoi(e) != 0;
+        }();
+        if (a16_env && !a_q8 && !A32 && A16) {
+            // opt-in (OWK_Q5_A16=1): f16 activation rows (the GELU outputs) quantized to Q8_0 inside the
+            // GEMM's waves. Measured slower: the separate quantize pass went 84.5 -> 39 ms per step but
+            // mlp.2's decode GEMM 441 -> 495 ms (every column tile re-quantizes the rows; RTF 772 -> 751)
+            ProfScope ps(prof, stream, "gemm_dec", gemm_flops(R, d, K), (double) d * K * qf_block_bytes(q.fmt) / 32.0 + 2.0 * R * K);
+            gemm_q5_rows_a16(stream, R, d, K, A16, q, ep);
+        } else {
+            linear("gemm_dec", EPI_PARTIAL, R, d, K, A16, A32, K, nullptr, q, ep, nullptr, true, a_q8);
+        }
         ProfScope ps(prof, stream, "layernorm");
         resid_layernorm(stream, R, d, q5_partial_splits(K), gws_.partial, bias, d_x_.as<float>(), lnw, lnb, hp.eps,
                         d_xn_.as<_Float16>(), d, lnw ? q8a() : nullptr, lnw ? q8d() : nullptr);

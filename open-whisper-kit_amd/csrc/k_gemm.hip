@@ -1473,7 +1473,11 @@ constexpr int GQ_MAX_SCALES = 32 * 160;  // M x K/32 activation scales in LDS
 // activation scales per thread: M * nb <= 32 * nb over blockDim = 64 * ceil(nb / J) threads
 // -> at most 32 * J / 64 + 1
 
-template <int MODE, int MT, int FMT, int GQ_J>  // FMT: QFmt; GQ_J K blocks per wave
+// A16: the activation is f16 rows (qa points at them) that each wave quantizes to Q8_0 itself
+// for its own K blocks -- x86 quantize_row_q8_0 on the exact f32 values of the f16 inputs (the
+// GELU table outputs feeding mlp.2), the 32 values of a block sit in 4 lanes of one row -- and
+// whose scales it publishes to LDS: no separate quantize launch for that matmul
+template <int MODE, int MT, int FMT, int GQ_J, bool A16 = false>  // FMT: QFmt; GQ_J K blocks per wave
 __global__ __launch_bounds__(GQ_MAXW * 64) void k_gemm_q5_rows(int M, int N, int K, const int8_t * __restrict__ qa,
                                                                const float * __restrict__ da, Q5W w, EpiParams ep) {
     constexpr int GQ_DA_PER_THREAD = 32 * GQ_J / 64 + 1;
@@ -1496,6 +1500,7 @@ __global__ __launch_bounds__(GQ_MAXW * 64) void k_gemm_q5_rows(int M, int N, int
     uint32_t qh[GQ_J];
     _Float16 dw[GQ_J], mw[GQ_J];
     long a[MT][GQ_J];
+    half8 ah[A16 ? MT : 1][A16 ? GQ_J : 1];
     // the tile's blocks are contiguous records (qf_tile_bytes): coalesced loads. Blocks past this
     // wave's range load a valid record and a zero activation (adds exact zeros). Record format at
     // compile time: the load phase stays branch-free.
@@ -1511,25 +1516,52 @@ __global__ __launch_bounds__(GQ_MAXW * 64) void k_gemm_q5_rows(int M, int N, int
 #pragma unroll
         for (int i = 0; i < MT; ++i) {
             const int ra = min(i * 16 + c16, M - 1);
-            const long t = *(const long *) (qa + (size_t) ra * K + kb * 32 + 8 * g);
-            a[i][j] = j < nj ? t : 0L;
+            if constexpr (A16) {
+                ah[i][j] = *(const half8 *) ((const _Float16 *) qa + (size_t) ra * K + kb * 32 + 8 * g);
+            } else {
+                const long t = *(const long *) (qa + (size_t) ra * K + kb * 32 + 8 * g);
+                a[i][j] = j < nj ? t : 0L;
+            }
         }
     }
     // activation scales of this block's K range (raw f32 d; at most GQ_DA_PER_THREAD per thread:
     // M <= 32, nbl <= nw * J) to LDS as [row][kb - kblo]; every load of the launch is issued before
     // the first wait (one round trip)
-    float dv[GQ_DA_PER_THREAD];
+    if constexpr (A16) {
 #pragma unroll
-    for (int u = 0; u < GQ_DA_PER_THREAD; ++u) {
-        const int i = tid + u * blockDim.x;
-        const int r = i / nbl;
-        dv[u] = i < M * nbl ? da[(size_t) r * nb + kblo + (i - r * nbl)] : 0.0f;
-    }
-    __builtin_amdgcn_sched_barrier(0);
+        for (int j = 0; j < GQ_J; ++j)
 #pragma unroll
-    for (int u = 0; u < GQ_DA_PER_THREAD; ++u) {
-        const int i = tid + u * blockDim.x;
-        if (i < M * nbl) sda[i] = dv[u];
+            for (int i = 0; i < MT; ++i) {
+                float x[8], m = 0.0f;
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                    x[e] = (float) ah[i][j][e];
+                    m = fmaxf(m, fabsf(x[e]));
+                }
+                m = fmaxf(m, __shfl_xor(m, 16, 64));  // the block's 4 lanes (g = 0..3) of row c16
+                m = fmaxf(m, __shfl_xor(m, 32, 64));
+                const float id = m != 0.0f ? 127.f / m : 0.0f;
+                uint64_t q = 0;
+#pragma unroll
+                for (int e = 0; e < 8; ++e) q |= (uint64_t) (uint8_t) (int8_t) rintf(x[e] * id) << (8 * e);
+                a[i][j] = j < nj ? (long) q : 0L;
+                const int ra = i * 16 + c16, kb = kb0 + j;
+                if (g == 0 && ra < M && j < nj) sda[ra * nbl + (kb - kblo)] = m / 127.f;  // raw f32 d
+            }
+    } else {
+        float dv[GQ_DA_PER_THREAD];
+#pragma unroll
+        for (int u = 0; u < GQ_DA_PER_THREAD; ++u) {
+            const int i = tid + u * blockDim.x;
+            const int r = i / nbl;
+            dv[u] = i < M * nbl ? da[(size_t) r * nb + kblo + (i - r * nbl)] : 0.0f;
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int u = 0; u < GQ_DA_PER_THREAD; ++u) {
+            const int i = tid + u * blockDim.x;
+            if (i < M * nbl) sda[i] = dv[u];
+        }
     }
     __syncthreads();
     floatx4 acc[MT], accm[MT];
@@ -1703,6 +1735,33 @@ template <int MODE> struct LaunchQ5 {
                                qa, da, w, ep);
     }
 };
+
+// decode-row quantized GEMM on f16 activation rows (A16 instantiation): EPI_PARTIAL only (mlp.2)
+void gemm_q5_rows_a16(hipStream_t s, int M, int N, int K, const _Float16 * A16, const Q5W & w, const EpiParams & ep) {
+    const int nb = K / 32;
+    if (!(M > 0 && M <= 32 && w.tiled && K % 32 == 0 && nb <= GQ_MAXW * GQ_JMAX && M * nb <= GQ_MAX_SCALES && ep.out32))
+        throw std::runtime_error("gemm_q5_rows_a16: unsupported shape");
+    const int KS = q5_partial_splits(K);
+    const int J = 3;
+    const int per = (nb + KS - 1) / KS;
+    const int nw = (per + J - 1) / J;
+    if (nw > GQ_MAXW) throw std::runtime_error("gemm_q5_rows_a16: plan");
+    const dim3 grid((N + 15) / 16, KS), block(nw * 64);
+    const int8_t * qa = (const int8_t *) A16;
+#define OWK_Q_A16(MT_, F_) hipLaunchKernelGGL((k_gemm_q5_rows<EPI_PARTIAL, MT_, F_, 3, true>), grid, block, 0, s, M, N, K, qa, \
+                                           nullptr, w, ep)
+#define OWK_Q_A16_F(MT_)                              \
+    switch (w.fmt) {                                  \
+        case QF_Q8_0: OWK_Q_A16(MT_, QF_Q8_0); break; \
+        case QF_Q4_0: OWK_Q_A16(MT_, QF_Q4_0); break; \
+        case QF_Q4_1: OWK_Q_A16(MT_, QF_Q4_1); break; \
+        case QF_Q5_1: OWK_Q_A16(MT_, QF_Q5_1); break; \
+        default: OWK_Q_A16(MT_, QF_Q5_0); break;      \
+    }
+    if (M <= 16) OWK_Q_A16_F(1) else OWK_Q_A16_F(2)
+#undef OWK_Q_A16_F
+#undef OWK_Q_A16
+}
 
 int qf_block_bytes(int f) {
     switch (f) {

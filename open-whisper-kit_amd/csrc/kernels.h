@@ -183,6 +183,8 @@ void gemm_q16(hipStream_t s, int mode, int M, int N, int K, const _Float16 * q16
 bool gemm_q16_applies(const Q5W & w, int M, int N, int K);
 // expand Q5W block arrays into wi / dwt (device buffers of N*K halves and K/32*npad floats)
 void quant_expand_f16(hipStream_t s, const Q5W & w, int N, int K, _Float16 * wi, float * dwt, int npad);
+// EPI_PARTIAL decode-row quantized GEMM whose activation rows are f16 (quantized to Q8_0 inside)
+void gemm_q5_rows_a16(hipStream_t s, int M, int N, int K, const _Float16 * A16, const Q5W & w, const EpiParams & ep);
 int q5_partial_splits(int K);
 size_t q5_partial_floats(int N, int K);  // workspace floats of a partial quantized GEMM (M <= 32)
 

@@ -1257,7 +1257,30 @@ int owk_debug_gemm_quant2(int device, int fmt, int M, int N, int K, const float 
         EpiParams ep;
         ep.out32 = dout.as<float>();
         ep.ldo = N;
-        DevBuf wi, dwt, q16, q16d;
+        DevBuf wi, dwt, q16, q16d, a16, part;
+        if (use_q16 == 2) {
+            // the decode-row A16 path (mlp.2): f16 rows of a, quantized inside the GEMM; split-K partial
+            // tiles summed here in split order (as resid_layernorm does)
+            std::vector<_Float16> ah((size_t) M * K);
+            for (size_t i = 0; i < ah.size(); ++i) ah[i] = (_Float16) a[i];
+            a16.alloc(ah.size() * 2);
+            OWK_HIP_CHECK(hipMemcpy(a16.ptr, ah.data(), ah.size() * 2, hipMemcpyHostToDevice));
+            const int ks = q5_partial_splits(K);
+            part.alloc((size_t) ks * M * N * 4);
+            EpiParams pp;
+            pp.out32 = part.as<float>();
+            gemm_q5_rows_a16(s, M, N, K, a16.as<_Float16>(), w, pp);
+            OWK_HIP_CHECK(hipStreamSynchronize(s));
+            std::vector<float> hp((size_t) ks * M * N);
+            OWK_HIP_CHECK(hipMemcpy(hp.data(), part.ptr, hp.size() * 4, hipMemcpyDeviceToHost));
+            for (size_t i = 0; i < (size_t) M * N; ++i) {
+                float acc = hp[i];
+                for (int k = 1; k < ks; ++k) acc += hp[(size_t) k * M * N + i];
+                out[i] = acc;
+            }
+            OWK_HIP_CHECK(hipStreamDestroy(s));
+            return 0;
+        }
         if (use_q16) {
             // the large-tile path of the encoder: expanded weights, f16 Q8_0 integers, gemm_q16
             w.npad = (N + 255) / 256 * 256;
