@@ -373,6 +373,28 @@ constexpr int G2_M = 256, G2_N = 256, G2_K = 32;
 constexpr int G2_OP = G2_M * G2_K * 2;     // 16 KB: one operand of one K-step
 constexpr int G2_SLOT = 2 * G2_OP;         // 32 KB
 
+// Tile of the (XCD-remapped, so per-XCD contiguous) index t: groups of TO_GM row panels swept column
+// by column, so the ~32 tiles an XCD runs at once cover 8 row panels x 4 column panels -- A and W
+// panels both re-used from that XCD's L2 (row-major order ran 1.6 row panels x all 20 column
+// panels of MLP0 at once: every W panel re-fetched per row panel, 2 GB of FETCH_SIZE per launch,
+// profiles/r02n_pmc_fetch_summary.txt)
+constexpr int TO_GM = 8;
+__device__ __forceinline__ void tile_order(int t, int ntiles, int nbn, int & bm, int & bn) {
+    static const bool grouped = true;
+    if (!grouped) {
+        bm = t / nbn;
+        bn = t - bm * nbn;
+        return;
+    }
+    const int nbm = ntiles / nbn;
+    const int per = TO_GM * nbn;
+    const int grp = t / per, first = grp * TO_GM;
+    const int gm = min(TO_GM, nbm - first);  // the last group may hold fewer row panels
+    const int r = t - grp * per;
+    bm = first + r % gm;
+    bn = r / gm;
+}
+
 template <int MODE, int G2_SLOTS, bool SWAP = true>
 __global__ __launch_bounds__(512, 2) void k_gemm_256(int M, int N, int K, const _Float16 * __restrict__ A, int lda,
                                                      const _Float16 * __restrict__ W, int ldw, EpiParams ep) {
@@ -392,7 +414,8 @@ __global__ __launch_bounds__(512, 2) void k_gemm_256(int M, int N, int K, const 
         const int base = xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q;
         bid = base + (bid >> 3);
     }
-    const int bm = bid / nbn, bn = bid - bm * nbn;
+    int bm, bn;
+    tile_order(bid, nb, nbn, bm, bn);
     const int m0 = bm * G2_M, n0 = bn * G2_N;
 
     // Output layout. Q/K-type tiles ("swap": every mode except the V tiles of EPI_QKV_ENC) compute
@@ -607,7 +630,8 @@ __global__ __launch_bounds__(512, 2) void k_gemm_q16(int M, int N, int K, const 
         const int base = xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q;
         bid = base + (bid >> 3);
     }
-    const int bm = bid / nbn, bn = bid - bm * nbn;
+    int bm, bn;
+    tile_order(bid, nbt, nbn, bm, bn);
     const int m0 = bm * GQ16_M, n0 = bn * G2_N;
 
     auto wsw = [](int r) { return ((r >> 2) ^ (r >> 3)) & 3; };
@@ -1128,14 +1152,11 @@ template <int MODE> struct Launch256 {
         const int nbm = (M + G2_M - 1) / G2_M, nbn = (N + G2_N - 1) / G2_N;
         EpiParams e = ep;
         e.vec = epi_vec_ok(MODE, ep, N) ? 1 : 0;
-        if (MODE == EPI_QKV_ENC && N > 2 * ep.d) {
-            // Q and K columns as C^T tiles, then the V columns (transposed image) as C tiles
-            const int n1 = 2 * ep.d, nb1 = (n1 + G2_N - 1) / G2_N, nb2 = (N - n1 + G2_N - 1) / G2_N;
-            hipLaunchKernelGGL((k_gemm_256<MODE, 4, true>), dim3(nbm * nb1), dim3(512), 0, s, M, n1, K, A, lda, W, ldw, e);
-            EpiParams ev = e;
-            ev.c_off = n1;
-            hipLaunchKernelGGL((k_gemm_256<MODE, 4, false>), dim3(nbm * nb2), dim3(512), 0, s, M, N - n1, K, A, lda,
-                               W + (size_t) n1 * ldw, ldw, ev);
+        if (MODE == EPI_QKV_ENC) {
+            // one launch of C tiles: the V columns need them (transposed image, 4 consecutive key
+            // positions per lane), and splitting Q/K off as C^T tiles measured slower in all
+            // (605 + 241 us against 623 us: two tails and A read twice; profiles/r02n_mfma_util.txt)
+            hipLaunchKernelGGL((k_gemm_256<MODE, 4, false>), dim3(nbm * nbn), dim3(512), 0, s, M, N, K, A, lda, W, ldw, e);
             return;
         }
         if (g_gemm256 == 5)
