@@ -80,6 +80,9 @@ struct whisper_state {
     whisper_vad_context * vad_context = nullptr;
     bool has_vad_segments = false;
     std::vector<std::pair<int64_t, int64_t>> vad_map;
+    // held by a whisper_full / owk_full_batch call that uses this state (its engine and results):
+    // calls on different states of one context run concurrently, as the reference allows
+    std::mutex mu;
 };
 
 struct whisper_context {
@@ -89,7 +92,7 @@ struct whisper_context {
     whisper_state * state = nullptr;
     std::string path_model;
     owk::Prof prof;
-    std::mutex mu;
+    std::mutex mu;  // whisper_full calls while the per-kernel recorder (prof, shared) is on
     whisper_timings timings{};
 };
 

@@ -733,6 +733,12 @@ const char * whisper_print_system_info(void) {
 int whisper_full_with_state(struct whisper_context * ctx, struct whisper_state * state, struct whisper_full_params params,
                             const float * samples, int n_samples) {
     try {
+        if (!state) throw std::runtime_error("null state");
+        // this state only (other states of the context may run concurrently); the context lock
+        // while the shared per-kernel recorder is on
+        std::unique_lock<std::mutex> ctx_lock(ctx->mu, std::defer_lock);
+        if (ctx->prof.on) ctx_lock.lock();
+        std::lock_guard<std::mutex> lk(state->mu);
         return full_batch(ctx, &state, &params, nullptr, &samples, &n_samples, 1);
     } catch (const std::exception & e) {
         log_msg(GGML_LOG_LEVEL_ERROR, "whisper_full_with_state: %s\n", e.what());
@@ -984,7 +990,16 @@ void whisper_log_set(ggml_log_callback log_callback, void * user_data) { set_log
 // ---------------------------------------------------------------------------------
 int owk_full_batch(struct whisper_context * ctx, struct whisper_state ** states, struct whisper_full_params params,
                    const struct owk_full_ext * ext, const float * const * samples, const int * n_samples, int n_clips) {
-    std::lock_guard<std::mutex> lk(ctx->mu);
+    // the states of this call, locked in address order (no lock-order inversion between concurrent
+    // calls); the context lock only while the shared per-kernel recorder is on
+    std::vector<whisper_state *> held(states, states + std::max(n_clips, 0));
+    std::sort(held.begin(), held.end());
+    held.erase(std::unique(held.begin(), held.end()), held.end());
+    std::vector<std::unique_lock<std::mutex>> locks;
+    std::unique_lock<std::mutex> ctx_lock(ctx->mu, std::defer_lock);
+    if (ctx->prof.on) ctx_lock.lock();
+    for (whisper_state * st : held)
+        if (st) locks.emplace_back(st->mu);
     std::vector<whisper_full_params> ps(std::max(n_clips, 1), params);
     // Clip groups on concurrent streams: the clips are independent, so G groups each run the
     // whole stage-major pipeline on their own engine (the engine of the group's first state:

@@ -234,3 +234,34 @@ def test_auto_language(lib, golden, model_path, clips):
         assert lib.whisper_full_lang_id_from_state(st) == meta["results"][f"{model}/jfk/lang_detect"][0]
         _compare(w.segments(st), meta["results"][f"{model}/jfk/full/auto_lang"]["segments"], f"{model}/auto",
                  tie=_tie(w, golden, model, "jfk", clips))
+
+
+def test_concurrent_states(lib, golden, model_path, clips):
+    """whisper_full on two states of ONE context from two host threads at once (the reference
+    allows it, ref include/whisper.h:45-46): each state's result equals the same call run alone."""
+    import threading
+
+    w = whisper(model_path, "tiny.en")
+    p, _ = _cfg_params(w, CONFIGS["greedy"])
+    want = {}
+    for clip in ("jfk", "synth30"):
+        st = w.new_state()
+        assert w.full(st, clips[clip], p) == 0
+        want[clip] = w.segments(st)
+    sts = {clip: w.new_state() for clip in ("jfk", "synth30")}
+    rets = {}
+
+    def run(clip):
+        for _ in range(3):
+            rets[clip] = w.full(sts[clip], clips[clip], p)
+            if rets[clip] != 0:
+                return
+
+    th = [threading.Thread(target=run, args=(c,)) for c in sts]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    for clip, st in sts.items():
+        assert rets[clip] == 0
+        assert w.segments(st) == want[clip], clip
