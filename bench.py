@@ -111,7 +111,7 @@ def phase_fractions(classes, ms_per_step):
     }
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=2)
@@ -121,7 +121,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-prof", action="store_true", help="disable per-class HIP-event timing")
     ap.add_argument("--verbose", action="store_true")
-    return ap.parse_args()
+    return ap.parse_args(argv)
 
 
 def log(*a):
@@ -181,18 +181,116 @@ def max_over_ranks(dt, world):
     return float(t.item())
 
 
-def main():
-    args = parse()
+class GpuRunner:
+    """The measured path: owk_full_batch over this rank's clips, audio resident in HBM. bench's
+    control plane (barriers, timing, max over ranks, the JSON line) drives it through setup /
+    step / sync / tokens_per_clip / profile / cpu_baseline; tests/test_dist_cpu.py drives the
+    same control plane with a CPU stand-in over gloo."""
+
+    def setup(self, args, rank, local, barrier):
+        import numpy as np
+        import torch
+
+        import owk
+        import owk_synth as S
+
+        # synthetic weights of the real architecture (rank 0 writes, the others wait)
+        cache = os.environ.get("OWK_MODEL_CACHE", "/tmp/owk_models")
+        if rank == 0:
+            t = time.perf_counter()
+            model_path = S.ensure_model(args.model, cache_dir=cache)
+            log(f"[bench] model {model_path} ready in {time.perf_counter() - t:.1f} s")
+        barrier()
+        self.model_path = S.ensure_model(args.model, cache_dir=cache)
+
+        torch.cuda.set_device(local)
+        dev = torch.device("cuda", local)
+        L = owk.load()
+        if L.owk_device_ok(local) != 1:
+            raise RuntimeError("libwhisper.so: no usable gfx950 device / code object")
+        owk.quiet()
+        self.w = w = owk.Whisper(self.model_path, device=local)
+        B = args.batch
+        # clips of this rank, resident in HBM for the timed region
+        self.host = [S.synth_audio(CLIP_SAMPLES, seed) for seed in clip_seeds(rank, B)]
+        self.audio = torch.from_numpy(np.stack(self.host)).to(dev).contiguous()
+        self.ptrs = [self.audio[i].data_ptr() for i in range(B)]
+        self.ns = [CLIP_SAMPLES] * B
+        self.states = [w.new_state() for _ in range(B)]
+        self.p = w.params(0, language="en", temperature_inc=0.0, no_timestamps=True, max_tokens=MAX_TOKENS)
+        self.sync()
+
+    def sync(self):
+        import torch
+
+        torch.cuda.synchronize()
+
+    def step(self):
+        ret = self.w.full_batch_device(self.states, self.ptrs, self.ns, self.p, suppress_eot=True)
+        if ret != 0:
+            raise RuntimeError(f"owk_full_batch returned {ret}")
+
+    def events(self, on):
+        # per-launch HIP events on/off (off in the timed region: captured decode graphs)
+        self.w.L.owk_prof_enable(self.w.ctx, 1 if on else 0)
+
+    def tokens_per_clip(self):
+        return [sum(len(s["tokens"]) for s in self.w.segments(st)) for st in self.states]
+
+    def profile(self):
+        """One more step of the same workload with a HIP event pair around every launch on the
+        engine stream (eager launches; events would otherwise split the graphs)."""
+        w = self.w
+        w.L.owk_prof_enable(w.ctx, 1)
+        w.L.owk_prof_reset(w.ctx)
+        self.step()
+        self.sync()
+        classes = {c: w.prof(c) for c in w.prof_classes()}
+        w.L.owk_prof_enable(w.ctx, 0)
+        return classes
+
+    def cpu_baseline(self):
+        base, ref_ids = cpu_baseline(self.model_path, self.host[0])
+        parity = None
+        if ref_ids is not None:
+            gpu_ids = [t[0] for s in self.w.segments(self.states[0]) for t in s["tokens"]]
+            first = next((i for i, (a, b) in enumerate(zip(gpu_ids, ref_ids)) if a != b),
+                         None if len(gpu_ids) == len(ref_ids) else min(len(gpu_ids), len(ref_ids)))
+            parity = {"tokens_equal": gpu_ids == ref_ids, "clip": 0, "n_tokens": len(ref_ids), "first_diff": first,
+                      "against": "cpu_baseline run: the reference ggml CPU path on the same clip, model and parameters"}
+        return base, parity
+
+
+def roofline(classes, ms_per_step):
+    """`roofline` of the class with the largest device time in the profiled step."""
+    dom = max(classes, key=lambda c: classes[c]["ms"])
+    d = classes[dom]
+    avg_ms = d["ms"] / max(1, d["launches"])
+    if dom in MFMA_CLASSES:
+        ach = d["flops"] / (d["ms"] * 1e-3) / 1e12
+        roof = {"bound": "mfma", "achieved": round(ach, 2), "peak": PEAK_F16_TFLOPS, "unit": "TFLOP/s",
+                "frac": round(ach / PEAK_F16_TFLOPS, 4), "traffic": None}
+    else:
+        ach = d["bytes"] / (d["ms"] * 1e-3) / 1e9
+        roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                "frac": round(ach / PEAK_HBM_GBS, 4), "traffic": None}
+    roof["traffic"] = pmc_traffic(dom)
+    roof["traffic_unit"] = "bytes/launch (PMC FETCH_SIZE x2, profiles/pmc_fetch_summary.txt)"
+    roof["kernel_class"] = dom
+    roof["measured"] = "HIP events on the engine stream, one extra profiled step (eager launches)"
+    roof["avg_launch_ms"] = round(avg_ms, 5)
+    roof["launches"] = d["launches"]
+    roof["phases"] = phase_fractions(classes, ms_per_step)
+    return roof
+
+
+def main(argv=None, runner=None):
+    args = parse(argv)
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
     local = int(os.environ.get("LOCAL_RANK", 0))
 
-    import numpy as np
-    import torch
     import torch.distributed as dist
-
-    import owk
-    import owk_synth as S
 
     if world > 1:
         dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -201,92 +299,36 @@ def main():
         if world > 1:
             dist.barrier()
 
-    # synthetic weights of the real architecture (rank 0 writes, the others wait)
-    cache = os.environ.get("OWK_MODEL_CACHE", "/tmp/owk_models")
-    if rank == 0:
-        t = time.perf_counter()
-        model_path = S.ensure_model(args.model, cache_dir=cache)
-        log(f"[bench] model {model_path} ready in {time.perf_counter() - t:.1f} s")
-    barrier()
-    model_path = S.ensure_model(args.model, cache_dir=cache)
-
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    L = owk.load()
-    if L.owk_device_ok(local) != 1:
-        raise RuntimeError("libwhisper.so: no usable gfx950 device / code object")
-    owk.quiet()
-    w = owk.Whisper(model_path, device=local)
+    run = runner if runner is not None else GpuRunner()
+    run.setup(args, rank, local, barrier)
     B = args.batch
-    # clips of this rank, resident in HBM for the timed region
-    host = [S.synth_audio(CLIP_SAMPLES, seed) for seed in clip_seeds(rank, B)]
-    audio = torch.from_numpy(np.stack(host)).to(dev).contiguous()
-    ptrs = [audio[i].data_ptr() for i in range(B)]
-    ns = [CLIP_SAMPLES] * B
-    states = [w.new_state() for _ in range(B)]
-    p = w.params(0, language="en", temperature_inc=0.0, no_timestamps=True, max_tokens=MAX_TOKENS)
-    torch.cuda.synchronize()
-
-    def step():
-        ret = w.full_batch_device(states, ptrs, ns, p, suppress_eot=True)
-        if ret != 0:
-            raise RuntimeError(f"owk_full_batch returned {ret}")
 
     for i in range(args.warmup):
         t = time.perf_counter()
-        step()
+        run.step()
         log(f"[bench] warmup {i}: {time.perf_counter() - t:.3f} s")
 
-    prof = not args.no_prof
-    w.L.owk_prof_enable(w.ctx, 0)  # timed region: captured decode graphs, no per-kernel events
+    run.events(False)  # timed region: captured decode graphs, no per-kernel events
     barrier()
-    torch.cuda.synchronize()
+    run.sync()
     t0 = time.perf_counter()
     for i in range(args.steps):
-        step()
+        run.step()
         if args.verbose:
             log(f"[bench] step {i}: {time.perf_counter() - t0:.3f} s")
-    torch.cuda.synchronize()
+    run.sync()
     barrier()
     dt = max_over_ranks(time.perf_counter() - t0, world)
 
     # every clip must have done the full fixed work (no skipped decoding)
-    ntok = [sum(len(s["tokens"]) for s in w.segments(st)) for st in states]
-    if min(ntok) != MAX_TOKENS + 1:
+    ntok = run.tokens_per_clip()
+    if len(ntok) != B or min(ntok) != MAX_TOKENS + 1:
         raise RuntimeError(f"fixed-work violation: tokens per clip {sorted(set(ntok))}")
 
-    # roofline: one more step of the same workload with a HIP event pair around every
-    # launch on the engine stream (eager launches; events would otherwise split the graphs)
-    classes = {}
-    if prof:
-        w.L.owk_prof_enable(w.ctx, 1)
-        w.L.owk_prof_reset(w.ctx)
-        step()
-        torch.cuda.synchronize()
-        for c in w.prof_classes():
-            classes[c] = w.prof(c)
-        w.L.owk_prof_enable(w.ctx, 0)
     roof = None
+    classes = run.profile() if not args.no_prof else {}
     if classes:
-        dom = max(classes, key=lambda c: classes[c]["ms"])
-        d = classes[dom]
-        avg_ms = d["ms"] / max(1, d["launches"])
-        mfma = dom in MFMA_CLASSES
-        if mfma:
-            ach = d["flops"] / (d["ms"] * 1e-3) / 1e12
-            roof = {"bound": "mfma", "achieved": round(ach, 2), "peak": PEAK_F16_TFLOPS, "unit": "TFLOP/s",
-                    "frac": round(ach / PEAK_F16_TFLOPS, 4), "traffic": None}
-        else:
-            ach = d["bytes"] / (d["ms"] * 1e-3) / 1e9
-            roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                    "frac": round(ach / PEAK_HBM_GBS, 4), "traffic": None}
-        roof["traffic"] = pmc_traffic(dom)
-        roof["traffic_unit"] = "bytes/launch (PMC FETCH_SIZE x2, profiles/pmc_fetch_summary.txt)"
-        roof["kernel_class"] = dom
-        roof["measured"] = "HIP events on the engine stream, one extra profiled step (eager launches)"
-        roof["avg_launch_ms"] = round(avg_ms, 5)
-        roof["launches"] = d["launches"]
-        roof["phases"] = phase_fractions(classes, 1e3 * dt / args.steps)
+        roof = roofline(classes, 1e3 * dt / args.steps)
         if rank == 0:
             tot = sum(v["ms"] for v in classes.values())
             for c, v in sorted(classes.items(), key=lambda kv: -kv[1]["ms"]):
@@ -320,22 +362,14 @@ def main():
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
-            base, ref_ids = cpu_baseline(model_path, host[0])
-            out["cpu_baseline"] = base
-            if ref_ids is not None:
-                gpu_ids = [t[0] for s in w.segments(states[0]) for t in s["tokens"]]
-                first = next((i for i, (a, b) in enumerate(zip(gpu_ids, ref_ids)) if a != b),
-                             None if len(gpu_ids) == len(ref_ids) else min(len(gpu_ids), len(ref_ids)))
-                out["parity"] = {"tokens_equal": gpu_ids == ref_ids, "clip": 0, "n_tokens": len(ref_ids),
-                                 "first_diff": first,
-                                 "against": "cpu_baseline run: the reference ggml CPU path on the same clip, "
-                                            "model and parameters"}
+            out["cpu_baseline"], out["parity"] = run.cpu_baseline()
         except Exception as e:  # report, never hide the GPU number
             log(f"[bench] cpu baseline failed: {e}")
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    return out
 
 
 if __name__ == "__main__":
