@@ -364,6 +364,7 @@ void attn_encoder(hipStream_t s, const _Float16 * q, const _Float16 * k, const _
 constexpr int AS_KC = 64;       // keys per chunk
 constexpr int AS_NBUF = 3;      // chunks in flight
 constexpr int AS_TILE = AS_KC * 128;
+constexpr int AS_RLB = 16;      // keys per readlane batch in the recurrence
 
 // inclusive max-scan over the 64 lanes (DPP: row_shr 1/2/4/8, then row_bcast 15/31)
 #define OWK_DPP_MAX(v, ctrl, rmask, bmask)                                                                       \
@@ -493,9 +494,12 @@ __global__ __launch_bounds__(64) void k_attn_step(const _Float16 * __restrict__ 
         {
             const char * kr = sK + lane * 128;
             float part[8];
+            half8 krow[8];  // the whole key row first: one LDS round trip, not four
+#pragma unroll
+            for (int cc = 0; cc < 8; ++cc) krow[cc] = *(const half8 *) (kr + ((cc ^ (lane & 7)) << 4));
 #pragma unroll
             for (int cc = 0; cc < 8; ++cc) {
-                const half8 kv = *(const half8 *) (kr + ((cc ^ (lane & 7)) << 4));
+                const half8 kv = krow[cc];
                 float a = 0.0f;
 #pragma unroll
                 for (int e = 0; e < 8; e += 2) {
@@ -516,16 +520,15 @@ __global__ __launch_bounds__(64) void k_attn_step(const _Float16 * __restrict__ 
         const float vs = nm ? 1.0f : e;
         M = fmaxf(M, __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, pm), 63)));
 
-        // 3. recurrence, lane = head dim. A full chunk's V column goes to registers first, so
+        // 3. recurrence, lane = head dim. The chunk's V column goes to registers first, so
         // the chunk's buffer is refilled (chunk c + AS_NBUF) before the sequential part runs:
-        // AS_NBUF chunks stay in flight across it
+        // AS_NBUF chunks stay in flight across it (rows nk.. of a partial chunk hold the
+        // clamped key n-1 and are read but not used)
         const _Float16 * vcol = (const _Float16 *) sV + lane;
         const bool full = nk == AS_KC;
         _Float16 vv[AS_KC];
-        if (full) {
 #pragma unroll
-            for (int kk = 0; kk < AS_KC; ++kk) vv[kk] = vcol[kk * 64];
-        }
+        for (int kk = 0; kk < AS_KC; ++kk) vv[kk] = vcol[kk * 64];
         if (c + AS_NBUF < nchunks) {
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // K and V reads of this buffer done
             stage(c % AS_NBUF, c + AS_NBUF);
@@ -533,31 +536,56 @@ __global__ __launch_bounds__(64) void k_attn_step(const _Float16 * __restrict__ 
         if (full && __builtin_amdgcn_ballot_w64(nm) == 0) {
             // no new maximum in the chunk (the common case once the first keys are seen):
             // every ms is 1, so acc*ms and S*ms are exact and each key costs one mixed FMA on
-            // acc and one add on S (vs broadcast by readlane)
+            // acc and one add on S (vs broadcast by readlane, 16 keys' worth into scalar registers
+            // at a time so the readlane -> VALU hazard wait is paid once per batch, not per key)
 #pragma unroll
-            for (int kk = 0; kk < AS_KC; ++kk) {
-                const float vsk = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, vs), kk));
-                acc = (_Float16) fmaf((float) vv[kk], vsk, (float) acc);
-                S = S + vsk;
+            for (int kb = 0; kb < AS_KC; kb += AS_RLB) {
+                float vsb[AS_RLB];
+#pragma unroll
+                for (int j = 0; j < AS_RLB; ++j)
+                    vsb[j] = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, vs), kb + j));
+#pragma unroll
+                for (int j = 0; j < AS_RLB; ++j) {
+                    acc = (_Float16) fmaf((float) vv[kb + j], vsb[j], (float) acc);
+                    S = S + vsb[j];
+                }
             }
         } else if (full) {
             // acc*ms with ms == 1 is exact, so the rescale is applied unconditionally (branch-free)
             // and each key costs two dependent mixed-precision FMAs (f32 math, f16 result)
 #pragma unroll
-            for (int kk = 0; kk < AS_KC; ++kk) {
-                const float msk = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, ms), kk));
-                const float vsk = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, vs), kk));
-                acc = (_Float16) ((float) acc * msk);
-                acc = (_Float16) fmaf((float) vv[kk], vsk, (float) acc);
-                S = fmaf(S, msk, vsk);
+            for (int kb = 0; kb < AS_KC; kb += AS_RLB / 2) {
+                float msb[AS_RLB / 2], vsb[AS_RLB / 2];
+#pragma unroll
+                for (int j = 0; j < AS_RLB / 2; ++j) {
+                    msb[j] = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, ms), kb + j));
+                    vsb[j] = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, vs), kb + j));
+                }
+#pragma unroll
+                for (int j = 0; j < AS_RLB / 2; ++j) {
+                    acc = (_Float16) ((float) acc * msb[j]);
+                    acc = (_Float16) fmaf((float) vv[kb + j], vsb[j], (float) acc);
+                    S = fmaf(S, msb[j], vsb[j]);
+                }
             }
-        } else {  // the last, partial chunk (nothing staged after it)
-            for (int kk = 0; kk < nk; ++kk) {
-                const float msk = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, ms), kk));
-                const float vsk = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, vs), kk));
-                acc = (_Float16) ((float) acc * msk);
-                acc = (_Float16) fmaf((float) vcol[kk * 64], vsk, (float) acc);
-                S = fmaf(S, msk, vsk);
+        } else {  // the last, partial chunk (nothing staged after it); keys nk.. are skipped
+#pragma unroll
+            for (int kb = 0; kb < AS_KC; kb += AS_RLB / 2) {
+                if (kb >= nk) break;
+                float msb[AS_RLB / 2], vsb[AS_RLB / 2];
+#pragma unroll
+                for (int j = 0; j < AS_RLB / 2; ++j) {
+                    msb[j] = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, ms), kb + j));
+                    vsb[j] = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, vs), kb + j));
+                }
+#pragma unroll
+                for (int j = 0; j < AS_RLB / 2; ++j) {
+                    if (kb + j < nk) {
+                        acc = (_Float16) ((float) acc * msb[j]);
+                        acc = (_Float16) fmaf((float) vv[kb + j], vsb[j], (float) acc);
+                        S = fmaf(S, msb[j], vsb[j]);
+                    }
+                }
             }
         }
     }
