@@ -100,10 +100,18 @@ def run_sequential(args, w, sf, pcm, n):
     w.full(warm, pcm[:CHUNK], p)  # warm-up: code objects, buffers, batch-1 graphs
     w.free_state(warm)
     st = w.new_state()
+    if args.prof:
+        w.L.owk_prof_enable(w.ctx, 1)
+        w.L.owk_prof_reset(w.ctx)
     t0 = time.perf_counter()
     ret = w.full(st, pcm, p)
     t_asr = time.perf_counter() - t0
     assert ret == 0, ret
+    if args.prof:
+        tot = {c: w.prof(c) for c in w.prof_classes()}
+        for c, v in sorted(tot.items(), key=lambda kv: -kv[1]["ms"]):
+            print(f"[prof] {c:20s} {v['ms']:10.2f} ms  launches {v['launches']:8d}", file=sys.stderr, flush=True)
+        w.L.owk_prof_enable(w.ctx, 0)
     segs_w = w.segments(st)
     n_tok = sum(len(s["tokens"]) for s in segs_w)
     n_dtw = sum(1 for s in segs_w for t in s["tokens"] if t[8] >= 0)
