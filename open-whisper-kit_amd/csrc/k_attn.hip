@@ -958,17 +958,21 @@ __global__ __launch_bounds__(256) void k_attn_decoder(const _Float16 * __restric
 // ----------------------------------------------------------------------------------
 constexpr int SM_MAX_KEYS = 2048;
 
-__global__ __launch_bounds__(256) void k_attn_softmax(const _Float16 * __restrict__ q, int ldq,
+// NT threads per block: 256, or 1024 when the pass has few (row, head) blocks (one row per step:
+// 20 blocks on 256 CUs) so each block keeps 4x the loads in flight
+template <int NT>
+__global__ __launch_bounds__(NT) void k_attn_softmax(const _Float16 * __restrict__ q, int ldq,
                                                       const _Float16 * __restrict__ kb, const _Float16 * __restrict__ vb,
                                                       int ld_kv, int hs, const AttnRow * __restrict__ rows,
                                                       const int * __restrict__ key_idx, float scale,
                                                       _Float16 * __restrict__ out, int ldo,
                                                       const int * __restrict__ amap, float * __restrict__ cap,
                                                       int cap_rows, float * __restrict__ out32) {
-    __shared__ float sp[SM_MAX_KEYS];
+    constexpr int NW = NT / 64, NG = NT / 8;  // waves; P . V key groups
+    __shared__ float sp[SM_MAX_KEYS > NG * 64 ? SM_MAX_KEYS : NG * 64];
     __shared__ _Float16 p16[SM_MAX_KEYS];
-    __shared__ float redf[4];
-    __shared__ double redd[4];
+    __shared__ float redf[NW];
+    __shared__ double redd[NW];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const AttnRow job = rows[blockIdx.y];
     if (job.mode != 2) return;
@@ -982,7 +986,7 @@ __global__ __launch_bounds__(256) void k_attn_softmax(const _Float16 * __restric
     // scores (lane = key; iterations unrolled so several keys' loads are in flight)
     float mx = -INFINITY;
 #pragma unroll 3
-    for (int i = tid; i < n; i += 256) {
+    for (int i = tid; i < n; i += NT) {
         const int cell = list ? list[i] : i;
         const half8 * kr = (const half8 *) (kh + (size_t) cell * ld_kv);
         float part[8];
@@ -1003,10 +1007,12 @@ __global__ __launch_bounds__(256) void k_attn_softmax(const _Float16 * __restric
     for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
     if (lane == 0) redf[wave] = mx;
     __syncthreads();
-    mx = fmaxf(fmaxf(redf[0], redf[1]), fmaxf(redf[2], redf[3]));
+    mx = redf[0];
+#pragma unroll
+    for (int w = 1; w < NW; ++w) mx = fmaxf(mx, redf[w]);
     // exp and the double-accumulated sum
     double sum = 0.0;
-    for (int i = tid; i < n; i += 256) {
+    for (int i = tid; i < n; i += NT) {
         const float e = expf(sp[i] - mx);
         sp[i] = e;
         sum += (double) e;
@@ -1015,10 +1021,15 @@ __global__ __launch_bounds__(256) void k_attn_softmax(const _Float16 * __restric
     for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o, 64);
     if (lane == 0) redd[wave] = sum;
     __syncthreads();
-    sum = (redd[0] + redd[1]) + (redd[2] + redd[3]);
+    if (NW == 4) {
+        sum = (redd[0] + redd[1]) + (redd[2] + redd[3]);
+    } else {
+        sum = redd[0];
+        for (int w = 1; w < NW; ++w) sum += redd[w];
+    }
     const float inv = (float) (1.0 / sum);
     const int a = amap ? amap[h] : -1;
-    for (int i = tid; i < n; i += 256) {
+    for (int i = tid; i < n; i += NT) {
         const float p = sp[i] * inv;
         p16[i] = (_Float16) p;
         if (a >= 0) cap[((size_t) a * n + i) * cap_rows + job.q_row] = p;
@@ -1029,15 +1040,15 @@ __global__ __launch_bounds__(256) void k_attn_softmax(const _Float16 * __restric
     // the 32 key-group partials are summed in fixed order through LDS
     const int kg = tid >> 3, seg = tid & 7;
     float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    for (int i0 = kg; i0 < n; i0 += 32 * 8) {
+    for (int i0 = kg; i0 < n; i0 += NG * 8) {
         half8 vv[8];
         float pp[8];
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
-            const int i = min(i0 + 32 * u, n - 1);
+            const int i = min(i0 + NG * u, n - 1);
             const int cell = list ? list[i] : i;
             vv[u] = *(const half8 *) (vh + (size_t) cell * ld_kv + seg * 8);
-            pp[u] = i0 + 32 * u < n ? (float) p16[i] : 0.0f;
+            pp[u] = i0 + NG * u < n ? (float) p16[i] : 0.0f;
         }
 #pragma unroll
         for (int u = 0; u < 8; ++u)
@@ -1050,7 +1061,7 @@ __global__ __launch_bounds__(256) void k_attn_softmax(const _Float16 * __restric
     __syncthreads();
     if (wave == 0) {
         float r = 0.0f;
-        for (int g = 0; g < 32; ++g) r += red[g * 64 + lane];
+        for (int g = 0; g < NG; ++g) r += red[g * 64 + lane];
         if (out32) out32[(size_t) job.q_row * ldo + h * 64 + lane] = r;
         else out[(size_t) job.q_row * ldo + h * 64 + lane] = (_Float16) r;
     }
@@ -1062,8 +1073,16 @@ void attn_decoder_softmax(hipStream_t s, const _Float16 * q, int ldq, const _Flo
                           float * out32) {
     if (n_rows <= 0) return;
     if (max_keys > SM_MAX_KEYS) throw std::runtime_error("attn_decoder_softmax: too many keys");
-    hipLaunchKernelGGL(k_attn_softmax, dim3(H, n_rows), dim3(256), 0, s, q, ldq, kbase, vbase, ld_kv, hs, rows_dev, key_idx,
-                       scale, out, ldo, amap, cap, cap_rows, out32);
+    static const bool wide_ok = [] {
+        const char * v = getenv("OWK_SM_WIDE");
+        return !(v && atoi(v) == 0);
+    }();
+    if (wide_ok && n_rows * H <= 128)
+        hipLaunchKernelGGL(k_attn_softmax<1024>, dim3(H, n_rows), dim3(1024), 0, s, q, ldq, kbase, vbase, ld_kv, hs, rows_dev,
+                           key_idx, scale, out, ldo, amap, cap, cap_rows, out32);
+    else
+        hipLaunchKernelGGL(k_attn_softmax<256>, dim3(H, n_rows), dim3(256), 0, s, q, ldq, kbase, vbase, ld_kv, hs, rows_dev,
+                           key_idx, scale, out, ldo, amap, cap, cap_rows, out32);
 }
 
 int attn_max_listed_keys() { return AS_MAX_LIST; }
