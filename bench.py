@@ -19,9 +19,12 @@ per clip (the n_text_ctx/2 - 4 decode-step ceiling of whisper_full, ref whisper.
 fixed work, identical on the CPU reference.
 
 Timed region: decoder passes replay captured HIP graphs (no per-kernel instrumentation).
-Roofline: one extra step of the same workload runs with a HIP event pair around every launch on
-the engine stream (owk_prof_*); `roofline` reports the class with the largest device time. The
-rocprofv3 summary of the same command is committed under profiles/.
+Roofline: one extra step of the same workload with owk_prof_enable(2): the decoder passes replay
+their captured graphs with a HIP event pair captured around every kernel-class launch (event-record
+nodes on the engine stream, read back after each replay), the encoder launches carry event pairs
+directly. `roofline` reports the class with the largest device time, its average launch time and
+the same kernel's average from the committed rocprofv3 --kernel-trace --stats summary of this
+command (profiles/, ROCPROF_STATS) for the cross-check.
 
 cpu_baseline: the reference ggml CPU path (oracle/_ref/libwhisper_ref.so, compiled from the
 reference sources by oracle/ref/Makefile) runs ONE clip of the same workload on this host's
@@ -48,7 +51,7 @@ MAX_TOKENS = 219          # completion at i >= max_tokens -> 220 tokens per clip
 # kernels of each class (mangled-name patterns, for the PMC traffic lookup): the decode-row GEMM
 # epilogue 7 (EPI_F32) is the logits matmul, every other decode-row launch is gemm_dec
 CLASS_KERNELS = {
-    "attn_cross": r"k_attn_cross2|k_attn_stepILb0ELb1E",
+    "attn_cross": r"k_attn_stepILb0ELb1E",
     "attn_self": r"k_attn_stepILb[01]ELb0E",
     "attn_encoder": r"k_attn_encoderE",
     "gemm_dec": r"k_gemm_rowsILi(?!7E)\d+E|k_gemm_rows_reduceILi(?!7E)\d+E",
@@ -57,6 +60,14 @@ CLASS_KERNELS = {
     "gemm_enc": r"k_gemm_256|k_gemm_bigILi[0-6]E",
 }
 PMC_SUMMARY = os.path.join(ROOT, "profiles", "pmc_fetch_summary.txt")
+# rocprofv3 --kernel-trace --stats summary of `python bench.py` on this tree (tools/gpu_round.sh ->
+# tools/prof_summary.py), committed per round
+ROCPROF_STATS = os.path.join(ROOT, "profiles", "r03_bench_kernel_stats.txt")
+# human-readable kernel of each class (the mangled names CLASS_KERNELS matches)
+CLASS_KERNEL_NAME = {"attn_cross": "owk::k_attn_step<false, true> (one_chunk cross attention, k_attn.hip)",
+                     "attn_self": "owk::k_attn_step<*, false>", "gemm_dec": "owk::k_gemm_rows<mode, MT, J>",
+                     "gemm_enc": "owk::k_gemm_256<mode, 4, swap>", "attn_encoder": "owk::k_attn_encoder",
+                     "layernorm": "owk::k_resid_layernorm / k_layernorm_f16", "gemm_logits": "owk::k_gemm_rows<7, MT, J>"}
 
 
 def pmc_traffic(cls):
@@ -76,6 +87,24 @@ def pmc_traffic(cls):
             n += int(parts[0])
             tot += float(parts[2])
     return round(tot / n * 1024 * 2) if n else None
+
+
+def rocprof_avg_ms(cls, path=None):
+    """Average launch duration (ms) of the class's kernels in the committed rocprofv3 stats summary
+    (calls-weighted over the matching kernels), or None."""
+    import re
+
+    path = path or ROCPROF_STATS
+    pat = CLASS_KERNELS.get(cls)
+    if not pat or not os.path.exists(path):
+        return None
+    tot, n = 0.0, 0
+    for line in open(path):
+        parts = line.split(None, 6)
+        if len(parts) == 7 and parts[0].isdigit() and re.search(pat, parts[6]):
+            n += int(parts[0])
+            tot += float(parts[1])
+    return round(tot / n / 1e3, 5) if n else None
 
 
 # the arithmetic each weight format computes in (kernels.h; DESIGN.md 2)
@@ -238,10 +267,10 @@ class GpuRunner:
         return [sum(len(s["tokens"]) for s in self.w.segments(st)) for st in self.states]
 
     def profile(self):
-        """One more step of the same workload with a HIP event pair around every launch on the
-        engine stream (eager launches; events would otherwise split the graphs)."""
+        """One more step of the same workload, decoder passes replaying their captured graphs with
+        a HIP event pair captured around every kernel-class launch (owk_prof_enable mode 2)."""
         w = self.w
-        w.L.owk_prof_enable(w.ctx, 1)
+        w.L.owk_prof_enable(w.ctx, 2)
         w.L.owk_prof_reset(w.ctx)
         self.step()
         self.sync()
@@ -277,9 +306,15 @@ def roofline(classes, ms_per_step):
     roof["traffic"] = pmc_traffic(dom)
     roof["traffic_unit"] = "bytes/launch (PMC FETCH_SIZE x2, profiles/pmc_fetch_summary.txt)"
     roof["kernel_class"] = dom
-    roof["measured"] = "HIP events on the engine stream, one extra profiled step (eager launches)"
+    roof["kernel"] = CLASS_KERNEL_NAME.get(dom, dom)
+    roof["measured"] = ("HIP events on the engine stream, one extra step: event pairs captured into the decode "
+                        "hipGraphs around each launch and read after every replay (owk_prof_enable 2)")
     roof["avg_launch_ms"] = round(avg_ms, 5)
     roof["launches"] = d["launches"]
+    rp = rocprof_avg_ms(dom)
+    roof["rocprof_avg_launch_ms"] = rp
+    roof["rocprof_stats"] = os.path.relpath(ROCPROF_STATS, ROOT) if rp is not None else None
+    roof["events_vs_rocprof"] = round(avg_ms / rp, 4) if rp else None
     roof["phases"] = phase_fractions(classes, ms_per_step)
     return roof
 

@@ -45,7 +45,11 @@ WHISPER_API int owk_vad_detect_batch(struct whisper_vad_context * vctx, const fl
 WHISPER_API int owk_vad_segments_raw(const float * probs, int n_probs, int n_window, struct whisper_vad_params params,
                                      int64_t * out_cs, int cap);
 
-/* per-kernel-class device timing with HIP events recorded on the engine stream */
+/* per-kernel-class device timing with HIP events recorded on the engine stream.
+ * enable = 1: eager launches with an event pair around each kernel-class launch;
+ * enable = 2: decoder passes replay their captured hipGraphs with the event pairs captured into
+ * the graph (event-record nodes around each launch), read back after every replay -- the timing
+ * of the production path without eager launch gaps; 0: off */
 WHISPER_API void owk_prof_enable(struct whisper_context * ctx, int enable);
 WHISPER_API void owk_prof_reset(struct whisper_context * ctx);
 /* total device milliseconds and launch count of one kernel class since reset;
@@ -86,8 +90,7 @@ WHISPER_API int owk_debug_gemm_q5(int device, int M, int N, int K, const float *
  * of that type; Q4_1 / Q5_1 take Q8_1 activations); d_out receives the raw f32 activation scales */
 WHISPER_API int owk_debug_gemm_quant(int device, int fmt, int M, int N, int K, const float * a, const uint8_t * w_blocks,
                                      float * out, int8_t * q_out, float * d_out);
-// use_q16 = 1: the large-tile encoder path (expanded f16 integers, gemm_q16; M >= 2048, symmetric formats);
-// 2: the decode-row path on f16 activation rows quantized inside the GEMM (M <= 32; out = the summed split-K partials)
+// use_q16 = 1: the large-tile encoder path (expanded f16 integers, gemm_q16; M >= 2048, symmetric formats)
 WHISPER_API int owk_debug_gemm_quant2(int device, int fmt, int M, int N, int K, const float * a, const uint8_t * w_blocks,
                                       float * out, int8_t * q_out, float * d_out, int use_q16);
 /* mode | 0x100: force the 128x128 large-GEMM kernel; | 0x400: 5-slot ring variant of the 256x256 kernel;

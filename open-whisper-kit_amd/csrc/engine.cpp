@@ -39,8 +39,10 @@ void Prof::flush() {
         t.flops += r.flops;
         t.bytes += r.bytes;
         t.n += 1;
-        pool.push_back(r.a);
-        pool.push_back(r.b);
+        if (!r.graph_owned) {
+            pool.push_back(r.a);
+            pool.push_back(r.b);
+        }
     }
     pending.clear();
 }
@@ -52,6 +54,7 @@ void Prof::reset() {
 
 Prof::~Prof() {
     for (auto & r : pending) {
+        if (r.graph_owned) continue;  // destroyed with their graph
         (void) hipEventDestroy(r.a);
         (void) hipEventDestroy(r.b);
     }
@@ -70,6 +73,10 @@ ProfScope::~ProfScope() {
     if (cls < 0) return;
     hipEvent_t b = p->ev();
     (void) hipEventRecord(b, s);
+    if (p->capturing) {  // recorded into the graph being captured; read after each replay
+        p->cap_recs.push_back({cls, a, b, flops, bytes, true});
+        return;
+    }
     p->pending.push_back({cls, a, b, flops, bytes});
     if (p->pending.size() > 4096) p->flush();
 }
@@ -90,22 +97,12 @@ Engine::Engine(const Model * m_, Prof * prof_) : m(m_), prof(prof_) {
     gws_part_.alloc(std::max<size_t>(fl, 1) * 4);
     gws_.partial = gws_part_.as<float>();
     gws_.partial_floats = fl;
-    // the second decode row group (OWK_DEC_SPLIT): its own stream and split-K workspace
-    OWK_HIP_CHECK(hipStreamCreateWithFlags(&stream2_, hipStreamNonBlocking));
-    OWK_HIP_CHECK(hipEventCreateWithFlags(&ev_fork_, hipEventDisableTiming));
-    OWK_HIP_CHECK(hipEventCreateWithFlags(&ev_join_, hipEventDisableTiming));
-    gws2_part_.alloc(std::max<size_t>(fl, 1) * 4);
-    gws2_.partial = gws2_part_.as<float>();
-    gws2_.partial_floats = fl;
 }
 
 Engine::~Engine() {
     clear_graphs();
     for (auto * b : mel_) delete b;
     if (stream) (void) hipStreamDestroy(stream);
-    if (stream2_) (void) hipStreamDestroy(stream2_);
-    if (ev_fork_) (void) hipEventDestroy(ev_fork_);
-    if (ev_join_) (void) hipEventDestroy(ev_join_);
 }
 
 void Engine::sync() { OWK_HIP_CHECK(hipStreamSynchronize(stream)); }
@@ -449,7 +446,14 @@ void Engine::stage_layout(int C, int KC) {
 }
 
 void Engine::clear_graphs() {
-    for (auto & kv : graphs_) (void) hipGraphExecDestroy(kv.second);
+    if (prof && !graphs_.empty()) prof->flush();  // no pending record may name a destroyed event
+    for (auto & kv : graphs_) {
+        (void) hipGraphExecDestroy(kv.second.ex);
+        for (auto & r : kv.second.recs) {
+            (void) hipEventDestroy(r.a);
+            (void) hipEventDestroy(r.b);
+        }
+    }
     graphs_.clear();
 }
 
@@ -457,8 +461,7 @@ uint64_t Engine::buffers_signature() const {
     uint64_t h = 1469598103934665603ull;
     for (const void * p : {d_x_.ptr, d_xn_.ptr, d_q_.ptr, d_ao_.ptr, d_h_.ptr, d_xl_.ptr, logits_.ptr, d_stg_.ptr,
                            q8a_.ptr, q8d_.ptr, d_xn32_.ptr, d_ao32_.ptr, d_xl32_.ptr,
-                           self_k_.ptr, self_v_.ptr, cross_k_.ptr, cross_v_.ptr, gws_part_.ptr, gws2_part_.ptr,
-                           ln_stats_.ptr})
+                           self_k_.ptr, self_v_.ptr, cross_k_.ptr, cross_v_.ptr, gws_part_.ptr})
         h = (h ^ (uint64_t) (uintptr_t) p) * 1099511628211ull;
     return h;
 }
@@ -499,7 +502,6 @@ void Engine::decode(const std::vector<DecodeRow> & rows, const std::vector<int> 
             const int C = dec_rows_cap_;
             d_x_.alloc((size_t) C * d * 4);
             d_xn_.alloc((size_t) C * d * 2);
-            ln_stats_.alloc((size_t) (d / 16) * 32 * 16 * 2);  // two row groups of <= 32 rows (OWK_DEC_SPLIT)
             d_q_.alloc((size_t) C * d * 2);
             d_ao_.alloc((size_t) C * d * 2);
             d_h_.alloc((size_t) C * 4 * d * 2);
@@ -574,15 +576,17 @@ void Engine::decode(const std::vector<DecodeRow> & rows, const std::vector<int> 
         sh.capture = true;
     }
     static const bool no_graph = getenv("OWK_NO_GRAPH") && atoi(getenv("OWK_NO_GRAPH")) != 0;
-    if ((prof && prof->on) || no_graph || capture) {  // per-kernel events, debugging, DTW: eager launches
+    const int pm = prof && prof->on ? prof->mode : 0;
+    if (pm == 1 || no_graph || capture) {  // eager per-kernel events, debugging, DTW: eager launches
         launch_decode(sh);
         return;
     }
     // replay a captured graph of the whole decoder pass (one launch instead of ~10 per layer)
     const uint64_t sig = buffers_signature();
-    if (sig != graphs_sig_) {
+    if (sig != graphs_sig_ || pm != graphs_prof_) {
         clear_graphs();
         graphs_sig_ = sig;
+        graphs_prof_ = pm;
     }
     const uint64_t key = (uint64_t) R | ((uint64_t) n_logit_rows << 20) | ((uint64_t) sh.self_oc << 40) |
                          ((uint64_t) sh.self_tl << 41) | ((uint64_t) sh.cross_oc << 42) | ((uint64_t) sh.cross_tl << 43) |
@@ -592,22 +596,34 @@ void Engine::decode(const std::vector<DecodeRow> & rows, const std::vector<int> 
     if (it == graphs_.end()) {
         if (graphs_.size() >= 64) clear_graphs();
         hipGraph_t g = nullptr;
+        GraphEntry ge;
         OWK_HIP_CHECK(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal));
+        if (pm) {
+            prof->capturing = true;
+            prof->cap_recs.clear();
+        }
         try {
             launch_decode(sh);
         } catch (...) {
+            if (pm) prof->capturing = false;
             (void) hipStreamEndCapture(stream, &g);
             if (g) (void) hipGraphDestroy(g);
             throw;
         }
+        if (pm) {
+            prof->capturing = false;
+            ge.recs.swap(prof->cap_recs);
+        }
         OWK_HIP_CHECK(hipStreamEndCapture(stream, &g));
-        hipGraphExec_t ex = nullptr;
-        const hipError_t e = hipGraphInstantiate(&ex, g, nullptr, nullptr, 0);
+        const hipError_t e = hipGraphInstantiate(&ge.ex, g, nullptr, nullptr, 0);
         (void) hipGraphDestroy(g);
         OWK_HIP_CHECK(e);
-        it = graphs_.emplace(key, ex).first;
+        it = graphs_.emplace(key, std::move(ge)).first;
     }
-    OWK_HIP_CHECK(hipGraphLaunch(it->second, stream));
+    // prof mode 2: read the previous replay's event pairs before their events are re-recorded
+    if (pm) prof->flush();
+    OWK_HIP_CHECK(hipGraphLaunch(it->second.ex, stream));
+    if (pm) prof->pending.insert(prof->pending.end(), it->second.recs.begin(), it->second.recs.end());
 }
 
 void Engine::launch_decode(const DecShape & sh) {
@@ -650,78 +666,34 @@ void Engine::launch_decode(const DecShape & sh) {
     const float kq_scale = powf(64.0f, -0.25f);
     const size_t self_stride = (size_t) cap_slots * kv_cells * d;
     const size_t cross_stride = (size_t) cap_slots * hp.n_audio_ctx * d;  // per layer (capacity)
-    // R <= 32 rows (F16 weights): the decoder's LayerNorms ride on the matmuls around them.
-    //  * attn.out / cross_attn.out (K = d): EPI_RESID_STATS adds bias + residual in the epilogue and
-    //    leaves per (16-column tile, row) statistics of the updated row; the next matmul (cross Q,
-    //    mlp.0) normalises its A operand from them (AlnParams) -- no LayerNorm launch;
-    //  * mlp.2 (K = 4d: long, so split over k): partial tiles, then one kernel adds them with bias +
-    //    residual and writes the next layer's attn_ln output (resid_layernorm).
-    // Plans (OWK_DEC_PLAN): 0 (default) partial tiles + resid_layernorm after all three residual
-    // matmuls; 1 the above (LayerNorm-operand GEMMs for cross Q and mlp.0); 2 statistics after all
-    // three (self Q/K/V normalises too). Measured on large-v3 x 32 clips (profiles/r02e_ab.txt): RTF
-    // 923 / 846 / 806 -- the LayerNorm-operand GEMMs (12 and 23 us) cost more than the LayerNorm
-    // launches they replace. Larger passes use the full-epilogue GEMMs and separate LayerNorms.
-    static const int plan_env = [] {
-        const char * v = getenv("OWK_DEC_PLAN");
-        return v && *v ? atoi(v) : 0;
-    }();
-    // two row groups on two streams (OWK_DEC_SPLIT=1): each half runs the whole layer chain for
-    // its rows; one half's latency-bound launches overlap the other's HBM-bound attention. Rows
-    // are independent inside a pass (a row reads only KV cells written before the pass and its
-    // own cell), so the halves share no data until the logits.
-    static const bool split_env = [] {
-        const char * v = getenv("OWK_DEC_SPLIT");
-        return v && atoi(v) != 0;
-    }();
-    // soft_max rows (flash_attn = false) and DTW captures run the soft_max attention launches inside
-    // the fused chain (the capture addresses rows absolutely: no row groups then)
+    // R <= 32 rows (F16 weights): each residual matmul (attn.out, cross_attn.out, mlp.2) writes
+    // split-K partial tiles and resid_layernorm adds them with bias + residual and emits the next
+    // LayerNorm's f16 rows (one launch where a full-epilogue GEMM plus a LayerNorm were). Round 2
+    // measured the alternatives slower and removed them (profiles/r02e_ab.txt: LayerNorm inside
+    // the consumer GEMM 846 RTF, statistics-producing residual GEMMs 806, against 923; two row
+    // groups on two streams 744). soft_max rows (flash_attn = false) and DTW captures run the
+    // soft_max attention launches inside the same chain. Larger passes use the full-epilogue
+    // GEMMs and separate LayerNorms.
     const bool fused = R <= 32 && !q5;
-    const int plan = fused ? plan_env : -1;
 
-    // the fused decoder (R <= 32, F16) over rows [r0, r0 + n) on stream s
-    auto fused_rows = [&](int r0, int n, hipStream_t s, const GemmWs * ws, double * lnst) {
-        float * x = d_x_.as<float>() + (size_t) r0 * d;
-        _Float16 * xn = d_xn_.as<_Float16>() + (size_t) r0 * d;
-        _Float16 * qb = d_q_.as<_Float16>();    // attention addresses rows by AttnRow::q_row (absolute)
+    auto fused_rows = [&]() {
+        hipStream_t s = stream;
+        float * x = d_x_.as<float>();
+        _Float16 * xn = d_xn_.as<_Float16>();
+        _Float16 * qb = d_q_.as<_Float16>();
         _Float16 * aob = d_ao_.as<_Float16>();
-        _Float16 * qr = qb + (size_t) r0 * d;
-        _Float16 * aor = aob + (size_t) r0 * d;
-        _Float16 * hr = d_h_.as<_Float16>() + (size_t) r0 * 4 * d;
-        auto aln_of = [&](const float * w, const float * b) {
-            AlnParams a;
-            a.x = x;
-            a.ldx = d;
-            a.stats = lnst;
-            a.ntiles = d / 16;
-            a.w = w;
-            a.b = b;
-            a.eps = hp.eps;
-            return a;
-        };
+        _Float16 * hr = d_h_.as<_Float16>();
+        const int n = R;
         auto gemm_rows = [&](int mode, int N, int K, const _Float16 * A, const _Float16 * Wt, const EpiParams & ep) {
             ProfScope ps(prof, s, "gemm_dec", 2.0 * n * (double) N * K, 2.0 * ((double) n * K + (double) N * K));
-            gemm(s, mode, n, N, K, A, K, nullptr, K, ep, ws, Wt);
-        };
-        auto gemm_ln = [&](int mode, int N, const _Float16 * Wt, const EpiParams & ep, const AlnParams & aln) {
-            ProfScope ps(prof, s, "gemm_dec", 2.0 * n * (double) N * d, 2.0 * ((double) n * d + (double) N * d));
-            gemm_rows_ln(s, mode, n, N, d, aln, Wt, ep, ws);
-        };
-        // residual matmul, bias + residual in the epilogue, row statistics for the next LayerNorm
-        auto resid_stats = [&](const _Float16 * A, const _Float16 * Wt, int K, const float * bias) {
-            EpiParams ep;
-            ep.bias = bias;
-            ep.resid = x;
-            ep.out32 = x;
-            ep.ldo = d;
-            ep.stats = lnst;
-            gemm_rows(EPI_RESID_STATS, d, K, A, Wt, ep);
+            gemm(s, mode, n, N, K, A, K, nullptr, K, ep, &gws_, Wt);
         };
         // residual matmul as partial tiles + resid_layernorm (lnw null: residual only)
         auto resid_ln = [&](const _Float16 * A, const _Float16 * Wt, int K, const float * bias, const float * lnw,
                             const float * lnb) {
             gemm_rows(EPI_PARTIAL, d, K, A, Wt, EpiParams());
             ProfScope ps(prof, s, "layernorm");
-            resid_layernorm(s, n, d, gemm_partial_splits(K), ws->partial, bias, x, lnw, lnb, hp.eps, xn, d);
+            resid_layernorm(s, n, d, gemm_partial_splits(K), gws_.partial, bias, x, lnw, lnb, hp.eps, xn, d);
         };
         for (int l = 0; l < hp.n_text_layer; ++l) {
             const DecLayerW & L = m->dec[l];
@@ -732,64 +704,55 @@ void Engine::launch_decode(const DecShape & sh) {
                 ep.bias = L.b_q;
                 ep.bias2 = L.b_v;
                 ep.scale = kq_scale;
-                ep.out16 = qr;
+                ep.out16 = qb;
                 ep.ldo = d;
                 ep.out16b = Kl;
                 ep.out16c = Vl;
                 ep.d = d;
-                ep.row_off = d_rowoff + r0;
+                ep.row_off = d_rowoff;
                 ep.Tpad = kv_cells * 64;
-                // the attn_ln output: from the previous layer's resid_layernorm (plans 0, 1; layer 0:
-                // the LayerNorm launch before the row groups) or normalised here (plan 2)
-                if (plan == 2 && l > 0) gemm_ln(EPI_QKV_DEC, 3 * d, L.t_qkv, ep, aln_of(L.attn_ln_w, L.attn_ln_b));
-                else gemm_rows(EPI_QKV_DEC, 3 * d, d, xn, L.t_qkv, ep);
+                // the attn_ln output: the previous layer's resid_layernorm (layer 0: the LayerNorm
+                // launch before the chain)
+                gemm_rows(EPI_QKV_DEC, 3 * d, d, xn, L.t_qkv, ep);
             }
             {
                 ProfScope ps(prof, s, "attn_self");
-                attn_decoder(s, qb, d, Kl, Vl, 64, kv_cells * 64, d_rs + r0, n, d_keys, H, 1.0f, max_keys, aob, d,
+                attn_decoder(s, qb, d, Kl, Vl, 64, kv_cells * 64, d_rs, n, d_keys, H, 1.0f, max_keys, aob, d,
                              self_oc, self_tl, nullptr, sh.self_list, nullptr, nullptr);
                 if (sh.self_sm)  // flash_attn = false rows: masked soft_max (scale 1; Q, K pre-scaled)
-                    attn_decoder_softmax(s, qb, d, Kl, Vl, 64, kv_cells * 64, d_rs + r0, n, d_keys, H, 1.0f, max_keys, aob,
+                    attn_decoder_softmax(s, qb, d, Kl, Vl, 64, kv_cells * 64, d_rs, n, d_keys, H, 1.0f, max_keys, aob,
                                          d, nullptr, nullptr, 0, nullptr);
             }
-            if (plan == 0) resid_ln(aor, L.t_o, d, L.b_o, L.cross_ln_w, L.cross_ln_b);
-            else resid_stats(aor, L.t_o, d, L.b_o);
+            resid_ln(aob, L.t_o, d, L.b_o, L.cross_ln_w, L.cross_ln_b);
             {
                 EpiParams ep;
                 ep.bias = L.cb_q;
-                ep.out16 = qr;
+                ep.out16 = qb;
                 ep.ldo = d;
-                if (plan == 0) gemm_rows(EPI_F16, d, d, xn, L.t_cq, ep);
-                else gemm_ln(EPI_F16, d, L.t_cq, ep, aln_of(L.cross_ln_w, L.cross_ln_b));
+                gemm_rows(EPI_F16, d, d, xn, L.t_cq, ep);
             }
             {
                 ProfScope ps(prof, s, "attn_cross", 4.0 * n * (double) n_ctx_pad * d, 2.0 * 2.0 * n * (double) T * d);
                 attn_decoder(s, qb, d, cross_k_.as<_Float16>() + l * cross_stride, cross_v_.as<_Float16>() + l * cross_stride,
-                             64, T * 64, d_rc + r0, n, nullptr, H, kq_scale, T, aob, d, cross_oc, cross_tl, nullptr, true,
+                             64, T * 64, d_rc, n, nullptr, H, kq_scale, T, aob, d, cross_oc, cross_tl, nullptr, true,
                              nullptr, nullptr);
                 if (sh.cross_sm)  // soft_max_ext over n_audio_ctx keys, DTW capture of the alignment heads
                     attn_decoder_softmax(s, qb, d, cross_k_.as<_Float16>() + l * cross_stride,
-                                         cross_v_.as<_Float16>() + l * cross_stride, 64, T * 64, d_rc + r0, n, nullptr, H,
+                                         cross_v_.as<_Float16>() + l * cross_stride, 64, T * 64, d_rc, n, nullptr, H,
                                          kq_scale, T, aob, d, sh.capture ? amap_.as<int>() + l * H : nullptr,
                                          sh.capture ? cap_.as<float>() : nullptr, R, nullptr);
             }
-            if (plan == 0) resid_ln(aor, L.t_co, d, L.cb_o, L.mlp_ln_w, L.mlp_ln_b);
-            else resid_stats(aor, L.t_co, d, L.cb_o);
+            resid_ln(aob, L.t_co, d, L.cb_o, L.mlp_ln_w, L.mlp_ln_b);
             {
                 EpiParams ep;
                 ep.bias = L.b_mlp0;
                 ep.gelu_tab = m->gelu_tab;
                 ep.out16 = hr;
                 ep.ldo = 4 * d;
-                if (plan == 0) gemm_rows(EPI_GELU_F16, 4 * d, d, xn, L.t_mlp0, ep);
-                else gemm_ln(EPI_GELU_F16, 4 * d, L.t_mlp0, ep, aln_of(L.mlp_ln_w, L.mlp_ln_b));
+                gemm_rows(EPI_GELU_F16, 4 * d, d, xn, L.t_mlp0, ep);
             }
-            if (plan == 2) {
-                resid_stats(hr, L.t_mlp1, 4 * d, L.b_mlp1);
-            } else {
-                const DecLayerW * nx = l + 1 < hp.n_text_layer ? &m->dec[l + 1] : nullptr;
-                resid_ln(hr, L.t_mlp1, 4 * d, L.b_mlp1, nx ? nx->attn_ln_w : nullptr, nx ? nx->attn_ln_b : nullptr);
-            }
+            const DecLayerW * nx = l + 1 < hp.n_text_layer ? &m->dec[l + 1] : nullptr;
+            resid_ln(hr, L.t_mlp1, 4 * d, L.b_mlp1, nx ? nx->attn_ln_w : nullptr, nx ? nx->attn_ln_b : nullptr);
         }
     };
     auto resid_full = [&](const _Float16 * A, const float * A32, const _Float16 * W, const _Float16 * Wt,
@@ -808,19 +771,7 @@ void Engine::launch_decode(const DecShape & sh) {
     };
     if (fused) {
         ln(m->dec[0].attn_ln_w, m->dec[0].attn_ln_b);  // layer 0's attn_ln of the embeddings
-        const bool split = split_env && R >= 16 && !(prof && prof->on) && !sh.self_sm && !sh.cross_sm && !sh.capture;
-        double * lnst = (double *) ln_stats_.ptr;
-        if (!split) {
-            fused_rows(0, R, stream, &gws_, lnst);
-        } else {
-            const int ra = R / 2;
-            OWK_HIP_CHECK(hipEventRecord(ev_fork_, stream));
-            OWK_HIP_CHECK(hipStreamWaitEvent(stream2_, ev_fork_, 0));
-            fused_rows(0, ra, stream, &gws_, lnst);
-            fused_rows(ra, R - ra, stream2_, &gws2_, lnst + (size_t) 2 * (d / 16) * 32);
-            OWK_HIP_CHECK(hipEventRecord(ev_join_, stream2_));
-            OWK_HIP_CHECK(hipStreamWaitEvent(stream, ev_join_, 0));
-        }
+        fused_rows();
     }
     // quantized decode passes of <= 32 rows (the bench's greedy steps): the residual matmuls (attn.out,
     // cross_attn.out, mlp.2) write split-K partial tiles and resid_layernorm adds them to the residual
@@ -832,19 +783,7 @@ void Engine::launch_decode(const DecShape & sh) {
         EpiParams ep;
         ep.out32 = gws_.partial;
         if (gws_.partial_floats < q5_partial_floats(d, K)) throw std::runtime_error("decode: partial workspace");
-        static const bool a16_env = [] {
-            const char * e = getenv("OWK_Q5_A16");
-            return e && atoi(e) != 0;
-        }();
-        if (a16_env && !a_q8 && !A32 && A16) {
-            // opt-in (OWK_Q5_A16=1): f16 activation rows (the GELU outputs) quantized to Q8_0 inside the
-            // GEMM's waves. Measured slower: the separate quantize pass went 84.5 -> 39 ms per step but
-            // mlp.2's decode GEMM 441 -> 495 ms (every column tile re-quantizes the rows; RTF 772 -> 751)
-            ProfScope ps(prof, stream, "gemm_dec", gemm_flops(R, d, K), (double) d * K * qf_block_bytes(q.fmt) / 32.0 + 2.0 * R * K);
-            gemm_q5_rows_a16(stream, R, d, K, A16, q, ep);
-        } else {
-            linear("gemm_dec", EPI_PARTIAL, R, d, K, A16, A32, K, nullptr, q, ep, nullptr, true, a_q8);
-        }
+        linear("gemm_dec", EPI_PARTIAL, R, d, K, A16, A32, K, nullptr, q, ep, nullptr, true, a_q8);
         ProfScope ps(prof, stream, "layernorm");
         resid_layernorm(stream, R, d, q5_partial_splits(K), gws_.partial, bias, d_x_.as<float>(), lnw, lnb, hp.eps,
                         d_xn_.as<_Float16>(), d, lnw ? q8a() : nullptr, lnw ? q8d() : nullptr);

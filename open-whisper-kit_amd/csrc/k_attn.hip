@@ -604,238 +604,6 @@ __global__ __launch_bounds__(64) void k_attn_step(const _Float16 * __restrict__ 
 }
 
 // ----------------------------------------------------------------------------------
-// Cross-attention decode step, two waves per (query row, head), same numerics as
-// k_attn_step (the reference's one_chunk recurrence, F16 V accumulator rounded per key).
-// One wave can keep at most ~63 KB of loads in flight (the vmcnt counter), and the K/V
-// stream of a (row, head) is latency-bound at that depth; splitting the roles doubles it:
-//   wave 0 (scores): K chunks of 64 keys straight to VGPRs (8 x 1 KB coalesced loads per
-//     chunk, XC_KBUF chunks ahead), lane (8i + g) layout -> dot with q over 8 dims per
-//     lane, 8-lane reduction, bpermute to lane = key; running-max scan -> (ms, vs) per key,
-//     published to an LDS ring;
-//   wave 1 (values): V chunks by global_load_lds into an LDS ring (XC_VBUF chunks ahead)
-//     and the sequential per-key recurrence.
-// The waves meet at one s_barrier per chunk (wave 0 one chunk ahead of wave 1); raw
-// barriers with explicit lgkmcnt waits keep both load streams in flight across them.
-// ----------------------------------------------------------------------------------
-constexpr int XC_KBUF = 4;   // K chunks in flight (registers of the score wave)
-constexpr int XC_VBUF = 6;   // V chunks in flight (LDS ring of the value wave)
-constexpr int XC_PBUF = 4;   // (ms, vs, flags) ring between the waves
-constexpr int XC_PREC = 64 * 2 * 4 + 16;  // bytes per ring entry: ms[64], vs[64], nomax flag
-
-__global__ __launch_bounds__(128) void k_attn_cross2(const _Float16 * __restrict__ q, int ldq,
-                                                     const _Float16 * __restrict__ kb, const _Float16 * __restrict__ vb,
-                                                     int hs, const AttnRow * __restrict__ rows, float scale,
-                                                     _Float16 * __restrict__ out, int ldo, float * __restrict__ out32,
-                                                     int8_t * __restrict__ q8, float * __restrict__ q8d) {
-    __shared__ __attribute__((aligned(1024))) char smem[XC_VBUF * AS_TILE + XC_PBUF * XC_PREC + 16];
-    char * vring = smem;
-    char * pring = smem + XC_VBUF * AS_TILE;
-    float * fin = (float *) (pring + XC_PBUF * XC_PREC);  // final running max (score -> value wave)
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const AttnRow job = rows[blockIdx.y];
-    if (job.mode != 0) return;  // block-uniform
-    const int h = blockIdx.x;
-    const int n = job.n_keys;
-    auto emit = [&](float y) {  // value wave: lane = head dim (k_attn_step's epilogue)
-        const size_t o = (size_t) job.q_row * ldo + h * 64 + lane;
-        if (out32) out32[o] = y;
-        else out[o] = (_Float16) y;
-        if (q8) {
-            float m = fabsf(y);
-#pragma unroll
-            for (int sh = 16; sh > 0; sh >>= 1) m = fmaxf(m, __shfl_xor(m, sh, 32));
-            const float id = m != 0.0f ? 127.f / m : 0.0f;
-            q8[o] = (int8_t) rintf(y * id);
-            if ((lane & 31) == 0) q8d[o >> 5] = m / 127.f;  // raw f32 d (kernels.h QFmt)
-        }
-    };
-    if (n <= 0) {  // block-uniform: no barrier reached by either wave
-        if (wave == 1) emit(0.0f);
-        return;
-    }
-    const int nchunks = (n + AS_KC - 1) / AS_KC;
-    const _Float16 * kh = kb + job.kv_base + (size_t) h * hs;
-    const _Float16 * vh = vb + job.kv_base + (size_t) h * hs;
-
-    if (wave == 0) {
-        // ---------------- score wave ----------------
-        // lane l: keys 8i + (l >> 3) of a chunk, dims 8 (l & 7) .. +8. q is uniform: scalar loads
-        // (lgkmcnt), so the vector-memory counter below counts K loads only.
-        const half8 * qp = (const half8 *) (q + (size_t) job.q_row * ldq + h * 64);
-        half8 qs[8];
-#pragma unroll
-        for (int c = 0; c < 8; ++c) qs[c] = qp[c];
-        half8 qv = qs[0];
-#pragma unroll
-        for (int c = 1; c < 8; ++c) qv = (lane & 7) == c ? qs[c] : qv;
-        const int g = lane >> 3;
-        float M = -INFINITY;
-        // K chunks straight to VGPRs by hand-issued loads: the compiler does not track them, so
-        // the waits are explicit and counted (XC_KBUF - 1 chunks of 8 loads stay in flight), tied
-        // to the registers they guard so no use can be scheduled above them. (Compiler-issued
-        // loads here got a full vmcnt(0) drain per chunk from the loop-carried registers.)
-        half8 kr[XC_KBUF][8];
-        auto kload = [&](half8 (&dst)[8], int c) {
-#pragma unroll
-            for (int i = 0; i < 8; ++i) {
-                const int key = max(min(c * AS_KC + 8 * i + g, n - 1), 0);
-                const _Float16 * src = kh + (size_t) key * 64 + 8 * (lane & 7);
-                asm volatile("global_load_dwordx4 %0, %1, off nt" : "=v"(dst[i]) : "v"(src) : "memory");
-            }
-        };
-#define OWK_KWAIT(N)                                                                                              \
-    asm volatile("s_waitcnt vmcnt(" #N ")"                                                                        \
-                 : "+v"(r[0]), "+v"(r[1]), "+v"(r[2]), "+v"(r[3]), "+v"(r[4]), "+v"(r[5]), "+v"(r[6]), "+v"(r[7]))
-        // Every slot is refilled after its use, past the last chunk too (keys clamped to n - 1): a
-        // conditional refill would merge old and new register values and hipcc would copy registers
-        // whose loads are still in flight. Chunk c has landed once 3 chunks of 8 loads remain.
-        auto kwait = [&](half8 (&r)[8]) {
-            static_assert(XC_KBUF == 4, "kwait counts 3 chunks of 8 loads behind the oldest");
-            asm volatile("s_waitcnt vmcnt(24)"
-                         : "+v"(r[0]), "+v"(r[1]), "+v"(r[2]), "+v"(r[3]), "+v"(r[4]), "+v"(r[5]), "+v"(r[6]), "+v"(r[7]));
-        };
-#pragma unroll
-        for (int b = 0; b < XC_KBUF; ++b) kload(kr[b], b);
-        // chunk c: scores, refill of its register slot, then barrier c
-        for (int t0 = 0; t0 < nchunks; t0 += XC_KBUF) {
-#pragma unroll
-            for (int b = 0; b < XC_KBUF; ++b) {
-                const int c = t0 + b;
-                if (c >= nchunks) break;
-                kwait(kr[b]);
-                float part[8];
-#pragma unroll
-                for (int i = 0; i < 8; ++i) {
-                    float a = 0.0f;
-#pragma unroll
-                    for (int e = 0; e < 8; e += 2) {
-                        const half2v k2 = {kr[b][i][e], kr[b][i][e + 1]}, q2 = {qv[e], qv[e + 1]};
-                        a = __builtin_amdgcn_fdot2(k2, q2, a, false);
-                    }
-                    // the 8 partials of a key in k_attn_step's order ((p0+p1)+(p2+p3))+((p4+p5)+(p6+p7))
-                    a += __shfl_xor(a, 1, 64);
-                    a += __shfl_xor(a, 2, 64);
-                    a += __shfl_xor(a, 4, 64);
-                    part[i] = a;
-                }
-                kload(kr[b], c + XC_KBUF);  // refill this slot (after its last use above)
-                // lane k <- score of key k = 8 (k >> 3) + (k & 7): register k >> 3 of lane 8 (k & 7)
-                const int src = (lane & 7) * 8;
-                float sk = 0.0f;
-#pragma unroll
-                for (int i = 0; i < 8; ++i) {
-                    const float v = __shfl(part[i], src, 64);
-                    sk = (lane >> 3) == i ? v : sk;
-                }
-                const int nk = min(AS_KC, n - c * AS_KC);
-                const float s = lane < nk ? sk * scale : -INFINITY;
-                const float pm = wave_incl_max(s);
-                const float mex = fmaxf(wave_shr1(pm, M), M);
-                const bool nm = lane < nk && s > mex;
-                const float e = expf(nm ? mex - s : s - mex);
-                float * pr = (float *) (pring + (c % XC_PBUF) * XC_PREC);
-                pr[lane] = nm ? e : 1.0f;                            // ms
-                pr[64 + lane] = nm ? 1.0f : (lane < nk ? e : 0.0f);  // vs (0: past the keys)
-                if (lane == 0) ((int *) (pr + 128))[0] = __builtin_amdgcn_ballot_w64(nm) == 0;
-                M = fmaxf(M, __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, pm), 63)));
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                __builtin_amdgcn_s_barrier();
-            }
-        }
-        // the refills past the end land before their registers are free for anything else (the
-        // empty statements keep the other slots live until after the wait: volatile asm keeps order)
-#define OWK_TIE(r) "+v"(r[0]), "+v"(r[1]), "+v"(r[2]), "+v"(r[3]), "+v"(r[4]), "+v"(r[5]), "+v"(r[6]), "+v"(r[7])
-        asm volatile("s_waitcnt vmcnt(0)" : OWK_TIE(kr[0]));
-        asm volatile("" : OWK_TIE(kr[1]));
-        asm volatile("" : OWK_TIE(kr[2]));
-        asm volatile("" : OWK_TIE(kr[3]));
-#undef OWK_TIE
-        if (lane == 0) fin[0] = M;
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();  // barrier nchunks: the final running max
-        return;
-    }
-
-    // ---------------- value wave ----------------
-    auto vstage = [&](int slot, int c) {
-        char * sV = vring + slot * AS_TILE;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            const int key = min(c * AS_KC + i * 8 + (lane >> 3), n - 1);
-            __builtin_amdgcn_global_load_lds((const void *) (vh + (size_t) key * 64 + (lane & 7) * 8),
-                                             (lds_ptr_t) (sV + i * 1024), 16, 0, 2);
-        }
-    };
-#pragma unroll
-    for (int b = 0; b < XC_VBUF; ++b)
-        if (b < nchunks) vstage(b, b);
-    float S = 0.0f;
-    _Float16 acc = (_Float16) 0.0f;
-    // barrier k (k = 0 .. nchunks) is the score wave's "chunk k published" (k = nchunks: final M);
-    // the value wave consumes chunk c after barrier c + 1, one chunk behind the scores, and the
-    // (ms, vs) ring entry of chunk c is rewritten (chunk c + XC_PBUF) only after barrier c + 3
-    static_assert(XC_PBUF >= 3, "ring entry reused before the value wave read it");
-    for (int c = -1; c < nchunks; ++c) {
-        __builtin_amdgcn_s_barrier();
-        if (c < 0) continue;
-        // chunk c's V landed: the chunks staged after it may stay in flight
-        const int ahead = min(XC_VBUF - 1, nchunks - 1 - c);
-        switch (ahead) {
-            case 5: wait_vmcnt<40>(); break;
-            case 4: wait_vmcnt<32>(); break;
-            case 3: wait_vmcnt<24>(); break;
-            case 2: wait_vmcnt<16>(); break;
-            case 1: wait_vmcnt<8>(); break;
-            default: wait_vmcnt<0>(); break;
-        }
-        const float * pr = (const float *) (pring + (c % XC_PBUF) * XC_PREC);
-        const float ms = pr[lane], vs = pr[64 + lane];
-        const bool nomax = ((const int *) (pr + 128))[0] != 0;
-        const _Float16 * vcol = (const _Float16 *) (vring + (c % XC_VBUF) * AS_TILE) + lane;
-        _Float16 vv[AS_KC];
-#pragma unroll
-        for (int kk = 0; kk < AS_KC; ++kk) vv[kk] = vcol[kk * 64];
-        if (c + XC_VBUF < nchunks) {
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this slot's V reads done
-            vstage(c % XC_VBUF, c + XC_VBUF);
-        }
-        if (nomax) {
-            // no new maximum in the chunk: every ms is 1 (exact), one mixed FMA + one add per key;
-            // keys past n have vs = 0 (acc and S unchanged, exactly)
-#pragma unroll
-            for (int kk = 0; kk < AS_KC; ++kk) {
-                const float vsk = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, vs), kk));
-                acc = (_Float16) fmaf((float) vv[kk], vsk, (float) acc);
-                S = S + vsk;
-            }
-        } else {
-#pragma unroll
-            for (int kk = 0; kk < AS_KC; ++kk) {
-                const float msk = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, ms), kk));
-                const float vsk = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, vs), kk));
-                acc = (_Float16) ((float) acc * msk);
-                acc = (_Float16) fmaf((float) vv[kk], vsk, (float) acc);
-                S = fmaf(S, msk, vsk);
-            }
-        }
-    }
-    // the last iteration's barrier was the score wave's final one (fin[0] = M written before it)
-    float M = fin[0];
-    for (int j = 0; j < job.n_zero_pad; ++j) {  // all-zero keys: s = 0, v = 0 (acc + 0*vs == acc)
-        if (0.0f > M) {
-            const float msz = expf(M - 0.0f);
-            M = 0.0f;
-            acc = (_Float16) ((float) acc * msz);
-            S = fmaf(S, msz, 1.0f);
-        } else {
-            S = fmaf(S, 1.0f, expf(0.0f - M));
-        }
-    }
-    const float S_inv = S == 0.0f ? 0.0f : 1.0f / S;
-    emit((float) acc * S_inv);
-}
-
-// ----------------------------------------------------------------------------------
 // Decoder attention for rows on the tiled path (prefills of >= 32 tokens: F32
 // accumulator over tiles of 16 keys, ops.cpp:8417-8510). Block = 4 waves = 4 heads.
 // ----------------------------------------------------------------------------------
@@ -959,7 +727,12 @@ __global__ __launch_bounds__(256) void k_attn_decoder(const _Float16 * __restric
 constexpr int SM_MAX_KEYS = 2048;
 
 // NT threads per block: 256, or 1024 when the pass has few (row, head) blocks (one row per step:
-// 20 blocks on 256 CUs) so each block keeps 4x the loads in flight
+// 20 blocks on 256 CUs) so each block keeps 4x the loads in flight. Every sum is taken in an order
+// that does not depend on NT (a row's output must not depend on how many rows share its pass):
+// the double softmax sum over 256 fixed key residues (mod 256) by the first 256 threads, and P.V
+// over SM_PV_GROUPS fixed key residues (mod 128), each summed in key order, then the groups in
+// group order.
+constexpr int SM_PV_GROUPS = 128;
 template <int NT>
 __global__ __launch_bounds__(NT) void k_attn_softmax(const _Float16 * __restrict__ q, int ldq,
                                                       const _Float16 * __restrict__ kb, const _Float16 * __restrict__ vb,
@@ -968,11 +741,15 @@ __global__ __launch_bounds__(NT) void k_attn_softmax(const _Float16 * __restrict
                                                       _Float16 * __restrict__ out, int ldo,
                                                       const int * __restrict__ amap, float * __restrict__ cap,
                                                       int cap_rows, float * __restrict__ out32) {
-    constexpr int NW = NT / 64, NG = NT / 8;  // waves; P . V key groups
-    __shared__ float sp[SM_MAX_KEYS > NG * 64 ? SM_MAX_KEYS : NG * 64];
+    constexpr int NW = NT / 64;
+    constexpr int TG = NT / 8;                    // thread groups of 8 (one 128-byte V row each)
+    constexpr int GPT = SM_PV_GROUPS / TG;        // key residues per thread group: 4 (NT 256) or 1 (NT 1024)
+    constexpr int U = 8 / GPT;                    // keys of each residue per iteration (8 loads in flight)
+    static_assert(GPT * TG == SM_PV_GROUPS && U * GPT == 8, "P.V group layout");
+    __shared__ float sp[SM_MAX_KEYS > SM_PV_GROUPS * 64 ? SM_MAX_KEYS : SM_PV_GROUPS * 64];
     __shared__ _Float16 p16[SM_MAX_KEYS];
     __shared__ float redf[NW];
-    __shared__ double redd[NW];
+    __shared__ double redd[4];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const AttnRow job = rows[blockIdx.y];
     if (job.mode != 2) return;
@@ -1010,23 +787,18 @@ __global__ __launch_bounds__(NT) void k_attn_softmax(const _Float16 * __restrict
     mx = redf[0];
 #pragma unroll
     for (int w = 1; w < NW; ++w) mx = fmaxf(mx, redf[w]);
-    // exp and the double-accumulated sum
-    double sum = 0.0;
-    for (int i = tid; i < n; i += NT) {
-        const float e = expf(sp[i] - mx);
-        sp[i] = e;
-        sum += (double) e;
-    }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o, 64);
-    if (lane == 0) redd[wave] = sum;
+    // exp (every thread), then the double-accumulated sum by threads 0..255 over keys = tid mod 256
+    for (int i = tid; i < n; i += NT) sp[i] = expf(sp[i] - mx);
     __syncthreads();
-    if (NW == 4) {
-        sum = (redd[0] + redd[1]) + (redd[2] + redd[3]);
-    } else {
-        sum = redd[0];
-        for (int w = 1; w < NW; ++w) sum += redd[w];
+    if (tid < 256) {
+        double sum = 0.0;
+        for (int i = tid; i < n; i += 256) sum += (double) sp[i];
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o, 64);
+        if (lane == 0) redd[wave] = sum;
     }
+    __syncthreads();
+    const double sum = (redd[0] + redd[1]) + (redd[2] + redd[3]);
     const float inv = (float) (1.0 / sum);
     const int a = amap ? amap[h] : -1;
     for (int i = tid; i < n; i += NT) {
@@ -1035,33 +807,44 @@ __global__ __launch_bounds__(NT) void k_attn_softmax(const _Float16 * __restrict
         if (a >= 0) cap[((size_t) a * n + i) * cap_rows + job.q_row] = p;
     }
     __syncthreads();
-    // P . V: thread t takes keys kg = t / 8, kg + 32, ... and head dims 8 (t % 8) .. +8 (one
-    // 16-byte load per key, 8 threads cover a 128-byte V row); 8 keys in flight per thread;
-    // the 32 key-group partials are summed in fixed order through LDS
-    const int kg = tid >> 3, seg = tid & 7;
-    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    for (int i0 = kg; i0 < n; i0 += NG * 8) {
-        half8 vv[8];
-        float pp[8];
+    // P . V: thread group tg (8 threads, head dims 8 seg .. +8: one 16-byte load per key) owns the
+    // key residues g = tg + TG j (mod SM_PV_GROUPS), each accumulated in key order
+    const int tg = tid >> 3, seg = tid & 7;
+    float acc[GPT][8];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            const int i = min(i0 + NG * u, n - 1);
-            const int cell = list ? list[i] : i;
-            vv[u] = *(const half8 *) (vh + (size_t) cell * ld_kv + seg * 8);
-            pp[u] = i0 + NG * u < n ? (float) p16[i] : 0.0f;
-        }
+    for (int j = 0; j < GPT; ++j)
 #pragma unroll
-        for (int u = 0; u < 8; ++u)
+        for (int e = 0; e < 8; ++e) acc[j][e] = 0.0f;
+    for (int i0 = 0; i0 < n; i0 += SM_PV_GROUPS * U) {
+        half8 vv[GPT][U];
+        float pp[GPT][U];
 #pragma unroll
-            for (int e = 0; e < 8; ++e) acc[e] = fmaf(pp[u], (float) vv[u][e], acc[e]);
+        for (int j = 0; j < GPT; ++j)
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int ii = i0 + tg + TG * j + SM_PV_GROUPS * u;
+                const int i = min(ii, n - 1);
+                const int cell = list ? list[i] : i;
+                vv[j][u] = *(const half8 *) (vh + (size_t) cell * ld_kv + seg * 8);
+                pp[j][u] = ii < n ? (float) p16[i] : 0.0f;
+            }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int j = 0; j < GPT; ++j)
+#pragma unroll
+                for (int e = 0; e < 8; ++e) acc[j][e] = fmaf(pp[j][u], (float) vv[j][u][e], acc[j][e]);
     }
-    float * red = sp;  // the scores are consumed: reuse as [32][64] partials
+    float * red = sp;  // the scores are consumed: reuse as [SM_PV_GROUPS][64] partials
+    __syncthreads();
 #pragma unroll
-    for (int e = 0; e < 8; ++e) red[kg * 64 + seg * 8 + e] = acc[e];
+    for (int j = 0; j < GPT; ++j)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) red[(tg + TG * j) * 64 + seg * 8 + e] = acc[j][e];
     __syncthreads();
     if (wave == 0) {
         float r = 0.0f;
-        for (int g = 0; g < NG; ++g) r += red[g * 64 + lane];
+        for (int g = 0; g < SM_PV_GROUPS; ++g) r += red[g * 64 + lane];
         if (out32) out32[(size_t) job.q_row * ldo + h * 64 + lane] = r;
         else out[(size_t) job.q_row * ldo + h * 64 + lane] = (_Float16) r;
     }
@@ -1073,6 +856,7 @@ void attn_decoder_softmax(hipStream_t s, const _Float16 * q, int ldq, const _Flo
                           float * out32) {
     if (n_rows <= 0) return;
     if (max_keys > SM_MAX_KEYS) throw std::runtime_error("attn_decoder_softmax: too many keys");
+    // outputs do not depend on the width (k_attn_softmax); OWK_SM_WIDE=0 keeps 256 threads (tests)
     static const bool wide_ok = [] {
         const char * v = getenv("OWK_SM_WIDE");
         return !(v && atoi(v) == 0);
@@ -1092,12 +876,9 @@ void attn_cross_kernel(hipStream_t s, int which, const _Float16 * q, int ldq, co
                        const _Float16 * vbase, int hs, const AttnRow * rows_dev, int n_rows, int H, float scale,
                        _Float16 * out, int ldo) {
     if (n_rows <= 0) return;
-    if (which == 2)
-        hipLaunchKernelGGL(k_attn_cross2, dim3(H, n_rows), dim3(128), 0, s, q, ldq, kbase, vbase, hs, rows_dev, scale, out,
-                           ldo, nullptr, nullptr, nullptr);
-    else
-        hipLaunchKernelGGL((k_attn_step<false, true>), dim3(H, n_rows), dim3(64), 0, s, q, ldq, kbase, vbase, 64, hs, rows_dev,
-                           nullptr, scale, out, ldo, nullptr, nullptr, nullptr);
+    if (which != 1) throw std::runtime_error("attn_cross_kernel: only the one-wave kernel (1) exists");
+    hipLaunchKernelGGL((k_attn_step<false, true>), dim3(H, n_rows), dim3(64), 0, s, q, ldq, kbase, vbase, 64, hs, rows_dev,
+                       nullptr, scale, out, ldo, nullptr, nullptr, nullptr);
 }
 
 void attn_decoder(hipStream_t s, const _Float16 * q, int ldq, const _Float16 * kbase, const _Float16 * vbase, int ld_kv,
@@ -1111,17 +892,8 @@ void attn_decoder(hipStream_t s, const _Float16 * q, int ldq, const _Float16 * k
             hipLaunchKernelGGL((k_attn_step<true, false>), dim3(H, n_rows), dim3(64), 0, s, q, ldq, kbase, vbase, ld_kv, hs,
                                rows_dev, key_idx, scale, out, ldo, out32, q8, q8d);
         } else {
-            // cross attention (no cell lists): the once-per-step K/V stream, one wave per (row, head);
-            // OWK_XATTN=2 selects the two-wave k_attn_cross2 (experimental: tests/test_gpu_kernels.py
-            // shows it diverging from k_attn_step beyond 3 key chunks)
-            static const bool one_wave = [] {
-                const char * v = getenv("OWK_XATTN");
-                return !(v && atoi(v) == 2);
-            }();
-            if (!key_idx && ld_kv == 64 && !one_wave)
-                hipLaunchKernelGGL(k_attn_cross2, dim3(H, n_rows), dim3(128), 0, s, q, ldq, kbase, vbase, hs, rows_dev,
-                                   scale, out, ldo, out32, q8, q8d);
-            else if (!key_idx)
+            // cross attention (no cell lists): the once-per-step K/V stream, one wave per (row, head)
+            if (!key_idx)
                 hipLaunchKernelGGL((k_attn_step<false, true>), dim3(H, n_rows), dim3(64), 0, s, q, ldq, kbase, vbase, ld_kv,
                                    hs, rows_dev, key_idx, scale, out, ldo, out32, q8, q8d);
             else

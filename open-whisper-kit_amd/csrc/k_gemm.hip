@@ -109,10 +109,6 @@ __device__ __forceinline__ void epi_store(const EpiParams & p, int r, int c, flo
     }
 }
 template <> __device__ __forceinline__ void epi_store<EPI_PARTIAL>(const EpiParams &, int, int, float) {}
-// EPI_RESID_STATS outside the decode-row GEMM (reduce kernel of a split launch): the residual part
-template <> __device__ __forceinline__ void epi_store<EPI_RESID_STATS>(const EpiParams & p, int r, int c, float acc) {
-    epi_store<EPI_RESID_F32>(p, r, c, acc);
-}
 
 // Eight consecutive outputs (row r, columns c .. c+7; c % 8 == 0) of one lane: the same values as
 // eight epi_store calls, written with 16-byte vector accesses where the mode's layout allows (the
@@ -237,7 +233,7 @@ static bool epi_vec_ok(int mode, const EpiParams & p, int N) {
         return false;
     switch (mode) {
         case EPI_QKV_ENC: case EPI_KV_CROSS: return p.d % 8 == 0;
-        case EPI_QKV_DEC: case EPI_PARTIAL: case EPI_RESID_STATS: return false;
+        case EPI_QKV_DEC: case EPI_PARTIAL: return false;
         default: return p.ldo % 8 == 0;
     }
 }
@@ -886,44 +882,17 @@ void tile_weights(hipStream_t s, const _Float16 * W, int N, int K, _Float16 * ou
 
 size_t tiled_weight_elems(int N, int K) { return (size_t) ((N + 15) / 16) * 16 * K; }
 
-// LayerNorm-operand launches (ALN) hold the f32 row slices, the LayerNorm weights and the
-// statistics next to the weight stream: at most 8 waves per block so each wave may use 256 VGPRs
-// (16-wave blocks cap a wave at 128 and spilled these to scratch)
-constexpr int GR_ALN_MAXW = 8;
-constexpr int RPW_ALN = 4;  // rows whose statistics one wave reduces
-
-template <int MODE, int MT, int J, bool ALN>
-__global__ __launch_bounds__(ALN ? GR_ALN_MAXW * 64 : GR_MAXW * 64) void k_gemm_rows(int M, int N, int K,
-                                                                                    const _Float16 * __restrict__ A,
-                                                                                    int lda, const _Float16 * __restrict__ Wt,
-                                                                                    EpiParams ep, float * __restrict__ part,
-                                                                                    AlnParams aln) {
-    // ALN: the A operand is LayerNorm(aln.x) computed here (AlnParams, kernels.h); its row
-    // statistics come from the producer's EPI_RESID_STATS partials, 4 rows per wave at most
-    constexpr int RPW = RPW_ALN;
+template <int MODE, int MT, int J>
+__global__ __launch_bounds__(GR_MAXW * 64) void k_gemm_rows(int M, int N, int K, const _Float16 * __restrict__ A,
+                                                            int lda, const _Float16 * __restrict__ Wt, EpiParams ep,
+                                                            float * __restrict__ part) {
     __shared__ floatx4 red[GR_MAXW][MT][64];
-    __shared__ float s_ln[2][32];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = blockDim.x >> 6;
     const int tile = blockIdx.x, n0 = tile * 16;
     const int nsteps = K >> 5;
     const int ks0 = (blockIdx.y * nw + wave) * J;
     const int nj = max(0, min(J, nsteps - ks0));
     const half8 z8 = {0, 0, 0, 0, 0, 0, 0, 0};
-
-    // ALN: the statistics partials first, then the weight stream (in-order vmcnt: the statistics
-    // are waited for while the weights stay in flight). Addresses are clamped and invalid entries
-    // zeroed after the load (a conditional load would make hipcc wait per load).
-    double2 stv[RPW][2];
-    if constexpr (ALN) {
-#pragma unroll
-        for (int q = 0; q < RPW; ++q)
-#pragma unroll
-            for (int hh = 0; hh < 2; ++hh) {
-                const int r = min(wave + q * nw, M - 1), t = min(lane + 64 * hh, aln.ntiles - 1);
-                stv[q][hh] = ((const double2 *) aln.stats)[(size_t) t * M + r];
-            }
-        __builtin_amdgcn_sched_barrier(0);  // issued before the weight stream
-    }
 
     // branch-free: every load is issued (k-step clamped into the matrix); operands past
     // this wave's k range are zeros so the extra MFMAs add exact zeros
@@ -936,81 +905,6 @@ __global__ __launch_bounds__(ALN ? GR_ALN_MAXW * 64 : GR_MAXW * 64) void k_gemm_
     }
     __builtin_amdgcn_sched_barrier(0);  // the weight loads stay ahead of everything below
 
-    if constexpr (ALN) {
-        // 1. row statistics (the counted vmcnt before the first use of stv leaves the weights in flight)
-        const int Kc = aln.ntiles * 16;  // LayerNorm width (= K)
-#pragma unroll
-        for (int q = 0; q < RPW; ++q) {
-            const int r = wave + q * nw;
-            double s1 = 0.0, m2 = 0.0;
-            double st[2] = {0.0, 0.0};
-#pragma unroll
-            for (int hh = 0; hh < 2; ++hh) {
-                const bool ok = lane + 64 * hh < aln.ntiles;
-                st[hh] = ok ? stv[q][hh].x : 0.0;
-                s1 += st[hh];
-            }
-#pragma unroll
-            for (int m = 32; m > 0; m >>= 1) s1 += __shfl_xor(s1, m, 64);
-            const float mean_f = (float) s1 / (float) Kc;  // ref: float sum / ne00
-            const double mean_d = s1 / (double) Kc;
-#pragma unroll
-            for (int hh = 0; hh < 2; ++hh) {
-                if (lane + 64 * hh < aln.ntiles) {
-                    const double dm = st[hh] / 16.0 - mean_d;
-                    m2 += stv[q][hh].y + 16.0 * dm * dm;  // Chan: combine per-tile (sum, M2)
-                }
-            }
-#pragma unroll
-            for (int m = 32; m > 0; m >>= 1) m2 += __shfl_xor(m2, m, 64);
-            const double dmf = mean_d - (double) mean_f;
-            m2 += (double) Kc * dmf * dmf;  // about the float mean, as ggml_vec_cvar_f32 centres
-            const float var = (float) (m2 / (double) Kc);
-            if (lane == 0 && r < M) {
-                s_ln[0][r] = mean_f;
-                s_ln[1][r] = 1.0f / sqrtf(var + aln.eps);
-            }
-        }
-        // 2. this wave's slices of x and of the LayerNorm weights (L2-resident: the producer just
-        // wrote x) -- issued after the statistics so both sets are never live together
-        float4 xa[MT][J][2], lw[J][2], lb[J][2];
-#pragma unroll
-        for (int j = 0; j < J; ++j) {
-            const int k = min(ks0 + j, nsteps - 1) * 32 + 8 * (lane >> 4);
-            lw[j][0] = *(const float4 *) (aln.w + k);
-            lw[j][1] = *(const float4 *) (aln.w + k + 4);
-            lb[j][0] = *(const float4 *) (aln.b + k);
-            lb[j][1] = *(const float4 *) (aln.b + k + 4);
-#pragma unroll
-            for (int i = 0; i < MT; ++i) {
-                const float * xp = aln.x + (size_t) min(i * 16 + (lane & 15), M - 1) * aln.ldx + k;
-                xa[i][j][0] = *(const float4 *) xp;
-                xa[i][j][1] = *(const float4 *) (xp + 4);
-            }
-        }
-        __syncthreads();  // s_ln of every row
-#pragma unroll
-        for (int i = 0; i < MT; ++i) {
-            const int r = min(i * 16 + (lane & 15), M - 1);
-            const float mean = s_ln[0][r], rstd = s_ln[1][r];
-#pragma unroll
-            for (int j = 0; j < J; ++j) {
-                half8 h;
-#pragma unroll
-                for (int e = 0; e < 8; ++e) {
-                    const float xv = e < 4 ? xa[i][j][0][e] : xa[i][j][1][e - 4];
-                    const float wv = e < 4 ? lw[j][0][e] : lw[j][1][e - 4];
-                    const float bv = e < 4 ? lb[j][0][e] : lb[j][1][e - 4];
-                    float v = xv - mean;  // ggml_norm: (x - mean) * scale, then ggml_mul, ggml_add
-                    v = v * rstd;
-                    v = v * wv;
-                    v = v + bv;
-                    h[e] = (_Float16) v;
-                }
-                a[i][j] = j < nj ? h : z8;
-            }
-        }
-    } else {
 #pragma unroll
         for (int i = 0; i < MT; ++i) {
             const _Float16 * ap = A + (size_t) min(i * 16 + (lane & 15), M - 1) * lda + 8 * (lane >> 4);
@@ -1020,7 +914,6 @@ __global__ __launch_bounds__(ALN ? GR_ALN_MAXW * 64 : GR_MAXW * 64) void k_gemm_
                 a[i][j] = j < nj ? t : z8;
             }
         }
-    }
 
     floatx4 acc[MT];
 #pragma unroll
@@ -1052,24 +945,7 @@ __global__ __launch_bounds__(ALN ? GR_ALN_MAXW * 64 : GR_MAXW * 64) void k_gemm_
         float sum = rp[0];
         for (int w = 1; w < nw; ++w) sum += rp[w * MT * 64 * 4];
         const int c = n0 + cc;
-        if constexpr (MODE == EPI_RESID_STATS) {
-            // x += acc + bias, then this tile's {sum, M2} of the updated row (16 lanes = 16 columns)
-            double dv = 0.0;
-            if (r < M && c < N) {
-                const size_t off = (size_t) r * ep.ldo + c;
-                const float v = ep.resid[off] + (sum + ep.bias[c]);
-                ep.out32[off] = v;
-                dv = v;
-            }
-            double s1 = dv;
-#pragma unroll
-            for (int m = 8; m > 0; m >>= 1) s1 += __shfl_xor(s1, m, 16);
-            const double dd = dv - s1 / 16.0;
-            double m2 = dd * dd;
-#pragma unroll
-            for (int m = 8; m > 0; m >>= 1) m2 += __shfl_xor(m2, m, 16);
-            if (cc == 0 && r < M) ((double2 *) ep.stats)[(size_t) tile * M + r] = double2{s1, m2};
-        } else if (r < M && c < N) {
+        if (r < M && c < N) {
             if constexpr (MODE == EPI_PARTIAL)
                 part[((size_t) blockIdx.y * M + r) * N + c] = sum;  // row-major [ks][M][N] for resid_layernorm
             else
@@ -1133,7 +1009,6 @@ template <template <int> class L, typename... Args> static void dispatch_mode(in
         case EPI_HALF_RESID: L<EPI_HALF_RESID>::run(args...); break;
         case EPI_RELU_F16: L<EPI_RELU_F16>::run(args...); break;
         case EPI_SIGMOID_F32: L<EPI_SIGMOID_F32>::run(args...); break;
-        case EPI_RESID_STATS: L<EPI_RESID_STATS>::run(args...); break;
         default: throw std::runtime_error("gemm: bad epilogue mode");
     }
 }
@@ -1145,7 +1020,13 @@ template <int MODE> struct LaunchBig {
         hipLaunchKernelGGL(k_gemm_big<MODE>, dim3(nbm * nbn), dim3(256), 0, s, M, N, K, A, lda, W, ldw, ep);
     }
 };
-static int g_gemm256 = -1;  // -1: from OWK_GEMM256 (default on); 5: the 5-slot ring
+// 256x256 kernel selection: OWK_GEMM256 (default 1; 0 forces the 128x128 tile), overridden per
+// thread by the debug hooks (gemm_set_256) so a hook never changes another thread's engine
+static thread_local int t_gemm256 = -1;  // -1: no override; 5: the 5-slot ring variant
+static int gemm256_mode() {
+    static const int env = env_int("OWK_GEMM256", 1);
+    return t_gemm256 >= 0 ? t_gemm256 : env;
+}
 template <int MODE> struct Launch256 {
     static void run(hipStream_t s, int M, int N, int K, const _Float16 * A, int lda, const _Float16 * W, int ldw,
                     const EpiParams & ep) {
@@ -1159,7 +1040,7 @@ template <int MODE> struct Launch256 {
             hipLaunchKernelGGL((k_gemm_256<MODE, 4, false>), dim3(nbm * nbn), dim3(512), 0, s, M, N, K, A, lda, W, ldw, e);
             return;
         }
-        if (g_gemm256 == 5)
+        if (gemm256_mode() == 5)
             hipLaunchKernelGGL((k_gemm_256<MODE, 5>), dim3(nbm * nbn), dim3(512), 0, s, M, N, K, A, lda, W, ldw, e);
         else
             hipLaunchKernelGGL((k_gemm_256<MODE, 4>), dim3(nbm * nbn), dim3(512), 0, s, M, N, K, A, lda, W, ldw, e);
@@ -1186,36 +1067,17 @@ template <int MODE> struct LaunchSkinny {
 };
 
 template <int MODE> struct LaunchRows {
-    template <int MT, int J, bool ALN>
+    template <int MT, int J>
     static void go(hipStream_t s, dim3 grid, int nw, int M, int N, int K, const _Float16 * A, int lda,
-                   const _Float16 * Wt, const EpiParams & ep, float * part, const AlnParams & aln) {
-        hipLaunchKernelGGL((k_gemm_rows<MODE, MT, J, ALN>), grid, dim3(nw * 64), 0, s, M, N, K, A, lda, Wt, ep, part,
-                           aln);
+                   const _Float16 * Wt, const EpiParams & ep, float * part) {
+        hipLaunchKernelGGL((k_gemm_rows<MODE, MT, J>), grid, dim3(nw * 64), 0, s, M, N, K, A, lda, Wt, ep, part);
         if (grid.y > 1 && MODE != EPI_PARTIAL)
             hipLaunchKernelGGL((k_gemm_rows_reduce<MODE, MT>), dim3(grid.x), dim3(MT * 64), 0, s, M, N, (int) grid.y,
                                part, ep);
     }
-    template <bool ALN>
-    static void run_t(hipStream_t s, int M, int N, int K, const _Float16 * A, int lda, const _Float16 * Wt,
-                      const EpiParams & ep, const GemmWs * ws, const AlnParams & aln) {
-        RowsPlan pl = rows_plan(K, MODE == EPI_PARTIAL);
-        if (MODE == EPI_RESID_STATS) {  // whole rows of K per block (the statistics need the final sums)
-            const int nsteps = K / 32;
-            pl.J = nsteps <= 32 ? 2 : nsteps <= 64 ? 4 : nsteps <= 128 ? 8 : 10;
-            pl.KS = 1;
-            pl.nw = (nsteps + pl.J - 1) / pl.J;
-            if (pl.nw > GR_MAXW || !ep.stats) throw std::runtime_error("gemm_rows: EPI_RESID_STATS shape");
-        }
-        if (ALN) {
-            // 8 waves (every row's statistics reduced by one wave, 4 rows per wave), the whole K
-            // in one block: J = ceil(k-steps / 8) <= 5 (K <= 1280, the widest Whisper decoder)
-            const int nsteps = K / 32;
-            pl.nw = GR_ALN_MAXW;
-            pl.J = std::max(2, (nsteps + GR_ALN_MAXW - 1) / GR_ALN_MAXW);
-            pl.KS = 1;
-            if (pl.J > 5 || M > RPW_ALN * GR_ALN_MAXW || !aln.stats || aln.ntiles * 16 != K || aln.ntiles > 128)
-                throw std::runtime_error("gemm_rows: unsupported LayerNorm-operand shape");
-        }
+    static void run(hipStream_t s, int M, int N, int K, const _Float16 * A, int lda, const _Float16 * Wt,
+                    const EpiParams & ep, const GemmWs * ws) {
+        const RowsPlan pl = rows_plan(K, MODE == EPI_PARTIAL);
         const int tiles = (N + 15) / 16;
         float * part = nullptr;
         if (pl.KS > 1 || MODE == EPI_PARTIAL) {
@@ -1225,52 +1087,15 @@ template <int MODE> struct LaunchRows {
         }
         const dim3 grid(tiles, pl.KS);
         const bool one = M <= 16;
-        if constexpr (ALN) {
-            if (MODE != EPI_F16 && MODE != EPI_GELU_F16 && MODE != EPI_QKV_DEC)
-                throw std::runtime_error("gemm_rows: LayerNorm operand for this epilogue");
-            else
-                switch (pl.J) {
-                    case 2: one ? go<1, 2, true>(s, grid, pl.nw, M, N, K, A, lda, Wt, ep, part, aln)
-                                : go<2, 2, true>(s, grid, pl.nw, M, N, K, A, lda, Wt, ep, part, aln); break;
-                    case 3: one ? go<1, 3, true>(s, grid, pl.nw, M, N, K, A, lda, Wt, ep, part, aln)
-                                : go<2, 3, true>(s, grid, pl.nw, M, N, K, A, lda, Wt, ep, part, aln); break;
-                    case 4: one ? go<1, 4, true>(s, grid, pl.nw, M, N, K, A, lda, Wt, ep, part, aln)
-                                : go<2, 4, true>(s, grid, pl.nw, M, N, K, A, lda, Wt, ep, part, aln); break;
-                    default: one ? go<1, 5, true>(s, grid, pl.nw, M, N, K, A, lda, Wt, ep, part, aln)
-                                 : go<2, 5, true>(s, grid, pl.nw, M, N, K, A, lda, Wt, ep, part, aln); break;
-                }
-            return;
-        }
         switch (pl.J) {
-            case 2: one ? go<1, 2, false>(s, grid, pl.nw, M, N, K, A, lda, Wt, ep, part, aln)
-                        : go<2, 2, false>(s, grid, pl.nw, M, N, K, A, lda, Wt, ep, part, aln); break;
-            case 4: one ? go<1, 4, false>(s, grid, pl.nw, M, N, K, A, lda, Wt, ep, part, aln)
-                        : go<2, 4, false>(s, grid, pl.nw, M, N, K, A, lda, Wt, ep, part, aln); break;
-            case 8:
-                if constexpr (!ALN) {
-                    one ? go<1, 8, false>(s, grid, pl.nw, M, N, K, A, lda, Wt, ep, part, aln)
-                        : go<2, 8, false>(s, grid, pl.nw, M, N, K, A, lda, Wt, ep, part, aln);
-                }
-                break;
-            default:
-                if constexpr (!ALN && MODE == EPI_RESID_STATS) {
-                    one ? go<1, 10, false>(s, grid, pl.nw, M, N, K, A, lda, Wt, ep, part, aln)
-                        : go<2, 10, false>(s, grid, pl.nw, M, N, K, A, lda, Wt, ep, part, aln);
-                } else {
-                    throw std::runtime_error("gemm_rows: no kernel for this plan");
-                }
-                break;
+            case 2: one ? go<1, 2>(s, grid, pl.nw, M, N, K, A, lda, Wt, ep, part)
+                        : go<2, 2>(s, grid, pl.nw, M, N, K, A, lda, Wt, ep, part); break;
+            case 4: one ? go<1, 4>(s, grid, pl.nw, M, N, K, A, lda, Wt, ep, part)
+                        : go<2, 4>(s, grid, pl.nw, M, N, K, A, lda, Wt, ep, part); break;
+            case 8: one ? go<1, 8>(s, grid, pl.nw, M, N, K, A, lda, Wt, ep, part)
+                        : go<2, 8>(s, grid, pl.nw, M, N, K, A, lda, Wt, ep, part); break;
+            default: throw std::runtime_error("gemm_rows: no kernel for this plan");
         }
-    }
-    static void run(hipStream_t s, int M, int N, int K, const _Float16 * A, int lda, const _Float16 * Wt,
-                    const EpiParams & ep, const GemmWs * ws) {
-        run_t<false>(s, M, N, K, A, lda, Wt, ep, ws, AlnParams());
-    }
-};
-template <int MODE> struct LaunchRowsLn {
-    static void run(hipStream_t s, int M, int N, int K, const AlnParams & aln, const _Float16 * Wt,
-                    const EpiParams & ep, const GemmWs * ws) {
-        LaunchRows<MODE>::template run_t<true>(s, M, N, K, nullptr, K, Wt, ep, ws, aln);
     }
 };
 
@@ -1494,11 +1319,7 @@ constexpr int GQ_MAX_SCALES = 32 * 160;  // M x K/32 activation scales in LDS
 // activation scales per thread: M * nb <= 32 * nb over blockDim = 64 * ceil(nb / J) threads
 // -> at most 32 * J / 64 + 1
 
-// A16: the activation is f16 rows (qa points at them) that each wave quantizes to Q8_0 itself
-// for its own K blocks -- x86 quantize_row_q8_0 on the exact f32 values of the f16 inputs (the
-// GELU table outputs feeding mlp.2), the 32 values of a block sit in 4 lanes of one row -- and
-// whose scales it publishes to LDS: no separate quantize launch for that matmul
-template <int MODE, int MT, int FMT, int GQ_J, bool A16 = false>  // FMT: QFmt; GQ_J K blocks per wave
+template <int MODE, int MT, int FMT, int GQ_J>  // FMT: QFmt; GQ_J K blocks per wave
 __global__ __launch_bounds__(GQ_MAXW * 64) void k_gemm_q5_rows(int M, int N, int K, const int8_t * __restrict__ qa,
                                                                const float * __restrict__ da, Q5W w, EpiParams ep) {
     constexpr int GQ_DA_PER_THREAD = 32 * GQ_J / 64 + 1;
@@ -1521,7 +1342,6 @@ __global__ __launch_bounds__(GQ_MAXW * 64) void k_gemm_q5_rows(int M, int N, int
     uint32_t qh[GQ_J];
     _Float16 dw[GQ_J], mw[GQ_J];
     long a[MT][GQ_J];
-    half8 ah[A16 ? MT : 1][A16 ? GQ_J : 1];
     // the tile's blocks are contiguous records (qf_tile_bytes): coalesced loads. Blocks past this
     // wave's range load a valid record and a zero activation (adds exact zeros). Record format at
     // compile time: the load phase stays branch-free.
@@ -1537,39 +1357,13 @@ __global__ __launch_bounds__(GQ_MAXW * 64) void k_gemm_q5_rows(int M, int N, int
 #pragma unroll
         for (int i = 0; i < MT; ++i) {
             const int ra = min(i * 16 + c16, M - 1);
-            if constexpr (A16) {
-                ah[i][j] = *(const half8 *) ((const _Float16 *) qa + (size_t) ra * K + kb * 32 + 8 * g);
-            } else {
-                const long t = *(const long *) (qa + (size_t) ra * K + kb * 32 + 8 * g);
-                a[i][j] = j < nj ? t : 0L;
-            }
+            const long t = *(const long *) (qa + (size_t) ra * K + kb * 32 + 8 * g);
+            a[i][j] = j < nj ? t : 0L;
         }
     }
     // activation scales of this block's K range (raw f32 d; at most GQ_DA_PER_THREAD per thread:
     // M <= 32, nbl <= nw * J) to LDS as [row][kb - kblo]; every load of the launch is issued before
     // the first wait (one round trip)
-    if constexpr (A16) {
-#pragma unroll
-        for (int j = 0; j < GQ_J; ++j)
-#pragma unroll
-            for (int i = 0; i < MT; ++i) {
-                float x[8], m = 0.0f;
-#pragma unroll
-                for (int e = 0; e < 8; ++e) {
-                    x[e] = (float) ah[i][j][e];
-                    m = fmaxf(m, fabsf(x[e]));
-                }
-                m = fmaxf(m, __shfl_xor(m, 16, 64));  // the block's 4 lanes (g = 0..3) of row c16
-                m = fmaxf(m, __shfl_xor(m, 32, 64));
-                const float id = m != 0.0f ? 127.f / m : 0.0f;
-                uint64_t q = 0;
-#pragma unroll
-                for (int e = 0; e < 8; ++e) q |= (uint64_t) (uint8_t) (int8_t) rintf(x[e] * id) << (8 * e);
-                a[i][j] = j < nj ? (long) q : 0L;
-                const int ra = i * 16 + c16, kb = kb0 + j;
-                if (g == 0 && ra < M && j < nj) sda[ra * nbl + (kb - kblo)] = m / 127.f;  // raw f32 d
-            }
-    } else {
         float dv[GQ_DA_PER_THREAD];
 #pragma unroll
         for (int u = 0; u < GQ_DA_PER_THREAD; ++u) {
@@ -1583,7 +1377,6 @@ __global__ __launch_bounds__(GQ_MAXW * 64) void k_gemm_q5_rows(int M, int N, int
             const int i = tid + u * blockDim.x;
             if (i < M * nbl) sda[i] = dv[u];
         }
-    }
     __syncthreads();
     floatx4 acc[MT], accm[MT];
 #pragma unroll
@@ -1757,33 +1550,6 @@ template <int MODE> struct LaunchQ5 {
     }
 };
 
-// decode-row quantized GEMM on f16 activation rows (A16 instantiation): EPI_PARTIAL only (mlp.2)
-void gemm_q5_rows_a16(hipStream_t s, int M, int N, int K, const _Float16 * A16, const Q5W & w, const EpiParams & ep) {
-    const int nb = K / 32;
-    if (!(M > 0 && M <= 32 && w.tiled && K % 32 == 0 && nb <= GQ_MAXW * GQ_JMAX && M * nb <= GQ_MAX_SCALES && ep.out32))
-        throw std::runtime_error("gemm_q5_rows_a16: unsupported shape");
-    const int KS = q5_partial_splits(K);
-    const int J = 3;
-    const int per = (nb + KS - 1) / KS;
-    const int nw = (per + J - 1) / J;
-    if (nw > GQ_MAXW) throw std::runtime_error("gemm_q5_rows_a16: plan");
-    const dim3 grid((N + 15) / 16, KS), block(nw * 64);
-    const int8_t * qa = (const int8_t *) A16;
-#define OWK_Q_A16(MT_, F_) hipLaunchKernelGGL((k_gemm_q5_rows<EPI_PARTIAL, MT_, F_, 3, true>), grid, block, 0, s, M, N, K, qa, \
-                                           nullptr, w, ep)
-#define OWK_Q_A16_F(MT_)                              \
-    switch (w.fmt) {                                  \
-        case QF_Q8_0: OWK_Q_A16(MT_, QF_Q8_0); break; \
-        case QF_Q4_0: OWK_Q_A16(MT_, QF_Q4_0); break; \
-        case QF_Q4_1: OWK_Q_A16(MT_, QF_Q4_1); break; \
-        case QF_Q5_1: OWK_Q_A16(MT_, QF_Q5_1); break; \
-        default: OWK_Q_A16(MT_, QF_Q5_0); break;      \
-    }
-    if (M <= 16) OWK_Q_A16_F(1) else OWK_Q_A16_F(2)
-#undef OWK_Q_A16_F
-#undef OWK_Q_A16
-}
-
 int qf_block_bytes(int f) {
     switch (f) {
         case QF_Q5_0: return 22;  // block_q5_0: d, qh[4], qs[16]
@@ -1849,11 +1615,12 @@ static void check_shape(int M, int N, int K, int lda, int ldw, int kmul) {
 
 // large GEMMs (the batched encoder, cross-KV, conv) take the 256x256 ring kernel; the rest
 // (small models, SortFormer chunks) the 128x128 tile. OWK_GEMM256=0 forces the 128x128 path.
-void gemm_set_256(int on) { g_gemm256 = on; }
-static bool use_256(int M, int N, int K) {
-    if (g_gemm256 < 0) g_gemm256 = env_int("OWK_GEMM256", 1);
-    return g_gemm256 && M >= 2048 && N >= 1024 && K % G2_K == 0;
+int gemm_set_256(int on) {
+    const int prev = t_gemm256;
+    t_gemm256 = on;
+    return prev;
 }
+static bool use_256(int M, int N, int K) { return gemm256_mode() && M >= 2048 && N >= 1024 && K % G2_K == 0; }
 
 void gemm_f16(hipStream_t s, int mode, int M, int N, int K, const _Float16 * A, int lda, const _Float16 * W, int ldw,
               const EpiParams & ep) {
@@ -1899,18 +1666,6 @@ size_t gemm_ws_floats(int N, int K) {
 }
 size_t gemm_partial_floats(int N, int K) { return (size_t) rows_plan(K, true).KS * ((N + 15) / 16) * 2 * 64 * 4; }
 int gemm_partial_splits(int K) { return rows_plan(K, true).KS; }
-
-void gemm_rows_ln(hipStream_t s, int mode, int M, int N, int K, const AlnParams & aln, const _Float16 * Wt,
-                  const EpiParams & ep, const GemmWs * ws) {
-    if (!(M > 0 && M <= 32 && K % 32 == 0 && N % 16 == 0 && Wt && aln && aln.ldx >= K))
-        throw std::runtime_error("gemm_rows_ln: unsupported shape");
-    switch (mode) {
-        case EPI_F16: LaunchRowsLn<EPI_F16>::run(s, M, N, K, aln, Wt, ep, ws); break;
-        case EPI_GELU_F16: LaunchRowsLn<EPI_GELU_F16>::run(s, M, N, K, aln, Wt, ep, ws); break;
-        case EPI_QKV_DEC: LaunchRowsLn<EPI_QKV_DEC>::run(s, M, N, K, aln, Wt, ep, ws); break;
-        default: throw std::runtime_error("gemm_rows_ln: unsupported epilogue");
-    }
-}
 
 void gemm(hipStream_t s, int mode, int M, int N, int K, const _Float16 * A, int lda, const _Float16 * W, int ldw,
           const EpiParams & ep, const GemmWs * ws, const _Float16 * Wt) {

@@ -208,61 +208,15 @@ __global__ __launch_bounds__(256) void k_resid_layernorm(int M, int N, int KS, c
     }
 }
 
-// The same finish with one wave per row (4 rows per 256-thread block): no block barriers, the
-// LayerNorm statistics by wave reductions (ln_row_regs, the non-split LayerNorm's code).
-__global__ __launch_bounds__(256) void k_resid_layernorm_w(int M, int N, int KS, const float * __restrict__ part,
-                                                           const float * __restrict__ bias, float * __restrict__ x,
-                                                           const float * __restrict__ w, const float * __restrict__ b,
-                                                           float eps, _Float16 * __restrict__ xn, int ldo,
-                                                           int8_t * __restrict__ q8, float * __restrict__ q8d) {
-    const int lane = threadIdx.x & 63;
-    const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (row >= M) return;
-    const int n4 = N >> 2;
-    float4 * xr = (float4 *) (x + (size_t) row * N);
-    float4 xv[LN_V4];
-#pragma unroll
-    for (int j = 0; j < LN_V4; ++j) {
-        const int i = lane + 64 * j;
-        float4 r = float4{0.f, 0.f, 0.f, 0.f};
-        if (i < n4) {
-            float4 a = ((const float4 *) (part + (size_t) row * N))[i];
-            for (int ks = 1; ks < KS; ++ks) {
-                const float4 p = ((const float4 *) (part + ((size_t) ks * M + row) * N))[i];
-                a.x += p.x; a.y += p.y; a.z += p.z; a.w += p.w;
-            }
-            const float4 bb = ((const float4 *) bias)[i];
-            const float4 res = xr[i];
-            r.x = res.x + (a.x + bb.x);
-            r.y = res.y + (a.y + bb.y);
-            r.z = res.z + (a.z + bb.z);
-            r.w = res.w + (a.w + bb.w);
-            xr[i] = r;
-        }
-        xv[j] = r;
-    }
-    if (!w) return;
-    ln_row_regs(xv, lane, N, w, b, eps, xn + (size_t) row * ldo, nullptr, q8 ? q8 + (size_t) row * N : nullptr,
-                q8 ? q8d + (size_t) row * (N / 32) : nullptr);
-}
-
 void resid_layernorm(hipStream_t s, int M, int N, int ks, const float * part, const float * bias, float * x,
                      const float * lnw, const float * lnb, float eps, _Float16 * xn, int ldo, int8_t * q8, float * q8d) {
     if (M <= 0) return;
     if (M > 32 || N % 16 != 0 || N > 4 * 256 * RL_V4) throw std::runtime_error("resid_layernorm: unsupported shape");
     if (q8 && (N % 32 != 0 || !q8d)) throw std::runtime_error("resid_layernorm: Q8_0 output needs N % 32 == 0");
-    // OWK_RLN_WAVE=1: one wave per row (opt-in; measured 159 -> 249 ms per step: the row's split
-    // partials are too many serial loads for one wave, profiles/r02e_ab.txt)
-    static const int wave_rows = [] {
-        const char * e = getenv("OWK_RLN_WAVE");
-        return e && *e ? atoi(e) : 0;
-    }();
-    if (wave_rows && N <= 4 * 64 * LN_V4)
-        hipLaunchKernelGGL(k_resid_layernorm_w, dim3((M + 3) / 4), dim3(256), 0, s, M, N, ks, part, bias, x, lnw, lnb, eps,
-                           xn, ldo, q8, q8d);
-    else
-        hipLaunchKernelGGL(k_resid_layernorm, dim3(M), dim3(256), 0, s, M, N, ks, part, bias, x, lnw, lnb, eps, xn, ldo,
-                           q8, q8d);
+    // (a one-wave-per-row variant measured slower: 159 -> 249 ms per step, the row's split partials
+    // are too many serial loads for one wave, profiles/r02e_ab.txt)
+    hipLaunchKernelGGL(k_resid_layernorm, dim3(M), dim3(256), 0, s, M, N, ks, part, bias, x, lnw, lnb, eps, xn, ldo,
+                       q8, q8d);
 }
 
 void layernorm_f16(hipStream_t s, const float * x, int rows, int d, const float * w, const float * b, float eps,

@@ -28,10 +28,6 @@ enum EpiMode : int {
     EPI_HALF_RESID = 11,// out32 = resid + (acc + bias) * 0.5         (macaron FFN half step)
     EPI_RELU_F16 = 12,  // out16 = f16(relu(acc + bias))              (transformer FFN, head)
     EPI_SIGMOID_F32 = 13,// out32 = sigmoid(acc + bias)               (speaker head)
-    EPI_RESID_STATS = 14,// decode-row GEMM only: EPI_RESID_F32, plus per (16-column tile, row) the
-                         // LayerNorm partial statistics of the updated row: stats[tile * M + r] =
-                         // {sum, sum of squares about the tile mean} (double) -- the next GEMM
-                         // normalises its A operand itself (AlnParams) instead of a LayerNorm launch
 };
 
 struct EpiParams {
@@ -52,7 +48,6 @@ struct EpiParams {
     const int64_t * row_off = nullptr;    // EPI_QKV_DEC: element offset of each row's KV cell in head 0
                                           // (head h at + h * Tpad: the cache is head-major)
     const int * slot_map = nullptr;       // EPI_KV_CROSS: clip index -> cross-KV slot (null = identity)
-    double * stats = nullptr;             // EPI_RESID_STATS: [N/16][M] {sum, M2} per tile and row
     int vec = 0;                          // set by the large-tile launcher: 16-byte vector epilogue allowed
     // quantized large-tile GEMM (gemm_q16): per-32-block scales, block-major [K/32][pad]
     const float * qs_da = nullptr;        // activation d (f16-rounded), rows permuted per 256-row tile
@@ -61,28 +56,18 @@ struct EpiParams {
     int c_off = 0;                        // large-tile launch over a column range: its first column
 };
 
-// The A operand of a decode-row GEMM as the LayerNorm of the f32 residual stream x (ggml_norm +
-// mul + add, ref ggml-cpu/ops.cpp:3578-3623, eps): row statistics from the producer GEMM's
-// EPI_RESID_STATS partials (mean = (float) sum / N as the reference's float sum / ne00; variance
-// from Chan's combination of the per-tile partials in double, about the float mean), then per
-// element f16(((x - mean) * rstd) * w + b) -- the reference's separate f32 ops, one rounding each.
-struct AlnParams {
-    const float * x = nullptr;      // [M][ldx]
-    int ldx = 0;
-    const double * stats = nullptr; // [ntiles][M] double2
-    int ntiles = 0;                 // = K / 16
-    const float * w = nullptr;
-    const float * b = nullptr;
-    float eps = 0.0f;
-    explicit operator bool() const { return x != nullptr; }
-};
-
 // large tiles (encoder / conv / cross-KV / long prefill): A [M,lda] f16, W [N,ldw] f16
 void gemm_f16(hipStream_t s, int mode, int M, int N, int K, const _Float16 * A, int lda,
               const _Float16 * W, int ldw, const EpiParams & ep);
 // skinny (decode steps, M <= 64): split-K across the waves of a block, LDS reduction
-// large-GEMM kernel choice (test/bench hook): 1 = 256x256 ring kernel where it applies, 0 = 128x128
-void gemm_set_256(int on);
+// this thread's 256x256-kernel override (-1 none, 0 force 128x128, 1 on, 5 the 5-slot ring);
+// returns the previous override (debug hooks restore it with GemmOverride)
+int gemm_set_256(int on);
+struct GemmOverride {
+    int prev;
+    explicit GemmOverride(int on) : prev(gemm_set_256(on)) {}
+    ~GemmOverride() { gemm_set_256(prev); }
+};
 void gemm_f16_skinny(hipStream_t s, int mode, int M, int N, int K, const _Float16 * A, int lda,
                      const _Float16 * W, int ldw, const EpiParams & ep);
 // split-K workspace of the decode-row GEMM (owned by the caller: one per stream)
@@ -105,10 +90,6 @@ void resid_layernorm(hipStream_t s, int M, int N, int ks, const float * part, co
 void gemm(hipStream_t s, int mode, int M, int N, int K, const _Float16 * A, int lda,
           const _Float16 * W, int ldw, const EpiParams & ep, const GemmWs * ws = nullptr,
           const _Float16 * Wt = nullptr);
-// decode-row GEMM (M <= 32) whose A operand is LayerNorm(aln.x) (see AlnParams); mode one of
-// EPI_F16 / EPI_GELU_F16 / EPI_QKV_DEC / EPI_RESID_F32 / EPI_RESID_STATS
-void gemm_rows_ln(hipStream_t s, int mode, int M, int N, int K, const AlnParams & aln, const _Float16 * Wt,
-                  const EpiParams & ep, const GemmWs * ws);
 // tiled weight copy for the decode-row GEMM: [ceil(N/16)][K/32][64 lanes][8] f16
 size_t tiled_weight_elems(int N, int K);
 void tile_weights(hipStream_t s, const _Float16 * W, int N, int K, _Float16 * out);
@@ -184,7 +165,6 @@ bool gemm_q16_applies(const Q5W & w, int M, int N, int K);
 // expand Q5W block arrays into wi / dwt (device buffers of N*K halves and K/32*npad floats)
 void quant_expand_f16(hipStream_t s, const Q5W & w, int N, int K, _Float16 * wi, float * dwt, int npad);
 // EPI_PARTIAL decode-row quantized GEMM whose activation rows are f16 (quantized to Q8_0 inside)
-void gemm_q5_rows_a16(hipStream_t s, int M, int N, int K, const _Float16 * A16, const Q5W & w, const EpiParams & ep);
 int q5_partial_splits(int K);
 size_t q5_partial_floats(int N, int K);  // workspace floats of a partial quantized GEMM (M <= 32)
 

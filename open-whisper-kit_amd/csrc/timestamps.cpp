@@ -216,6 +216,12 @@ std::vector<int32_t> dtw_time_indices(const float * cap, int n_ah, int n_audio_c
                                       int medfilt) {
     std::vector<int32_t> out;
     const int n_audio = n_frames / 2;
+    // the capture holds n_audio_ctx positions per head: the reference asserts n_frames <= 2 *
+    // n_audio_ctx (ref whisper.cpp:8850; a reduced audio_ctx with a longer window); fail the call
+    // instead of reading past the capture
+    if (n_frames > 2 * n_audio_ctx)
+        throw std::runtime_error("DTW timestamps: n_frames " + std::to_string(n_frames) + " > 2 * n_audio_ctx " +
+                                 std::to_string(n_audio_ctx) + " (ref whisper.cpp:8850 asserts)");
     if (n_ah <= 0 || n_audio <= medfilt || n_tok <= sot_len + 1) return out;
     // copy the first n_audio positions and normalise over tokens (ggml_norm, eps 1e-9;
     // ops.cpp:3578-3623: float mean of a double sum, centred variance accumulated in double

@@ -750,6 +750,7 @@ int whisper_full_with_state(struct whisper_context * ctx, struct whisper_state *
 int whisper_full(struct whisper_context * ctx, struct whisper_full_params params, const float * samples, int n_samples) {
     std::vector<float> vad_samples;
     if (params.vad) {
+        std::lock_guard<std::mutex> lk(ctx->state->mu);  // the pre-pass writes the default state's VAD fields
         if (!vad_filter(ctx, ctx->state, params, samples, n_samples, vad_samples)) {
             log_msg(GGML_LOG_LEVEL_ERROR, "whisper_full: failed to compute VAD\n");
             return -1;
@@ -771,6 +772,7 @@ int whisper_full_parallel(struct whisper_context * ctx, struct whisper_full_para
     if (n_processors == 1) return whisper_full(ctx, params, samples, n_samples);
     std::vector<float> vad_samples;  // ref 7812-7824
     if (params.vad) {
+        std::lock_guard<std::mutex> lk(ctx->state->mu);
         if (!vad_filter(ctx, ctx->state, params, samples, n_samples, vad_samples)) {
             log_msg(GGML_LOG_LEVEL_ERROR, "whisper_full_parallel: failed to compute VAD\n");
             return -1;
@@ -808,6 +810,14 @@ int whisper_full_parallel(struct whisper_context * ctx, struct whisper_full_para
     }
     int ret = 0;
     try {
+        // the states of this call (the context's default state and the fresh ones), locked in
+        // address order like owk_full_batch; the context lock while the shared recorder is on
+        std::vector<whisper_state *> held(states);
+        std::sort(held.begin(), held.end());
+        std::vector<std::unique_lock<std::mutex>> locks;
+        std::unique_lock<std::mutex> ctx_lock(ctx->mu, std::defer_lock);
+        if (ctx->prof.on) ctx_lock.lock();
+        for (whisper_state * st : held) locks.emplace_back(st->mu);
         ret = full_batch(ctx, states.data(), ps.data(), nullptr, ptr.data(), ns.data(), n_processors);
     } catch (const std::exception & e) {
         log_msg(GGML_LOG_LEVEL_ERROR, "whisper_full_parallel: %s\n", e.what());
@@ -1001,48 +1011,20 @@ int owk_full_batch(struct whisper_context * ctx, struct whisper_state ** states,
     for (whisper_state * st : held)
         if (st) locks.emplace_back(st->mu);
     std::vector<whisper_full_params> ps(std::max(n_clips, 1), params);
-    // Clip groups on concurrent streams: the clips are independent, so G groups each run the
-    // whole stage-major pipeline on their own engine (the engine of the group's first state:
-    // own HIP stream, buffers and captured decode graphs) from their own host thread. The
-    // hardware queues then interleave one group's latency-bound decode kernels (small GEMMs,
-    // LayerNorms, launch gaps) with another group's HBM-bound attention. Per-clip results do
-    // not depend on the grouping. Opt-in (OWK_STREAM_GROUPS): measured on MI355X with 32
-    // large-v3 clips, 2 groups of 16 take exactly as long as one batch of 32 and 4 groups of
-    // 8 take 2.3x as long -- the dependent-kernel boundaries do not overlap across queues.
-    int groups = 1;
-    if (const char * g = getenv("OWK_STREAM_GROUPS")) groups = atoi(g);
-    if (ctx->prof.on) groups = 1;  // per-kernel HIP events live in one shared recorder
-    groups = std::max(1, std::min(groups, n_clips));
-    if (groups == 1) {
-        try {
-            return full_batch(ctx, states, ps.data(), ext, samples, n_samples, n_clips);
-        } catch (const std::exception & e) {
-            log_msg(GGML_LOG_LEVEL_ERROR, "owk_full_batch: %s\n", e.what());
-            return -6;
-        }
+    // (Round 2 measured clip groups on concurrent streams: 2 x 16 clips took exactly as long as one
+    // batch of 32 and 4 x 8 took 2.3x as long, so the engine runs one stage-major batch per call.)
+    try {
+        return full_batch(ctx, states, ps.data(), ext, samples, n_samples, n_clips);
+    } catch (const std::exception & e) {
+        log_msg(GGML_LOG_LEVEL_ERROR, "owk_full_batch: %s\n", e.what());
+        return -6;
     }
-    std::vector<int> ret(groups, 0);
-    std::vector<std::thread> th;
-    for (int g = 0; g < groups; ++g) {
-        const int c0 = (int) ((int64_t) n_clips * g / groups), c1 = (int) ((int64_t) n_clips * (g + 1) / groups);
-        th.emplace_back([&, g, c0, c1] {
-            try {
-                ret[g] = full_batch(ctx, states + c0, ps.data() + c0, ext, samples + c0, n_samples + c0, c1 - c0);
-            } catch (const std::exception & e) {
-                log_msg(GGML_LOG_LEVEL_ERROR, "owk_full_batch: %s\n", e.what());
-                ret[g] = -6;
-            }
-        });
-    }
-    for (auto & t : th) t.join();
-    for (int r : ret)
-        if (r != 0) return r;
-    return 0;
 }
 
 void owk_prof_enable(struct whisper_context * ctx, int enable) {
     ctx->prof.flush();
     ctx->prof.on = enable != 0;
+    ctx->prof.mode = enable == 2 ? 2 : 1;
 }
 
 void owk_prof_reset(struct whisper_context * ctx) { ctx->prof.reset(); }
@@ -1164,8 +1146,7 @@ __global__ static void k_fill_rand_f16(_Float16 * p, size_t n, uint32_t seed) {
 double owk_debug_gemm_bench(int device, int mode, int M, int N, int K, int iters) {
     const bool force128 = mode & 0x100, rnd = mode & 0x200, ring5 = mode & 0x400;
     mode &= 0xFF;
-    struct Restore { ~Restore() { gemm_set_256(1); } } restore;
-    gemm_set_256(force128 ? 0 : ring5 ? 5 : 1);
+    GemmOverride ov(force128 ? 0 : ring5 ? 5 : 1);
     try {
         OWK_HIP_CHECK(hipSetDevice(device));
         hipStream_t s;
@@ -1272,30 +1253,7 @@ int owk_debug_gemm_quant2(int device, int fmt, int M, int N, int K, const float 
         EpiParams ep;
         ep.out32 = dout.as<float>();
         ep.ldo = N;
-        DevBuf wi, dwt, q16, q16d, a16, part;
-        if (use_q16 == 2) {
-            // the decode-row A16 path (mlp.2): f16 rows of a, quantized inside the GEMM; split-K partial
-            // tiles summed here in split order (as resid_layernorm does)
-            std::vector<_Float16> ah((size_t) M * K);
-            for (size_t i = 0; i < ah.size(); ++i) ah[i] = (_Float16) a[i];
-            a16.alloc(ah.size() * 2);
-            OWK_HIP_CHECK(hipMemcpy(a16.ptr, ah.data(), ah.size() * 2, hipMemcpyHostToDevice));
-            const int ks = q5_partial_splits(K);
-            part.alloc((size_t) ks * M * N * 4);
-            EpiParams pp;
-            pp.out32 = part.as<float>();
-            gemm_q5_rows_a16(s, M, N, K, a16.as<_Float16>(), w, pp);
-            OWK_HIP_CHECK(hipStreamSynchronize(s));
-            std::vector<float> hp((size_t) ks * M * N);
-            OWK_HIP_CHECK(hipMemcpy(hp.data(), part.ptr, hp.size() * 4, hipMemcpyDeviceToHost));
-            for (size_t i = 0; i < (size_t) M * N; ++i) {
-                float acc = hp[i];
-                for (int k = 1; k < ks; ++k) acc += hp[(size_t) k * M * N + i];
-                out[i] = acc;
-            }
-            OWK_HIP_CHECK(hipStreamDestroy(s));
-            return 0;
-        }
+        DevBuf wi, dwt, q16, q16d;
         if (use_q16) {
             // the large-tile path of the encoder: expanded weights, f16 Q8_0 integers, gemm_q16
             w.npad = (N + 255) / 256 * 256;
@@ -1451,7 +1409,7 @@ double owk_debug_gemm_epi_diff(int device, int mode, int M, int N, int K, int d,
             ep.pos = pos.as<float>();
             ep.gelu_tab = gt.as<uint16_t>();
             if (mode == EPI_RESID_F32 || mode == EPI_HALF_RESID) ep.out32 = res[k].as<float>();  // in place, as the engine
-            gemm_set_256(k == 0 ? 0 : 1);
+            GemmOverride ov(k == 0 ? 0 : 1);
             gemm_f16(s, mode, M, N, K, da.as<_Float16>(), K, dw.as<_Float16>(), K, ep);
             OWK_HIP_CHECK(hipStreamSynchronize(s));
             out32[k].resize(n32);
@@ -1461,7 +1419,6 @@ double owk_debug_gemm_epi_diff(int device, int mode, int M, int N, int K, int d,
                 OWK_HIP_CHECK(hipMemcpy(out16[j][k].data(), o16[j][k].ptr, n16 * 2, hipMemcpyDeviceToHost));
             }
         }
-        gemm_set_256(1);
         double mx = 0.0;
         for (size_t i = 0; i < n32; ++i) mx = std::max(mx, (double) std::fabs(out32[0][i] - out32[1][i]));
         for (int j = 0; j < 3; ++j)

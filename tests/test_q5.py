@@ -264,40 +264,3 @@ def test_quant_gemm_q16_vs_reference(kind):
     assert err < 2e-6, (kind, err)
 
 
-@pytest.mark.gpu
-@pytest.mark.parametrize("kind", list(QFMT))
-@pytest.mark.parametrize("M", [1, 17, 32])
-def test_quant_gemm_rows_a16_vs_reference(kind, M):
-    """The decode-row quantized GEMM that quantizes its f16 activation rows itself (mlp.2 of a
-    quantized decode pass: the GELU outputs) against the reference's ggml_mul_mat on the same f16
-    values (exact as f32): quantize_row_q8_0 / _q8_1 + vec_dot. K = 4 * 1280 split over 4 partial
-    launches as in the decoder."""
-    import sys
-    import owk_synth as S
-
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import ref_oracle as R
-
-    if not R.available():
-        pytest.skip("reference oracle not built")
-    L = owk.load()
-    fmt, wtype, bb = QFMT[kind]
-    N, K = 1280, 5120
-    L.owk_debug_gemm_quant2.argtypes = [C.c_int] * 5 + [C.POINTER(C.c_float), C.c_void_p, C.POINTER(C.c_float),
-                                                        C.c_void_p, C.c_void_p, C.c_int]
-    rng = np.random.default_rng(M + 3)
-    a = (rng.standard_normal((M, K)) * 0.7).astype(np.float16).astype(np.float32)
-    wf = (rng.standard_normal((N, K)) / np.sqrt(K) + 0.02).astype(np.float32)
-    blocks = S._QKIND[kind][2](wf)
-    out = np.zeros((M, N), np.float32)
-    assert L.owk_debug_gemm_quant2(0, fmt, M, N, K, a.ctypes.data_as(C.POINTER(C.c_float)), blocks,
-                                   out.ctypes.data_as(C.POINTER(C.c_float)), None, None, 2) == 0
-    RL = R.lib()
-    RL.ref_mul_mat.argtypes = [C.c_int, C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_float), C.c_int,
-                               C.POINTER(C.c_float), C.c_int]
-    ref = np.zeros((M, N), np.float32)
-    assert RL.ref_mul_mat(wtype, blocks, N, K, a.ctypes.data_as(C.POINTER(C.c_float)), M,
-                          ref.ctypes.data_as(C.POINTER(C.c_float)), 8) == 0
-    err = np.abs(out - ref).max() / np.abs(ref).max()
-    print(f"{kind} M={M}: decode-row A16 max rel err vs ggml_mul_mat {err:.2e}")
-    assert err < 2e-6, (kind, M, err)
