@@ -19,12 +19,14 @@ per clip (the n_text_ctx/2 - 4 decode-step ceiling of whisper_full, ref whisper.
 fixed work, identical on the CPU reference.
 
 Timed region: decoder passes replay captured HIP graphs (no per-kernel instrumentation).
-Roofline: one extra step of the same workload with owk_prof_enable(2): the decoder passes replay
-their captured graphs with a HIP event pair captured around every kernel-class launch (event-record
-nodes on the engine stream, read back after each replay), the encoder launches carry event pairs
-directly. `roofline` reports the class with the largest device time, its average launch time and
-the same kernel's average from the committed rocprofv3 --kernel-trace --stats summary of this
-command (profiles/, ROCPROF_STATS) for the cross-check.
+Roofline: extra steps of the same workload with HIP events on the engine stream (eager launches:
+captured graphs cannot carry timing events). One step with an event pair around every launch gives
+the per-class table (`phases`); then each of the TOP_CLASSES largest classes is timed in a step of
+its own where only its launches carry events (owk_prof_select), so the host stays ahead of the
+device and each pair brackets its kernel alone -- an eager all-class step inflates short kernels by
+the host launch gaps. `roofline` reports the class with the largest such device time, its average
+launch time and, for the cross-check, the same kernel's average from the committed rocprofv3
+--kernel-trace --stats summary of this command (profiles/, ROCPROF_STATS).
 
 cpu_baseline: the reference ggml CPU path (oracle/_ref/libwhisper_ref.so, compiled from the
 reference sources by oracle/ref/Makefile) runs ONE clip of the same workload on this host's
@@ -48,6 +50,7 @@ CLIP_SAMPLES = 480000     # 30 s at 16 kHz
 # decode-step classes (weights or KV streamed once per step for 32 rows) are HBM-bound
 MFMA_CLASSES = {"gemm_enc", "gemm_cross", "gemm_conv", "gemm_dec_big", "gemm_logits_big", "attn_encoder"}
 MAX_TOKENS = 219          # completion at i >= max_tokens -> 220 tokens per clip
+TOP_CLASSES = 3           # classes re-timed alone for the roofline
 # kernels of each class (mangled-name patterns, for the PMC traffic lookup): the decode-row GEMM
 # epilogue 7 (EPI_F32) is the logits matmul, every other decode-row launch is gemm_dec
 CLASS_KERNELS = {
@@ -266,16 +269,18 @@ class GpuRunner:
     def tokens_per_clip(self):
         return [sum(len(s["tokens"]) for s in self.w.segments(st)) for st in self.states]
 
-    def profile(self):
-        """One more step of the same workload, decoder passes replaying their captured graphs with
-        a HIP event pair captured around every kernel-class launch (owk_prof_enable mode 2)."""
+    def profile(self, only=None):
+        """One more step of the same workload with HIP event pairs on the engine stream around the
+        launches of the `only` classes (None: every class)."""
         w = self.w
-        w.L.owk_prof_enable(w.ctx, 2)
+        w.L.owk_prof_select(w.ctx, ",".join(only).encode() if only else None)
+        w.L.owk_prof_enable(w.ctx, 1)
         w.L.owk_prof_reset(w.ctx)
         self.step()
         self.sync()
         classes = {c: w.prof(c) for c in w.prof_classes()}
         w.L.owk_prof_enable(w.ctx, 0)
+        w.L.owk_prof_select(w.ctx, None)
         return classes
 
     def cpu_baseline(self):
@@ -290,10 +295,12 @@ class GpuRunner:
         return base, parity
 
 
-def roofline(classes, ms_per_step):
-    """`roofline` of the class with the largest device time in the profiled step."""
-    dom = max(classes, key=lambda c: classes[c]["ms"])
-    d = classes[dom]
+def roofline(classes, ms_per_step, alone=None):
+    """`roofline` of the class with the largest device time; `alone` = {class: record} of the top
+    classes each timed in a step where only its launches carry events (preferred when given)."""
+    src = alone or classes
+    dom = max(src, key=lambda c: src[c]["ms"])
+    d = src[dom]
     avg_ms = d["ms"] / max(1, d["launches"])
     if dom in MFMA_CLASSES:
         ach = d["flops"] / (d["ms"] * 1e-3) / 1e12
@@ -307,9 +314,14 @@ def roofline(classes, ms_per_step):
     roof["traffic_unit"] = "bytes/launch (PMC FETCH_SIZE x2, profiles/pmc_fetch_summary.txt)"
     roof["kernel_class"] = dom
     roof["kernel"] = CLASS_KERNEL_NAME.get(dom, dom)
-    roof["measured"] = ("HIP events on the engine stream, one extra step: event pairs captured into the decode "
-                        "hipGraphs around each launch and read after every replay (owk_prof_enable 2)")
+    roof["measured"] = ("HIP events on the engine stream around this class's launches only, in a step of its own "
+                        "(eager launches, owk_prof_select), minus the mean interval of an empty event pair recorded "
+                        "after each bracketed launch" if alone else
+                        "HIP events on the engine stream around every launch, one extra step (eager launches)")
     roof["avg_launch_ms"] = round(avg_ms, 5)
+    if "marker_us" in d:
+        roof["event_marker_pair_us"] = round(d["marker_us"], 3)
+        roof["avg_launch_ms_raw_events"] = round(d["event_ms_raw"] / max(1, d["launches"]), 5)
     roof["launches"] = d["launches"]
     rp = rocprof_avg_ms(dom)
     roof["rocprof_avg_launch_ms"] = rp
@@ -363,7 +375,28 @@ def main(argv=None, runner=None):
     roof = None
     classes = run.profile() if not args.no_prof else {}
     if classes:
-        roof = roofline(classes, 1e3 * dt / args.steps)
+        top = sorted(classes, key=lambda c: -classes[c]["ms"])[:TOP_CLASSES]
+        alone = {}
+        for c in top:
+            got = run.profile([c])
+            if c not in got:
+                continue
+            v = dict(got[c])
+            # subtract what the two markers add to each bracketed interval: the mean of the empty
+            # event pairs recorded right after every bracketed launch of the same step
+            cal = got.get("_event_pair")
+            v["event_ms_raw"] = v["ms"]
+            if cal and cal["launches"]:
+                v["marker_us"] = 1e3 * cal["ms"] / cal["launches"]
+                v["ms"] = max(0.0, v["ms"] - v["launches"] * cal["ms"] / cal["launches"])
+            alone[c] = v
+        roof = roofline(classes, 1e3 * dt / args.steps, alone or None)
+        if rank == 0:
+            for c, v in alone.items():
+                log(f"[bench] alone {c:16s} {v['ms']:10.2f} ms  launches {v['launches']:7d}  "
+                    f"avg {1e3 * v['ms'] / max(1, v['launches']):8.2f} us (raw {1e3 * v['event_ms_raw'] / max(1, v['launches']):8.2f}"
+                    f", marker pair {v.get('marker_us', 0):.2f} us; all-class step "
+                    f"{1e3 * classes[c]['ms'] / max(1, classes[c]['launches']):8.2f} us)")
         if rank == 0:
             tot = sum(v["ms"] for v in classes.values())
             for c, v in sorted(classes.items(), key=lambda kv: -kv[1]["ms"]):

@@ -45,12 +45,12 @@ WHISPER_API int owk_vad_detect_batch(struct whisper_vad_context * vctx, const fl
 WHISPER_API int owk_vad_segments_raw(const float * probs, int n_probs, int n_window, struct whisper_vad_params params,
                                      int64_t * out_cs, int cap);
 
-/* per-kernel-class device timing with HIP events recorded on the engine stream.
- * enable = 1: eager launches with an event pair around each kernel-class launch;
- * enable = 2: decoder passes replay their captured hipGraphs with the event pairs captured into
- * the graph (event-record nodes around each launch), read back after every replay -- the timing
- * of the production path without eager launch gaps; 0: off */
+/* per-kernel-class device timing with HIP events recorded on the engine stream (eager launches
+ * while enabled: captured graphs cannot carry timing events) */
 WHISPER_API void owk_prof_enable(struct whisper_context * ctx, int enable);
+/* time only these kernel classes (comma-separated; NULL or "" = all): the other launches carry no
+ * events, so the host stays ahead of the device and each event pair brackets its kernel alone */
+WHISPER_API void owk_prof_select(struct whisper_context * ctx, const char * classes);
 WHISPER_API void owk_prof_reset(struct whisper_context * ctx);
 /* total device milliseconds and launch count of one kernel class since reset;
  * returns 0 if the class is known */
@@ -79,6 +79,12 @@ WHISPER_API double owk_debug_gemm_epi_diff(int device, int mode, int M, int N, i
  * Returns the count written (<= cap_out) or -1. */
 WHISPER_API int owk_debug_dtw(const float * cap, int n_ah, int n_audio_ctx, int n_tok, int sot_len, int n_frames,
                               int medfilt, int * out, int cap_out);
+/* test hook (host only): the GBNF constraint of grammar.cpp (ref whisper.cpp:5498-5905) on a caller's
+ * rules and vocabulary (vocab[id] = token text, ids < eot are the text tokens): accept the n_accept
+ * tokens, then write the ids the constraint penalises (up to cap); returns their count, -1 on error */
+WHISPER_API int owk_debug_grammar_rejects(const whisper_grammar_element ** rules, size_t n_rules, size_t i_start_rule,
+                                          const char * const * vocab, int n_vocab, int eot, const int * accept,
+                                          int n_accept, int * out, int cap);
 /* test hook: alignment-head probabilities captured by the state's last DTW re-decode,
  * [head][n_audio_ctx][rows of that pass]; returns the float count (copies when out != NULL) */
 WHISPER_API long owk_debug_capture(struct whisper_state * state, float * out, long cap);
@@ -96,6 +102,9 @@ WHISPER_API int owk_debug_gemm_quant2(int device, int fmt, int M, int N, int K, 
 /* mode | 0x100: force the 128x128 large-GEMM kernel; | 0x400: 5-slot ring variant of the 256x256 kernel;
  * | 0x200: uniform random operands (else zeros) */
 WHISPER_API double owk_debug_gemm_bench(int device, int mode, int M, int N, int K, int iters);
+/* the decoder's per-layer matmul + residual/LayerNorm chain (no attention) of a large-v3-shaped model,
+ * R rows, distinct random weights per layer, one captured hipGraph: device microseconds per layer */
+WHISPER_API double owk_debug_decode_chain(int device, int R, int n_layers, int iters);
 
 /* library identity: 1 when the gfx950 HIP code object is present and a device is usable */
 WHISPER_API int owk_device_ok(int device);

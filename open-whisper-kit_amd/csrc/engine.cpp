@@ -39,10 +39,8 @@ void Prof::flush() {
         t.flops += r.flops;
         t.bytes += r.bytes;
         t.n += 1;
-        if (!r.graph_owned) {
-            pool.push_back(r.a);
-            pool.push_back(r.b);
-        }
+        pool.push_back(r.a);
+        pool.push_back(r.b);
     }
     pending.clear();
 }
@@ -54,7 +52,6 @@ void Prof::reset() {
 
 Prof::~Prof() {
     for (auto & r : pending) {
-        if (r.graph_owned) continue;  // destroyed with their graph
         (void) hipEventDestroy(r.a);
         (void) hipEventDestroy(r.b);
     }
@@ -64,6 +61,7 @@ Prof::~Prof() {
 ProfScope::ProfScope(Prof * p_, hipStream_t s_, const char * name, double flops_, double bytes_)
     : p(p_), s(s_), flops(flops_), bytes(bytes_) {
     if (!p || !p->on) return;
+    if (!p->only.empty() && std::find(p->only.begin(), p->only.end(), name) == p->only.end()) return;
     cls = p->cls_id(name);
     a = p->ev();
     OWK_HIP_CHECK(hipEventRecord(a, s));
@@ -73,11 +71,15 @@ ProfScope::~ProfScope() {
     if (cls < 0) return;
     hipEvent_t b = p->ev();
     (void) hipEventRecord(b, s);
-    if (p->capturing) {  // recorded into the graph being captured; read after each replay
-        p->cap_recs.push_back({cls, a, b, flops, bytes, true});
-        return;
-    }
     p->pending.push_back({cls, a, b, flops, bytes});
+    if (!p->only.empty()) {
+        // calibration: an event pair with nothing between, right after the bracketed launch (class
+        // "_event_pair"): what the markers themselves add to every bracketed interval
+        hipEvent_t c = p->ev(), d = p->ev();
+        (void) hipEventRecord(c, s);
+        (void) hipEventRecord(d, s);
+        p->pending.push_back({p->cls_id("_event_pair"), c, d, 0.0, 0.0});
+    }
     if (p->pending.size() > 4096) p->flush();
 }
 
@@ -446,14 +448,7 @@ void Engine::stage_layout(int C, int KC) {
 }
 
 void Engine::clear_graphs() {
-    if (prof && !graphs_.empty()) prof->flush();  // no pending record may name a destroyed event
-    for (auto & kv : graphs_) {
-        (void) hipGraphExecDestroy(kv.second.ex);
-        for (auto & r : kv.second.recs) {
-            (void) hipEventDestroy(r.a);
-            (void) hipEventDestroy(r.b);
-        }
-    }
+    for (auto & kv : graphs_) (void) hipGraphExecDestroy(kv.second);
     graphs_.clear();
 }
 
@@ -576,17 +571,15 @@ void Engine::decode(const std::vector<DecodeRow> & rows, const std::vector<int> 
         sh.capture = true;
     }
     static const bool no_graph = getenv("OWK_NO_GRAPH") && atoi(getenv("OWK_NO_GRAPH")) != 0;
-    const int pm = prof && prof->on ? prof->mode : 0;
-    if (pm == 1 || no_graph || capture) {  // eager per-kernel events, debugging, DTW: eager launches
+    if ((prof && prof->on) || no_graph || capture) {  // per-kernel events, debugging, DTW: eager launches
         launch_decode(sh);
         return;
     }
     // replay a captured graph of the whole decoder pass (one launch instead of ~10 per layer)
     const uint64_t sig = buffers_signature();
-    if (sig != graphs_sig_ || pm != graphs_prof_) {
+    if (sig != graphs_sig_) {
         clear_graphs();
         graphs_sig_ = sig;
-        graphs_prof_ = pm;
     }
     const uint64_t key = (uint64_t) R | ((uint64_t) n_logit_rows << 20) | ((uint64_t) sh.self_oc << 40) |
                          ((uint64_t) sh.self_tl << 41) | ((uint64_t) sh.cross_oc << 42) | ((uint64_t) sh.cross_tl << 43) |
@@ -596,34 +589,22 @@ void Engine::decode(const std::vector<DecodeRow> & rows, const std::vector<int> 
     if (it == graphs_.end()) {
         if (graphs_.size() >= 64) clear_graphs();
         hipGraph_t g = nullptr;
-        GraphEntry ge;
         OWK_HIP_CHECK(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal));
-        if (pm) {
-            prof->capturing = true;
-            prof->cap_recs.clear();
-        }
         try {
             launch_decode(sh);
         } catch (...) {
-            if (pm) prof->capturing = false;
             (void) hipStreamEndCapture(stream, &g);
             if (g) (void) hipGraphDestroy(g);
             throw;
         }
-        if (pm) {
-            prof->capturing = false;
-            ge.recs.swap(prof->cap_recs);
-        }
         OWK_HIP_CHECK(hipStreamEndCapture(stream, &g));
-        const hipError_t e = hipGraphInstantiate(&ge.ex, g, nullptr, nullptr, 0);
+        hipGraphExec_t ex = nullptr;
+        const hipError_t e = hipGraphInstantiate(&ex, g, nullptr, nullptr, 0);
         (void) hipGraphDestroy(g);
         OWK_HIP_CHECK(e);
-        it = graphs_.emplace(key, std::move(ge)).first;
+        it = graphs_.emplace(key, ex).first;
     }
-    // prof mode 2: read the previous replay's event pairs before their events are re-recorded
-    if (pm) prof->flush();
-    OWK_HIP_CHECK(hipGraphLaunch(it->second.ex, stream));
-    if (pm) prof->pending.insert(prof->pending.end(), it->second.recs.begin(), it->second.recs.end());
+    OWK_HIP_CHECK(hipGraphLaunch(it->second, stream));
 }
 
 void Engine::launch_decode(const DecShape & sh) {
@@ -688,7 +669,10 @@ void Engine::launch_decode(const DecShape & sh) {
             ProfScope ps(prof, s, "gemm_dec", 2.0 * n * (double) N * K, 2.0 * ((double) n * K + (double) N * K));
             gemm(s, mode, n, N, K, A, K, nullptr, K, ep, &gws_, Wt);
         };
-        // residual matmul as partial tiles + resid_layernorm (lnw null: residual only)
+        // residual matmul as partial tiles + resid_layernorm (lnw null: residual only). (Round 3
+        // measured the finish inside the matmul launch -- write-through partials, an agent-scope
+        // ticket, the last blocks polling the arrivals and doing the rows -- slower: the per-layer
+        // chain 51.6 -> 58.1 us, tools/chain_sweep.py; the tail costs more than the boundary.)
         auto resid_ln = [&](const _Float16 * A, const _Float16 * Wt, int K, const float * bias, const float * lnw,
                             const float * lnb) {
             gemm_rows(EPI_PARTIAL, d, K, A, Wt, EpiParams());

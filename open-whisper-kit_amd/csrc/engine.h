@@ -12,23 +12,19 @@
 namespace owk {
 
 // per-kernel-class HIP-event timing + algorithmic work counters
-// mode 1: eager launches with an event pair around each; mode 2: decoder passes replay their
-// captured graphs, the event pairs are captured INTO the graphs (event-record nodes around each
-// kernel-class launch) and read back after every replay -- per-kernel times without the eager
-// launch gaps (owk_prof_enable)
+// eager launches with an event pair around each kernel-class launch on the engine stream; with a
+// class selection (owk_prof_select) only the selected classes carry events: the host then stays
+// ahead of the device and an event pair brackets its kernel alone (no host launch gap inside)
 struct Prof {
     bool on = false;
-    int mode = 1;
-    bool capturing = false;  // a decode graph is being captured: scopes go to cap_recs
+    std::vector<std::string> only;  // empty: every class
     struct Rec {
         int cls;
         hipEvent_t a, b;
         double flops, bytes;
-        bool graph_owned = false;  // events belong to a captured graph (not returned to the pool)
     };
     std::vector<std::string> names;
     std::vector<Rec> pending;
-    std::vector<Rec> cap_recs;
     std::vector<hipEvent_t> pool;
     struct Tot {
         double ms = 0, flops = 0, bytes = 0;
@@ -176,13 +172,8 @@ private:
     PinnedBuf stg_;   // host image of the per-pass inputs
     DevBuf d_stg_;    // its device copy (fixed sections, see stage_layout)
     size_t st_tok_ = 0, st_pos_ = 0, st_rowoff_ = 0, st_rs_ = 0, st_rc_ = 0, st_lsel_ = 0, st_keys_ = 0, st_bytes_ = 0;
-    struct GraphEntry {
-        hipGraphExec_t ex = nullptr;
-        std::vector<Prof::Rec> recs;  // prof mode 2: the event pairs captured into the graph
-    };
-    std::map<uint64_t, GraphEntry> graphs_;
+    std::map<uint64_t, hipGraphExec_t> graphs_;
     uint64_t graphs_sig_ = 0;
-    int graphs_prof_ = 0;  // prof mode the cached graphs were captured in (0: no events)
 
     // Q5_0 models: f32 activations feeding the quantized GEMMs and their Q8_0 copy
     void linear(const char * cls, int mode, int M, int N, int K, const _Float16 * A16, const float * A32, int lda,

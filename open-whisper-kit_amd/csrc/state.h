@@ -8,6 +8,7 @@
 #include <vector>
 
 #include "engine.h"
+#include "grammar.h"
 #include "kv_cells.h"
 #include "model.h"
 #include "owk.h"
@@ -30,7 +31,7 @@ struct Sequence {
     double sum_logprobs_all = 0, sum_logprobs = 0, avg_logprobs = 0, entropy = 0, score = 0;
 };
 
-// whisper_decoder (ref 797-820) minus grammar state
+// whisper_decoder (ref 797-820)
 struct Decoder {
     Sequence sequence;
     int i_batch = 0;        // logits row of this decoder in the current decode call
@@ -39,6 +40,7 @@ struct Decoder {
     std::vector<float> probs, logits, logprobs;  // host copies (sampling / beam / callback paths)
     TokenOut gtok{};        // device-side greedy pick for the current logits
     std::mt19937 rng;
+    Grammar grammar;        // GBNF parse state (whisper_full_params.grammar_rules)
 };
 
 constexpr int MAX_DECODERS = 8;  // WHISPER_MAX_DECODERS (ref 142)

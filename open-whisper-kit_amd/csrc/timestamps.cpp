@@ -196,7 +196,7 @@ int wrap_segment(whisper_context * ctx, whisper_state * st, int max_len, bool sp
             res++;
         } else {
             acc += cur;
-            text += txt;
+            text += txt.c_str();  // C string (ref 6121)
         }
     }
     st->result_all.back().text = std::move(text);

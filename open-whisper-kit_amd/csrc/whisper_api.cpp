@@ -1024,10 +1024,25 @@ int owk_full_batch(struct whisper_context * ctx, struct whisper_state ** states,
 void owk_prof_enable(struct whisper_context * ctx, int enable) {
     ctx->prof.flush();
     ctx->prof.on = enable != 0;
-    ctx->prof.mode = enable == 2 ? 2 : 1;
 }
 
 void owk_prof_reset(struct whisper_context * ctx) { ctx->prof.reset(); }
+
+void owk_prof_select(struct whisper_context * ctx, const char * classes) {
+    ctx->prof.flush();
+    ctx->prof.only.clear();
+    if (!classes) return;
+    std::string cur;
+    for (const char * c = classes;; ++c) {
+        if (*c == ',' || *c == 0) {
+            if (!cur.empty()) ctx->prof.only.push_back(cur);
+            cur.clear();
+            if (*c == 0) break;
+        } else {
+            cur += *c;
+        }
+    }
+}
 
 int owk_prof_read(struct whisper_context * ctx, const char * cls, double * total_ms, long * launches) {
     ctx->prof.flush();
@@ -1131,6 +1146,33 @@ int owk_debug_dtw(const float * cap, int n_ah, int n_audio_ctx, int n_tok, int s
     }
 }
 
+int owk_debug_grammar_rejects(const whisper_grammar_element ** rules, size_t n_rules, size_t i_start_rule,
+                              const char * const * vocab, int n_vocab, int eot, const int * accept, int n_accept, int * out,
+                              int cap) {
+    try {
+        if (!vocab || eot < 0 || eot > n_vocab) throw std::runtime_error("bad vocabulary");
+        std::vector<std::string> v(vocab, vocab + n_vocab);
+        owk::Grammar g;
+        g.init(rules, n_rules, i_start_rule);
+        for (int i = 0; i < n_accept; ++i) {
+            if (accept[i] < 0 || accept[i] >= n_vocab) throw std::runtime_error("accepted token out of range");
+            g.accept(v[accept[i]]);
+        }
+        std::vector<float> logits(n_vocab, 0.0f);
+        g.suppress(v, eot, 1.0f, logits.data());
+        int n = 0;
+        for (int id = 0; id < n_vocab; ++id)
+            if (logits[id] != 0.0f) {
+                if (n < cap) out[n] = id;
+                ++n;
+            }
+        return n;
+    } catch (const std::exception & ex) {
+        log_msg(GGML_LOG_LEVEL_ERROR, "owk_debug_grammar_rejects: %s\n", ex.what());
+        return -1;
+    }
+}
+
 // uniform random f16 in [-1, 1) from a per-element hash: GEMM timings on random data (zero-filled
 // operands run 15-21 % faster through DVFS, CDNA guide 5.4 rule 25)
 __global__ static void k_fill_rand_f16(_Float16 * p, size_t n, uint32_t seed) {
@@ -1200,6 +1242,105 @@ double owk_debug_gemm_bench(int device, int mode, int M, int N, int K, int iters
         return 1e3 * ms / iters;
     } catch (const std::exception & ex) {
         log_msg(GGML_LOG_LEVEL_ERROR, "owk_debug_gemm_bench: %s\n", ex.what());
+        return -1;
+    }
+}
+
+// The decoder's per-layer matmul + residual/LayerNorm chain of a large-v3-shaped model (d = 1280,
+// 32 layers, R rows) WITHOUT the attention kernels, as the engine's fused R <= 32 path launches it
+// (engine.cpp launch_decode): QKV (EPI_QKV_DEC) -> O partial + resid_layernorm -> cross Q -> cross-O
+// partial + resid_layernorm -> mlp.0 (GELU) -> mlp.2 partial + resid_layernorm. Distinct random
+// weights per layer (1.47 GB: every replay streams them from HBM as a decode step does), the whole
+// chain captured in one hipGraph; returns device microseconds per layer (events around replays).
+double owk_debug_decode_chain(int device, int R, int n_layers, int iters) {
+    try {
+        OWK_HIP_CHECK(hipSetDevice(device));
+        if (R < 1 || R > 32 || n_layers < 1) throw std::runtime_error("bad shape");
+        const int d = 1280;
+        hipStream_t s;
+        OWK_HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+        struct LW { DevBuf qkv, o, cq, co, m0, m1; };
+        std::vector<LW> lw(n_layers);
+        auto fill = [&](DevBuf & b, int N, int K) {
+            b.alloc(tiled_weight_elems(N, K) * 2);
+            hipLaunchKernelGGL(k_fill_rand_f16, dim3(4096), dim3(256), 0, s, b.as<_Float16>(), tiled_weight_elems(N, K),
+                               (uint32_t) (size_t) b.ptr);
+        };
+        for (auto & l : lw) {
+            fill(l.qkv, 3 * d, d); fill(l.o, d, d); fill(l.cq, d, d); fill(l.co, d, d); fill(l.m0, 4 * d, d);
+            fill(l.m1, d, 4 * d);
+        }
+        DevBuf x, xn, q, ao, h, kc, vc, bias, bias4, lnw, lnb, part, rowoff, gt;
+        x.alloc((size_t) R * d * 4); xn.alloc((size_t) R * d * 2); q.alloc((size_t) R * d * 2); ao.alloc((size_t) R * d * 2);
+        h.alloc((size_t) R * 4 * d * 2);
+        const int cells = 512;
+        kc.alloc((size_t) 32 * cells * d * 2); vc.alloc((size_t) 32 * cells * d * 2);
+        bias.alloc((size_t) 3 * d * 4); bias4.alloc((size_t) 4 * d * 4); lnw.alloc((size_t) d * 4); lnb.alloc((size_t) d * 4);
+        gt.alloc(65536 * 2);
+        for (DevBuf * b : {&x, &xn, &q, &ao, &h, &bias, &bias4, &lnb, &gt}) OWK_HIP_CHECK(hipMemsetAsync(b->ptr, 0, b->bytes, s));
+        std::vector<float> ones(d, 1.0f);
+        OWK_HIP_CHECK(hipMemcpy(lnw.ptr, ones.data(), d * 4, hipMemcpyHostToDevice));
+        std::vector<int64_t> ro(R);
+        for (int r = 0; r < R; ++r) ro[r] = (int64_t) r * cells * d + 7 * 64;
+        rowoff.alloc(R * 8);
+        OWK_HIP_CHECK(hipMemcpy(rowoff.ptr, ro.data(), R * 8, hipMemcpyHostToDevice));
+        size_t fl = 0;
+        for (int N : {3 * d, d, 4 * d})
+            for (int K : {d, 4 * d}) fl = std::max(fl, std::max(gemm_ws_floats(N, K), gemm_partial_floats(N, K)));
+        part.alloc(fl * 4);
+        GemmWs ws;
+        ws.partial = part.as<float>();
+        ws.partial_floats = fl;
+        auto resid = [&](int site, const _Float16 * A, const _Float16 * Wt, int K) {
+            (void) site;
+            gemm(s, EPI_PARTIAL, R, d, K, A, K, nullptr, K, EpiParams(), &ws, Wt);
+            resid_layernorm(s, R, d, gemm_partial_splits(K), ws.partial, bias.as<float>(), x.as<float>(), lnw.as<float>(),
+                            lnb.as<float>(), 1e-5f, xn.as<_Float16>(), d);
+        };
+        auto chain = [&]() {
+            for (int l = 0; l < n_layers; ++l) {
+                const LW & L = lw[l];
+                EpiParams e1;
+                e1.bias = bias.as<float>(); e1.bias2 = bias.as<float>(); e1.scale = 0.35f;
+                e1.out16 = q.as<_Float16>(); e1.ldo = d; e1.out16b = kc.as<_Float16>(); e1.out16c = vc.as<_Float16>();
+                e1.d = d; e1.row_off = rowoff.as<int64_t>(); e1.Tpad = cells * 64;
+                gemm(s, EPI_QKV_DEC, R, 3 * d, d, xn.as<_Float16>(), d, nullptr, d, e1, &ws, L.qkv.as<_Float16>());
+                resid(3 * l, ao.as<_Float16>(), L.o.as<_Float16>(), d);
+                EpiParams e2;
+                e2.bias = bias.as<float>(); e2.out16 = q.as<_Float16>(); e2.ldo = d;
+                gemm(s, EPI_F16, R, d, d, xn.as<_Float16>(), d, nullptr, d, e2, &ws, L.cq.as<_Float16>());
+                resid(3 * l + 1, ao.as<_Float16>(), L.co.as<_Float16>(), d);
+                EpiParams e3;
+                e3.bias = bias4.as<float>(); e3.gelu_tab = gt.as<uint16_t>(); e3.out16 = h.as<_Float16>(); e3.ldo = 4 * d;
+                gemm(s, EPI_GELU_F16, R, 4 * d, d, xn.as<_Float16>(), d, nullptr, d, e3, &ws, L.m0.as<_Float16>());
+                resid(3 * l + 2, h.as<_Float16>(), L.m1.as<_Float16>(), 4 * d);
+            }
+        };
+        OWK_HIP_CHECK(hipStreamSynchronize(s));
+        hipGraph_t g = nullptr;
+        hipGraphExec_t ex = nullptr;
+        OWK_HIP_CHECK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+        chain();
+        OWK_HIP_CHECK(hipStreamEndCapture(s, &g));
+        OWK_HIP_CHECK(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
+        (void) hipGraphDestroy(g);
+        for (int i = 0; i < 2; ++i) OWK_HIP_CHECK(hipGraphLaunch(ex, s));
+        hipEvent_t e0, e1;
+        OWK_HIP_CHECK(hipEventCreate(&e0));
+        OWK_HIP_CHECK(hipEventCreate(&e1));
+        OWK_HIP_CHECK(hipEventRecord(e0, s));
+        for (int i = 0; i < iters; ++i) OWK_HIP_CHECK(hipGraphLaunch(ex, s));
+        OWK_HIP_CHECK(hipEventRecord(e1, s));
+        OWK_HIP_CHECK(hipEventSynchronize(e1));
+        float ms = 0;
+        OWK_HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
+        (void) hipEventDestroy(e0);
+        (void) hipEventDestroy(e1);
+        (void) hipGraphExecDestroy(ex);
+        OWK_HIP_CHECK(hipStreamDestroy(s));
+        return 1e3 * ms / iters / n_layers;
+    } catch (const std::exception & ex) {
+        log_msg(GGML_LOG_LEVEL_ERROR, "owk_debug_decode_chain: %s\n", ex.what());
         return -1;
     }
 }

@@ -137,8 +137,14 @@ static void host_process_logits(whisper_context * ctx, whisper_state * st, Decod
             if (lp[i] > -INFINITY) s += expf(lp[i] - lpmax);
         if (s > 0.0f) ts_lp = logf(s) + lpmax;
         const float tx = *std::max_element(lp.begin(), lp.begin() + v.beg);
-        if (ts_lp > tx)
+        if (ts_lp > tx) {
             for (int i = 0; i < v.beg; ++i) { L[i] = -INFINITY; lp[i] = -INFINITY; }
+        } else if (p.n_grammar_rules > 0) {
+            // grammar: penalise the text tokens no parse stack accepts, then log_softmax again
+            // (ref 6362-6384)
+            dec.grammar.suppress(v.id_to_token, v.eot, p.grammar_penalty, L.data());
+            host_logprobs(L, lp);
+        }
     }
     dec.probs.resize(n);
     for (int i = 0; i < n; ++i) dec.probs[i] = L[i] == -INFINITY ? 0.0f : expf(lp[i]);
@@ -259,6 +265,7 @@ struct Clip {
         int decoder_idx, seek_delta;
         bool has_ts;
         Sequence sequence;
+        Grammar grammar;
     };
     std::vector<std::vector<BeamCand>> bc_per_dec;
     std::vector<BeamCand> beam_candidates;
@@ -466,6 +473,9 @@ struct Clip {
             d.failed = false;
             d.completed = false;
             d.has_ts = false;
+            // ref 7113-7117 (a rule count of 0 leaves the grammar inactive)
+            if (p.grammar_rules != nullptr) d.grammar.init(p.grammar_rules, p.n_grammar_rules, p.i_start_rule);
+            else d.grammar = Grammar{};
         }
         prompt.clear();
         if (p.n_max_text_ctx > 0 && t_cur < HISTORY_TEMP_CUTOFF) {
@@ -528,7 +538,7 @@ struct Clip {
             } else {
                 const auto toks = sample_topk(vocab(), d, p.beam_search.beam_size);
                 for (const auto & tok : toks) {
-                    bc_per_dec[j].push_back({j, d.seek_delta, d.has_ts, d.sequence});
+                    bc_per_dec[j].push_back({j, d.seek_delta, d.has_ts, d.sequence, d.grammar});
                     bc_per_dec[j].back().sequence.tokens.push_back(tok);
                     bc_per_dec[j].back().sequence.sum_logprobs_all += tok.plog;
                 }
@@ -556,6 +566,7 @@ struct Clip {
                 d.seek_delta = cur.seek_delta;
                 d.has_ts = cur.has_ts;
                 d.sequence = cur.sequence;
+                d.grammar = cur.grammar;
                 st->kv.seq_cp(cur.decoder_idx, MAX_DECODERS + j, -1, -1);
             }
             for (int j = 0; j < n_decoders_cur; ++j) {
@@ -583,6 +594,7 @@ struct Clip {
                 result_len = i + 1;
                 d.has_ts = true;
             }
+            d.grammar.accept(vocab().id_to_token[token.id]);  // ref 7391
             if (token.id == vocab().eot || (p.max_tokens > 0 && i >= p.max_tokens) ||
                 (d.has_ts && seek + d.seek_delta + delta_min >= seek_end)) {
                 if (result_len == 0 && !p.no_timestamps) {
@@ -686,7 +698,8 @@ struct Clip {
             std::string text;
             bool speaker_turn_next = false;
             for (int k = 0; k < (int) toks.size(); k++) {
-                if (p.print_special || toks[k].id < eot) text += vocab().id_to_token[toks[k].id];
+                // C string, as the reference's whisper_token_to_str (ref 7651): a NUL-byte token adds nothing
+                if (p.print_special || toks[k].id < eot) text += vocab().id_to_token[toks[k].id].c_str();
                 if (p.tdrz_enable && toks[k].id == vocab().solm) speaker_turn_next = true;
                 if (toks[k].id > beg && !p.single_segment) {
                     const int64_t t1 = seek + 2 * (toks[k].tid - beg);
@@ -818,10 +831,6 @@ int full_batch(whisper_context * ctx, whisper_state ** states, const whisper_ful
     const whisper_full_params & params = params_v[0];
     // params.vad is whisper_full's pre-pass (whisper_api.cpp); like the reference's
     // whisper_full_with_state, the per-state path ignores it
-    if (params.n_grammar_rules > 0) {
-        log_msg(GGML_LOG_LEVEL_ERROR, "whisper_full: grammar-constrained decoding is not supported by this engine build\n");
-        return -1;
-    }
     const Model & M = *ctx->model;
     OWK_HIP_CHECK(hipSetDevice(M.device));
     whisper_state * st0 = states[0];
@@ -853,7 +862,8 @@ int full_batch(whisper_context * ctx, whisper_state ** states, const whisper_ful
         k.pcm = samples[c];
         k.n = n_samples[c];
         k.slot = c;
-        k.device_logits = params.logits_filter_callback == nullptr;
+        // a logits_filter_callback or a grammar needs the logits on the host mid-filter (ref 6254, 6363)
+        k.device_logits = params.logits_filter_callback == nullptr && params.n_grammar_rules == 0;
         k.suppress_eot = ext && ext->suppress_eot;
         k.pcm_on_device = ext && ext->samples_on_device;
         whisper_state * st = states[c];

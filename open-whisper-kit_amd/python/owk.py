@@ -194,6 +194,7 @@ def load(path: str | None = None) -> C.CDLL:
     L.whisper_lang_max_id.restype = ip
     L.whisper_log_set.argtypes = [vp, vp]
     L.owk_prof_enable.argtypes = [vp, ip]
+    L.owk_prof_select.argtypes = [vp, C.c_char_p]
     L.owk_prof_reset.argtypes = [vp]
     L.owk_prof_read.argtypes = [vp, C.c_char_p, C.POINTER(C.c_double), C.POINTER(C.c_long)]
     L.owk_prof_work.argtypes = [vp, C.c_char_p, C.POINTER(C.c_double), C.POINTER(C.c_double)]

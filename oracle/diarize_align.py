@@ -117,3 +117,19 @@ def align(words, segments, fill_nearest=False, sentence_smoothing=True, max_word
 def rttm_generate(segments, filename):
     return "\n".join(f"SPEAKER {filename} 1 {float(f32(s[1])):.2f} {float(f32(f32(s[2]) - f32(s[1]))):.2f} "
                      f"<NA> <NA> {s[0]} <NA> <NA>" for s in segments)
+
+
+def rttm_parse(text):
+    """RTTMParser.parse (ref RTTMParser.swift:13-50): lines of >= 8 space-separated fields, Float start and
+    duration, end = start + duration (f32), sorted by start (stable) -> [(speaker, start, end)]."""
+    out = []
+    for line in text.split("\n"):
+        f = [x for x in line.split(" ") if x]
+        if len(f) < 8:
+            continue
+        try:
+            start, dur = f32(float(f[3])), f32(float(f[4]))
+        except ValueError:
+            continue
+        out.append((f[7], start, f32(start + dur)))
+    return sorted(out, key=lambda s: s[1])

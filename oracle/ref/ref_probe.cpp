@@ -10,6 +10,7 @@
 //   - decoder logits                 (whisper_decode_internal, whisper.cpp:2848-2978)
 //   - whisper_full with a flat config struct (whisper_full_with_state, whisper.cpp:6827-7776)
 #include "whisper.cpp"
+#include "grammar-parser.h"
 
 #include <mutex>
 
@@ -314,8 +315,25 @@ long ref_capture_get(int i, int * op, int64_t * ne, float * out, long cap) {
 // ggml's CPU mul_mat on one weight tensor: w (N rows of K, ggml type wtype, raw blocks)
 // times a (M rows of K, f32) -> out [M][N] f32. Pins the quantized-weight GEMM numerics.
 int ref_mul_mat(int wtype, const void * w, int N, int K, const float * a, int M, float * out, int n_threads) {
+    if (M <= 0 || N <= 0 || K <= 0 || n_threads <= 0) return -1;
     const size_t wbytes = ggml_row_size((ggml_type) wtype, K) * N;
-    ggml_init_params ip = {wbytes + (size_t) M * K * 4 + (size_t) M * N * 4 + 64 * ggml_tensor_overhead() +
+    // the context holds the operands, the result, the graph AND the compute plan's work buffer
+    // (ggml_graph_compute_with_ctx allocates it there: src1 converted to the weight's vec_dot
+    // type, M rows of K, plus per-thread padding), sized from the operands -- planned on a
+    // metadata-only context first
+    size_t work = 0;
+    {
+        ggml_init_params mp = {64 * ggml_tensor_overhead() + ggml_graph_overhead(), nullptr, true};
+        ggml_context * mc = ggml_init(mp);
+        if (!mc) return -1;
+        ggml_tensor * y0 = ggml_mul_mat(mc, ggml_new_tensor_2d(mc, (ggml_type) wtype, K, N),
+                                        ggml_new_tensor_2d(mc, GGML_TYPE_F32, K, M));
+        ggml_cgraph * g0 = ggml_new_graph(mc);
+        ggml_build_forward_expand(g0, y0);
+        work = ggml_graph_plan(g0, n_threads, nullptr).work_size;
+        ggml_free(mc);
+    }
+    ggml_init_params ip = {wbytes + (size_t) M * K * 4 + (size_t) M * N * 4 + work + 64 * ggml_tensor_overhead() +
                                ggml_graph_overhead() + (1 << 20), nullptr, false};
     ggml_context * c = ggml_init(ip);
     if (!c) return -1;
@@ -330,6 +348,50 @@ int ref_mul_mat(int wtype, const void * w, int N, int K, const float * a, int M,
     if (rc == 0) memcpy(out, y->data, (size_t) M * N * 4);
     ggml_free(c);
     return rc;
+}
+
+// GBNF grammar (ref examples/grammar-parser.cpp, compiled into this probe) -> the reference's own
+// grammar engine (whisper_grammar_init / _accept_token / whisper_suppress_invalid_grammar,
+// whisper.cpp:5498-5905): parse `gbnf`, start at rule `root`, accept `accept` tokens, then return
+// the ids the constraint penalises (penalty 1 on zero logits). Also the parsed rules, flattened:
+// rule r's elements at [rule_off[r], rule_off[r + 1]) of (types, values), END included.
+int ref_grammar_parse(const char * gbnf, const char * root, int * types, uint32_t * values, int cap, int * rule_off,
+                      int cap_rules, int * n_rules, int * i_start) {
+    const auto st = grammar_parser::parse(gbnf);
+    if (st.rules.empty() || !st.symbol_ids.count(root)) return -1;
+    int n = 0;
+    *n_rules = (int) st.rules.size();
+    *i_start = (int) st.symbol_ids.at(root);
+    for (size_t r = 0; r < st.rules.size(); ++r) {
+        if ((int) r < cap_rules) rule_off[r] = n;
+        for (const auto & e : st.rules[r]) {
+            if (n < cap) { types[n] = (int) e.type; values[n] = e.value; }
+            ++n;
+        }
+    }
+    if ((int) st.rules.size() < cap_rules) rule_off[st.rules.size()] = n;
+    return n;
+}
+
+int ref_grammar_rejects(void * vctx, const char * gbnf, const char * root, const int * accept, int n_accept, int * out,
+                        int cap) {
+    whisper_context * ctx = (whisper_context *) vctx;
+    const auto st = grammar_parser::parse(gbnf);
+    if (st.rules.empty() || !st.symbol_ids.count(root)) return -1;
+    auto rules = st.c_rules();
+    whisper_grammar g = whisper_grammar_init(rules.data(), rules.size(), st.symbol_ids.at(root));
+    for (int i = 0; i < n_accept; ++i) whisper_grammar_accept_token(*ctx, g, accept[i]);
+    whisper_full_params p = whisper_full_default_params(WHISPER_SAMPLING_GREEDY);
+    p.grammar_penalty = 1.0f;
+    std::vector<float> logits(whisper_n_vocab(ctx), 0.0f);
+    whisper_suppress_invalid_grammar(*ctx, p, logits, g);
+    int n = 0;
+    for (int id = 0; id < (int) logits.size(); ++id)
+        if (logits[id] != 0.0f) {
+            if (n < cap) out[n] = id;
+            ++n;
+        }
+    return n;
 }
 
 } // extern "C"

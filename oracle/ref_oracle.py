@@ -12,7 +12,7 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-REF_LIB = os.path.join(HERE, "_ref", "libwhisper_ref.so")
+REF_LIB = os.environ.get("OWK_REF_LIB", os.path.join(HERE, "_ref", "libwhisper_ref.so"))
 
 
 class RefFullCfg(C.Structure):

@@ -7,7 +7,12 @@ OUR libwhisper.so are built by `make callers` (open-whisper-kit_amd/lib/callers/
 tests/test_callers.py runs that one on the GPU and compares its full JSON output with this file.
 
 Cases: the CLI defaults (beam 5 + best-of 5, temperature fallback; ref cli.cpp:45-84) and `-nf`
-(no fallback), each as `-ojf` full JSON (segments, tokens with ids/p/t0/t1).
+(no fallback), each as `-ojf` full JSON (segments, tokens with ids/p/t0/t1); and GBNF
+grammar-constrained decoding (`--grammar <text> --grammar-rule root`, parsed by the reference's
+examples/grammar-parser.cpp inside the CLI; beam search as the CLI selects it with a grammar,
+ref cli.cpp:1170-1171, 1225-1238; constraint logic ref src/whisper.cpp:5498-5905): a word list
+with alternation and repetition, and character classes with ranges and a negated class (the
+latter ends on a partial UTF-8 byte token), without and with timestamps.
 
 Usage (container with /root/reference):  python tests/golden/make_golden_cli.py
 """
@@ -24,7 +29,14 @@ import owk_synth as S  # noqa: E402
 OUT = os.path.dirname(os.path.abspath(__file__))
 SEED = 1234
 MODEL = "tiny.en"
-CASES = {"default": [], "nofallback": ["-nf"]}
+GRAMMARS = {
+    "words": 'root ::= (" " word ",")+ " " word "."\nword ::= "red" | "green" | "blue" | "yellow" | "purple"\n',
+    "moves": 'root ::= move (" " move)* [^a-z0-9 ]\nmove ::= " "? [a-h] [1-8] | " castle"\n',
+}
+CASES = {"default": [], "nofallback": ["-nf"],
+         "grammar_words": ["-nf", "-nt", "--grammar", GRAMMARS["words"], "--grammar-rule", "root"],
+         "grammar_moves": ["-nf", "-nt", "--grammar", GRAMMARS["moves"], "--grammar-rule", "root", "--grammar-penalty", "50"],
+         "grammar_words_ts": ["-nf", "--grammar", GRAMMARS["words"], "--grammar-rule", "root"]}
 
 
 def run_cli(exe, model_path, wav, extra, workdir):

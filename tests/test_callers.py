@@ -78,7 +78,7 @@ def _cli_json(model_path, extra, tmp_path):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("case", ["default", "nofallback"])
+@pytest.mark.parametrize("case", ["default", "nofallback", "grammar_words", "grammar_moves", "grammar_words_ts"])
 def test_whisper_cli_configs0(case, model_path, tmp_path):
     g = json.load(open(os.path.join(GOLDEN, "cli_golden.json")))
     assert g["model"] == "tiny.en"

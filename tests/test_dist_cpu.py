@@ -85,9 +85,10 @@ class _CpuRunner:
 
         return [bench.MAX_TOKENS + 1] * self.B if self.steps else []
 
-    def profile(self):
-        return {"attn_cross": {"ms": 2.0, "launches": 4, "flops": 1e9, "bytes": 8e9},
+    def profile(self, only=None):
+        allc = {"attn_cross": {"ms": 2.0, "launches": 4, "flops": 1e9, "bytes": 8e9},
                 "gemm_enc": {"ms": 1.0, "launches": 2, "flops": 2e12, "bytes": 1e8}}
+        return {c: v for c, v in allc.items() if not only or c in only}
 
     def cpu_baseline(self):
         raise AssertionError("world > 1: no cpu baseline")

@@ -1,0 +1,174 @@
+"""BASELINE configs[4] pinned at its workload against the reference (tests/golden/make_golden_c4.py ->
+c4_golden.json / .npz): full-depth synthetic large-v3, flash_attn = false, DTW token timestamps
+(WHISPER_AHEADS_LARGE_V3), ONE whisper_full over 60 s of real speech (the sequential window loop with
+seek advance and prompt carry, no_context = false, token_timestamps; ref src/whisper.cpp:7034-7769,
+8837-8998), streaming SortFormer in 2 s blocks (ref streaming-sortformer/src/sortformer.cpp:2776-3265)
+and the DiarizationAligner (ref Sources/OpenWhisperKit/DiarizationAligner.swift) over the tokens and
+the RTTM.
+
+* free run: token ids, segments, token timestamps identical up to a near-tie bounded by the measured
+  logit error of this soft_max context (parity_util, first window's prefill / step-1 logits);
+* teacher-forced onto the reference's per-window decoded tokens (parity_util.Forcer): the same
+  tokens, and every token's t_dtw, t0 and t1 EXACTLY the reference's;
+* streaming diarization: per-feed frame counts identical, probabilities within 2x the reference's
+  own 1e-7-perturbation noise floor, RTTM text identical;
+* alignment of the teacher-forced tokens with the GPU RTTM (libwhisper.so's C++ aligner): every
+  word's speaker and every utterance identical to the reference pipeline's.
+"""
+import ctypes as C
+import json
+import os
+
+import numpy as np
+import pytest
+
+import owk
+from parity_util import TIE_FACTOR, Forcer, compare_segments
+
+pytestmark = pytest.mark.gpu
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+@pytest.fixture(scope="module")
+def c4():
+    path = os.path.join(GOLDEN, "c4_golden.json")
+    if not os.path.exists(path):
+        pytest.skip("c4_golden.json not generated")
+    return json.load(open(path)), np.load(os.path.join(GOLDEN, "c4_golden.npz"))
+
+
+@pytest.fixture(scope="module")
+def test60():
+    import owk_synth as S
+
+    return S.read_wav_16k_mono(os.path.join(GOLDEN, "sf_test60.wav"))
+
+
+@pytest.fixture(scope="module")
+def w4(c4):
+    import owk_synth as S
+
+    meta, _ = c4
+    path = S.ensure_model("large-v3", meta["seed"], os.environ.get("OWK_MODEL_CACHE", "/tmp/owk_models"))
+    assert S.file_sha256(path) == meta["model_sha256"], "synthetic large-v3 differs from the fixture's"
+    owk.quiet()
+    w = owk.Whisper(path, flash_attn=False, dtw_preset=meta["aheads_preset"])
+    w.L.whisper_token_to_str.restype = C.c_char_p
+    w.L.whisper_token_to_str.argtypes = [C.c_void_p, C.c_int]
+    yield w
+    w.close()
+
+
+def _logit_error(w, meta, arr, pcm):
+    """max |logit - reference| of the first window's prefill and step-1 top-64 logits"""
+    L = w.L
+    st = w.new_state()
+    assert L.whisper_pcm_to_mel_with_state(w.ctx, st, owk.fptr(pcm), len(pcm), 1) == 0
+    assert L.whisper_encode_with_state(w.ctx, st, 0, 1) == 0
+    prompt = meta["results"]["prefill_prompt"]
+    toks = (C.c_int32 * len(prompt))(*prompt)
+    assert L.whisper_decode_with_state(w.ctx, st, toks, len(prompt), 0, 1) == 0
+    lg = np.ctypeslib.as_array(L.whisper_get_logits_from_state(st), shape=(len(prompt) * w.n_vocab,))
+    lg = lg[(len(prompt) - 1) * w.n_vocab:].copy()
+    e1 = float(np.abs(lg[arr["prefill_top_idx"]] - arr["prefill_top_val"]).max())
+    one = (C.c_int32 * 1)(meta["results"]["step1_token"])
+    assert L.whisper_decode_with_state(w.ctx, st, one, 1, len(prompt), 1) == 0
+    lg2 = np.ctypeslib.as_array(L.whisper_get_logits_from_state(st), shape=(w.n_vocab,)).copy()
+    e2 = float(np.abs(lg2[arr["step1_top_idx"]] - arr["step1_top_val"]).max())
+    return max(e1, e2)
+
+
+def _params(w, meta):
+    return w.params(0, **meta["params"])
+
+
+def test_configs4_transcription(c4, w4, test60):
+    meta, arr = c4
+    want = meta["results"]["full"]
+    eps = _logit_error(w4, meta, arr, test60)
+    print(f"[c4] measured logit error {eps:.2e}")
+    st = w4.new_state()
+    assert w4.full(st, test60, _params(w4, meta)) == want["ret"]
+    got = w4.segments(st)
+    assert len(want["segments"]) > 1 and want["segments"][-1]["t1"] > 3000
+    compare_segments(got, want["segments"], "c4/free", tie=TIE_FACTOR * eps)
+
+
+def _forced_run(w, meta, pcm):
+    p = _params(w, meta)
+    force = Forcer(meta["results"]["windows"], w.L.whisper_token_eot(w.ctx), w.n_vocab, owk.TokenData)
+    p.logits_filter_callback = C.cast(force.cfunc, C.c_void_p)
+    st = w.new_state()
+    assert w.full(st, pcm, p) == meta["results"]["full"]["ret"]
+    return w.segments(st)
+
+
+def test_configs4_dtw_teacher_forced(c4, w4, test60):
+    meta, _ = c4
+    want = meta["results"]["full"]["segments"]
+    got = _forced_run(w4, meta, test60)
+    r_ids = [t[0] for s in want for t in s["tokens"]]
+    assert [t[0] for s in got for t in s["tokens"]] == r_ids, "teacher-forced decode left the reference tokens"
+    assert [(s["t0"], s["t1"]) for s in got] == [(s["t0"], s["t1"]) for s in want]
+    g = [(t[6], t[7], t[8]) for s in got for t in s["tokens"]]
+    r = [(t[6], t[7], t[8]) for s in want for t in s["tokens"]]
+    diff = [(i, a, b) for i, (a, b) in enumerate(zip(g, r)) if a != b]
+    print(f"[c4] {len(r_ids)} tokens over {len(meta['results']['windows'])} windows; (t0, t1, t_dtw) differ on "
+          f"{len(diff)}: {diff[:6]}")
+    assert not diff, f"token timestamps differ: {diff[:10]}"
+
+
+def _stream(pcm, block):
+    import sortformer as SF
+    import sortformer_synth as SS
+
+    mm = json.load(open(os.path.join(GOLDEN, "sf_golden.json")))
+    path = os.path.join(os.environ.get("OWK_MODEL_CACHE", "/tmp/owk_models"), f"synth-sortformer-s{mm['seed']}.gguf")
+    if not os.path.exists(path):
+        assert SS.write_model(path, mm["seed"]) == mm["sha256"]
+    sf = SF.Sortformer(path)
+    st = sf.stream("2s")
+    outs, counts = [], []
+    for i in range(0, len(pcm), block):
+        o = st.feed(pcm[i:i + block])
+        outs.append(o)
+        counts.append(int(o.shape[0]))
+    fl = st.flush()
+    outs.append(fl)
+    counts.append(int(fl.shape[0]))
+    st.close()
+    sf.close()
+    return np.concatenate(outs, 0), counts
+
+
+def test_configs4_stream_and_align(c4, w4, test60):
+    import sortformer as SF
+
+    meta, arr = c4
+    probs, counts = _stream(test60, meta["block"])
+    assert counts == meta["results"]["stream_counts"]
+    ref = arr["stream_probs"]
+    err = np.abs(probs.astype(np.float64) - ref)
+    fl = meta["results"]["noise_floor/stream"]
+    print(f"[c4] stream probs max|diff| {err.max():.2e} mean {err.mean():.2e} (reference floor {fl})")
+    assert err.max() <= 2 * fl["max"] + 1e-6 and err.mean() <= 2 * fl["mean"] + 1e-7
+    rttm = SF.to_rttm(probs, 0.5, 11, "audio")
+    assert rttm == meta["results"]["rttm"], "RTTM differs from the reference's"
+
+    # aligner over the teacher-forced tokens (Swift WordTiming per token) and the GPU RTTM
+    got = _forced_run(w4, meta, test60)
+    words = []
+    for s in got:
+        for t in s["tokens"]:
+            txt = w4.L.whisper_token_to_str(w4.ctx, t[0]).decode("utf-8", "replace")
+            words.append((txt, float(np.float32(t[6]) / np.float32(100.0)), float(np.float32(t[7]) / np.float32(100.0)),
+                          float(t[2])))
+    want_words = meta["results"]["words"]
+    assert [(x[0], x[1], x[2]) for x in words] == [(x[0], x[1], x[2]) for x in want_words]
+    al = owk.align(words, owk.rttm_parse(rttm))
+    exp = meta["results"]["aligned"]
+    assert [x[3] for x in al["words"]] == exp["speakers"]
+    assert [(u["speaker"], u["words"][0], len(u["words"])) for u in al["segments"]] == [tuple(u) for u in exp["utterances"]]
+    assert al["text"] == exp["text"]
+    print(f"[c4] aligned {len(words)} words into {len(al['segments'])} utterances, identical to the reference")

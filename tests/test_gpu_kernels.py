@@ -129,3 +129,4 @@ def test_gemm256_epilogue_matches_128(case):
     print(f"{case}: max|256 - 128| = {diff:.3g}")
     assert diff >= 0
     assert diff <= 1e-6, f"{case}: epilogues differ by {diff}"
+
