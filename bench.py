@@ -22,11 +22,12 @@ Timed region: decoder passes replay captured HIP graphs (no per-kernel instrumen
 Roofline: extra steps of the same workload with HIP events on the engine stream (eager launches:
 captured graphs cannot carry timing events). One step with an event pair around every launch gives
 the per-class table (`phases`); then each of the TOP_CLASSES largest classes is timed in a step of
-its own where only its launches carry events (owk_prof_select), so the host stays ahead of the
-device and each pair brackets its kernel alone -- an eager all-class step inflates short kernels by
-the host launch gaps. `roofline` reports the class with the largest such device time, its average
-launch time and, for the cross-check, the same kernel's average from the committed rocprofv3
---kernel-trace --stats summary of this command (profiles/, ROCPROF_STATS).
+its own where only its launches are timed (owk_prof_select), with events bound to the kernel
+dispatches themselves (hipExtLaunchKernel start/stop events: the first bracketed kernel's start to
+the last one's end, the timestamps rocprofv3 reports, no hipEventRecord marker packets in the
+interval). `roofline` reports the class with the largest such device time, its average launch time
+and, for the cross-check, the same kernel's average from the committed rocprofv3 --kernel-trace
+--stats summary of this command (profiles/, ROCPROF_STATS).
 
 cpu_baseline: the reference ggml CPU path (oracle/_ref/libwhisper_ref.so, compiled from the
 reference sources by oracle/ref/Makefile) runs ONE clip of the same workload on this host's
@@ -314,14 +315,13 @@ def roofline(classes, ms_per_step, alone=None):
     roof["traffic_unit"] = "bytes/launch (PMC FETCH_SIZE x2, profiles/pmc_fetch_summary.txt)"
     roof["kernel_class"] = dom
     roof["kernel"] = CLASS_KERNEL_NAME.get(dom, dom)
-    roof["measured"] = ("HIP events on the engine stream around this class's launches only, in a step of its own "
-                        "(eager launches, owk_prof_select), minus the mean interval of an empty event pair recorded "
-                        "after each bracketed launch" if alone else
+    roof["measured"] = ("HIP events bound to this class's kernel dispatches on the engine stream "
+                        "(hipExtLaunchKernel start/stop events), in a step of its own where only this class is timed "
+                        "(eager launches, owk_prof_select)" if alone else
                         "HIP events on the engine stream around every launch, one extra step (eager launches)")
     roof["avg_launch_ms"] = round(avg_ms, 5)
-    if "marker_us" in d:
-        roof["event_marker_pair_us"] = round(d["marker_us"], 3)
-        roof["avg_launch_ms_raw_events"] = round(d["event_ms_raw"] / max(1, d["launches"]), 5)
+    if alone and dom in classes:
+        roof["avg_launch_ms_marker_events"] = round(classes[dom]["ms"] / max(1, classes[dom]["launches"]), 5)
     roof["launches"] = d["launches"]
     rp = rocprof_avg_ms(dom)
     roof["rocprof_avg_launch_ms"] = rp
@@ -382,20 +382,12 @@ def main(argv=None, runner=None):
             if c not in got:
                 continue
             v = dict(got[c])
-            # subtract what the two markers add to each bracketed interval: the mean of the empty
-            # event pairs recorded right after every bracketed launch of the same step
-            cal = got.get("_event_pair")
-            v["event_ms_raw"] = v["ms"]
-            if cal and cal["launches"]:
-                v["marker_us"] = 1e3 * cal["ms"] / cal["launches"]
-                v["ms"] = max(0.0, v["ms"] - v["launches"] * cal["ms"] / cal["launches"])
             alone[c] = v
         roof = roofline(classes, 1e3 * dt / args.steps, alone or None)
         if rank == 0:
             for c, v in alone.items():
                 log(f"[bench] alone {c:16s} {v['ms']:10.2f} ms  launches {v['launches']:7d}  "
-                    f"avg {1e3 * v['ms'] / max(1, v['launches']):8.2f} us (raw {1e3 * v['event_ms_raw'] / max(1, v['launches']):8.2f}"
-                    f", marker pair {v.get('marker_us', 0):.2f} us; all-class step "
+                    f"avg {1e3 * v['ms'] / max(1, v['launches']):8.2f} us (marker events in the all-class step "
                     f"{1e3 * classes[c]['ms'] / max(1, classes[c]['launches']):8.2f} us)")
         if rank == 0:
             tot = sum(v["ms"] for v in classes.values())

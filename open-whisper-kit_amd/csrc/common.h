@@ -1,6 +1,7 @@
 // Shared host/device definitions for the MI355X (gfx950) Whisper engine.
 #pragma once
 
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -87,4 +88,29 @@ struct PinnedBuf {
     template <typename T> T * as() const { return (T *) ptr; }
 };
 
+// Kernel-bound timing (the selected-class measurement of owk_prof_select / bench.py): while armed,
+// launches go through hipExtLaunchKernel with the events bound to the dispatches themselves, so
+// hipEventElapsedTime(start, stop) spans the first bracketed kernel's start to the last one's end --
+// the dispatch timestamps rocprofv3 reports, without the marker packets of hipEventRecord
+struct KTimer {
+    hipEvent_t start = nullptr, stop = nullptr;  // stop == nullptr: disarmed
+    int launches = 0;
+};
+inline KTimer * ktimer() {
+    static thread_local KTimer t;
+    return &t;
+}
+
 } // namespace owk
+
+#define OWK_LAUNCH(K, G, B, SHM, ST, ...)                                                            \
+    do {                                                                                             \
+        ::owk::KTimer * owk_kt_ = ::owk::ktimer();                                                   \
+        if (__builtin_expect(owk_kt_->stop != nullptr, 0)) {                                         \
+            hipExtLaunchKernelGGL(K, G, B, SHM, ST, owk_kt_->launches == 0 ? owk_kt_->start : nullptr, \
+                                  owk_kt_->stop, 0, __VA_ARGS__);                                    \
+            owk_kt_->launches++;                                                                     \
+        } else {                                                                                     \
+            hipLaunchKernelGGL(K, G, B, SHM, ST, __VA_ARGS__);                                       \
+        }                                                                                            \
+    } while (0)

@@ -64,21 +64,35 @@ ProfScope::ProfScope(Prof * p_, hipStream_t s_, const char * name, double flops_
     if (!p->only.empty() && std::find(p->only.begin(), p->only.end(), name) == p->only.end()) return;
     cls = p->cls_id(name);
     a = p->ev();
+    if (!p->only.empty()) {
+        // selected classes: events bound to the class's own kernel dispatches (KTimer), no markers
+        KTimer * kt = ktimer();
+        if (kt->stop) throw std::runtime_error("prof: nested selected-class scopes");
+        kt->start = a;
+        kt->stop = p->ev();
+        kt->launches = 0;
+        return;
+    }
     OWK_HIP_CHECK(hipEventRecord(a, s));
 }
 
 ProfScope::~ProfScope() {
     if (cls < 0) return;
-    hipEvent_t b = p->ev();
-    (void) hipEventRecord(b, s);
-    p->pending.push_back({cls, a, b, flops, bytes});
     if (!p->only.empty()) {
-        // calibration: an event pair with nothing between, right after the bracketed launch (class
-        // "_event_pair"): what the markers themselves add to every bracketed interval
-        hipEvent_t c = p->ev(), d = p->ev();
-        (void) hipEventRecord(c, s);
-        (void) hipEventRecord(d, s);
-        p->pending.push_back({p->cls_id("_event_pair"), c, d, 0.0, 0.0});
+        KTimer * kt = ktimer();
+        const hipEvent_t b = kt->stop;
+        const int n = kt->launches;
+        *kt = KTimer{};
+        if (n > 0) {
+            p->pending.push_back({cls, a, b, flops, bytes});
+        } else {  // a scope that launched nothing: no record
+            p->pool.push_back(a);
+            p->pool.push_back(b);
+        }
+    } else {
+        hipEvent_t b = p->ev();
+        (void) hipEventRecord(b, s);
+        p->pending.push_back({cls, a, b, flops, bytes});
     }
     if (p->pending.size() > 4096) p->flush();
 }

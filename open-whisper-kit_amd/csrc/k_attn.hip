@@ -336,14 +336,14 @@ __global__ __launch_bounds__(256, 2) void k_attn_encoder_sm(const _Float16 * __r
 void attn_encoder_softmax(hipStream_t s, const _Float16 * q, const _Float16 * k, const _Float16 * vt, int n_clips, int T,
                           int Tpad, int H, float scale, _Float16 * out, float * out32) {
     if (Tpad < ((T + FA_KT - 1) / FA_KT) * FA_KT) throw std::runtime_error("attn_encoder_softmax: Tpad too small");
-    hipLaunchKernelGGL(k_attn_encoder_sm, dim3((T + 63) / 64, H, n_clips), dim3(256), 0, s, q, k, vt, T, Tpad, H, scale,
+    OWK_LAUNCH(k_attn_encoder_sm, dim3((T + 63) / 64, H, n_clips), dim3(256), 0, s, q, k, vt, T, Tpad, H, scale,
                        out, out32);
 }
 
 void attn_encoder(hipStream_t s, const _Float16 * q, const _Float16 * k, const _Float16 * vt, int n_clips, int T,
                   int Tpad, int H, float scale, int n_zero_pad, _Float16 * out, float * out32) {
     if (Tpad < ((T + FA_KT - 1) / FA_KT) * FA_KT) throw std::runtime_error("attn_encoder: Tpad too small");
-    hipLaunchKernelGGL(k_attn_encoder, dim3((T + 63) / 64, H, n_clips), dim3(256), 0, s, q, k, vt, T, Tpad, H, scale,
+    OWK_LAUNCH(k_attn_encoder, dim3((T + 63) / 64, H, n_clips), dim3(256), 0, s, q, k, vt, T, Tpad, H, scale,
                        n_zero_pad, out, out32);
 }
 
@@ -862,10 +862,10 @@ void attn_decoder_softmax(hipStream_t s, const _Float16 * q, int ldq, const _Flo
         return !(v && atoi(v) == 0);
     }();
     if (wide_ok && n_rows * H <= 128)
-        hipLaunchKernelGGL(k_attn_softmax<1024>, dim3(H, n_rows), dim3(1024), 0, s, q, ldq, kbase, vbase, ld_kv, hs, rows_dev,
+        OWK_LAUNCH(k_attn_softmax<1024>, dim3(H, n_rows), dim3(1024), 0, s, q, ldq, kbase, vbase, ld_kv, hs, rows_dev,
                            key_idx, scale, out, ldo, amap, cap, cap_rows, out32);
     else
-        hipLaunchKernelGGL(k_attn_softmax<256>, dim3(H, n_rows), dim3(256), 0, s, q, ldq, kbase, vbase, ld_kv, hs, rows_dev,
+        OWK_LAUNCH(k_attn_softmax<256>, dim3(H, n_rows), dim3(256), 0, s, q, ldq, kbase, vbase, ld_kv, hs, rows_dev,
                            key_idx, scale, out, ldo, amap, cap, cap_rows, out32);
 }
 
@@ -877,7 +877,7 @@ void attn_cross_kernel(hipStream_t s, int which, const _Float16 * q, int ldq, co
                        _Float16 * out, int ldo) {
     if (n_rows <= 0) return;
     if (which != 1) throw std::runtime_error("attn_cross_kernel: only the one-wave kernel (1) exists");
-    hipLaunchKernelGGL((k_attn_step<false, true>), dim3(H, n_rows), dim3(64), 0, s, q, ldq, kbase, vbase, 64, hs, rows_dev,
+    OWK_LAUNCH((k_attn_step<false, true>), dim3(H, n_rows), dim3(64), 0, s, q, ldq, kbase, vbase, 64, hs, rows_dev,
                        nullptr, scale, out, ldo, nullptr, nullptr, nullptr);
 }
 
@@ -889,21 +889,21 @@ void attn_decoder(hipStream_t s, const _Float16 * q, int ldq, const _Float16 * k
     if (any_one_chunk) {
         if (key_idx && oc_listed) {
             if (max_keys > AS_MAX_LIST) throw std::runtime_error("attn_decoder: too many listed keys");
-            hipLaunchKernelGGL((k_attn_step<true, false>), dim3(H, n_rows), dim3(64), 0, s, q, ldq, kbase, vbase, ld_kv, hs,
+            OWK_LAUNCH((k_attn_step<true, false>), dim3(H, n_rows), dim3(64), 0, s, q, ldq, kbase, vbase, ld_kv, hs,
                                rows_dev, key_idx, scale, out, ldo, out32, q8, q8d);
         } else {
             // cross attention (no cell lists): the once-per-step K/V stream, one wave per (row, head)
             if (!key_idx)
-                hipLaunchKernelGGL((k_attn_step<false, true>), dim3(H, n_rows), dim3(64), 0, s, q, ldq, kbase, vbase, ld_kv,
+                OWK_LAUNCH((k_attn_step<false, true>), dim3(H, n_rows), dim3(64), 0, s, q, ldq, kbase, vbase, ld_kv,
                                    hs, rows_dev, key_idx, scale, out, ldo, out32, q8, q8d);
             else
-                hipLaunchKernelGGL((k_attn_step<false, false>), dim3(H, n_rows), dim3(64), 0, s, q, ldq, kbase, vbase, ld_kv,
+                OWK_LAUNCH((k_attn_step<false, false>), dim3(H, n_rows), dim3(64), 0, s, q, ldq, kbase, vbase, ld_kv,
                                    hs, rows_dev, key_idx, scale, out, ldo, out32, q8, q8d);
         }
     }
     if (any_tiled) {
         if (max_keys > DA_MAX_KEYS) throw std::runtime_error("attn_decoder: too many keys");
-        hipLaunchKernelGGL(k_attn_decoder, dim3((H + 3) / 4, n_rows), dim3(256), 0, s, q, ldq, kbase, vbase, ld_kv,
+        OWK_LAUNCH(k_attn_decoder, dim3((H + 3) / 4, n_rows), dim3(256), 0, s, q, ldq, kbase, vbase, ld_kv,
                            hs, rows_dev, key_idx, H, scale, out, ldo, out32);
     }
 }

@@ -877,7 +877,7 @@ __global__ void k_tile_weights(const _Float16 * __restrict__ W, int N, int K, _F
 
 void tile_weights(hipStream_t s, const _Float16 * W, int N, int K, _Float16 * out) {
     if (K % 32) throw std::runtime_error("tile_weights: K % 32");
-    hipLaunchKernelGGL(k_tile_weights, dim3(2048), dim3(256), 0, s, W, N, K, out);
+    OWK_LAUNCH(k_tile_weights, dim3(2048), dim3(256), 0, s, W, N, K, out);
 }
 
 size_t tiled_weight_elems(int N, int K) { return (size_t) ((N + 15) / 16) * 16 * K; }
@@ -1018,7 +1018,7 @@ template <int MODE> struct LaunchBig {
     static void run(hipStream_t s, int M, int N, int K, const _Float16 * A, int lda, const _Float16 * W, int ldw,
                     const EpiParams & ep) {
         const int nbm = (M + GB_M - 1) / GB_M, nbn = (N + GB_N - 1) / GB_N;
-        hipLaunchKernelGGL(k_gemm_big<MODE>, dim3(nbm * nbn), dim3(256), 0, s, M, N, K, A, lda, W, ldw, ep);
+        OWK_LAUNCH(k_gemm_big<MODE>, dim3(nbm * nbn), dim3(256), 0, s, M, N, K, A, lda, W, ldw, ep);
     }
 };
 // 256x256 kernel selection: OWK_GEMM256 (default 1; 0 forces the 128x128 tile), overridden per
@@ -1038,13 +1038,13 @@ template <int MODE> struct Launch256 {
             // one launch of C tiles: the V columns need them (transposed image, 4 consecutive key
             // positions per lane), and splitting Q/K off as C^T tiles measured slower in all
             // (605 + 241 us against 623 us: two tails and A read twice; profiles/r02n_mfma_util.txt)
-            hipLaunchKernelGGL((k_gemm_256<MODE, 4, false>), dim3(nbm * nbn), dim3(512), 0, s, M, N, K, A, lda, W, ldw, e);
+            OWK_LAUNCH((k_gemm_256<MODE, 4, false>), dim3(nbm * nbn), dim3(512), 0, s, M, N, K, A, lda, W, ldw, e);
             return;
         }
         if (gemm256_mode() == 5)
-            hipLaunchKernelGGL((k_gemm_256<MODE, 5>), dim3(nbm * nbn), dim3(512), 0, s, M, N, K, A, lda, W, ldw, e);
+            OWK_LAUNCH((k_gemm_256<MODE, 5>), dim3(nbm * nbn), dim3(512), 0, s, M, N, K, A, lda, W, ldw, e);
         else
-            hipLaunchKernelGGL((k_gemm_256<MODE, 4>), dim3(nbm * nbn), dim3(512), 0, s, M, N, K, A, lda, W, ldw, e);
+            OWK_LAUNCH((k_gemm_256<MODE, 4>), dim3(nbm * nbn), dim3(512), 0, s, M, N, K, A, lda, W, ldw, e);
     }
 };
 template <int MODE> struct Launch256Q {
@@ -1057,13 +1057,13 @@ template <int MODE> struct Launch256Q {
         e.qs_dw = w.dwt;
         e.qs_mpad = mpad;
         e.qs_npad = w.npad;
-        hipLaunchKernelGGL(k_gemm_q16<MODE>, dim3(nbm * nbn), dim3(512), 0, s, M, N, K, q16, w.wi, e);
+        OWK_LAUNCH(k_gemm_q16<MODE>, dim3(nbm * nbn), dim3(512), 0, s, M, N, K, q16, w.wi, e);
     }
 };
 template <int MODE> struct LaunchSkinny {
     static void run(hipStream_t s, int M, int N, int K, const _Float16 * A, int lda, const _Float16 * W, int ldw,
                     const EpiParams & ep) {
-        hipLaunchKernelGGL(k_gemm_skinny<MODE>, dim3((N + 15) / 16), dim3(512), 0, s, M, N, K, A, lda, W, ldw, ep);
+        OWK_LAUNCH(k_gemm_skinny<MODE>, dim3((N + 15) / 16), dim3(512), 0, s, M, N, K, A, lda, W, ldw, ep);
     }
 };
 
@@ -1073,9 +1073,9 @@ template <int MODE> struct LaunchRows {
                    const _Float16 * Wt, const EpiParams & ep, float * part) {
         // non-temporal weight loads: every decode-step weight is read once per step (3.5 % off the
         // per-layer matmul chain, tools/chain_sweep.py: 51.6 -> 49.8 us)
-        hipLaunchKernelGGL((k_gemm_rows<MODE, MT, J, true>), grid, dim3(nw * 64), 0, s, M, N, K, A, lda, Wt, ep, part);
+        OWK_LAUNCH((k_gemm_rows<MODE, MT, J, true>), grid, dim3(nw * 64), 0, s, M, N, K, A, lda, Wt, ep, part);
         if (grid.y > 1 && MODE != EPI_PARTIAL)
-            hipLaunchKernelGGL((k_gemm_rows_reduce<MODE, MT>), dim3(grid.x), dim3(MT * 64), 0, s, M, N, (int) grid.y,
+            OWK_LAUNCH((k_gemm_rows_reduce<MODE, MT>), dim3(grid.x), dim3(MT * 64), 0, s, M, N, (int) grid.y,
                                part, ep);
     }
     static void run(hipStream_t s, int M, int N, int K, const _Float16 * A, int lda, const _Float16 * Wt,
@@ -1133,9 +1133,9 @@ void quantize_q8(hipStream_t s, const float * A32, const _Float16 * A16, int lda
     const size_t blocks = (size_t) M * (K / 32);
     const int grid = (int) std::min<size_t>((blocks * 32 + 255) / 256, 65536);
     if (A32)
-        hipLaunchKernelGGL(k_quantize_q8<float>, dim3(grid), dim3(256), 0, s, A32, lda, M, K, q, dq);
+        OWK_LAUNCH(k_quantize_q8<float>, dim3(grid), dim3(256), 0, s, A32, lda, M, K, q, dq);
     else
-        hipLaunchKernelGGL(k_quantize_q8<_Float16>, dim3(grid), dim3(256), 0, s, A16, lda, M, K, q, dq);
+        OWK_LAUNCH(k_quantize_q8<_Float16>, dim3(grid), dim3(256), 0, s, A16, lda, M, K, q, dq);
 }
 
 // Q8_0 rows of A as exact f16 integers for gemm_q16 (same rounding as k_quantize_q8) and the
@@ -1172,9 +1172,9 @@ void quantize_q8_f16(hipStream_t s, const float * A32, const _Float16 * A16, int
     const size_t blocks = (size_t) M * (K / 32);
     const int grid = (int) std::min<size_t>((blocks * 32 + 255) / 256, 65536);
     if (A32)
-        hipLaunchKernelGGL(k_quantize_q8_f16<float>, dim3(grid), dim3(256), 0, s, A32, lda, M, K, q16, dat, mpad);
+        OWK_LAUNCH(k_quantize_q8_f16<float>, dim3(grid), dim3(256), 0, s, A32, lda, M, K, q16, dat, mpad);
     else
-        hipLaunchKernelGGL(k_quantize_q8_f16<_Float16>, dim3(grid), dim3(256), 0, s, A16, lda, M, K, q16, dat, mpad);
+        OWK_LAUNCH(k_quantize_q8_f16<_Float16>, dim3(grid), dim3(256), 0, s, A16, lda, M, K, q16, dat, mpad);
 }
 
 typedef int intx4 __attribute__((ext_vector_type(4)));
@@ -1246,7 +1246,7 @@ __global__ void k_expand_q16(Q5W w, int N, int K, _Float16 * __restrict__ wi, fl
 
 void quant_expand_f16(hipStream_t s, const Q5W & w, int N, int K, _Float16 * wi, float * dwt, int npad) {
     if (K % 32 || npad < N || qf_has_m(w.fmt)) throw std::runtime_error("quant_expand_f16: shape or format");
-    hipLaunchKernelGGL(k_expand_q16, dim3(2048), dim3(256), 0, s, w, N, K, wi, dwt, npad);
+    OWK_LAUNCH(k_expand_q16, dim3(2048), dim3(256), 0, s, w, N, K, wi, dwt, npad);
 }
 
 // skinny: M <= 64 rows; one 16-column tile per block, 8 waves split the K blocks, partial
@@ -1531,7 +1531,7 @@ template <int MODE> struct LaunchQ5 {
             const int nw = (per + J - 1) / J;
             if (nw > GQ_MAXW) throw std::runtime_error("gemm_q5: decode-row plan");
             const dim3 grid((N + 15) / 16, KS), block(nw * 64);
-#define OWK_Q_ROWS(MT_, F_, J_) hipLaunchKernelGGL((k_gemm_q5_rows<MODE, MT_, F_, J_>), grid, block, 0, s, M, N, K, qa, da, w, ep)
+#define OWK_Q_ROWS(MT_, F_, J_) OWK_LAUNCH((k_gemm_q5_rows<MODE, MT_, F_, J_>), grid, block, 0, s, M, N, K, qa, da, w, ep)
 #define OWK_Q_ROWS_J(MT_, F_) do { if (J == 3) OWK_Q_ROWS(MT_, F_, 3); else OWK_Q_ROWS(MT_, F_, GQ_JMAX); } while (0)
 #define OWK_Q_ROWS_F(MT_)                                                 \
     switch (w.fmt) {                                                      \
@@ -1546,9 +1546,9 @@ template <int MODE> struct LaunchQ5 {
 #undef OWK_Q_ROWS_J
 #undef OWK_Q_ROWS
         } else if (M <= 64)
-            hipLaunchKernelGGL(k_gemm_q5_skinny<MODE>, dim3((N + 15) / 16), dim3(512), 0, s, M, N, K, qa, da, w, ep);
+            OWK_LAUNCH(k_gemm_q5_skinny<MODE>, dim3((N + 15) / 16), dim3(512), 0, s, M, N, K, qa, da, w, ep);
         else
-            hipLaunchKernelGGL(k_gemm_q5_big<MODE>, dim3(((M + 63) / 64) * ((N + 63) / 64)), dim3(256), 0, s, M, N, K,
+            OWK_LAUNCH(k_gemm_q5_big<MODE>, dim3(((M + 63) / 64) * ((N + 63) / 64)), dim3(256), 0, s, M, N, K,
                                qa, da, w, ep);
     }
 };

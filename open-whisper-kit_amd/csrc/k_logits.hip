@@ -205,7 +205,7 @@ __global__ __launch_bounds__(LG_THREADS) void k_row_max(const float * __restrict
 
 void logits_row_max(hipStream_t s, const float * logits, int n_rows, int n_vocab, float * out_dev) {
     if (n_rows <= 0) return;
-    hipLaunchKernelGGL(k_row_max, dim3(n_rows), dim3(LG_THREADS), 0, s, logits, n_vocab, out_dev);
+    OWK_LAUNCH(k_row_max, dim3(n_rows), dim3(LG_THREADS), 0, s, logits, n_vocab, out_dev);
 }
 
 // dst_rows[i] <- logits row src_rows[i]  (dst index -1: zero fill)
@@ -232,7 +232,7 @@ __global__ void k_copy_rows(const float * __restrict__ logits, int n_vocab, cons
 
 void logits_copy_rows(hipStream_t s, const float * logits, int n_vocab, const int2 * map_dev, int n, float * dst) {
     if (n <= 0) return;
-    hipLaunchKernelGGL(k_copy_rows, dim3(n * CR_SPLIT), dim3(256), 0, s, logits, n_vocab, map_dev, dst);
+    OWK_LAUNCH(k_copy_rows, dim3(n * CR_SPLIT), dim3(256), 0, s, logits, n_vocab, map_dev, dst);
 }
 
 // Emulated state->logits row maxima (see whisper_full.cpp): entry (slot, row, logit_row,
@@ -258,7 +258,7 @@ __global__ __launch_bounds__(LG_THREADS) void k_rowmax_update(const float * __re
 void rowmax_update(hipStream_t s, const float * logits, int n_vocab, const int4 * ent_dev, int n, float * rmx,
                    int stride) {
     if (n <= 0) return;
-    hipLaunchKernelGGL(k_rowmax_update, dim3(n), dim3(LG_THREADS), 0, s, logits, n_vocab, ent_dev, rmx, stride);
+    OWK_LAUNCH(k_rowmax_update, dim3(n), dim3(LG_THREADS), 0, s, logits, n_vocab, ent_dev, rmx, stride);
 }
 
 // No-speech probability after a prefill (ref whisper.cpp:7185-7195): soft-max of the
@@ -297,13 +297,13 @@ __global__ __launch_bounds__(LG_THREADS) void k_nosp(const float * __restrict__ 
 void nosp_probs(hipStream_t s, const float * row0, int n_vocab, const int2 * req_dev, int n, const float * rmx,
                 int stride, int nosp, float * out_dev) {
     if (n <= 0) return;
-    hipLaunchKernelGGL(k_nosp, dim3(n), dim3(LG_THREADS), 0, s, row0, n_vocab, req_dev, rmx, stride, nosp, out_dev);
+    OWK_LAUNCH(k_nosp, dim3(n), dim3(LG_THREADS), 0, s, row0, n_vocab, req_dev, rmx, stride, nosp, out_dev);
 }
 
 void process_logits(hipStream_t s, float * logits, int n_vocab, const LogitJob * jobs_dev, int n_jobs,
                     const VocabInfo & vi, TokenOut * out_dev, float * logprobs_out, float * probs_out) {
     if (n_jobs <= 0) return;
-    hipLaunchKernelGGL(k_process_logits, dim3(n_jobs), dim3(LG_THREADS), 0, s, logits, n_vocab, jobs_dev, vi, out_dev,
+    OWK_LAUNCH(k_process_logits, dim3(n_jobs), dim3(LG_THREADS), 0, s, logits, n_vocab, jobs_dev, vi, out_dev,
                        logprobs_out, probs_out);
 }
 

@@ -215,7 +215,7 @@ void resid_layernorm(hipStream_t s, int M, int N, int ks, const float * part, co
     if (q8 && (N % 32 != 0 || !q8d)) throw std::runtime_error("resid_layernorm: Q8_0 output needs N % 32 == 0");
     // (a one-wave-per-row variant measured slower: 159 -> 249 ms per step, the row's split partials
     // are too many serial loads for one wave, profiles/r02e_ab.txt)
-    hipLaunchKernelGGL(k_resid_layernorm, dim3(M), dim3(256), 0, s, M, N, ks, part, bias, x, lnw, lnb, eps, xn, ldo,
+    OWK_LAUNCH(k_resid_layernorm, dim3(M), dim3(256), 0, s, M, N, ks, part, bias, x, lnw, lnb, eps, xn, ldo,
                        q8, q8d);
 }
 
@@ -224,7 +224,7 @@ void layernorm_f16(hipStream_t s, const float * x, int rows, int d, const float 
     if (rows <= 0) return;
     if (d % 4 != 0 || d > 4 * 64 * LN_V4 || ldo % 4 != 0) throw std::runtime_error("layernorm_f16: unsupported width");
     if (q8 && (d % 32 != 0 || !q8d)) throw std::runtime_error("layernorm_f16: Q8_0 output needs d % 32 == 0");
-    hipLaunchKernelGGL(k_layernorm_f16, dim3((rows + 3) / 4), dim3(256), 0, s, x, rows, d, w, b, eps, out, ldo,
+    OWK_LAUNCH(k_layernorm_f16, dim3((rows + 3) / 4), dim3(256), 0, s, x, rows, d, w, b, eps, out, ldo,
                        row_idx, out32, q8, q8d);
 }
 
@@ -241,7 +241,7 @@ __global__ void k_embed(const _Float16 * __restrict__ te, const float * __restri
 void embed_tokens(hipStream_t s, const _Float16 * te, const float * pe, const int * tok, const int * pos, int rows,
                   int d, float * x) {
     if (rows <= 0) return;
-    hipLaunchKernelGGL(k_embed, dim3(rows), dim3(256), 0, s, te, pe, tok, pos, rows, d, x);
+    OWK_LAUNCH(k_embed, dim3(rows), dim3(256), 0, s, te, pe, tok, pos, rows, d, x);
 }
 
 __global__ void k_embed_q5(const uint8_t * __restrict__ qs, const uint32_t * __restrict__ qh,
@@ -319,14 +319,14 @@ void embed_tokens_q5(hipStream_t s, const Q5W & te, const float * pe, const int 
                      float * x) {
     if (rows <= 0) return;
     if (te.fmt == QF_Q4_1 || te.fmt == QF_Q5_1)
-        hipLaunchKernelGGL(k_embed_q1, dim3(rows), dim3(256), 0, s, te.qs, te.fmt == QF_Q5_1 ? te.qh : nullptr, te.d,
+        OWK_LAUNCH(k_embed_q1, dim3(rows), dim3(256), 0, s, te.qs, te.fmt == QF_Q5_1 ? te.qh : nullptr, te.d,
                            te.m, pe, tok, pos, rows, d, x);
     else if (te.fmt == QF_Q4_0)
-        hipLaunchKernelGGL(k_embed_q4, dim3(rows), dim3(256), 0, s, te.qs, te.d, pe, tok, pos, rows, d, x);
+        OWK_LAUNCH(k_embed_q4, dim3(rows), dim3(256), 0, s, te.qs, te.d, pe, tok, pos, rows, d, x);
     else if (te.fmt == QF_Q8_0)
-        hipLaunchKernelGGL(k_embed_q8, dim3(rows), dim3(256), 0, s, (const int8_t *) te.qs, te.d, pe, tok, pos, rows, d, x);
+        OWK_LAUNCH(k_embed_q8, dim3(rows), dim3(256), 0, s, (const int8_t *) te.qs, te.d, pe, tok, pos, rows, d, x);
     else
-        hipLaunchKernelGGL(k_embed_q5, dim3(rows), dim3(256), 0, s, te.qs, te.qh, te.d, pe, tok, pos, rows, d, x);
+        OWK_LAUNCH(k_embed_q5, dim3(rows), dim3(256), 0, s, te.qs, te.qh, te.d, pe, tok, pos, rows, d, x);
 }
 
 // ----------------------------------------------------------------------------------
@@ -389,7 +389,7 @@ __global__ __launch_bounds__(256) void k_mel(const MelJob * __restrict__ jobs, c
 void mel_spectrogram(hipStream_t s, const MelJob * jobs_dev, int n_jobs, int max_frames, const float * filters,
                      int n_mel, const double * twiddle, const float * hann) {
     if (n_jobs <= 0 || max_frames <= 0) return;
-    hipLaunchKernelGGL(k_mel, dim3(max_frames, n_jobs), dim3(256), 0, s, jobs_dev, filters, n_mel, hann, twiddle);
+    OWK_LAUNCH(k_mel, dim3(max_frames, n_jobs), dim3(256), 0, s, jobs_dev, filters, n_mel, hann, twiddle);
 }
 
 // global max over the whole (padded) clip, clamp to max-8, (x+4)/4 (whisper.cpp:3228-3244)
@@ -415,7 +415,7 @@ __global__ __launch_bounds__(1024) void k_mel_norm(const MelJob * __restrict__ j
 
 void mel_normalize(hipStream_t s, const MelJob * jobs_dev, int n_jobs, int n_mel) {
     if (n_jobs <= 0) return;
-    hipLaunchKernelGGL(k_mel_norm, dim3(n_jobs), dim3(1024), 0, s, jobs_dev, n_mel);
+    OWK_LAUNCH(k_mel_norm, dim3(n_jobs), dim3(1024), 0, s, jobs_dev, n_mel);
 }
 
 // ----------------------------------------------------------------------------------
@@ -444,7 +444,7 @@ __global__ void k_conv1_im2col(const MelWindow * __restrict__ wins, int n_mel, i
 }
 
 void conv1_im2col(hipStream_t s, const MelWindow * win_dev, int n_clips, int n_mel, int n_ctx2, int kpad, _Float16 * A) {
-    hipLaunchKernelGGL(k_conv1_im2col, dim3(512, n_clips), dim3(256), 0, s, win_dev, n_mel, n_ctx2, kpad, A);
+    OWK_LAUNCH(k_conv1_im2col, dim3(512, n_clips), dim3(256), 0, s, win_dev, n_mel, n_ctx2, kpad, A);
 }
 
 // conv2: stride 2, padding 1, input is the f16 conv1 output [clip][t_in][d]
@@ -465,7 +465,7 @@ __global__ void k_conv2_im2col(const _Float16 * __restrict__ x, int t_in, int d,
 }
 
 void conv2_im2col(hipStream_t s, const _Float16 * x, int n_clips, int t_in, int d, _Float16 * A) {
-    hipLaunchKernelGGL(k_conv2_im2col, dim3(1024, n_clips), dim3(256), 0, s, x, t_in, d, A);
+    OWK_LAUNCH(k_conv2_im2col, dim3(1024, n_clips), dim3(256), 0, s, x, t_in, d, A);
 }
 
 } // namespace owk

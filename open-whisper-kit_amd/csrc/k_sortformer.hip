@@ -63,7 +63,7 @@ __global__ __launch_bounds__(256) void k_sf_mel(const float * __restrict__ pcm, 
 void mel(hipStream_t s, const float * pcm, int n_samples, const float * win512, const float * tw, const float * fb,
          int n_mels, int n_compute, int n_frames_out, float * out) {
     if (n_frames_out <= 0) return;
-    hipLaunchKernelGGL(k_sf_mel, dim3(n_frames_out), dim3(256), 0, s, pcm, n_samples, win512, (const float2 *) tw, fb,
+    OWK_LAUNCH(k_sf_mel, dim3(n_frames_out), dim3(256), 0, s, pcm, n_samples, win512, (const float2 *) tw, fb,
                        n_mels, n_compute, n_frames_out, out);
 }
 
@@ -101,7 +101,7 @@ __global__ __launch_bounds__(256) void k_sf_conv0(const float * __restrict__ mel
 void conv0(hipStream_t s, const float * mel, int ld, int c0, int T_in, int n_mels, const float * w, const float * b,
            int C, float * out, int T1, int F1) {
     if (C > 256) throw std::runtime_error("sf::conv0: C > 256");
-    hipLaunchKernelGGL(k_sf_conv0, dim3(T1, (F1 + 7) / 8), dim3(256), 0, s, mel, ld, c0, T_in, n_mels, w, b, C, out,
+    OWK_LAUNCH(k_sf_conv0, dim3(T1, (F1 + 7) / 8), dim3(256), 0, s, mel, ld, c0, T_in, n_mels, w, b, C, out,
                        F1);
 }
 
@@ -133,7 +133,7 @@ void dwconv(hipStream_t s, const float * in, int Ti, int Fi, int C, const float 
             int To, int Fo) {
     const size_t total = (size_t) To * Fo * C;
     if (!total) return;
-    hipLaunchKernelGGL(k_sf_dwconv, dim3((unsigned) ((total + 255) / 256)), dim3(256), 0, s, in, Ti, Fi, C, w, b, out,
+    OWK_LAUNCH(k_sf_dwconv, dim3((unsigned) ((total + 255) / 256)), dim3(256), 0, s, in, Ti, Fi, C, w, b, out,
                        To, Fo);
 }
 
@@ -192,9 +192,9 @@ void pwconv(hipStream_t s, const float * in, int P, int C, const float * w, cons
     if (P <= 0) return;
     const dim3 grid((P + 63) / 64, (C + 63) / 64);
     if (flatten)
-        hipLaunchKernelGGL(k_sf_pwconv<1>, grid, dim3(256), 0, s, in, P, C, w, b, Fo, out32, out16, ld16);
+        OWK_LAUNCH(k_sf_pwconv<1>, grid, dim3(256), 0, s, in, P, C, w, b, Fo, out32, out16, ld16);
     else
-        hipLaunchKernelGGL(k_sf_pwconv<0>, grid, dim3(256), 0, s, in, P, C, w, b, Fo, out32, out16, ld16);
+        OWK_LAUNCH(k_sf_pwconv<0>, grid, dim3(256), 0, s, in, P, C, w, b, Fo, out32, out16, ld16);
 }
 
 // ---------------------------------------------------------------------------------
@@ -206,7 +206,7 @@ __global__ void k_sf_scale(const float * __restrict__ x, size_t n, float sc, flo
 }
 void scale(hipStream_t s, const float * x, size_t n, float sc, float * out) {
     if (!n) return;
-    hipLaunchKernelGGL(k_sf_scale, dim3((unsigned) ((n + 255) / 256)), dim3(256), 0, s, x, n, sc, out);
+    OWK_LAUNCH(k_sf_scale, dim3((unsigned) ((n + 255) / 256)), dim3(256), 0, s, x, n, sc, out);
 }
 __global__ void k_sf_relu_f16(const float * __restrict__ x, size_t n, _Float16 * __restrict__ out) {
     const size_t i = (size_t) blockIdx.x * blockDim.x + threadIdx.x;
@@ -214,7 +214,7 @@ __global__ void k_sf_relu_f16(const float * __restrict__ x, size_t n, _Float16 *
 }
 void relu_f16(hipStream_t s, const float * x, size_t n, _Float16 * out) {
     if (!n) return;
-    hipLaunchKernelGGL(k_sf_relu_f16, dim3((unsigned) ((n + 255) / 256)), dim3(256), 0, s, x, n, out);
+    OWK_LAUNCH(k_sf_relu_f16, dim3((unsigned) ((n + 255) / 256)), dim3(256), 0, s, x, n, out);
 }
 __global__ void k_sf_to_f16(const float * __restrict__ x, size_t n, _Float16 * __restrict__ out) {
     const size_t i = (size_t) blockIdx.x * blockDim.x + threadIdx.x;
@@ -222,7 +222,7 @@ __global__ void k_sf_to_f16(const float * __restrict__ x, size_t n, _Float16 * _
 }
 void to_f16(hipStream_t s, const float * x, size_t n, _Float16 * out) {
     if (!n) return;
-    hipLaunchKernelGGL(k_sf_to_f16, dim3((unsigned) ((n + 255) / 256)), dim3(256), 0, s, x, n, out);
+    OWK_LAUNCH(k_sf_to_f16, dim3((unsigned) ((n + 255) / 256)), dim3(256), 0, s, x, n, out);
 }
 
 // ---------------------------------------------------------------------------------
@@ -366,7 +366,7 @@ static void launch_attn(hipStream_t s, const float * qkv, int ldq, int kcol, int
     const size_t lds = ((size_t) AQ * Tpad + (size_t) AKT * (DH + 4) + (REL ? (size_t) (AQ - 1 + AKT) * (DH + 4) : 0)) *
                        sizeof(float);
     if (lds > 160 * 1024) throw std::runtime_error("sf::attention: T too large for the LDS score tile");
-    hipLaunchKernelGGL((k_sf_attn<DH, REL>), dim3(H, (T + AQ - 1) / AQ), dim3(256), lds, s, qkv, ldq, kcol, vcol, T, H,
+    OWK_LAUNCH((k_sf_attn<DH, REL>), dim3(H, (T + AQ - 1) / AQ), dim3(256), lds, s, qkv, ldq, kcol, vcol, T, H,
                        u, v, P, sc, out, Tpad);
 }
 
@@ -410,7 +410,7 @@ __global__ void k_sf_glu_dwconv(const float * __restrict__ x, int T, int C, cons
 void glu_dwconv(hipStream_t s, const float * x, int T, int C, const float * w, int k, const float * b, _Float16 * out) {
     const size_t n = (size_t) T * C;
     if (!n) return;
-    hipLaunchKernelGGL(k_sf_glu_dwconv, dim3((unsigned) ((n + 255) / 256)), dim3(256), 0, s, x, T, C, w, k, b, out);
+    OWK_LAUNCH(k_sf_glu_dwconv, dim3((unsigned) ((n + 255) / 256)), dim3(256), 0, s, x, T, C, w, k, b, out);
 }
 
 }  // namespace sf

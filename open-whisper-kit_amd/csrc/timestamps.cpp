@@ -77,7 +77,7 @@ void compute_token_timestamps(whisper_context * ctx, whisper_state * st, int i_s
             }
         }
         const int64_t tt = t_beg + 2 * (token.tid - v.beg);
-        tk[j].vlen = voice_length(v.id_to_token[token.id]);
+        tk[j].vlen = voice_length(v.id_to_token[token.id].c_str());  // C string, as ref 8510
         if (token.pt > thold_pt && token.ptsum > thold_ptsum && token.tid > tid_last && tt <= t1) {
             if (j > 0) tk[j - 1].t1 = tt;
             tk[j].t0 = tt;

@@ -10,7 +10,7 @@ tests/golden/sf_test60.wav = the first 60 s of the reference's streaming-sortfor
     same seed), flash_attn = false, dtw_token_timestamps with WHISPER_AHEADS_LARGE_V3
     (ref 394, 8837-8998), greedy, temperature_inc = 0, token_timestamps, no_context = false;
     recorded: segments with every token's (id, t0, t1, t_dtw, p), and the per-window DECODED
-    token lists (decoder-call prefixes traced, logits untouched: make_golden_large_floor.windows_of)
+    token lists (decoder-call prefixes traced, logits untouched; traced_windows below)
     so a GPU run can be teacher-forced onto them;
   * sortformer_stream_feed in 2 s blocks with the "2s" preset, then flush (ref
     streaming-sortformer/src/sortformer.cpp:2776-3265): probabilities, per-feed frame counts, the
@@ -39,7 +39,6 @@ import ref_oracle as R  # noqa: E402
 import sortformer as SF  # noqa: E402
 import sortformer_synth as SS  # noqa: E402
 from make_golden_large import SEED  # noqa: E402
-from make_golden_large_floor import windows_of  # noqa: E402
 
 OUT = os.path.dirname(os.path.abspath(__file__))
 REF_SF = os.path.join(ROOT, "oracle", "_ref", "libsortformer_ref.so")
@@ -61,6 +60,24 @@ def stream_run(sf, pcm):
     counts.append(int(fl.shape[0]))
     st.close()
     return np.concatenate(outs, 0), counts
+
+
+def traced_windows(ref):
+    """Per-window decoded token prefixes from the traced decoder calls (a window starts where the
+    traced prefix is empty again) and, per window, whether its end is OPEN: a window whose longest
+    traced prefix is n_max - 1 = 219 tokens stopped at the n_text_ctx/2 - 4 step limit (ref
+    whisper.cpp:7219), so its last sampled token follows no traced call. A teacher-forced run
+    forces the prefix and leaves that last step to the decoder (tests/parity_util.Forcer); every
+    other window ended on <|endoftext|> right after its longest prefix."""
+    off, prefix, _, _ = ref.recorded()
+    longest = []
+    for i in range(len(off) - 1):
+        p = prefix[off[i]:off[i + 1]].tolist()
+        if not p:
+            longest.append([])
+        elif len(p) > len(longest[-1]):
+            longest[-1] = p
+    return longest, [len(w) + 1 >= 220 for w in longest]
 
 
 def words_of(L, ctx, segs):
@@ -109,20 +126,27 @@ def main():
     # the next call), decoder-call prefixes traced with the logits untouched (record_topk = 2; the
     # other fixtures assert that tracing changes nothing, make_golden_nofa_windows.py)
     ref.close()
-    ref = R.Ref(path, flash_attn=False, dtw_preset=AHEADS_LARGE_V3)
-    t = time.time()
-    ret, segs = ref.full(pcm, n_threads=NT, record_topk=2, **PARAMS)
-    print("whisper_full", ret, len(segs), "segments", sum(len(s["tokens"]) for s in segs), "tokens",
-          f"{time.time() - t:.0f} s", flush=True)
-    flat = [t[0] for s in segs for t in s["tokens"]]
-    wins = windows_of(ref, flat)
-    assert wins is not None and len(wins) >= 2, f"need >= 2 traced windows, got {wins and len(wins)}"
-    assert segs[-1]["t1"] > 3000, "the transcription must span more than one 30 s window"
-    meta["results"]["full"] = {"ret": ret, "segments": segs}
-    meta["results"]["windows"] = wins
-    words = words_of(L, ref.ctx, segs)
-    ref.close()
-    print("windows", [len(w) for w in wins], flush=True)
+    stage1 = os.path.join(cache, f"c4_stage1-{meta['model_sha256'][:16]}.json")  # the 15-min run, kept
+    if os.path.exists(stage1):
+        st1 = json.load(open(stage1))
+    else:
+        ref = R.Ref(path, flash_attn=False, dtw_preset=AHEADS_LARGE_V3)
+        t = time.time()
+        ret, segs = ref.full(pcm, n_threads=NT, record_topk=2, **PARAMS)
+        print("whisper_full", ret, len(segs), "segments", sum(len(s["tokens"]) for s in segs), "tokens",
+              f"{time.time() - t:.0f} s", flush=True)
+        wins, open_end = traced_windows(ref)
+        st1 = {"ret": ret, "segments": segs, "windows": wins, "open": open_end, "words": words_of(L, ref.ctx, segs)}
+        ref.close()
+        with open(stage1, "w") as f:
+            json.dump(st1, f)
+    segs = st1["segments"]
+    assert len(st1["windows"]) >= 2 and segs[-1]["t1"] > 3000, "the transcription must span more than one 30 s window"
+    meta["results"]["full"] = {"ret": st1["ret"], "segments": segs}
+    meta["results"]["windows"] = st1["windows"]
+    meta["results"]["windows_open"] = st1["open"]
+    words = [tuple(w) for w in st1["words"]]
+    print("windows", [len(w) for w in st1["windows"]], "open", st1["open"], flush=True)
 
     # --- streaming diarization, 2 s blocks ---
     mm = json.load(open(os.path.join(OUT, "sf_golden.json")))

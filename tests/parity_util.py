@@ -123,10 +123,13 @@ class Forcer:
     logit but the forced token's is set to -inf (whisper.cpp:6254 is where the reference's own
     callback point sits). A call with no decoded tokens yet starts the next window (greedy,
     temperature_inc = 0: one call per step). Used to compare what is computed FROM a token sequence
-    (DTW timestamps) independently of a near-tie parting of the free runs."""
+    (DTW timestamps) independently of a near-tie parting of the free runs. `open_end[i]`: window i
+    stopped at the decode-step limit after its last listed token's step, so the step after it is
+    left to the decoder (its token followed no traced call)."""
 
-    def __init__(self, windows, eot, n_vocab, token_data_type):
+    def __init__(self, windows, eot, n_vocab, token_data_type, open_end=None):
         self.windows, self.eot, self.n_vocab = [list(w) for w in windows], eot, n_vocab
+        self.open_end = list(open_end) if open_end is not None else [False] * len(self.windows)
         self.calls = 0
         self.window = -1
         TD = C.POINTER(token_data_type)
@@ -139,6 +142,8 @@ class Forcer:
             self.window += 1
         lg = np.ctypeslib.as_array(logits, shape=(self.n_vocab,))
         win = self.windows[self.window] if 0 <= self.window < len(self.windows) else []
+        if n_tokens >= len(win) and 0 <= self.window < len(self.windows) and self.open_end[self.window]:
+            return
         t = win[n_tokens] if n_tokens < len(win) else self.eot
         # the forced token far above every other logit (the others are kept, so the timestamp
         # distribution -- the token's best timestamp "tid" and pt -- stays the decoder's own)

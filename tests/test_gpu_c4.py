@@ -97,7 +97,8 @@ def test_configs4_transcription(c4, w4, test60):
 
 def _forced_run(w, meta, pcm):
     p = _params(w, meta)
-    force = Forcer(meta["results"]["windows"], w.L.whisper_token_eot(w.ctx), w.n_vocab, owk.TokenData)
+    force = Forcer(meta["results"]["windows"], w.L.whisper_token_eot(w.ctx), w.n_vocab, owk.TokenData,
+                   meta["results"]["windows_open"])
     p.logits_filter_callback = C.cast(force.cfunc, C.c_void_p)
     st = w.new_state()
     assert w.full(st, pcm, p) == meta["results"]["full"]["ret"]
