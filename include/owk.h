@@ -93,12 +93,19 @@ WHISPER_API long owk_debug_capture(struct whisper_state * state, float * out, lo
 WHISPER_API int owk_debug_gemm_q5(int device, int M, int N, int K, const float * a, const uint8_t * w_blocks, float * out,
                                   int8_t * q_out, float * d_out);
 /* the same for any block format fmt (0 Q5_0, 1 Q8_0, 2 Q4_0, 3 Q4_1, 4 Q5_1: w_blocks are ggml blocks
- * of that type; Q4_1 / Q5_1 take Q8_1 activations); d_out receives the raw f32 activation scales */
+ * of that type; Q4_1 / Q5_1 take Q8_1 activations); d_out receives the raw f32 activation scales.
+ * fmt 5..9 = Q2_K, Q3_K, Q4_K, Q5_K, Q6_K (K % 256 == 0; Q8_K activations, the K-quant model path at
+ * every M): q_out receives the activation rows in the virtual-block layout [M][kx] (kx = K * 9/8 for
+ * Q2_K / Q4_K / Q5_K, K for Q3_K, 2K for Q6_K), d_out the Q8_K scale per row and 256-block [M][K/256] */
 WHISPER_API int owk_debug_gemm_quant(int device, int fmt, int M, int N, int K, const float * a, const uint8_t * w_blocks,
                                      float * out, int8_t * q_out, float * d_out);
 // use_q16 = 1: the large-tile encoder path (expanded f16 integers, gemm_q16; M >= 2048, symmetric formats)
 WHISPER_API int owk_debug_gemm_quant2(int device, int fmt, int M, int N, int K, const float * a, const uint8_t * w_blocks,
                                       float * out, int8_t * q_out, float * d_out, int use_q16);
+/* host-only test hook (no device): N rows of ggml K-quant blocks (fmt 5..9 as above) -> the virtual-block
+ * expansion the GEMMs run on (wi [N][kx] f16 bits, dwt [kx/32][N] f32; either may be NULL) and the f32
+ * row dequantization of the token embedding (deq [N][K], may be NULL); 0 on success */
+WHISPER_API int owk_debug_kquant(int fmt, int N, int K, const uint8_t * w_blocks, uint16_t * wi, float * dwt, float * deq);
 /* mode | 0x100: force the 128x128 large-GEMM kernel; | 0x400: 5-slot ring variant of the 256x256 kernel;
  * | 0x200: uniform random operands (else zeros) */
 WHISPER_API double owk_debug_gemm_bench(int device, int mode, int M, int N, int K, int iters);

@@ -1,5 +1,6 @@
 // Batch-major device engine (see engine.h).
 #include "engine.h"
+#include "kquant.h"
 
 #include <algorithm>
 #include <cmath>
@@ -231,6 +232,20 @@ void Engine::linear(const char * cls, int mode, int M, int N, int K, const _Floa
         gemm_q16(stream, mode, M, N, K, q16a_.as<_Float16>(), q16d_.as<float>(), mpad, q, ep);
         return;
     }
+    if (qf_is_k(q.fmt)) {
+        // K-quants: Q8_K rows in the virtual-block layout (kquant.h), then the f16 MFMA ring kernel
+        // over the virtual K at every shape
+        const int mpad = (M + 255) / 256 * 256, kx = q.kx;
+        if (q16a_.bytes < (size_t) M * kx * 2 || q16d_.bytes < (size_t) (kx / 32) * mpad * 4)
+            throw std::runtime_error("linear: K-quant operand buffers not reserved");
+        {
+            ProfScope ps(prof, stream, "quantize_q8");
+            quantize_q8k_f16(stream, A32, A16, lda, M, K, q.fmt, q16a_.as<_Float16>(), q16d_.as<float>(), mpad);
+        }
+        ProfScope ps(prof, stream, cls, gemm_flops(M, N, K), (double) N * K * kq_block_bytes(q.fmt) / 256.0 + (double) M * K);
+        gemm_q16(stream, mode, M, N, kx, q16a_.as<_Float16>(), q16d_.as<float>(), mpad, q, ep);
+        return;
+    }
     if (!a_q8) {
         ProfScope ps(prof, stream, "quantize_q8");
         quantize_q8(stream, A32, A16, lda, M, K, q8a_.as<int8_t>(), q8d_.as<float>());
@@ -272,8 +287,9 @@ void Engine::encode(const std::vector<int> & slots, const std::vector<int> & off
             // gemm_q16 operands (reserved here: growing them inside linear() would free a buffer
             // queued kernels may still read)
             const size_t mpad = ((size_t) M + 255) / 256 * 256;
-            q16a_.alloc(std::max(q16a_.bytes, (size_t) M * 4 * d * 2));
-            q16d_.alloc(std::max(q16d_.bytes, (size_t) (4 * d / 32) * mpad * 4));
+            const size_t kmax = m->kq ? (size_t) kq_kx(m->qfmt, 4 * d) : (size_t) 4 * d;  // K-quants: the virtual K
+            q16a_.alloc(std::max(q16a_.bytes, (size_t) M * kmax * 2));
+            q16d_.alloc(std::max(q16d_.bytes, kmax / 32 * mpad * 4));
         }
     }
     e_a1_.alloc((size_t) n * T2 * kp1 * 2);
@@ -346,7 +362,7 @@ void Engine::encode(const std::vector<int> & slots, const std::vector<int> & off
             ep.T = T;
             ep.Tpad = Tpad;
             linear("gemm_enc", EPI_QKV_ENC, M, 3 * d, d, e_xn_.as<_Float16>(), m->q5 ? e_xn32_.as<float>() : nullptr, d,
-                   L.w_qkv, L.q_qkv, ep, nullptr, false, m->q5);
+                   L.w_qkv, L.q_qkv, ep, nullptr, false, m->q5 && !m->kq);
         }
         {
             // 4*T*Tpad_kv*d flops (QK^T and PV over the 1536 reference keys)
@@ -379,7 +395,7 @@ void Engine::encode(const std::vector<int> & slots, const std::vector<int> & off
             ep.out16 = e_h_.as<_Float16>();
             ep.ldo = 4 * d;
             linear("gemm_enc", EPI_GELU_F16, M, 4 * d, d, e_xn_.as<_Float16>(), m->q5 ? e_xn32_.as<float>() : nullptr, d,
-                   L.w_mlp0, L.q_mlp0, ep, nullptr, false, m->q5);
+                   L.w_mlp0, L.q_mlp0, ep, nullptr, false, m->q5 && !m->kq);
         }
         {
             EpiParams ep;
@@ -413,7 +429,7 @@ void Engine::encode(const std::vector<int> & slots, const std::vector<int> & off
         ep.slot_map = e_slotmap_.as<int>();
         // Q5_0: the final LayerNorm wrote the encoder output's Q8_0 rows once for all layers
         linear("gemm_cross", EPI_KV_CROSS, M, 2 * d, d, e_enc_.as<_Float16>(), m->q5 ? e_enc32_.as<float>() : nullptr, d,
-               L.cw_kv, L.q_ckv, ep, nullptr, false, m->q5);
+               L.cw_kv, L.q_ckv, ep, nullptr, false, m->q5 && !m->kq);
     }
 }
 
@@ -469,7 +485,7 @@ void Engine::clear_graphs() {
 uint64_t Engine::buffers_signature() const {
     uint64_t h = 1469598103934665603ull;
     for (const void * p : {d_x_.ptr, d_xn_.ptr, d_q_.ptr, d_ao_.ptr, d_h_.ptr, d_xl_.ptr, logits_.ptr, d_stg_.ptr,
-                           q8a_.ptr, q8d_.ptr, d_xn32_.ptr, d_ao32_.ptr, d_xl32_.ptr,
+                           q8a_.ptr, q8d_.ptr, d_xn32_.ptr, d_ao32_.ptr, d_xl32_.ptr, q16a_.ptr, q16d_.ptr,
                            self_k_.ptr, self_v_.ptr, cross_k_.ptr, cross_v_.ptr, gws_part_.ptr})
         h = (h ^ (uint64_t) (uintptr_t) p) * 1099511628211ull;
     return h;
@@ -519,6 +535,13 @@ void Engine::decode(const std::vector<DecodeRow> & rows, const std::vector<int> 
                 d_ao32_.alloc((size_t) C * d * 4);
                 q8a_.alloc(std::max(q8a_.bytes, (size_t) C * 4 * d));
                 q8d_.alloc(std::max(q8d_.bytes, (size_t) C * 4 * d / 32 * 4));
+            }
+            if (m->kq) {  // f32 LayerNorm rows (quantized to Q8_K like the reference) + gemm_q16 operands
+                d_xn32_.alloc((size_t) C * d * 4);
+                d_xl32_.alloc((size_t) C * d * 4);
+                const size_t mpad = ((size_t) C + 255) / 256 * 256, kmax = (size_t) kq_kx(m->qfmt, 4 * d);
+                q16a_.alloc(std::max(q16a_.bytes, (size_t) C * kmax * 2));
+                q16d_.alloc(std::max(q16d_.bytes, kmax / 32 * mpad * 4));
             }
             logits_.alloc((size_t) C * nv * 4);
         }
@@ -650,12 +673,15 @@ void Engine::launch_decode(const DecShape & sh) {
     float * ao32 = q5 ? d_ao32_.as<float>() : nullptr;
     // Q5_0: attention passes whose rows all take the one_chunk kernel emit the Q8_0 rows
     // themselves; otherwise their f32 output is quantized by the GEMM call
-    const bool fq_self = q5 && self_oc && !self_tl && !sh.self_sm;
-    const bool fq_cross = q5 && cross_oc && !cross_tl && !sh.cross_sm;
+    const bool kq = m->kq;  // K-quants: GEMMs quantize f32 rows to Q8_K themselves (no producer rows)
+    const bool fq_self = q5 && !kq && self_oc && !self_tl && !sh.self_sm;
+    const bool fq_cross = q5 && !kq && cross_oc && !cross_tl && !sh.cross_sm;
+    float * xn32 = kq ? d_xn32_.as<float>() : nullptr;  // the f32 LayerNorm rows a K-quant GEMM quantizes
 
     {
         ProfScope ps(prof, stream, "embed");
-        if (q5) embed_tokens_q5(stream, m->q_te, m->d_pe, d_tok, d_pos, R, d, d_x_.as<float>());
+        if (kq) embed_tokens_f32(stream, m->te32.as<float>(), m->d_pe, d_tok, d_pos, R, d, d_x_.as<float>());
+        else if (q5) embed_tokens_q5(stream, m->q_te, m->d_pe, d_tok, d_pos, R, d, d_x_.as<float>());
         else embed_tokens(stream, m->d_te, m->d_pe, d_tok, d_pos, R, d, d_x_.as<float>());
     }
     const float kq_scale = powf(64.0f, -0.25f);
@@ -764,7 +790,7 @@ void Engine::launch_decode(const DecShape & sh) {
     };
     auto ln = [&](const float * w, const float * b) {
         ProfScope ps(prof, stream, "layernorm");
-        layernorm_f16(stream, d_x_.as<float>(), R, d, w, b, hp.eps, d_xn_.as<_Float16>(), d, nullptr, nullptr, q8a(),
+        layernorm_f16(stream, d_x_.as<float>(), R, d, w, b, hp.eps, d_xn_.as<_Float16>(), d, nullptr, xn32, q8a(),
                       q8d());
     };
     if (fused) {
@@ -775,7 +801,7 @@ void Engine::launch_decode(const DecShape & sh) {
     // cross_attn.out, mlp.2) write split-K partial tiles and resid_layernorm adds them to the residual
     // stream with bias and emits the next LayerNorm as f16 AND as Q8_0 rows (the next GEMM's operand):
     // one launch where a full-epilogue GEMM plus a LayerNorm launch were
-    const bool q5p = q5 && R <= 32 && !sh.self_sm && !sh.cross_sm && !sh.capture;
+    const bool q5p = q5 && !kq && R <= 32 && !sh.self_sm && !sh.cross_sm && !sh.capture;
     auto resid_q5p = [&](const _Float16 * A16, const float * A32, const Q5W & q, int K, const float * bias,
                          const float * lnw, const float * lnb, bool a_q8) {
         EpiParams ep;
@@ -857,7 +883,7 @@ void Engine::launch_decode(const DecShape & sh) {
             ep.d = d;
             ep.row_off = d_rowoff;
             ep.Tpad = kv_cells * 64;
-            G("qkv", EPI_QKV_DEC, 3 * d, d, d_xn_.as<_Float16>(), nullptr, L.w_qkv, L.t_qkv, L.q_qkv, ep, R, q5);
+            G("qkv", EPI_QKV_DEC, 3 * d, d, d_xn_.as<_Float16>(), xn32, L.w_qkv, L.t_qkv, L.q_qkv, ep, R, q5 && !kq);
         }
         {
             ProfScope ps(prof, stream, "attn_self");
@@ -877,7 +903,7 @@ void Engine::launch_decode(const DecShape & sh) {
             ep.bias = L.cb_q;
             ep.out16 = d_q_.as<_Float16>();
             ep.ldo = d;
-            G("cq", EPI_F16, d, d, d_xn_.as<_Float16>(), nullptr, L.cw_q, L.t_cq, L.q_cq, ep, R, q5);
+            G("cq", EPI_F16, d, d, d_xn_.as<_Float16>(), xn32, L.cw_q, L.t_cq, L.q_cq, ep, R, q5 && !kq);
         }
         {
             // bytes: cross K and V of each row's clip (the HBM-bound part of a decode step)
@@ -900,7 +926,7 @@ void Engine::launch_decode(const DecShape & sh) {
             ep.gelu_tab = m->gelu_tab;
             ep.out16 = d_h_.as<_Float16>();
             ep.ldo = 4 * d;
-            G("mlp0", EPI_GELU_F16, 4 * d, d, d_xn_.as<_Float16>(), nullptr, L.w_mlp0, L.t_mlp0, L.q_mlp0, ep, R, q5);
+            G("mlp0", EPI_GELU_F16, 4 * d, d, d_xn_.as<_Float16>(), xn32, L.w_mlp0, L.t_mlp0, L.q_mlp0, ep, R, q5 && !kq);
         }
         resid_full(d_h_.as<_Float16>(), nullptr, L.w_mlp1, L.t_mlp1, L.q_mlp1, 4 * d, L.b_mlp1);
     }
@@ -908,13 +934,13 @@ void Engine::launch_decode(const DecShape & sh) {
         {
             ProfScope ps(prof, stream, "layernorm");
             layernorm_f16(stream, d_x_.as<float>(), n_logit_rows, d, m->d_ln_w, m->d_ln_b, hp.eps, d_xl_.as<_Float16>(),
-                          d, d_lsel, nullptr, q8a(), q8d());
+                          d, d_lsel, kq ? d_xl32_.as<float>() : nullptr, q8a(), q8d());
         }
         EpiParams ep;
         ep.out32 = logits_.as<float>();
         ep.ldo = nv;
         linear(n_logit_rows <= 64 ? "gemm_logits" : "gemm_logits_big", EPI_F32, n_logit_rows, nv, d,
-               d_xl_.as<_Float16>(), nullptr, d, m->d_te, m->q_te, ep, m->d_te_t, true, q5);
+               d_xl_.as<_Float16>(), kq ? d_xl32_.as<float>() : nullptr, d, m->d_te, m->q_te, ep, m->d_te_t, true, q5 && !kq);
     }
 }
 

@@ -183,8 +183,10 @@ private:
     DevBuf q8a_, q8d_;
     DevBuf q16a_, q16d_;  // gemm_q16 operands: Q8_0 integers as f16 [M][K], scales [K/32][mpad]
     // Q5_0 models: the Q8_0 activation buffers producers write for the next linear (else null)
-    int8_t * q8a() { return m->q5 ? q8a_.as<int8_t>() : nullptr; }
-    float * q8d() { return m->q5 ? q8d_.as<float>() : nullptr; }
+    // Q8_0 / Q8_1 rows written by producers (LayerNorm, attention); K-quant models quantize to Q8_K
+    // in linear() from the f32 rows instead
+    int8_t * q8a() { return m->q5 && !m->kq ? q8a_.as<int8_t>() : nullptr; }
+    float * q8d() { return m->q5 && !m->kq ? q8d_.as<float>() : nullptr; }
     DevBuf e_xn32_, e_ao32_, d_xn32_, d_ao32_, d_xl32_;
 
     DevBuf amap_, cap_;  // DTW: head map [L][H], captured probabilities [n_ah][T][cap_rows_]

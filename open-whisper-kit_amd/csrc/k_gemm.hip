@@ -1177,6 +1177,102 @@ void quantize_q8_f16(hipStream_t s, const float * A32, const _Float16 * A16, int
         OWK_LAUNCH(k_quantize_q8_f16<_Float16>, dim3(grid), dim3(256), 0, s, A16, lda, M, K, q16, dat, mpad);
 }
 
+// Q8_K rows for the K-quant formats (kernels.h quantize_q8k_f16; ref quantize_row_q8_K_ref,
+// ggml-quants.c:2555-2592) in the virtual-block layout of kquant.h: one 256-thread block per
+// (row, super-block). LAY 0: 8 blocks of q + one block [16 bsums | 16 zeros]; 1: 8 blocks of q;
+// 2: 16 blocks [16 q | 16 zeros]. Every virtual block of the super-block carries d = 1 / iscale.
+template <typename TA, int LAY>
+__global__ __launch_bounds__(256) void k_quantize_q8k_f16(const TA * __restrict__ A, int lda, int M, int K,
+                                                          _Float16 * __restrict__ q, float * __restrict__ dat,
+                                                          int mpad) {
+    __shared__ uint32_t s_key[256];
+    __shared__ float s_x[256];
+    const int nsb = K >> 8;
+    const int r = blockIdx.x / nsb, sb = blockIdx.x - r * nsb;
+    if (r >= M) return;
+    const int t = threadIdx.x;
+    const float x = (float) A[(size_t) r * lda + sb * 256 + t];
+    s_x[t] = x;
+    // the FIRST element of largest |x| (the reference's scan keeps the earliest on ties): a tree
+    // reduction of (|x| bits, index) pairs
+    __shared__ int s_idx[256];
+    s_key[t] = __float_as_uint(fabsf(x));
+    s_idx[t] = t;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if (t < o) {
+            const uint32_t a = s_key[t], b = s_key[t + o];
+            const int ia = s_idx[t], ib = s_idx[t + o];
+            if (b > a || (b == a && ib < ia)) {
+                s_key[t] = b;
+                s_idx[t] = ib;
+            }
+        }
+        __syncthreads();
+    }
+    const float amax = __uint_as_float(s_key[0]);
+    const float mx = s_x[s_idx[0]];
+    int qv = 0;
+    float d = 0.0f;
+    if (amax != 0.0f) {
+        const float iscale = -127.f / mx;
+        qv = min(127, (int) rintf(iscale * x));
+        d = 1.0f / iscale;
+    }
+    // sums of 16 (one group of 16 lanes of a wave)
+    int bs = qv;
+#pragma unroll
+    for (int o = 8; o > 0; o >>= 1) bs += __shfl_xor(bs, o, 16);
+    const int kx = LAY == 0 ? (K >> 8) * 288 : LAY == 1 ? K : (K >> 8) * 512;
+    _Float16 * out = q + (size_t) r * kx;
+    const int g = t >> 4, e = t & 15;
+    int kb0, nblk;
+    if (LAY == 0) {
+        out += sb * 288;
+        out[t] = (_Float16) (float) qv;
+        if (e == 0) out[256 + g] = (_Float16) (float) bs;
+        if (t < 16) out[272 + t] = (_Float16) 0.0f;
+        kb0 = sb * 9;
+        nblk = 9;
+    } else if (LAY == 1) {
+        out += sb * 256;
+        out[t] = (_Float16) (float) qv;
+        kb0 = sb * 8;
+        nblk = 8;
+    } else {
+        out += sb * 512;
+        out[g * 32 + e] = (_Float16) (float) qv;
+        out[g * 32 + 16 + e] = (_Float16) 0.0f;
+        kb0 = sb * 16;
+        nblk = 16;
+    }
+    if (t < nblk) {
+        const int tt = r & 127;
+        const int pr = (r & ~127) | (tt & 64) | ((tt & 15) << 2) | ((tt >> 4) & 3);
+        dat[(size_t) (kb0 + t) * mpad + pr] = d;
+    }
+}
+
+void quantize_q8k_f16(hipStream_t s, const float * A32, const _Float16 * A16, int lda, int M, int K, int fmt,
+                      _Float16 * q16, float * dat, int mpad) {
+    if (M <= 0) return;
+    if (K % 256 || !qf_is_k(fmt) || mpad < (M + 127) / 128 * 128) throw std::runtime_error("quantize_q8k_f16: shape");
+    const int lay = fmt == QF_Q3_K ? 1 : fmt == QF_Q6_K ? 2 : 0;
+    const size_t blocks = (size_t) M * (K / 256);
+    if (blocks > 0x7fffffff) throw std::runtime_error("quantize_q8k_f16: too many rows");
+#define OWK_Q8K(T, P, L) OWK_LAUNCH((k_quantize_q8k_f16<T, L>), dim3((unsigned) blocks), dim3(256), 0, s, P, lda, M, K, q16, dat, mpad)
+    if (A32) {
+        if (lay == 0) OWK_Q8K(float, A32, 0);
+        else if (lay == 1) OWK_Q8K(float, A32, 1);
+        else OWK_Q8K(float, A32, 2);
+    } else {
+        if (lay == 0) OWK_Q8K(_Float16, A16, 0);
+        else if (lay == 1) OWK_Q8K(_Float16, A16, 1);
+        else OWK_Q8K(_Float16, A16, 2);
+    }
+#undef OWK_Q8K
+}
+
 typedef int intx4 __attribute__((ext_vector_type(4)));
 
 // 8 consecutive weights (group g = elements 8g..8g+7) of one block as int8, the B/A operand of
@@ -1652,6 +1748,7 @@ void gemm_q5(hipStream_t s, int mode, int M, int N, int K, const int8_t * qa, co
 }
 
 bool gemm_q16_applies(const Q5W & w, int M, int N, int K) {
+    if (qf_is_k(w.fmt)) return w.wi && w.dwt && K % G2_K == 0;  // K-quants: every shape, K = the virtual K
     return w.wi && w.dwt && use_256(M, N, K) && !qf_has_m(w.fmt);
 }
 

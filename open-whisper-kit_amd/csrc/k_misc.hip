@@ -244,6 +244,22 @@ void embed_tokens(hipStream_t s, const _Float16 * te, const float * pe, const in
     OWK_LAUNCH(k_embed, dim3(rows), dim3(256), 0, s, te, pe, tok, pos, rows, d, x);
 }
 
+// K-quant models: rows of the host-dequantized f32 embedding (ref get_rows -> dequantize_row_q*_K)
+__global__ void k_embed_f32(const float * __restrict__ te, const float * __restrict__ pe, const int * __restrict__ tok,
+                            const int * __restrict__ pos, int rows, int d, float * __restrict__ x) {
+    const int r = blockIdx.x;
+    if (r >= rows) return;
+    const float * t = te + (size_t) tok[r] * d;
+    const float * p = pe + (size_t) pos[r] * d;
+    for (int i = threadIdx.x; i < d; i += blockDim.x) x[(size_t) r * d + i] = t[i] + p[i];
+}
+
+void embed_tokens_f32(hipStream_t s, const float * te, const float * pe, const int * tok, const int * pos, int rows,
+                      int d, float * x) {
+    if (rows <= 0) return;
+    OWK_LAUNCH(k_embed_f32, dim3(rows), dim3(256), 0, s, te, pe, tok, pos, rows, d, x);
+}
+
 __global__ void k_embed_q5(const uint8_t * __restrict__ qs, const uint32_t * __restrict__ qh,
                            const _Float16 * __restrict__ dd, const float * __restrict__ pe,
                            const int * __restrict__ tok, const int * __restrict__ pos, int rows, int d,

@@ -111,7 +111,11 @@ void tile_weights(hipStream_t s, const _Float16 * W, int N, int K, _Float16 * ou
 // Q8_1 block sum (quantize_row_q8_1, x86 quants.c:388): the GEMMs form it from the int8
 // activations and the UNROUNDED f32 scale, so activation producers store the raw f32
 // d = amax / 127 and every consumer rounds it to f16 itself (the stored block_q8_*.d).
-enum QFmt : int { QF_Q5_0 = 0, QF_Q8_0 = 1, QF_Q4_0 = 2, QF_Q4_1 = 3, QF_Q5_1 = 4 };
+//   Q2_K .. Q6_K (ftype 10-14): 256-weight super-blocks x Q8_K activations (kquant.h): the
+//   f16-MFMA ring kernel (gemm_q16) over "virtual" 32-blocks, at every row count
+enum QFmt : int { QF_Q5_0 = 0, QF_Q8_0 = 1, QF_Q4_0 = 2, QF_Q4_1 = 3, QF_Q5_1 = 4,
+                  QF_Q2_K = 5, QF_Q3_K = 6, QF_Q4_K = 7, QF_Q5_K = 8, QF_Q6_K = 9 };
+__host__ __device__ constexpr bool qf_is_k(int f) { return f >= QF_Q2_K && f <= QF_Q6_K; }
 __host__ __device__ constexpr bool qf_has_qh(int f) { return f == QF_Q5_0 || f == QF_Q5_1; }
 __host__ __device__ constexpr bool qf_has_m(int f) { return f == QF_Q4_1 || f == QF_Q5_1; }
 __host__ __device__ constexpr int qf_qs_bytes(int f) { return f == QF_Q8_0 ? 32 : 16; }  // per 32 weights
@@ -140,7 +144,8 @@ struct Q5W {
     const float * dwt = nullptr;
     int npad = 0;
     int fmt = QF_Q5_0;
-    explicit operator bool() const { return qs != nullptr; }
+    int kx = 0;  // K-quant formats: the virtual K of wi / dwt (kquant.h); only wi / dwt are set
+    explicit operator bool() const { return qs != nullptr || (qf_is_k(fmt) && wi != nullptr); }
 };
 size_t quant_tiled_bytes(int fmt, int N, int K);
 // ggml block rows -> the split arrays (qh / m may be null for formats without them)
@@ -162,6 +167,12 @@ void quantize_q8_f16(hipStream_t s, const float * A32, const _Float16 * A16, int
 void gemm_q16(hipStream_t s, int mode, int M, int N, int K, const _Float16 * q16, const float * dat, int mpad,
               const Q5W & w, const EpiParams & ep);
 bool gemm_q16_applies(const Q5W & w, int M, int N, int K);
+// Q8_K rows of A (quantize_row_q8_K_ref, ggml-quants.c:2555-2592: per 256 the signed value of the
+// first largest |x|, iscale = -127 / max, q = min(127, rne(iscale * x)), d = 1 / iscale, int sums
+// per 16) laid out for the K-quant format `fmt` (kquant.h): q16 [M][kq_kx(fmt, K)] exact f16, dat
+// [kx / 32][mpad] f32 (rows permuted like quantize_q8_f16)
+void quantize_q8k_f16(hipStream_t s, const float * A32, const _Float16 * A16, int lda, int M, int K, int fmt,
+                      _Float16 * q16, float * dat, int mpad);
 // expand Q5W block arrays into wi / dwt (device buffers of N*K halves and K/32*npad floats)
 void quant_expand_f16(hipStream_t s, const Q5W & w, int N, int K, _Float16 * wi, float * dwt, int npad);
 // EPI_PARTIAL decode-row quantized GEMM whose activation rows are f16 (quantized to Q8_0 inside)
@@ -182,6 +193,8 @@ void layernorm_f16(hipStream_t s, const float * x, int rows, int d, const float 
 void embed_tokens(hipStream_t s, const _Float16 * tok_emb, const float * pos_emb, const int * tokens,
                   const int * pos, int rows, int d, float * x);
 // the same from a Q5_0 token embedding (ggml get_rows -> dequantize_row_q5_0: d * (q - 16))
+void embed_tokens_f32(hipStream_t s, const float * tok_emb, const float * pos_emb, const int * tokens, const int * pos,
+                      int rows, int d, float * x);
 void embed_tokens_q5(hipStream_t s, const Q5W & te, const float * pos_emb, const int * tokens, const int * pos,
                      int rows, int d, float * x);
 

@@ -9,6 +9,7 @@
 // plus device constants: the f16 GELU table, mel filterbank, DFT twiddles, Hann window.
 #include "model.h"
 #include "kernels.h"
+#include "kquant.h"
 
 #include <cmath>
 #include <cstdarg>
@@ -229,12 +230,19 @@ Model * load_model(whisper_model_loader * loader, int device, std::string & err)
         case 7: m->qfmt = QF_Q8_0; break;
         case 8: m->qfmt = QF_Q5_0; break;
         case 9: m->qfmt = QF_Q5_1; break;
+        // MOSTLY_Q2_K .. Q6_K (10-14): 256-weight super-blocks x Q8_K activations (kquant.h)
+        case 10: m->qfmt = QF_Q2_K; break;
+        case 11: m->qfmt = QF_Q3_K; break;
+        case 12: m->qfmt = QF_Q4_K; break;
+        case 13: m->qfmt = QF_Q5_K; break;
+        case 14: m->qfmt = QF_Q6_K; break;
         default:
             err = "unsupported ftype " + std::to_string(hp.ftype) +
-                  " (this engine build loads F16, Q4_0, Q4_1, Q5_0, Q5_1 and Q8_0 models)";
+                  " (this engine build loads F16, Q4_0, Q4_1, Q5_0, Q5_1, Q8_0 and Q2_K-Q6_K models)";
             return nullptr;
     }
-    m->q5 = hp.ftype != 1;  // quantized weights x Q8_0 / Q8_1 activations
+    m->q5 = hp.ftype != 1;  // quantized weights x Q8_0 / Q8_1 / Q8_K activations
+    m->kq = qf_is_k(m->qfmt) && m->q5;
 
     // mel filters
     m->n_filters_mel = r.get<int32_t>();
@@ -316,18 +324,22 @@ Model * load_model(whisper_model_loader * loader, int device, std::string & err)
         if (nel != expect) { err = "tensor '" + name + "' has wrong size in model file"; return nullptr; }
         // quantized models: every 2-D weight is of the model's block type (whisper-quantize)
         const bool want_q5 = m->q5 && sp.f16 && sp.ne.size() == 2;
-        const int qtype = m->q5 ? qf_ggml_type(m->qfmt) : -1, qbytes = m->q5 ? qf_block_bytes(m->qfmt) : 0;
+        const int qtype = !m->q5 ? -1 : m->kq ? kq_ggml_type(m->qfmt) : qf_ggml_type(m->qfmt);
+        const int qblk = m->kq ? 256 : 32, qbytes = !m->q5 ? 0 : m->kq ? kq_block_bytes(m->qfmt) : qf_block_bytes(m->qfmt);
         if (want_q5 ? ttype != qtype : (ttype != 0 && ttype != 1)) {
             err = "tensor '" + name + "': unsupported type " + std::to_string(ttype);
             return nullptr;
         }
         if (sp.f16 && !want_q5 && ttype != 1) { err = "tensor '" + name + "': expected F16 weights"; return nullptr; }
-        if (want_q5 && sp.ne[0] % 32) { err = "tensor '" + name + "': row length not a multiple of 32"; return nullptr; }
+        if (want_q5 && sp.ne[0] % qblk) {
+            err = "tensor '" + name + "': row length not a multiple of " + std::to_string(qblk);
+            return nullptr;
+        }
         HostTensor & t = ht[it->second];
         t.f16 = ttype == 1;
         t.q5 = want_q5;
         t.nelem = nel;
-        t.data.resize(want_q5 ? (size_t) nel / 32 * qbytes : (size_t) nel * (t.f16 ? 2 : 4));
+        t.data.resize(want_q5 ? (size_t) nel / qblk * qbytes : (size_t) nel * (t.f16 ? 2 : 4));
         r.read(t.data.data(), t.data.size());
         if (!r.ok) { err = "truncated tensor data for '" + name + "'"; return nullptr; }
         t.loaded = true;
@@ -446,7 +458,71 @@ Model * load_model(whisper_model_loader * loader, int device, std::string & err)
     };
     // Q5_0 matrices: split block arrays (kernels.h Q5W), row groups concatenated like the F16 packs
     std::map<std::string, Q5W> q5m;
-    if (m->q5 && n_loaded > 0) {
+    if (m->kq && n_loaded > 0) {
+        // K-quants: every 2-D linear (row groups concatenated like the F16 packs) as the virtual-block
+        // f16 integers + scales of kquant.h, the one layout every GEMM shape runs on (gemm_q16)
+        std::vector<std::vector<std::string>> groups;
+        groups.push_back({"decoder.token_embedding.weight"});
+        for (int i = 0; i < hp.n_audio_layer; ++i) {
+            const std::string p = "encoder.blocks." + std::to_string(i) + ".";
+            groups.push_back({p + "attn.query.weight", p + "attn.key.weight", p + "attn.value.weight"});
+            for (const char * n : {"attn.out.weight", "mlp.0.weight", "mlp.2.weight"}) groups.push_back({p + n});
+        }
+        for (int i = 0; i < hp.n_text_layer; ++i) {
+            const std::string p = "decoder.blocks." + std::to_string(i) + ".";
+            groups.push_back({p + "attn.query.weight", p + "attn.key.weight", p + "attn.value.weight"});
+            groups.push_back({p + "cross_attn.key.weight", p + "cross_attn.value.weight"});
+            for (const char * n : {"attn.out.weight", "cross_attn.query.weight", "cross_attn.out.weight", "mlp.0.weight",
+                                   "mlp.2.weight"})
+                groups.push_back({p + n});
+        }
+        const int f = m->qfmt;
+        auto al = [](size_t b) { return (b + 255) & ~(size_t) 255; };
+        struct KPlan { int N, K, kx, npad; size_t wi, dwt; };
+        std::vector<KPlan> kp;
+        size_t tot = 0;
+        for (const auto & gr : groups) {
+            KPlan pl{0, (int) S[idx.at(gr[0])].ne[0], 0, 0, 0, 0};
+            for (const auto & n : gr) pl.N += (int) S[idx.at(n)].ne[1];
+            pl.kx = kq_kx(f, pl.K);
+            pl.npad = (pl.N + 255) / 256 * 256;
+            pl.wi = tot;
+            tot += al((size_t) pl.N * pl.kx * 2);
+            pl.dwt = tot;
+            tot += al((size_t) (pl.kx / 32) * pl.npad * 4);
+            kp.push_back(pl);
+        }
+        m->q16blob.alloc(tot);
+        char * b16 = (char *) m->q16blob.ptr;
+        for (size_t gi = 0; gi < groups.size(); ++gi) {
+            const KPlan & pl = kp[gi];
+            std::vector<uint8_t> raw;
+            for (const auto & n : groups[gi]) raw.insert(raw.end(), host(n).data.begin(), host(n).data.end());
+            std::vector<uint16_t> wi((size_t) pl.N * pl.kx);
+            std::vector<float> dwt((size_t) (pl.kx / 32) * pl.npad);
+            kq_expand_host(f, raw.data(), pl.N, pl.K, wi.data(), dwt.data(), pl.npad);
+            OWK_HIP_CHECK(hipMemcpy(b16 + pl.wi, wi.data(), wi.size() * 2, hipMemcpyHostToDevice));
+            OWK_HIP_CHECK(hipMemcpy(b16 + pl.dwt, dwt.data(), dwt.size() * 4, hipMemcpyHostToDevice));
+            Q5W w;
+            w.fmt = f;
+            w.wi = (const _Float16 *) (b16 + pl.wi);
+            w.dwt = (const float *) (b16 + pl.dwt);
+            w.npad = pl.npad;
+            w.kx = pl.kx;
+            q5m[groups[gi][0]] = w;
+        }
+        // token embedding rows for get_rows: the reference dequantizes them to f32 (ggml get_rows)
+        {
+            const HostTensor & t = host("decoder.token_embedding.weight");
+            const int nv = (int) hp.n_vocab, dd = (int) d;
+            const size_t rb = (size_t) dd / 256 * kq_block_bytes(f);
+            std::vector<float> te((size_t) nv * dd);
+            for (int v = 0; v < nv; ++v) kq_dequant_row_host(f, t.data.data() + (size_t) v * rb, dd, te.data() + (size_t) v * dd);
+            m->te32.alloc(te.size() * 4);
+            OWK_HIP_CHECK(hipMemcpy(m->te32.ptr, te.data(), te.size() * 4, hipMemcpyHostToDevice));
+        }
+    }
+    if (m->q5 && !m->kq && n_loaded > 0) {
         std::vector<std::vector<std::string>> groups;
         groups.push_back({"decoder.token_embedding.weight"});
         const size_t n_dec_first = 0;  // token embedding: a decode (logits) matrix too

@@ -87,6 +87,9 @@ struct Model {
     int qfmt = 0;                        // their block format (kernels.h QFmt)
     DevBuf q5blob;
     DevBuf q16blob;  // Q5W::wi / dwt of the encoder and cross-K/V matrices (symmetric formats)
+    bool kq = false;                     // K-quant model (MOSTLY_Q2_K .. Q6_K, kquant.h): every 2-D linear
+                                         // as Q5W::wi / dwt in q16blob, the embedding rows dequantized
+    DevBuf te32;                         // K-quants: token embedding [n_vocab][d] f32 (dequantize_row_q*_K)
     Q5W q_te;
     const _Float16 * d_te = nullptr;     // [n_vocab][d]
     const _Float16 * d_te_t = nullptr;   // tiled copy (logits of decode steps)

@@ -12,6 +12,7 @@
 #include <thread>
 
 #include "state.h"
+#include "kquant.h"
 
 using namespace owk;
 
@@ -1345,6 +1346,85 @@ double owk_debug_decode_chain(int device, int R, int n_layers, int iters) {
     }
 }
 
+// K-quant formats (kquant.h): the model's path for every shape -- host expansion to the virtual
+// blocks, Q8_K activation rows (quantize_q8k_f16), gemm_q16 over the virtual K. q_out: the virtual
+// activation row values [M][kq_kx] as int8 (the bsums of layout 0 saturate: only q is checked),
+// d_out: the Q8_K d of every row and super-block [M][K/256]
+static int debug_gemm_kquant(int device, int fmt, int M, int N, int K, const float * a, const uint8_t * w_blocks,
+                             float * out, int8_t * q_out, float * d_out) {
+    OWK_HIP_CHECK(hipSetDevice(device));
+    hipStream_t s;
+    OWK_HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    const int kx = kq_kx(fmt, K), nkb = kx / 32, nsb = K / 256;
+    const int npad = (N + 255) / 256 * 256, mpad = (M + 255) / 256 * 256;
+    std::vector<uint16_t> wi((size_t) N * kx);
+    std::vector<float> dwt((size_t) nkb * npad);
+    kq_expand_host(fmt, w_blocks, N, K, wi.data(), dwt.data(), npad);
+    DevBuf da, dwi, ddw, q16, q16d, dout;
+    da.alloc((size_t) M * K * 4);
+    dwi.alloc(wi.size() * 2);
+    ddw.alloc(dwt.size() * 4);
+    q16.alloc((size_t) M * kx * 2);
+    q16d.alloc((size_t) nkb * mpad * 4);
+    dout.alloc((size_t) M * N * 4);
+    OWK_HIP_CHECK(hipMemcpy(da.ptr, a, (size_t) M * K * 4, hipMemcpyHostToDevice));
+    OWK_HIP_CHECK(hipMemcpy(dwi.ptr, wi.data(), wi.size() * 2, hipMemcpyHostToDevice));
+    OWK_HIP_CHECK(hipMemcpy(ddw.ptr, dwt.data(), dwt.size() * 4, hipMemcpyHostToDevice));
+    Q5W w;
+    w.fmt = fmt;
+    w.wi = dwi.as<_Float16>();
+    w.dwt = ddw.as<float>();
+    w.npad = npad;
+    w.kx = kx;
+    quantize_q8k_f16(s, da.as<float>(), nullptr, K, M, K, fmt, q16.as<_Float16>(), q16d.as<float>(), mpad);
+    EpiParams ep;
+    ep.out32 = dout.as<float>();
+    ep.ldo = N;
+    gemm_q16(s, EPI_F32, M, N, kx, q16.as<_Float16>(), q16d.as<float>(), mpad, w, ep);
+    OWK_HIP_CHECK(hipStreamSynchronize(s));
+    OWK_HIP_CHECK(hipMemcpy(out, dout.ptr, (size_t) M * N * 4, hipMemcpyDeviceToHost));
+    if (q_out) {
+        std::vector<_Float16> h((size_t) M * kx);
+        OWK_HIP_CHECK(hipMemcpy(h.data(), q16.ptr, h.size() * 2, hipMemcpyDeviceToHost));
+        for (size_t i = 0; i < h.size(); ++i) q_out[i] = (int8_t) std::max(-128.0f, std::min(127.0f, (float) h[i]));
+    }
+    if (d_out) {
+        std::vector<float> h((size_t) nkb * mpad);
+        OWK_HIP_CHECK(hipMemcpy(h.data(), q16d.ptr, h.size() * 4, hipMemcpyDeviceToHost));
+        const int per = nkb / nsb;
+        for (int r = 0; r < M; ++r) {
+            const int t = r & 127, pr = (r & ~127) | (t & 64) | ((t & 15) << 2) | ((t >> 4) & 3);
+            for (int sb = 0; sb < nsb; ++sb) d_out[(size_t) r * nsb + sb] = h[(size_t) sb * per * mpad + pr];
+        }
+    }
+    OWK_HIP_CHECK(hipStreamDestroy(s));
+    return 0;
+}
+
+// host-only K-quant decoding (tests/test_kquant.py, CPU): N rows of ggml blocks -> the virtual-block
+// expansion (wi [N][kx] f16 bits, dwt [kx/32][N]) and / or the reference's f32 row dequantization
+int owk_debug_kquant(int fmt, int N, int K, const uint8_t * w_blocks, uint16_t * wi, float * dwt, float * deq) {
+    try {
+        if (!qf_is_k(fmt) || N <= 0 || K % 256) throw std::runtime_error("bad format or shape");
+        if (wi || dwt) {
+            const int kx = kq_kx(fmt, K);
+            std::vector<uint16_t> w((size_t) N * kx);
+            std::vector<float> d((size_t) (kx / 32) * N);
+            kq_expand_host(fmt, w_blocks, N, K, w.data(), d.data(), N);
+            if (wi) memcpy(wi, w.data(), w.size() * 2);
+            if (dwt) memcpy(dwt, d.data(), d.size() * 4);
+        }
+        if (deq) {
+            const size_t rb = (size_t) K / 256 * kq_block_bytes(fmt);
+            for (int n = 0; n < N; ++n) kq_dequant_row_host(fmt, w_blocks + n * rb, K, deq + (size_t) n * K);
+        }
+    } catch (const std::exception & ex) {
+        log_msg(GGML_LOG_LEVEL_ERROR, "owk_debug_kquant: %s\n", ex.what());
+        return -1;
+    }
+    return 0;
+}
+
 int owk_debug_gemm_quant(int device, int fmt, int M, int N, int K, const float * a, const uint8_t * w_blocks,
                          float * out, int8_t * q_out, float * d_out) {
     return owk_debug_gemm_quant2(device, fmt, M, N, K, a, w_blocks, out, q_out, d_out, 0);
@@ -1353,6 +1433,7 @@ int owk_debug_gemm_quant(int device, int fmt, int M, int N, int K, const float *
 int owk_debug_gemm_quant2(int device, int fmt, int M, int N, int K, const float * a, const uint8_t * w_blocks,
                           float * out, int8_t * q_out, float * d_out, int use_q16) {
     try {
+        if (qf_is_k(fmt)) return debug_gemm_kquant(device, fmt, M, N, K, a, w_blocks, out, q_out, d_out);
         if (fmt < QF_Q5_0 || fmt > QF_Q5_1 || K % 32) throw std::runtime_error("bad format or K");
         OWK_HIP_CHECK(hipSetDevice(device));
         hipStream_t s;

@@ -16,6 +16,12 @@ tokens are within 2x the logit floor of each other.
 
 Usage (in a container that has /root/reference):  python tests/golden/make_golden_q5.py [q8_0]
 (q8_0 / q4_0 / q4_1 / q5_1: the same fixtures for those files -> q8_ / q4_ / q41_ / q51_golden.*)
+
+K-quants (q2_k / q3_k / q4_k / q5_k / q6_k -> q2k_ .. q6k_golden.*): the files are written by the
+reference's own quantizer (oracle/_ref/whisper-quantize, ggml quantize_row_q*_K_ref) -- there is no
+Python restatement of its iterative scale search -- on base.en instead of tiny.en (K-quant rows are
+multiples of 256: tiny's 384-wide rows do not quantize) and l3-mini. The reference runs its
+q*_K x q8_K path (CPU repack 8x8 kernels for q4_K / q2_K, as x86 builds with AVX2 / AVX-512 do).
 """
 import json
 import os
@@ -32,10 +38,24 @@ import ref_oracle as R  # noqa: E402
 
 OUT = os.path.dirname(os.path.abspath(__file__))
 SEED = 1234
-MODELS = ["tiny.en", "l3-mini"]
 TF_TOKENS = 48
 KIND = sys.argv[1] if len(sys.argv) > 1 else "q5_0"
-assert KIND in ("q5_0", "q8_0", "q4_0", "q4_1", "q5_1")
+K_KINDS = ("q2_k", "q3_k", "q4_k", "q5_k", "q6_k")
+assert KIND in ("q5_0", "q8_0", "q4_0", "q4_1", "q5_1") + K_KINDS
+MODELS = ["base.en", "l3-mini"] if KIND in K_KINDS else ["tiny.en", "l3-mini"]
+QUANT = os.path.join(ROOT, "oracle", "_ref", "whisper-quantize")
+
+
+def quantize(src, dst):
+    """The quantized file's SHA-256: owk_synth's restatement for the 32-blocks, the reference's own
+    whisper-quantize for the K-quants."""
+    if KIND not in K_KINDS:
+        return S.quantize_q5_0(src, dst, kind=KIND)
+    import hashlib
+    import subprocess
+
+    subprocess.run([QUANT, src, dst, KIND], check=True, capture_output=True)
+    return hashlib.sha256(open(dst, "rb").read()).hexdigest()
 
 
 def main():
@@ -48,8 +68,7 @@ def main():
         src = os.path.join(cache, f"synth-{model}-s{SEED}.bin")
         S.write_model(src, model, SEED)
         path = os.path.join(cache, f"synth-{model}-{KIND}-s{SEED}.bin")
-        quant = lambda s, d: S.quantize_q5_0(s, d, kind=KIND)
-        meta["models"][model] = {"sha256": quant(src, path)}
+        meta["models"][model] = {"sha256": quantize(src, path)}
         ref = R.Ref(path)
         multilingual = S.MODELS[model][0] >= 51865
         for cname, pcm in audio.items():
@@ -118,7 +137,7 @@ def main():
                 meta["results"][f"{key}/noise_floor/agree/{cfg}"] = min(agree)
             print(model, cname, "floors", meta["results"][key + "/noise_floor/enc_rows"], dl, flush=True)
         ref.close()
-    stem = {"q4_1": "q41", "q5_1": "q51"}.get(KIND, KIND[:2]) + "_golden"
+    stem = {"q4_1": "q41", "q5_1": "q51"}.get(KIND, KIND[:2] + ("k" if KIND in K_KINDS else "")) + "_golden"
     meta["kind"] = KIND
     np.savez_compressed(os.path.join(OUT, stem + ".npz"), **arrays)
     with open(os.path.join(OUT, stem + ".json"), "w") as f:

@@ -205,5 +205,94 @@ def test_large_dtw(large, clips, model, clip):
     r_dtw = [t[8] for s in want["segments"] for t in s["tokens"]]
     diff = [(i, a, b) for i, (a, b) in enumerate(zip(g_dtw, r_dtw)) if a != b]
     print(f"[large-dtw] {key}: t_dtw differs on {len(diff)}/{len(r_dtw)} tokens {diff[:8]}")
-    assert all(abs(a - b) <= 20 and a >= 0 and b >= 0 for _, a, b in diff), f"t_dtw differs: {diff[:10]}"
-    assert len(diff) <= 0.05 * len(r_dtw), f"t_dtw differs on {len(diff)}/{len(r_dtw)} tokens: {diff[:10]}"
+    # on the reference's own tokens the DTW timestamps are exact (measured: 0 differences)
+    assert not diff, f"t_dtw differs on {len(diff)}/{len(r_dtw)} tokens: {diff[:10]}"
+
+
+class StepRecorder:
+    """logits_filter_callback for the Q5_0 teacher-forced agreement test: for the watched states,
+    records per decode step the greedy pick over the tokens the pick can take (text tokens below
+    <|endoftext|>; not " " at the first step -- the reference's filters, whisper.cpp:6213-6250,
+    with the fixed-work EOT suppression) and the logits of the golden's candidate set, then forces
+    the reference's token (Forcer's +40 above the maximum). Other states run untouched."""
+
+    def __init__(self, watch, eot, blank, n_vocab, token_data_type):
+        self.watch, self.eot, self.blank, self.n_vocab = watch, eot, blank, n_vocab  # watch: state -> (tokens, cand)
+        self.pick = {s: {} for s in watch}
+        self.cand_val = {s: {} for s in watch}
+        TD = C.POINTER(token_data_type)
+        proto = C.CFUNCTYPE(None, C.c_void_p, C.c_void_p, TD, C.c_int, C.POINTER(C.c_float), C.c_void_p)
+        self.cfunc = proto(self._cb)
+
+    def _cb(self, ctx, state, tokens, n_tokens, logits, user):
+        if state not in self.watch:
+            return
+        toks, cand = self.watch[state]
+        if n_tokens >= len(toks):
+            return
+        lg = np.ctypeslib.as_array(logits, shape=(self.n_vocab,))
+        allowed = lg[:self.eot].copy()
+        if n_tokens == 0:
+            allowed[self.blank] = -np.inf
+        self.pick[state][n_tokens] = int(allowed.argmax())
+        self.cand_val[state][n_tokens] = lg[cand[n_tokens]].copy()
+        fin = np.isfinite(lg)
+        lg[toks[n_tokens]] = float(lg[fin].max()) + 40.0
+
+
+def test_q5_teacher_forced_agreement(large, clips):
+    """large-v3 Q5_0, 32 clips in one owk_full_batch, fixed work (220 tokens): the golden slots are
+    teacher-forced onto the reference's 220 tokens; per step, the GPU's greedy pick must equal the
+    reference's token on >= 95 % of the steps, and every disagreement must be a near-tie the
+    reference itself does not resolve: the reference's logit gap between its token and the GPU's
+    pick is within 2x its own 1e-7-perturbation spread at that step (tests/golden/make_golden_q5tf.py).
+    Also reports the per-step logit error over the candidates against that spread."""
+    path = os.path.join(GOLDEN, "q5tf_golden.json")
+    if not os.path.exists(path):
+        pytest.skip("q5tf_golden.json not generated")
+    tf = json.load(open(path))
+    tarr = np.load(os.path.join(GOLDEN, "q5tf_golden.npz"))
+    meta, _ = large
+    model = "large-v3-q5_0"
+    assert tf["sha256"] == meta["models"][model]["sha256"]
+    owk.quiet()
+    w = whisper(meta, model)
+    states = [w.new_state() for _ in range(BATCH)]
+    watch = {}
+    for slot, clip in [(0, "jfk"), (17, "synth30")]:
+        key = f"{model}/{clip}"
+        watch[states[slot]] = (tarr[key + "/tokens"].tolist(), tarr[key + "/cand"])
+    rec = StepRecorder(watch, tf["eot"], tf["blank"], w.n_vocab, owk.TokenData)
+    p = w.params(0, language="en", temperature_inc=0.0, no_timestamps=True, max_tokens=FIXED_MAX_TOKENS)
+    p.logits_filter_callback = C.cast(rec.cfunc, C.c_void_p)
+    assert w.full_batch(states, _batch_clips(clips), p, suppress_eot=True) == 0
+    for slot, clip in [(0, "jfk"), (17, "synth30")]:
+        key = f"{model}/{clip}"
+        st = states[slot]
+        toks = tarr[key + "/tokens"]
+        cand, cval, floor = tarr[key + "/cand"], tarr[key + "/cand_val"], tarr[key + "/floor"]
+        n = len(toks)
+        assert sorted(rec.pick[st]) == list(range(n)), f"{key}: recorded {len(rec.pick[st])} of {n} steps"
+        got_ids = [t[0] for s in w.segments(st) for t in s["tokens"]]
+        assert got_ids == toks.tolist(), f"{key}: the teacher-forced run left the reference tokens"
+        disagree = []
+        err_ratio = []
+        for i in range(n):
+            err_ratio.append(float(np.abs(rec.cand_val[st][i] - cval[i]).max() / max(floor[i], 1e-6)))
+            g = rec.pick[st][i]
+            if g == toks[i]:
+                continue
+            where = np.nonzero(cand[i] == g)[0]
+            assert where.size, f"{key} step {i}: GPU pick {g} is not among the reference's top {cand.shape[1]}"
+            ref_gap = float(cval[i, 0] - cval[i, where[0]])
+            disagree.append((i, int(toks[i]), g, ref_gap, float(floor[i])))
+        rate = 1 - len(disagree) / n
+        print(f"[q5tf] {key}: greedy pick equals the reference token on {n - len(disagree)}/{n} steps ({100 * rate:.1f} %); "
+              f"disagreements (step, ref, gpu, ref gap, ref floor): {disagree}; logit error / floor: "
+              f"median {np.median(err_ratio):.2f} max {max(err_ratio):.2f}")
+        assert rate >= 0.95, f"{key}: agreement {rate:.3f} < 0.95"
+        for i, _, _, gap, fl in disagree:
+            assert gap <= 2 * fl, f"{key} step {i}: reference gap {gap:.3e} above 2x its noise floor {fl:.3e}"
+    for s in states:
+        w.L.whisper_free_state(s)
+    w._states = [s for s in w._states if s not in states]
