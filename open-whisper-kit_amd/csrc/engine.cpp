@@ -3,6 +3,7 @@
 #include "kquant.h"
 
 #include <algorithm>
+#include <map>
 #include <cmath>
 #include <cstring>
 
@@ -240,7 +241,8 @@ void Engine::linear(const char * cls, int mode, int M, int N, int K, const _Floa
             throw std::runtime_error("linear: K-quant operand buffers not reserved");
         {
             ProfScope ps(prof, stream, "quantize_q8");
-            quantize_q8k_f16(stream, A32, A16, lda, M, K, q.fmt, q16a_.as<_Float16>(), q16d_.as<float>(), mpad);
+            quantize_q8k_f16(stream, A32, A16, lda, M, K, q.fmt, q16a_.as<_Float16>(), q16d_.as<float>(), mpad,
+                             qf_k_repacked(q.fmt) ? kq_rmul_ : nullptr);
         }
         ProfScope ps(prof, stream, cls, gemm_flops(M, N, K), (double) N * K * kq_block_bytes(q.fmt) / 256.0 + (double) M * K);
         gemm_q16(stream, mode, M, N, kx, q16a_.as<_Float16>(), q16d_.as<float>(), mpad, q, ep);
@@ -343,6 +345,17 @@ void Engine::encode(const std::vector<int> & slots, const std::vector<int> & off
         G("gemm_conv", EPI_CONV2, M, d, 3 * d, e_a2_.as<_Float16>(), 3 * d, m->conv2_w, ep);
     }
 
+    // K-quants with repacked reference weights: each clip's T rows are one reference matmul, whose
+    // complete groups of 4 rows take the repack quantizer (kernels.h qf_k_repacked)
+    kq_rmul_ = nullptr;
+    if (m->kq && qf_k_repacked(m->qfmt)) {
+        std::vector<uint8_t> rm((size_t) M);
+        for (int i = 0; i < n; ++i)
+            for (int t = 0; t < T; ++t) rm[(size_t) i * T + t] = t < T - T % 4;
+        e_rmul_.alloc(rm.size());
+        OWK_HIP_CHECK(hipMemcpy(e_rmul_.ptr, rm.data(), rm.size(), hipMemcpyHostToDevice));
+        kq_rmul_ = e_rmul_.as<uint8_t>();
+    }
     const float kq_scale = 1.0f / sqrtf((float) 64);
     for (int l = 0; l < hp.n_audio_layer; ++l) {
         const EncLayerW & L = m->enc[l];
@@ -431,6 +444,7 @@ void Engine::encode(const std::vector<int> & slots, const std::vector<int> & off
         linear("gemm_cross", EPI_KV_CROSS, M, 2 * d, d, e_enc_.as<_Float16>(), m->q5 ? e_enc32_.as<float>() : nullptr, d,
                L.cw_kv, L.q_ckv, ep, nullptr, false, m->q5 && !m->kq);
     }
+    kq_rmul_ = nullptr;
 }
 
 void Engine::download_enc(int index, float * host) const {
@@ -473,6 +487,7 @@ void Engine::stage_layout(int C, int KC) {
     st_rs_ = sec((size_t) C * sizeof(AttnRow));
     st_rc_ = sec((size_t) C * sizeof(AttnRow));
     st_lsel_ = sec((size_t) C * 4);
+    st_rmul_ = sec((size_t) C);
     st_keys_ = sec((size_t) KC * 4);
     st_bytes_ = o;
 }
@@ -595,6 +610,17 @@ void Engine::decode(const std::vector<DecodeRow> & rows, const std::vector<int> 
         (x.mode_cross == 2 ? sh.cross_sm : x.mode_cross ? sh.cross_tl : sh.cross_oc) = true;
         if (x.logit_row >= 0) lsel[x.logit_row] = r;
     }
+    if (m->kq && qf_k_repacked(m->qfmt)) {
+        // each clip's rows of this pass are one reference decode batch (its decoders' tokens, or a
+        // prompt): the rows of its complete groups of 4 take the repack quantizer
+        uint8_t * rm = (uint8_t *) (h + st_rmul_);
+        std::map<int, int> cnt, seen;
+        for (int r = 0; r < R; ++r) cnt[rows[r].slot]++;
+        for (int r = 0; r < R; ++r) {
+            const int c = cnt[rows[r].slot], i = seen[rows[r].slot]++;
+            rm[r] = i < c - c % 4;
+        }
+    }
     if (nk) memcpy(h + st_keys_, key_list.data(), (size_t) nk * 4);
     OWK_HIP_CHECK(hipMemcpyAsync(d_stg_.ptr, h, st_keys_ + (size_t) nk * 4, hipMemcpyHostToDevice, stream));
     if (sh.self_oc && sh.max_keys > attn_max_listed_keys()) throw std::runtime_error("decode: too many self-attention keys");
@@ -674,6 +700,7 @@ void Engine::launch_decode(const DecShape & sh) {
     // Q5_0: attention passes whose rows all take the one_chunk kernel emit the Q8_0 rows
     // themselves; otherwise their f32 output is quantized by the GEMM call
     const bool kq = m->kq;  // K-quants: GEMMs quantize f32 rows to Q8_K themselves (no producer rows)
+    kq_rmul_ = kq && qf_k_repacked(m->qfmt) ? (const uint8_t *) (dv + st_rmul_) : nullptr;
     const bool fq_self = q5 && !kq && self_oc && !self_tl && !sh.self_sm;
     const bool fq_cross = q5 && !kq && cross_oc && !cross_tl && !sh.cross_sm;
     float * xn32 = kq ? d_xn32_.as<float>() : nullptr;  // the f32 LayerNorm rows a K-quant GEMM quantizes
@@ -936,6 +963,7 @@ void Engine::launch_decode(const DecShape & sh) {
             layernorm_f16(stream, d_x_.as<float>(), n_logit_rows, d, m->d_ln_w, m->d_ln_b, hp.eps, d_xl_.as<_Float16>(),
                           d, d_lsel, kq ? d_xl32_.as<float>() : nullptr, q8a(), q8d());
         }
+        kq_rmul_ = nullptr;  // the token embedding is not repacked (a get_rows tensor): quantize_row_q8_K
         EpiParams ep;
         ep.out32 = logits_.as<float>();
         ep.ldo = nv;

@@ -161,6 +161,8 @@ private:
     // encoder workspace
     DevBuf e_a1_, e_c1_, e_a2_, e_x_, e_xn_, e_q_, e_k_, e_vt_, e_ao_, e_h_, e_enc_, e_enc32_;
     DevBuf e_win_, e_slotmap_;
+    DevBuf e_rmul_;                       // encoder rows' Q8_K rounding path (K-quants, repacked formats)
+    const uint8_t * kq_rmul_ = nullptr;   // the rows' path of the linears being issued (null: all fma)
     int enc_rows_cap_ = 0;
     int last_enc_n_ = 0;
     int vt_T_ = 0;  // n_ctx() the transposed-V buffer was zeroed for
@@ -172,6 +174,7 @@ private:
     PinnedBuf stg_;   // host image of the per-pass inputs
     DevBuf d_stg_;    // its device copy (fixed sections, see stage_layout)
     size_t st_tok_ = 0, st_pos_ = 0, st_rowoff_ = 0, st_rs_ = 0, st_rc_ = 0, st_lsel_ = 0, st_keys_ = 0, st_bytes_ = 0;
+    size_t st_rmul_ = 0;  // K-quants (repacked formats): per-row Q8_K rounding path (quantize_q8k_f16)
     std::map<uint64_t, hipGraphExec_t> graphs_;
     uint64_t graphs_sig_ = 0;
 

@@ -1181,10 +1181,16 @@ void quantize_q8_f16(hipStream_t s, const float * A32, const _Float16 * A16, int
 // ggml-quants.c:2555-2592) in the virtual-block layout of kquant.h: one 256-thread block per
 // (row, super-block). LAY 0: 8 blocks of q + one block [16 bsums | 16 zeros]; 1: 8 blocks of q;
 // 2: 16 blocks [16 q | 16 zeros]. Every virtual block of the super-block carries d = 1 / iscale.
+// Rounding: quantize_row_q8_K_ref's nearest_int(iscale * x) is `iscale * x + 12582912.f` and its bits,
+// which gcc (-std=gnu11: -ffp-contract=fast, the reference's CMake default) contracts into ONE fused
+// multiply-add -- the exact product rounded once. rmul[r] != 0 selects the x86 repack quantizer
+// instead (ggml_quantize_mat_q8_K_4x8, ggml-cpu/arch/x86/repack.cpp:290-420: the rows of complete
+// groups of 4 of a Q4_K / Q2_K matmul): the product rounded to f32 first, then to nearest even, and
+// iscale = -127 / amax when some element equals +amax, else 127 / amax.
 template <typename TA, int LAY>
 __global__ __launch_bounds__(256) void k_quantize_q8k_f16(const TA * __restrict__ A, int lda, int M, int K,
                                                           _Float16 * __restrict__ q, float * __restrict__ dat,
-                                                          int mpad) {
+                                                          int mpad, const uint8_t * __restrict__ rmul) {
     __shared__ uint32_t s_key[256];
     __shared__ float s_x[256];
     const int nsb = K >> 8;
@@ -1212,12 +1218,23 @@ __global__ __launch_bounds__(256) void k_quantize_q8k_f16(const TA * __restrict_
     }
     const float amax = __uint_as_float(s_key[0]);
     const float mx = s_x[s_idx[0]];
+    const bool mul_path = rmul && rmul[r];
+    const bool pos_max = __syncthreads_or(x == amax);  // uniform: every thread reaches it
     int qv = 0;
     float d = 0.0f;
     if (amax != 0.0f) {
-        const float iscale = -127.f / mx;
-        qv = min(127, (int) rintf(iscale * x));
-        d = 1.0f / iscale;
+        if (mul_path) {
+            const float iscale = pos_max ? -127.f / amax : 127.f / amax;
+            float p = x * iscale;
+            asm volatile("" : "+v"(p));  // the rounded product (no contraction into the rounding)
+            qv = min(127, (int) rintf(p));
+            d = 1.0f / iscale;
+        } else {
+            const float iscale = -127.f / mx;
+            const float v = __builtin_fmaf(iscale, x, 12582912.f);
+            qv = min(127, (__float_as_int(v) & 0x007fffff) - 0x00400000);
+            d = 1.0f / iscale;
+        }
     }
     // sums of 16 (one group of 16 lanes of a wave)
     int bs = qv;
@@ -1254,13 +1271,13 @@ __global__ __launch_bounds__(256) void k_quantize_q8k_f16(const TA * __restrict_
 }
 
 void quantize_q8k_f16(hipStream_t s, const float * A32, const _Float16 * A16, int lda, int M, int K, int fmt,
-                      _Float16 * q16, float * dat, int mpad) {
+                      _Float16 * q16, float * dat, int mpad, const uint8_t * rmul) {
     if (M <= 0) return;
     if (K % 256 || !qf_is_k(fmt) || mpad < (M + 127) / 128 * 128) throw std::runtime_error("quantize_q8k_f16: shape");
     const int lay = fmt == QF_Q3_K ? 1 : fmt == QF_Q6_K ? 2 : 0;
     const size_t blocks = (size_t) M * (K / 256);
     if (blocks > 0x7fffffff) throw std::runtime_error("quantize_q8k_f16: too many rows");
-#define OWK_Q8K(T, P, L) OWK_LAUNCH((k_quantize_q8k_f16<T, L>), dim3((unsigned) blocks), dim3(256), 0, s, P, lda, M, K, q16, dat, mpad)
+#define OWK_Q8K(T, P, L) OWK_LAUNCH((k_quantize_q8k_f16<T, L>), dim3((unsigned) blocks), dim3(256), 0, s, P, lda, M, K, q16, dat, mpad, rmul)
     if (A32) {
         if (lay == 0) OWK_Q8K(float, A32, 0);
         else if (lay == 1) OWK_Q8K(float, A32, 1);

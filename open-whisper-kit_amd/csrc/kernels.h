@@ -170,9 +170,14 @@ bool gemm_q16_applies(const Q5W & w, int M, int N, int K);
 // Q8_K rows of A (quantize_row_q8_K_ref, ggml-quants.c:2555-2592: per 256 the signed value of the
 // first largest |x|, iscale = -127 / max, q = min(127, rne(iscale * x)), d = 1 / iscale, int sums
 // per 16) laid out for the K-quant format `fmt` (kquant.h): q16 [M][kq_kx(fmt, K)] exact f16, dat
-// [kx / 32][mpad] f32 (rows permuted like quantize_q8_f16)
+// [kx / 32][mpad] f32 (rows permuted like quantize_q8_f16). rmul (optional, [M]): rows quantized the
+// way the reference's x86 repack path does (ggml_quantize_mat_q8_K_4x8: Q4_K / Q2_K weights, the rows
+// of complete groups of 4 of each matmul; k_gemm.hip has the two roundings)
 void quantize_q8k_f16(hipStream_t s, const float * A32, const _Float16 * A16, int lda, int M, int K, int fmt,
-                      _Float16 * q16, float * dat, int mpad);
+                      _Float16 * q16, float * dat, int mpad, const uint8_t * rmul = nullptr);
+// the reference repacks these K-quant weights for its x86 matmuls (ggml-cpu/repack.cpp:3076-3097:
+// Q4_K with AVX2, Q2_K with AVX-512; every whisper linear has N % 8 == 0)
+__host__ __device__ constexpr bool qf_k_repacked(int f) { return f == QF_Q4_K || f == QF_Q2_K; }
 // expand Q5W block arrays into wi / dwt (device buffers of N*K halves and K/32*npad floats)
 void quant_expand_f16(hipStream_t s, const Q5W & w, int N, int K, _Float16 * wi, float * dwt, int npad);
 // EPI_PARTIAL decode-row quantized GEMM whose activation rows are f16 (quantized to Q8_0 inside)

@@ -62,7 +62,7 @@ def stream_run(sf, pcm):
     return np.concatenate(outs, 0), counts
 
 
-def traced_windows(ref):
+def traced_windows(ref, flat):
     """Per-window decoded token prefixes from the traced decoder calls (a window starts where the
     traced prefix is empty again) and, per window, whether its end is OPEN: a window whose longest
     traced prefix is n_max - 1 = 219 tokens stopped at the n_text_ctx/2 - 4 step limit (ref
@@ -77,7 +77,12 @@ def traced_windows(ref):
             longest.append([])
         elif len(p) > len(longest[-1]):
             longest[-1] = p
-    return longest, [len(w) + 1 >= 220 for w in longest]
+    open_end = [len(w) + 1 >= 220 for w in longest]
+    # the last window may also end on a kept token that follows no call: a timestamp reaching the
+    # end of the audio (ref 7359-7441) -- the last result token, forced like the rest
+    if flat and not open_end[-1] and (not longest[-1] or longest[-1][-1] != flat[-1]):
+        longest[-1].append(flat[-1])
+    return longest, open_end
 
 
 def words_of(L, ctx, segs):
@@ -135,7 +140,7 @@ def main():
         ret, segs = ref.full(pcm, n_threads=NT, record_topk=2, **PARAMS)
         print("whisper_full", ret, len(segs), "segments", sum(len(s["tokens"]) for s in segs), "tokens",
               f"{time.time() - t:.0f} s", flush=True)
-        wins, open_end = traced_windows(ref)
+        wins, open_end = traced_windows(ref, [t[0] for s in segs for t in s["tokens"]])
         st1 = {"ret": ret, "segments": segs, "windows": wins, "open": open_end, "words": words_of(L, ref.ctx, segs)}
         ref.close()
         with open(stage1, "w") as f:
