@@ -262,29 +262,32 @@ def test_init_rejects_bad_files(tmp_path):
 
 
 @pytest.mark.gpu
-def test_gpu_whisper_full_parallel_with_vad(vctx, model_path, clips):
-    """whisper_full_parallel(params.vad, 2 processors) (ref 7801-7929 with the VAD pre-pass
-    of 7812-7824): succeeds, and every segment time maps back inside the original audio in
-    order (no reference fixture covers the split-chunk merge: parity unpinned here)."""
+@pytest.mark.parametrize("clip", ["jfk", "composite"])
+def test_gpu_whisper_full_parallel_with_vad(vctx, model_path, clips, clip):
+    """whisper_full_parallel(params.vad, 2 processors) (ref 7801-7929 with the VAD pre-pass of
+    7812-7824 and the segment-time mapping of 7947-8025) against the reference's own run on the same
+    clip and model (tests/golden/make_golden_vad_parallel.py): segment times and token ids identical."""
+    want = json.load(open(os.path.join(GOLDEN, "vad_golden.json")))["full"].get(f"{clip}/parallel2")
+    if want is None:
+        pytest.skip("no whisper_full_parallel + VAD fixture (make_golden_vad_parallel.py)")
     w = owk.Whisper(model_path("tiny.en"))
     try:
         L = w.L
         p = w.params(0, temperature_inc=0.0, language="en")
         p.vad = True
         p.vad_model_path = VAD_MODEL.encode()
-        pcm = np.ascontiguousarray(clips["composite"], np.float32)
-        assert L.whisper_full_parallel(w.ctx, p, owk.fptr(pcm), len(pcm), 2) == 0
+        pcm = np.ascontiguousarray(clips[clip], np.float32)
+        assert L.whisper_full_parallel(w.ctx, p, owk.fptr(pcm), len(pcm), 2) == want["ret"]
         L.whisper_full_get_segment_t0.restype = C.c_int64
         L.whisper_full_get_segment_t1.restype = C.c_int64
         L.whisper_full_get_segment_t0.argtypes = [C.c_void_p, C.c_int]
         L.whisper_full_get_segment_t1.argtypes = [C.c_void_p, C.c_int]
-        n = L.whisper_full_n_segments(w.ctx)
-        assert n >= 1
-        dur_cs = len(pcm) * 100 // 16000
-        prev = -1
-        for i in range(n):
-            t0, t1 = L.whisper_full_get_segment_t0(w.ctx, i), L.whisper_full_get_segment_t1(w.ctx, i)
-            assert 0 <= t0 <= t1 <= dur_cs + 10 and t0 >= prev, (i, t0, t1)
-            prev = t0
+        L.whisper_full_get_token_id.argtypes = [C.c_void_p, C.c_int, C.c_int]
+        L.whisper_full_n_tokens.argtypes = [C.c_void_p, C.c_int]
+        got = [{"t0": L.whisper_full_get_segment_t0(w.ctx, i), "t1": L.whisper_full_get_segment_t1(w.ctx, i),
+                "tokens": [L.whisper_full_get_token_id(w.ctx, i, j) for j in range(L.whisper_full_n_tokens(w.ctx, i))]}
+               for i in range(L.whisper_full_n_segments(w.ctx))]
+        print(f"[vad-parallel] {clip}: {len(got)} segments {[(g['t0'], g['t1']) for g in got]}")
+        assert got == want["segments"]
     finally:
         w.close()
