@@ -219,20 +219,6 @@ void Engine::linear(const char * cls, int mode, int M, int N, int K, const _Floa
     // the reference rounds each activation row to Q8_0 / Q8_1 (x86 quantize_row_q8_0 / _q8_1) before
     // the block dot; bytes: the weight blocks (18-34 B per 32) + the int8 activations. a_q8: the
     // producer (LayerNorm, one_chunk attention) already wrote q8a_ / q8d_
-    if (gemm_q16_applies(q, M, N, K)) {
-        // large tiles: Q8_0 integers as exact f16 + block-major scales, the f16 MFMA ring kernel; the
-        // rows are quantized from the f32 activation (A32) where the producer keeps one, as the reference
-        const int mpad = (M + 255) / 256 * 256;
-        if (q16a_.bytes < (size_t) M * K * 2 || q16d_.bytes < (size_t) (K / 32) * mpad * 4)
-            throw std::runtime_error("linear: gemm_q16 operand buffers not reserved");
-        {
-            ProfScope ps(prof, stream, "quantize_q8");
-            quantize_q8_f16(stream, A32, A16, lda, M, K, q16a_.as<_Float16>(), q16d_.as<float>(), mpad);
-        }
-        ProfScope ps(prof, stream, cls, gemm_flops(M, N, K), 2.0 * ((double) M * K + (double) N * K));
-        gemm_q16(stream, mode, M, N, K, q16a_.as<_Float16>(), q16d_.as<float>(), mpad, q, ep);
-        return;
-    }
     if (qf_is_k(q.fmt)) {
         // K-quants: Q8_K rows in the virtual-block layout (kquant.h), then the f16 MFMA ring kernel
         // over the virtual K at every shape
@@ -246,6 +232,20 @@ void Engine::linear(const char * cls, int mode, int M, int N, int K, const _Floa
         }
         ProfScope ps(prof, stream, cls, gemm_flops(M, N, K), (double) N * K * kq_block_bytes(q.fmt) / 256.0 + (double) M * K);
         gemm_q16(stream, mode, M, N, kx, q16a_.as<_Float16>(), q16d_.as<float>(), mpad, q, ep);
+        return;
+    }
+    if (gemm_q16_applies(q, M, N, K)) {
+        // large tiles: Q8_0 integers as exact f16 + block-major scales, the f16 MFMA ring kernel; the
+        // rows are quantized from the f32 activation (A32) where the producer keeps one, as the reference
+        const int mpad = (M + 255) / 256 * 256;
+        if (q16a_.bytes < (size_t) M * K * 2 || q16d_.bytes < (size_t) (K / 32) * mpad * 4)
+            throw std::runtime_error("linear: gemm_q16 operand buffers not reserved");
+        {
+            ProfScope ps(prof, stream, "quantize_q8");
+            quantize_q8_f16(stream, A32, A16, lda, M, K, q16a_.as<_Float16>(), q16d_.as<float>(), mpad);
+        }
+        ProfScope ps(prof, stream, cls, gemm_flops(M, N, K), 2.0 * ((double) M * K + (double) N * K));
+        gemm_q16(stream, mode, M, N, K, q16a_.as<_Float16>(), q16d_.as<float>(), mpad, q, ep);
         return;
     }
     if (!a_q8) {

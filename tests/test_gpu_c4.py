@@ -79,6 +79,9 @@ def _logit_error(w, meta, arr, pcm):
     return max(e1, e2)
 
 
+_free_run = {}  # test_configs4_transcription's result, aligned by test_configs4_stream_and_align
+
+
 def _params(w, meta):
     return w.params(0, **meta["params"])
 
@@ -93,6 +96,14 @@ def test_configs4_transcription(c4, w4, test60):
     got = w4.segments(st)
     assert len(want["segments"]) > 1 and want["segments"][-1]["t1"] > 3000
     compare_segments(got, want["segments"], "c4/free", tie=TIE_FACTOR * eps)
+    g_ids = [t[0] for x in got for t in x["tokens"]]
+    r_ids = [t[0] for x in want["segments"] for t in x["tokens"]]
+    if g_ids == r_ids:  # no near-tie parting: the DTW timestamps of the free run are the reference's too
+        diff = [(i, a[8], b[8]) for i, (a, b) in enumerate(zip([t for x in got for t in x["tokens"]],
+                                                                [t for x in want["segments"] for t in x["tokens"]])) if a[8] != b[8]]
+        print(f"[c4] free run: {len(g_ids)} tokens identical, t_dtw differs on {len(diff)}")
+        assert not diff, diff[:10]
+    _free_run["segments"] = got
 
 
 def _forced_run(w, meta, pcm):
@@ -111,13 +122,15 @@ def test_configs4_dtw_teacher_forced(c4, w4, test60):
     got = _forced_run(w4, meta, test60)
     r_ids = [t[0] for s in want for t in s["tokens"]]
     assert [t[0] for s in got for t in s["tokens"]] == r_ids, "teacher-forced decode left the reference tokens"
-    assert [(s["t0"], s["t1"]) for s in got] == [(s["t0"], s["t1"]) for s in want]
-    g = [(t[6], t[7], t[8]) for s in got for t in s["tokens"]]
-    r = [(t[6], t[7], t[8]) for s in want for t in s["tokens"]]
+    # t_dtw is computed FROM the tokens (alignment-head attention, DTW): exact. The token-level t0 / t1
+    # come from the decoder's timestamp probabilities, which forcing the text tokens changes (the free
+    # run above compares them)
+    g = [t[8] for s in got for t in s["tokens"]]
+    r = [t[8] for s in want for t in s["tokens"]]
     diff = [(i, a, b) for i, (a, b) in enumerate(zip(g, r)) if a != b]
-    print(f"[c4] {len(r_ids)} tokens over {len(meta['results']['windows'])} windows; (t0, t1, t_dtw) differ on "
+    print(f"[c4] {len(r_ids)} tokens over {len(meta['results']['windows'])} windows; t_dtw differs on "
           f"{len(diff)}: {diff[:6]}")
-    assert not diff, f"token timestamps differ: {diff[:10]}"
+    assert not diff, f"t_dtw differs: {diff[:10]}"
 
 
 def _stream(pcm, block):
@@ -181,8 +194,15 @@ def test_configs4_stream_and_align(c4, w4, test60):
           f"{int(bad.sum())} outside the reference's threshold noise band")
     assert not bad.any(), np.argwhere(bad)[:10]
 
-    # aligner over the teacher-forced tokens (Swift WordTiming per token) and the GPU RTTM
-    got = _forced_run(w4, meta, test60)
+    # aligner over the free run's tokens (Swift WordTiming per token: text, t0, t1, p) and the RTTMs
+    got = _free_run.get("segments")
+    if got is None:
+        st = w4.new_state()
+        assert w4.full(st, test60, _params(w4, meta)) == meta["results"]["full"]["ret"]
+        got = w4.segments(st)
+    r_ids = [t[0] for s in meta["results"]["full"]["segments"] for t in s["tokens"]]
+    if [t[0] for s in got for t in s["tokens"]] != r_ids:
+        pytest.skip("the free run parted from the reference at a near-tie: no word-level comparison")
     words = []
     for s in got:
         for t in s["tokens"]:
