@@ -25,15 +25,25 @@ def main():
     os.makedirs(cache, exist_ok=True)
     path = os.path.join(cache, f"synth-tiny.en-s{SEED}.bin")
     assert S.write_model(path, "tiny.en", SEED) == meta["full_model_sha256"]
-    ref = R.Ref(path)
-    L.ref_set_vad(VAD_MODEL.encode())
     for cname in ("jfk", "composite"):
+        ref = R.Ref(path)
+        L.ref_set_vad(VAD_MODEL.encode())
         ret, segs = ref.full(clips[cname], temperature_inc=0.0, n_processors=2)
-        meta["full"][f"{cname}/parallel2"] = {"ret": ret, "segments": [
+        ref.close()
+        # a second, recorded run (record_topk truncates the logits after recording them, which moves
+        # timestamp probabilities, so the fixture's segments come from the plain run above): every
+        # decoder call's prefix and top logits -- the two chunks' calls interleave in the shared
+        # recorder, a prefix names its call -- so a parting can be shown to be a near-tie
+        ref = R.Ref(path)
+        ref.full(clips[cname], temperature_inc=0.0, n_processors=2, record_topk=4)
+        off, prefix, ids, vals = ref.recorded()
+        ref.close()
+        calls = [{"prefix": prefix[off[i]:off[i + 1]].tolist(), "top": ids[i][:4].tolist(),
+                  "val": [float(v) for v in vals[i][:4]]} for i in range(len(off) - 1)]
+        meta["full"][f"{cname}/parallel2"] = {"ret": ret, "calls": calls, "segments": [
             {"t0": s["t0"], "t1": s["t1"], "tokens": [t[0] for t in s["tokens"]]} for s in segs]}
         print(cname, ret, len(segs), "segments", [(s["t0"], s["t1"]) for s in segs][:8])
     L.ref_set_vad(None)
-    ref.close()
     json.dump(meta, open(path_json, "w"), indent=1)
 
 

