@@ -25,7 +25,7 @@ ALL_OBJS := $(patsubst $(SRC)/%.hip,$(OBJDIR)/%.hip.o,$(HIP_SRCS)) \
 # libsortformer.so: the SortFormer C ABI (include/sortformer.h) + the shared GEMM/LayerNorm kernels
 SF_ONLY  := $(OBJDIR)/sortformer.cpp.o $(OBJDIR)/k_sortformer.hip.o
 OBJS     := $(filter-out $(SF_ONLY),$(ALL_OBJS))
-SF_OBJS  := $(SF_ONLY) $(OBJDIR)/k_gemm.hip.o $(OBJDIR)/k_misc.hip.o
+SF_OBJS  := $(SF_ONLY) $(OBJDIR)/k_gemm.hip.o $(OBJDIR)/k_misc.hip.o $(OBJDIR)/kquant.cpp.o
 HDRS     := $(wildcard $(SRC)/*.h) $(wildcard include/*.h)
 
 all: $(LIB) $(SFLIB)

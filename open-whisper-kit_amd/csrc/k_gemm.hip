@@ -93,8 +93,11 @@ __device__ __forceinline__ void epi_store(const EpiParams & p, int r, int c, flo
         if (p.out16) p.out16[o] = (_Float16) v;
     } else if constexpr (MODE == EPI_SILU_F16) {
         // ggml_silu_f32 (ggml-cpu/vec.h): x / (1 + exp(-x))
+        // out32 (optional): the f32 value too, the operand a quantized consumer matmul rounds to Q8
         const float v = acc + p.bias[c];
-        p.out16[(size_t) r * p.ldo + c] = (_Float16) (v / (1.0f + expf(-v)));
+        const float y = v / (1.0f + expf(-v));
+        if (p.out16) p.out16[(size_t) r * p.ldo + c] = (_Float16) y;
+        if (p.out32) p.out32[(size_t) r * p.ldo + c] = y;
     } else if constexpr (MODE == EPI_HALF_RESID) {
         // ggml_add(x, b) -> ggml_scale(0.5) -> ggml_add(residual, .) (sortformer.cpp:1163-1167)
         const float v = (acc + p.bias[c]) * 0.5f;
@@ -102,7 +105,9 @@ __device__ __forceinline__ void epi_store(const EpiParams & p, int r, int c, flo
         p.out32[o] = p.resid[o] + v;
     } else if constexpr (MODE == EPI_RELU_F16) {
         const float v = acc + p.bias[c];
-        p.out16[(size_t) r * p.ldo + c] = (_Float16) (v > 0.0f ? v : 0.0f);
+        const float y = v > 0.0f ? v : 0.0f;
+        if (p.out16) p.out16[(size_t) r * p.ldo + c] = (_Float16) y;
+        if (p.out32) p.out32[(size_t) r * p.ldo + c] = y;
     } else if constexpr (MODE == EPI_SIGMOID_F32) {
         const float v = acc + p.bias[c];
         p.out32[(size_t) r * p.ldo + c] = 1.0f / (1.0f + expf(-v));
@@ -216,7 +221,8 @@ __device__ __forceinline__ void epi_row8(const EpiParams & p, int r, int c, cons
             const float x = acc[e] + bb[e];
             v[e] = MODE == EPI_SILU_F16 ? x / (1.0f + expf(-x)) : (x > 0.0f ? x : 0.0f);
         }
-        *(half8 *) (p.out16 + o) = to_half8(v);
+        if (p.out16) *(half8 *) (p.out16 + o) = to_half8(v);
+        if (p.out32) store8(p.out32 + o, v);
     } else if constexpr (MODE == EPI_SIGMOID_F32) {
         load8(p.bias + c, bb);
 #pragma unroll

@@ -240,7 +240,7 @@ template <int DH, bool REL>
 __global__ __launch_bounds__(256) void k_sf_attn(const float * __restrict__ qkv, int ldq, int kcol, int vcol, int T,
                                                  int H, const float * __restrict__ ub, const float * __restrict__ vb,
                                                  const float * __restrict__ P, float sc, _Float16 * __restrict__ out,
-                                                 int Tpad) {
+                                                 float * __restrict__ out32, int Tpad) {
     extern __shared__ float smem[];
     constexpr int LDK = DH + 4;
     float * S = smem;                       // [AQ][Tpad]
@@ -354,31 +354,34 @@ __global__ __launch_bounds__(256) void k_sf_attn(const float * __restrict__ qkv,
         const int o = tid + 256 * m;
         if (o < AQ * DH) {
             const int oq = o / DH, d = o - oq * DH;
-            if (q0 + oq < T) out[(size_t) (q0 + oq) * ldp + h * DH + d] = (_Float16) acc[m];
+            if (q0 + oq < T) {
+                if (out32) out32[(size_t) (q0 + oq) * ldp + h * DH + d] = acc[m];
+                else out[(size_t) (q0 + oq) * ldp + h * DH + d] = (_Float16) acc[m];
+            }
         }
     }
 }
 
 template <int DH, bool REL>
 static void launch_attn(hipStream_t s, const float * qkv, int ldq, int kcol, int vcol, int T, int H, const float * u,
-                        const float * v, const float * P, float sc, _Float16 * out) {
+                        const float * v, const float * P, float sc, _Float16 * out, float * out32) {
     const int Tpad = (T + AKT - 1) / AKT * AKT;
     const size_t lds = ((size_t) AQ * Tpad + (size_t) AKT * (DH + 4) + (REL ? (size_t) (AQ - 1 + AKT) * (DH + 4) : 0)) *
                        sizeof(float);
     if (lds > 160 * 1024) throw std::runtime_error("sf::attention: T too large for the LDS score tile");
     OWK_LAUNCH((k_sf_attn<DH, REL>), dim3(H, (T + AQ - 1) / AQ), dim3(256), lds, s, qkv, ldq, kcol, vcol, T, H,
-                       u, v, P, sc, out, Tpad);
+                       u, v, P, sc, out, out32, Tpad);
 }
 
 void attention(hipStream_t s, int dh, bool rel, const float * qkv, int ldq, int kcol, int vcol, int T, int H,
-               const float * u, const float * v, const float * P, float sc, _Float16 * out) {
+               const float * u, const float * v, const float * P, float sc, _Float16 * out, float * out32) {
     if (T <= 0) return;
     if (dh == 64 && rel)
-        launch_attn<64, true>(s, qkv, ldq, kcol, vcol, T, H, u, v, P, sc, out);
+        launch_attn<64, true>(s, qkv, ldq, kcol, vcol, T, H, u, v, P, sc, out, out32);
     else if (dh == 24 && !rel)
-        launch_attn<24, false>(s, qkv, ldq, kcol, vcol, T, H, u, v, P, sc, out);
+        launch_attn<24, false>(s, qkv, ldq, kcol, vcol, T, H, u, v, P, sc, out, out32);
     else if (dh == 64 && !rel)
-        launch_attn<64, false>(s, qkv, ldq, kcol, vcol, T, H, u, v, P, sc, out);
+        launch_attn<64, false>(s, qkv, ldq, kcol, vcol, T, H, u, v, P, sc, out, out32);
     else
         throw std::runtime_error("sf::attention: unsupported head size");
 }

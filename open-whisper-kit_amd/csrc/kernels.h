@@ -24,9 +24,9 @@ enum EpiMode : int {
                         // resid_layernorm (bias + residual + next LayerNorm in one pass)
     // SortFormer (streaming-sortformer/src/sortformer.cpp) epilogues
     EPI_BIAS_F32 = 9,   // out32 = acc (+ bias[c]); out16 (optional) = f16 of the same value
-    EPI_SILU_F16 = 10,  // out16 = f16(silu(acc + bias))              (conformer FFN linear1)
+    EPI_SILU_F16 = 10,  // out16 = f16(silu(acc + bias)); out32 (optional) the f32 value (conformer FFN linear1)
     EPI_HALF_RESID = 11,// out32 = resid + (acc + bias) * 0.5         (macaron FFN half step)
-    EPI_RELU_F16 = 12,  // out16 = f16(relu(acc + bias))              (transformer FFN, head)
+    EPI_RELU_F16 = 12,  // out16 = f16(relu(acc + bias)); out32 (optional) (transformer FFN, head)
     EPI_SIGMOID_F32 = 13,// out32 = sigmoid(acc + bias)               (speaker head)
 };
 

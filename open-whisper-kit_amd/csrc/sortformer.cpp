@@ -10,6 +10,7 @@
 #include "sortformer.h"
 #include "owk_sortformer.h"
 
+#include "kquant.h"
 #include "sf_kernels.h"
 
 #include <algorithm>
@@ -43,10 +44,28 @@ bool sf_verbose() {
 // ---------------------------------------------------------------------------------
 struct GgufTensor {
     std::vector<int64_t> ne;
-    int type = 0;  // 0 F32, 1 F16
+    int type = 0;  // ggml type: 0 F32, 1 F16, or a quantized block type (qfmt >= 0)
+    int qfmt = -1; // QFmt of a quantized tensor (sortformer-quantize writes Q8_0 / Q4_K / Q5_K)
     const uint8_t * data = nullptr;
     size_t nbytes = 0;
 };
+
+// ggml type id -> QFmt (kernels.h) of the block formats the quantized GEMMs take; -1 otherwise
+int gguf_qfmt(int t) {
+    switch (t) {
+        case 2: return QF_Q4_0;
+        case 3: return QF_Q4_1;
+        case 6: return QF_Q5_0;
+        case 7: return QF_Q5_1;
+        case 8: return QF_Q8_0;
+        case 10: return QF_Q2_K;
+        case 11: return QF_Q3_K;
+        case 12: return QF_Q4_K;
+        case 13: return QF_Q5_K;
+        case 14: return QF_Q6_K;
+        default: return -1;
+    }
+}
 
 struct Gguf {
     std::vector<uint8_t> file;
@@ -116,14 +135,22 @@ struct Gguf {
             }
             const size_t data0 = (off + alignment - 1) / alignment * alignment;
             for (auto & ti : infos) {
-                if (ti.type != 0 && ti.type != 1)
-                    throw std::runtime_error("tensor " + ti.name + ": only F32/F16 GGUF tensors are supported");
                 size_t n = 1;
                 for (auto e : ti.ne) n *= (size_t) e;
                 GgufTensor t;
                 t.ne = ti.ne;
                 t.type = ti.type;
-                t.nbytes = n * (ti.type == 0 ? 4 : 2);
+                if (ti.type == 0 || ti.type == 1) {
+                    t.nbytes = n * (ti.type == 0 ? 4 : 2);
+                } else {
+                    // quantized rows (ggml_quantize_chunk blocks along ne[0])
+                    t.qfmt = gguf_qfmt(ti.type);
+                    if (t.qfmt < 0 || ti.ne.empty())
+                        throw std::runtime_error("tensor " + ti.name + ": unsupported GGUF tensor type " + std::to_string(ti.type));
+                    const int qk = qf_is_k(t.qfmt) ? 256 : 32;
+                    if (ti.ne[0] % qk) throw std::runtime_error("tensor " + ti.name + ": row not a whole number of blocks");
+                    t.nbytes = n / qk * (qf_is_k(t.qfmt) ? kq_block_bytes(t.qfmt) : qf_block_bytes(t.qfmt));
+                }
                 if (data0 + ti.off + t.nbytes > file.size()) throw std::runtime_error("tensor data out of file");
                 t.data = file.data() + data0 + ti.off;
                 tensors[ti.name] = t;
@@ -148,20 +175,34 @@ struct Blob {
     size_t add(const void * p, size_t n) {
         const size_t off = (host.size() + 255) / 256 * 256;
         host.resize(off + n);
-        memcpy(host.data() + off, p, n);
+        if (p) memcpy(host.data() + off, p, n);
         return off;
     }
+    template <typename V> size_t addv(const V & v) { return add(v.data(), v.size() * sizeof(v[0])); }
 };
 
+// one linear's weights: F16 [N][K] in the weight blob, or a quantized GGUF tensor (the reference's
+// sortformer-quantize output, streaming-sortformer/tools/quantize.cpp:52-90) kept as the block arrays
+// of kernels.h's Q5W -- 32-block formats split (qs / qh / d / m) plus the exact-f16 integer image the
+// large-tile kernel reads, K-quants as the virtual-block image of kquant.h -- in the quantized blob
+struct Lin {
+    size_t off = (size_t) -1;  // F16 weights (blob offset); -1: quantized
+    int fmt = -1, N = 0, K = 0, kx = 0, npad = 0;
+    size_t qs = 0, qh = 0, d = 0, m = 0, wi = 0, dwt = 0;  // quantized blob offsets
+    Q5W q;                                                 // resolved after the upload
+    bool quant() const { return fmt >= 0; }
+};
 struct ConfLayer {
-    size_t ln_ff1_w, ln_ff1_b, ff1_up, ff1_up_b, ff1_dn, ff1_dn_b;
-    size_t ln_sa_w, ln_sa_b, qkv, qkv_b, out, out_b, pos, pbu, pbv;
-    size_t ln_cv_w, ln_cv_b, pw1, pw1_b, dw, dw_b, pw2, pw2_b;
-    size_t ln_ff2_w, ln_ff2_b, ff2_up, ff2_up_b, ff2_dn, ff2_dn_b;
+    size_t ln_ff1_w, ln_ff1_b, ff1_up_b, ff1_dn_b;
+    size_t ln_sa_w, ln_sa_b, qkv_b, out_b, pbu, pbv;
+    size_t ln_cv_w, ln_cv_b, pw1_b, dw, dw_b, pw2_b;
+    size_t ln_ff2_w, ln_ff2_b, ff2_up_b, ff2_dn_b;
     size_t ln_out_w, ln_out_b;
+    Lin ff1_up, ff1_dn, qkv, out, pos, pw1, pw2, ff2_up, ff2_dn;
 };
 struct TransLayer {
-    size_t qkv, qkv_b, out, out_b, ln1_w, ln1_b, up, up_b, dn, dn_b, ln2_w, ln2_b;
+    size_t qkv_b, out_b, ln1_w, ln1_b, up_b, dn_b, ln2_w, ln2_b;
+    Lin qkv, out, up, dn;
 };
 
 // streaming configuration / state (ref:1652-1727)
@@ -197,11 +238,16 @@ struct sortformer_context {
 
     DevBuf w;  // weight blob
     size_t fb, win512, tw;
-    size_t c0_w, c0_b, c2_w, c2_b, c3_w, c3_b, c5_w, c5_b, c6_w, c6_b, pre_out, pre_out_b;
+    size_t c0_w, c0_b, c2_w, c2_b, c3_w, c3_b, c5_w, c5_b, c6_w, c6_b, pre_out_b;
+    Lin pre_out;
     std::vector<ConfLayer> conf;
-    size_t proj, proj_b;
+    Lin proj;
+    size_t proj_b;
     std::vector<TransLayer> trans;
-    size_t hid, hid_b, spk, spk_b;
+    Lin hid, spk;
+    size_t hid_b, spk_b;
+    DevBuf qw;          // quantized linears (Lin::qs .. dwt)
+    bool quant = false; // any linear quantized: producers also keep their f32 outputs
 
     // position-embedding cache (ref:140-142, 1127-1136): f16 table of the current n_pos
     int pos_n = 0;
@@ -210,6 +256,9 @@ struct sortformer_context {
     // scratch (grown on demand)
     DevBuf s_pcm, s_mel, s_c1, s_c2, s_c3, s_c4, s_flat, s_pre;
     DevBuf s_x, s_y, s_xn, s_h, s_qkv, s_P, s_ao, s_cv, s_g, s_t32, s_t16, s_pred;
+    // quantized models: f32 activations (LayerNorm rows, SiLU / ReLU outputs, attention outputs,
+    // the position table) and the Q8 operand buffers of the quantized GEMMs
+    DevBuf s_xn32, s_h32, s_ao32, pos32, s_q8, s_q8d, s_q16, s_q16d;
 
     template <typename T> T * wp(size_t off) const { return (T *) ((uint8_t *) w.ptr + off); }
     float * f(size_t off) const { return wp<float>(off); }
@@ -244,6 +293,7 @@ void load_weights(sortformer_context * ctx, const Gguf & g) {
         return *t;
     };
     auto as_f32 = [&](const GgufTensor & t) {
+        if (t.qfmt >= 0) throw std::runtime_error("quantized GGUF tensor where F32/F16 is expected");
         size_t n = t.nbytes / (t.type == 0 ? 4 : 2);
         std::vector<float> v(n);
         if (t.type == 0) memcpy(v.data(), t.data, t.nbytes);
@@ -251,19 +301,74 @@ void load_weights(sortformer_context * ctx, const Gguf & g) {
         return v;
     };
     auto as_f16 = [&](const GgufTensor & t) {
+        if (t.qfmt >= 0) throw std::runtime_error("quantized GGUF tensor where F32/F16 is expected");
         size_t n = t.nbytes / (t.type == 0 ? 4 : 2);
         std::vector<uint16_t> v(n);
         if (t.type == 1) memcpy(v.data(), t.data, t.nbytes);
         else for (size_t i = 0; i < n; ++i) v[i] = f32_to_f16_host(((const float *) t.data)[i]);
         return v;
     };
-    auto F = [&](const std::string & name) { auto v = as_f32(T(name)); return blob.add(v.data(), v.size() * 4); };
-    auto Hh = [&](const std::string & name) { auto v = as_f16(T(name)); return blob.add(v.data(), v.size() * 2); };
-    auto Hcat = [&](std::initializer_list<std::string> names) {
-        std::vector<uint16_t> all;
-        for (auto & n : names) { auto v = as_f16(T(n)); all.insert(all.end(), v.begin(), v.end()); }
-        return blob.add(all.data(), all.size() * 2);
+    Blob qb;
+    // a linear's weights (several GGUF tensors packed along the output rows, like q/k/v): F16 in the
+    // blob, or the quantized tensors' blocks (every part of one type) as Lin's arrays in qb. K is the
+    // product of all dims but the last (the 1x1 conv weights [1][K][N] reshape to 2-D, ref:1240-1241)
+    auto Lcat = [&](std::initializer_list<std::string> names) {
+        Lin L;
+        std::vector<const GgufTensor *> ts;
+        for (auto & n : names) ts.push_back(&T(n));
+        auto kdim = [](const GgufTensor & t) {
+            int64_t k = 1;
+            for (size_t i = 0; i + 1 < t.ne.size(); ++i) k *= t.ne[i];
+            return k;
+        };
+        const int64_t K = kdim(*ts[0]);
+        int64_t N = 0;
+        for (auto * t : ts) {
+            if (t->ne.size() < 2 || kdim(*t) != K) throw std::runtime_error("linear weight shape mismatch");
+            if (t->qfmt != ts[0]->qfmt) throw std::runtime_error("packed linear weights of mixed types");
+            N += t->ne.back();
+        }
+        L.N = (int) N;
+        L.K = (int) K;
+        if (ts[0]->qfmt < 0) {
+            std::vector<uint16_t> all;
+            for (auto * t : ts) { auto v = as_f16(*t); all.insert(all.end(), v.begin(), v.end()); }
+            L.off = blob.addv(all);
+            return L;
+        }
+        const int q = L.fmt = ts[0]->qfmt;
+        std::vector<uint8_t> raw;
+        for (auto * t : ts) raw.insert(raw.end(), t->data, t->data + t->nbytes);
+        L.npad = (L.N + 255) / 256 * 256;
+        if (qf_is_k(q)) {
+            // the virtual-block f16 integers + scales every GEMM shape runs on (gemm_q16, kquant.h)
+            L.kx = kq_kx(q, L.K);
+            std::vector<uint16_t> wi((size_t) L.N * L.kx);
+            std::vector<float> dwt((size_t) (L.kx / 32) * L.npad);
+            kq_expand_host(q, raw.data(), L.N, L.K, wi.data(), dwt.data(), L.npad);
+            L.wi = qb.addv(wi);
+            L.dwt = qb.addv(dwt);
+        } else {
+            const size_t nbk = (size_t) L.N * (L.K / 32);
+            std::vector<uint8_t> qs(nbk * qf_qs_bytes(q));
+            std::vector<uint32_t> qh(qf_has_qh(q) ? nbk : 0);
+            std::vector<uint16_t> dd(nbk), mm(qf_has_m(q) ? nbk : 0);
+            quant_split_host(q, raw.data(), L.N, L.K, qs.data(), qh.empty() ? nullptr : qh.data(), dd.data(),
+                             mm.empty() ? nullptr : mm.data());
+            L.qs = qb.addv(qs);
+            L.d = qb.addv(dd);
+            if (!qh.empty()) L.qh = qb.addv(qh);
+            if (!mm.empty()) L.m = qb.addv(mm);
+            if (!qf_has_m(q)) {  // symmetric formats: exact-f16 integer image for the large-tile kernel
+                L.wi = qb.add(nullptr, (size_t) L.N * L.K * 2);
+                L.dwt = qb.add(nullptr, (size_t) (L.K / 32) * L.npad * 4);
+            }
+        }
+        ctx->quant = true;
+        return L;
     };
+    auto Lw = [&](const std::string & name) { return Lcat({name}); };
+    auto F = [&](const std::string & name) { auto v = as_f32(T(name)); return blob.add(v.data(), v.size() * 4); };
     auto Fcat = [&](std::initializer_list<std::string> names) {
         std::vector<float> all;
         for (auto & n : names) { auto v = as_f32(T(n)); all.insert(all.end(), v.begin(), v.end()); }
@@ -311,53 +416,84 @@ void load_weights(sortformer_context * ctx, const Gguf & g) {
         if (ow.ne.size() != 2 || ow.ne[1] != ctx->d_model || ow.ne[0] != (int64_t) ctx->c_sub * (ctx->n_mels / 8))
             throw std::runtime_error("unexpected pre_encode.out shape");
     }
-    ctx->pre_out = Hh(pe + "out.weight"); ctx->pre_out_b = F(pe + "out.bias");
+    ctx->pre_out = Lw(pe + "out.weight"); ctx->pre_out_b = F(pe + "out.bias");
 
     ctx->conf.resize(ctx->n_conf);
     for (int i = 0; i < ctx->n_conf; ++i) {
         const std::string p = "encoder.layers." + std::to_string(i) + ".";
         ConfLayer & L = ctx->conf[i];
         L.ln_ff1_w = F(p + "norm_feed_forward1.weight"); L.ln_ff1_b = F(p + "norm_feed_forward1.bias");
-        L.ff1_up = Hh(p + "feed_forward1.linear1.weight"); L.ff1_up_b = F(p + "feed_forward1.linear1.bias");
-        L.ff1_dn = Hh(p + "feed_forward1.linear2.weight"); L.ff1_dn_b = F(p + "feed_forward1.linear2.bias");
+        L.ff1_up = Lw(p + "feed_forward1.linear1.weight"); L.ff1_up_b = F(p + "feed_forward1.linear1.bias");
+        L.ff1_dn = Lw(p + "feed_forward1.linear2.weight"); L.ff1_dn_b = F(p + "feed_forward1.linear2.bias");
         L.ln_sa_w = F(p + "norm_self_att.weight"); L.ln_sa_b = F(p + "norm_self_att.bias");
-        L.qkv = Hcat({p + "self_attn.linear_q.weight", p + "self_attn.linear_k.weight", p + "self_attn.linear_v.weight"});
+        L.qkv = Lcat({p + "self_attn.linear_q.weight", p + "self_attn.linear_k.weight", p + "self_attn.linear_v.weight"});
         L.qkv_b = Fcat({p + "self_attn.linear_q.bias", p + "self_attn.linear_k.bias", p + "self_attn.linear_v.bias"});
-        L.out = Hh(p + "self_attn.linear_out.weight"); L.out_b = F(p + "self_attn.linear_out.bias");
-        L.pos = Hh(p + "self_attn.linear_pos.weight");
+        L.out = Lw(p + "self_attn.linear_out.weight"); L.out_b = F(p + "self_attn.linear_out.bias");
+        L.pos = Lw(p + "self_attn.linear_pos.weight");
         L.pbu = F(p + "self_attn.pos_bias_u"); L.pbv = F(p + "self_attn.pos_bias_v");
         L.ln_cv_w = F(p + "norm_conv.weight"); L.ln_cv_b = F(p + "norm_conv.bias");
-        L.pw1 = Hh(p + "conv.pointwise_conv1.weight"); L.pw1_b = F(p + "conv.pointwise_conv1.bias");
+        L.pw1 = Lw(p + "conv.pointwise_conv1.weight"); L.pw1_b = F(p + "conv.pointwise_conv1.bias");
         L.dw = F(p + "conv.depthwise_conv.weight"); L.dw_b = F(p + "conv.depthwise_conv.bias");
-        L.pw2 = Hh(p + "conv.pointwise_conv2.weight"); L.pw2_b = F(p + "conv.pointwise_conv2.bias");
+        L.pw2 = Lw(p + "conv.pointwise_conv2.weight"); L.pw2_b = F(p + "conv.pointwise_conv2.bias");
         L.ln_ff2_w = F(p + "norm_feed_forward2.weight"); L.ln_ff2_b = F(p + "norm_feed_forward2.bias");
-        L.ff2_up = Hh(p + "feed_forward2.linear1.weight"); L.ff2_up_b = F(p + "feed_forward2.linear1.bias");
-        L.ff2_dn = Hh(p + "feed_forward2.linear2.weight"); L.ff2_dn_b = F(p + "feed_forward2.linear2.bias");
+        L.ff2_up = Lw(p + "feed_forward2.linear1.weight"); L.ff2_up_b = F(p + "feed_forward2.linear1.bias");
+        L.ff2_dn = Lw(p + "feed_forward2.linear2.weight"); L.ff2_dn_b = F(p + "feed_forward2.linear2.bias");
         L.ln_out_w = F(p + "norm_out.weight"); L.ln_out_b = F(p + "norm_out.bias");
     }
-    ctx->proj = Hh("sortformer_modules.encoder_proj.weight");
+    ctx->proj = Lw("sortformer_modules.encoder_proj.weight");
     ctx->proj_b = F("sortformer_modules.encoder_proj.bias");
     ctx->trans.resize(ctx->n_trans);
     for (int i = 0; i < ctx->n_trans; ++i) {
         const std::string p = "transformer_encoder.layers." + std::to_string(i) + ".";
         TransLayer & L = ctx->trans[i];
-        L.qkv = Hcat({p + "first_sub_layer.query_net.weight", p + "first_sub_layer.key_net.weight",
+        L.qkv = Lcat({p + "first_sub_layer.query_net.weight", p + "first_sub_layer.key_net.weight",
                       p + "first_sub_layer.value_net.weight"});
         L.qkv_b = Fcat({p + "first_sub_layer.query_net.bias", p + "first_sub_layer.key_net.bias",
                         p + "first_sub_layer.value_net.bias"});
-        L.out = Hh(p + "first_sub_layer.out_projection.weight"); L.out_b = F(p + "first_sub_layer.out_projection.bias");
+        L.out = Lw(p + "first_sub_layer.out_projection.weight"); L.out_b = F(p + "first_sub_layer.out_projection.bias");
         L.ln1_w = F(p + "layer_norm_1.weight"); L.ln1_b = F(p + "layer_norm_1.bias");
-        L.up = Hh(p + "second_sub_layer.dense_in.weight"); L.up_b = F(p + "second_sub_layer.dense_in.bias");
-        L.dn = Hh(p + "second_sub_layer.dense_out.weight"); L.dn_b = F(p + "second_sub_layer.dense_out.bias");
+        L.up = Lw(p + "second_sub_layer.dense_in.weight"); L.up_b = F(p + "second_sub_layer.dense_in.bias");
+        L.dn = Lw(p + "second_sub_layer.dense_out.weight"); L.dn_b = F(p + "second_sub_layer.dense_out.bias");
         L.ln2_w = F(p + "layer_norm_2.weight"); L.ln2_b = F(p + "layer_norm_2.bias");
     }
-    ctx->hid = Hh("sortformer_modules.first_hidden_to_hidden.weight");
+    ctx->hid = Lw("sortformer_modules.first_hidden_to_hidden.weight");
     ctx->hid_b = F("sortformer_modules.first_hidden_to_hidden.bias");
-    ctx->spk = Hh("sortformer_modules.single_hidden_to_spks.weight");
+    ctx->spk = Lw("sortformer_modules.single_hidden_to_spks.weight");
     ctx->spk_b = F("sortformer_modules.single_hidden_to_spks.bias");
 
     ctx->w.alloc(blob.host.size());
     OWK_HIP_CHECK(hipMemcpy(ctx->w.ptr, blob.host.data(), blob.host.size(), hipMemcpyHostToDevice));
+    if (ctx->quant) {
+        ctx->qw.alloc(qb.host.size());
+        OWK_HIP_CHECK(hipMemcpy(ctx->qw.ptr, qb.host.data(), qb.host.size(), hipMemcpyHostToDevice));
+        uint8_t * base = (uint8_t *) ctx->qw.ptr;
+        auto resolve = [&](Lin & L) {
+            if (!L.quant()) return;
+            Q5W & q = L.q;
+            q.fmt = L.fmt;
+            q.npad = L.npad;
+            q.kx = L.kx;
+            q.wi = L.wi || qf_is_k(L.fmt) ? (const _Float16 *) (base + L.wi) : nullptr;
+            q.dwt = q.wi ? (const float *) (base + L.dwt) : nullptr;
+            if (!qf_is_k(L.fmt)) {
+                q.qs = base + L.qs;
+                q.d = (const _Float16 *) (base + L.d);
+                if (qf_has_qh(L.fmt)) q.qh = (const uint32_t *) (base + L.qh);
+                if (qf_has_m(L.fmt)) q.m = (const _Float16 *) (base + L.m);
+                if (q.wi) quant_expand_f16(ctx->stream, q, L.N, L.K, (_Float16 *) q.wi, (float *) q.dwt, q.npad);
+            }
+        };
+        resolve(ctx->pre_out);
+        resolve(ctx->proj);
+        resolve(ctx->hid);
+        resolve(ctx->spk);
+        for (auto & L : ctx->conf)
+            for (Lin * l : {&L.ff1_up, &L.ff1_dn, &L.qkv, &L.out, &L.pos, &L.pw1, &L.pw2, &L.ff2_up, &L.ff2_dn}) resolve(*l);
+        for (auto & L : ctx->trans)
+            for (Lin * l : {&L.qkv, &L.out, &L.up, &L.dn}) resolve(*l);
+        OWK_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+        SF_LOG("sortformer_init: %.1f MB of quantized linears\n", qb.host.size() / 1e6);
+    }
     SF_LOG("sortformer_init: %.1f MB of weights resident on device %d\n", blob.host.size() / 1e6, ctx->device);
 }
 
@@ -369,6 +505,46 @@ void dev_guard(sortformer_context * ctx) { OWK_HIP_CHECK(hipSetDevice(ctx->devic
 template <typename Tp> Tp * grow(DevBuf & b, size_t n) {
     b.alloc(n * sizeof(Tp));
     return b.as<Tp>();
+}
+
+// y = W x with the fused epilogue `mode` (the reference's ggml_mul_mat + bias / activation / residual).
+// F16 weights take the f16 activation A16 (ggml converts src1 to F16, the vec_dot_type of F16).
+// Quantized weights round the f32 activation A32 to the weight's vec_dot_type -- Q8_0 / Q8_1 per 32
+// (x86 quantize_row_q8_0 / _q8_1) or Q8_K per 256 (quantize_row_q8_K) -- as ggml_compute_forward_mul_mat
+// does for its f32 src1 (ggml-cpu.c), then the block dots: large tiles on the f16 MFMA ring kernel over
+// the exact integers (gemm_q16), other shapes on the int8 MFMA kernels (gemm_q5). A32 null: the f16
+// activation is quantized instead (only where the reference's operand is itself f16-exact).
+void sf_lin(sortformer_context * ctx, int mode, int M, int N, int K, const _Float16 * A16, const float * A32, int lda,
+            const Lin & w, const EpiParams & ep) {
+    hipStream_t s = ctx->stream;
+    if (M <= 0) return;
+    if (w.N != N || w.K != K) throw std::runtime_error("sortformer: linear shape mismatch");
+    if (!w.quant()) {
+        gemm(s, mode, M, N, K, A16, lda, ctx->h(w.off), K, ep);
+        return;
+    }
+    const Q5W & q = w.q;
+    const int mpad = (M + 255) / 256 * 256;
+    if (qf_is_k(q.fmt)) {
+        _Float16 * q16 = grow<_Float16>(ctx->s_q16, (size_t) M * q.kx);
+        float * q16d = grow<float>(ctx->s_q16d, (size_t) (q.kx / 32) * mpad);
+        quantize_q8k_f16(s, A32, A32 ? nullptr : A16, lda, M, K, q.fmt, q16, q16d, mpad);
+        gemm_q16(s, mode, M, N, q.kx, q16, q16d, mpad, q, ep);
+    } else if (gemm_q16_applies(q, M, N, K)) {
+        _Float16 * q16 = grow<_Float16>(ctx->s_q16, (size_t) M * K);
+        float * q16d = grow<float>(ctx->s_q16d, (size_t) (K / 32) * mpad);
+        quantize_q8_f16(s, A32, A32 ? nullptr : A16, lda, M, K, q16, q16d, mpad);
+        gemm_q16(s, mode, M, N, K, q16, q16d, mpad, q, ep);
+    } else {
+        int8_t * qa = grow<int8_t>(ctx->s_q8, (size_t) M * K);
+        float * da = grow<float>(ctx->s_q8d, (size_t) M * (K / 32));
+        quantize_q8(s, A32, A32 ? nullptr : A16, lda, M, K, qa, da);
+        gemm_q5(s, mode, M, N, K, qa, da, q, ep);
+    }
+}
+// f32 copy of an activation for a quantized consumer (null when the consumer is F16)
+float * f32_for(sortformer_context * ctx, const Lin & consumer, DevBuf & buf, size_t n) {
+    return consumer.quant() ? grow<float>(buf, n) : nullptr;
 }
 
 struct MelDims {
@@ -423,7 +599,7 @@ int run_preenc(sortformer_context * ctx, const float * mel, int ld, int c0, int 
     ep.bias = ctx->f(ctx->pre_out_b);
     ep.out32 = out;
     ep.ldo = ctx->d_model;
-    gemm(s, EPI_BIAS_F32, T3, ctx->d_model, C * F3, flat, C * F3, ctx->h(ctx->pre_out), C * F3, ep);
+    sf_lin(ctx, EPI_BIAS_F32, T3, ctx->d_model, C * F3, flat, nullptr, C * F3, ctx->pre_out, ep);
     return T3;
 }
 
@@ -433,18 +609,24 @@ void ensure_pos(sortformer_context * ctx, int T) {
     const int n_pos = 2 * T - 1, d = ctx->d_model;
     if (ctx->pos_n == n_pos) return;
     std::vector<uint16_t> pe((size_t) n_pos * d);
+    std::vector<float> pe32((size_t) n_pos * d);  // quantized linear_pos: the f32 table is its operand
     const int half = d / 2;
     for (int p = 0; p < n_pos; ++p) {
         const float pos = (float) (T - 1 - p);
         for (int j = 0; j < half; ++j) {
             const float freq = 1.0f / powf(10000.0f, (2.0f * j) / (float) d);
             const float angle = pos * freq;
-            pe[(size_t) p * d + 2 * j] = f32_to_f16_host(sinf(angle));
-            pe[(size_t) p * d + 2 * j + 1] = f32_to_f16_host(cosf(angle));
+            pe32[(size_t) p * d + 2 * j] = sinf(angle);
+            pe32[(size_t) p * d + 2 * j + 1] = cosf(angle);
         }
     }
+    for (size_t i = 0; i < pe.size(); ++i) pe[i] = f32_to_f16_host(pe32[i]);
     _Float16 * dst = grow<_Float16>(ctx->pos16, pe.size());
     OWK_HIP_CHECK(hipMemcpyAsync(dst, pe.data(), pe.size() * 2, hipMemcpyHostToDevice, ctx->stream));
+    if (ctx->quant) {
+        float * d32 = grow<float>(ctx->pos32, pe32.size());
+        OWK_HIP_CHECK(hipMemcpyAsync(d32, pe32.data(), pe32.size() * 4, hipMemcpyHostToDevice, ctx->stream));
+    }
     OWK_HIP_CHECK(hipStreamSynchronize(ctx->stream));  // pe is a host temporary
     ctx->pos_n = n_pos;
 }
@@ -476,47 +658,55 @@ float * run_conformer(sortformer_context * ctx, float * x, const Segs & segs, in
     const float eps = 1e-5f;
     for (int il = 0; il <= last; ++il) {
         const ConfLayer & L = ctx->conf[il];
-        auto ffn = [&](size_t lnw, size_t lnb, size_t up, size_t upb, size_t dn, size_t dnb) {
-            layernorm_f16(s, x, T, d, ctx->f(lnw), ctx->f(lnb), eps, xn, d);
+        auto ffn = [&](size_t lnw, size_t lnb, const Lin & up, size_t upb, const Lin & dn, size_t dnb) {
+            float * xn32 = f32_for(ctx, up, ctx->s_xn32, (size_t) T * d);
+            layernorm_f16(s, x, T, d, ctx->f(lnw), ctx->f(lnb), eps, xn, d, nullptr, xn32);
+            float * h32 = f32_for(ctx, dn, ctx->s_h32, (size_t) T * 4 * d);
             EpiParams e1;
-            e1.bias = ctx->f(upb); e1.out16 = hbuf; e1.ldo = 4 * d;
-            gemm(s, EPI_SILU_F16, T, 4 * d, d, xn, d, ctx->h(up), d, e1);
+            e1.bias = ctx->f(upb); e1.out16 = hbuf; e1.out32 = h32; e1.ldo = 4 * d;
+            sf_lin(ctx, EPI_SILU_F16, T, 4 * d, d, xn, xn32, d, up, e1);
             EpiParams e2;
             e2.bias = ctx->f(dnb); e2.resid = x; e2.out32 = x; e2.ldo = d;
-            gemm(s, EPI_HALF_RESID, T, d, 4 * d, hbuf, 4 * d, ctx->h(dn), 4 * d, e2);
+            sf_lin(ctx, EPI_HALF_RESID, T, d, 4 * d, hbuf, h32, 4 * d, dn, e2);
         };
         // FFN1 (ref:1159-1168)
         ffn(L.ln_ff1_w, L.ln_ff1_b, L.ff1_up, L.ff1_up_b, L.ff1_dn, L.ff1_dn_b);
         // relative-position MHSA (ref:1170-1235)
-        layernorm_f16(s, x, T, d, ctx->f(L.ln_sa_w), ctx->f(L.ln_sa_b), eps, xn, d);
         {
+            float * xn32 = f32_for(ctx, L.qkv, ctx->s_xn32, (size_t) T * d);
+            layernorm_f16(s, x, T, d, ctx->f(L.ln_sa_w), ctx->f(L.ln_sa_b), eps, xn, d, nullptr, xn32);
             EpiParams e;
             e.bias = ctx->f(L.qkv_b); e.out32 = qkv; e.ldo = 3 * d;
-            gemm(s, EPI_BIAS_F32, T, 3 * d, d, xn, d, ctx->h(L.qkv), d, e);
+            sf_lin(ctx, EPI_BIAS_F32, T, 3 * d, d, xn, xn32, d, L.qkv, e);
             EpiParams ep;
             ep.out32 = P; ep.ldo = d;
-            gemm(s, EPI_F32, 2 * Tmax - 1, d, d, ctx->pos16.as<_Float16>(), d, ctx->h(L.pos), d, ep);
+            sf_lin(ctx, EPI_F32, 2 * Tmax - 1, d, d, ctx->pos16.as<_Float16>(), L.pos.quant() ? ctx->pos32.as<float>() : nullptr,
+                   d, L.pos, ep);
             // positions Tb-1 .. -(Tb-1) of a shorter sequence are rows Tmax-Tb .. of the table
+            float * ao32 = f32_for(ctx, L.out, ctx->s_ao32, (size_t) T * d);
             for (const auto & sg : segs)
                 sf::attention(s, CONF_DH, true, qkv + (size_t) sg.first * 3 * d, 3 * d, d, 2 * d, sg.second, CONF_H,
                               ctx->f(L.pbu), ctx->f(L.pbv), P + (size_t) (Tmax - sg.second) * d,
-                              1.0f / sqrtf((float) CONF_DH), ao + (size_t) sg.first * d);
+                              1.0f / sqrtf((float) CONF_DH), ao + (size_t) sg.first * d,
+                              ao32 ? ao32 + (size_t) sg.first * d : nullptr);
             EpiParams eo;
             eo.bias = ctx->f(L.out_b); eo.resid = x; eo.out32 = x; eo.ldo = d;
-            gemm(s, EPI_RESID_F32, T, d, d, ao, d, ctx->h(L.out), d, eo);
+            sf_lin(ctx, EPI_RESID_F32, T, d, d, ao, ao32, d, L.out, eo);
         }
-        // conv module (ref:1237-1274)
-        layernorm_f16(s, x, T, d, ctx->f(L.ln_cv_w), ctx->f(L.ln_cv_b), eps, xn, d);
+        // conv module (ref:1237-1274); sortformer-quantize leaves the 1x1 convs F16 (their rows are
+        // ne[0] = 1 wide, quantize.cpp:167-169)
         {
+            float * xn32 = f32_for(ctx, L.pw1, ctx->s_xn32, (size_t) T * d);
+            layernorm_f16(s, x, T, d, ctx->f(L.ln_cv_w), ctx->f(L.ln_cv_b), eps, xn, d, nullptr, xn32);
             EpiParams e;
             e.bias = ctx->f(L.pw1_b); e.out32 = cv; e.ldo = 2 * d;
-            gemm(s, EPI_BIAS_F32, T, 2 * d, d, xn, d, ctx->h(L.pw1), d, e);
+            sf_lin(ctx, EPI_BIAS_F32, T, 2 * d, d, xn, xn32, d, L.pw1, e);
             for (const auto & sg : segs)
                 sf::glu_dwconv(s, cv + (size_t) sg.first * 2 * d, sg.second, d, ctx->f(L.dw), CONF_K, ctx->f(L.dw_b),
                                g + (size_t) sg.first * d);
             EpiParams eo;
             eo.bias = ctx->f(L.pw2_b); eo.resid = x; eo.out32 = x; eo.ldo = d;
-            gemm(s, EPI_RESID_F32, T, d, d, g, d, ctx->h(L.pw2), d, eo);
+            sf_lin(ctx, EPI_RESID_F32, T, d, d, g, nullptr, d, L.pw2, eo);
         }
         // FFN2 (ref:1276-1285)
         ffn(L.ln_ff2_w, L.ln_ff2_b, L.ff2_up, L.ff2_up_b, L.ff2_dn, L.ff2_dn_b);
@@ -539,7 +729,7 @@ void run_projection(sortformer_context * ctx, const _Float16 * x16, int T) {
     _Float16 * o16 = grow<_Float16>(ctx->s_t16, (size_t) T * TF_D);
     EpiParams e;
     e.bias = ctx->f(ctx->proj_b); e.out32 = o32; e.out16 = o16; e.ldo = TF_D;
-    gemm(ctx->stream, EPI_BIAS_F32, T, TF_D, ctx->d_model, x16, ctx->d_model, ctx->h(ctx->proj), ctx->d_model, e);
+    sf_lin(ctx, EPI_BIAS_F32, T, TF_D, ctx->d_model, x16, nullptr, ctx->d_model, ctx->proj, e);
 }
 
 // transformer layers 0..last over s_t32 / s_t16 (in place) (ref:1467-1520)
@@ -556,22 +746,26 @@ void run_transformer(sortformer_context * ctx, const Segs & segs, int last) {
     const float eps = 1e-5f;
     for (int il = 0; il <= last; ++il) {
         const TransLayer & L = ctx->trans[il];
+        // x32 holds the f32 of x16 (the projection output, then each layer's final LayerNorm)
         EpiParams e;
         e.bias = ctx->f(L.qkv_b); e.out32 = qkv; e.ldo = 3 * TF_D;
-        gemm(s, EPI_BIAS_F32, T, 3 * TF_D, TF_D, x16, TF_D, ctx->h(L.qkv), TF_D, e);
+        sf_lin(ctx, EPI_BIAS_F32, T, 3 * TF_D, TF_D, x16, x32, TF_D, L.qkv, e);
+        float * ao32 = f32_for(ctx, L.out, ctx->s_ao32, (size_t) T * TF_D);
         for (const auto & sg : segs)
             sf::attention(s, TF_DH, false, qkv + (size_t) sg.first * 3 * TF_D, 3 * TF_D, TF_D, 2 * TF_D, sg.second, TF_H,
-                          nullptr, nullptr, nullptr, 1.0f / sqrtf((float) TF_DH), ao + (size_t) sg.first * TF_D);
+                          nullptr, nullptr, nullptr, 1.0f / sqrtf((float) TF_DH), ao + (size_t) sg.first * TF_D,
+                          ao32 ? ao32 + (size_t) sg.first * TF_D : nullptr);
         EpiParams eo;
         eo.bias = ctx->f(L.out_b); eo.resid = x32; eo.out32 = y; eo.ldo = TF_D;
-        gemm(s, EPI_RESID_F32, T, TF_D, TF_D, ao, TF_D, ctx->h(L.out), TF_D, eo);
+        sf_lin(ctx, EPI_RESID_F32, T, TF_D, TF_D, ao, ao32, TF_D, L.out, eo);
         layernorm_f16(s, y, T, TF_D, ctx->f(L.ln1_w), ctx->f(L.ln1_b), eps, x16, TF_D, nullptr, x32);
+        float * h32 = f32_for(ctx, L.dn, ctx->s_h32, (size_t) T * TF_FF);
         EpiParams eu;
-        eu.bias = ctx->f(L.up_b); eu.out16 = hbuf; eu.ldo = TF_FF;
-        gemm(s, EPI_RELU_F16, T, TF_FF, TF_D, x16, TF_D, ctx->h(L.up), TF_D, eu);
+        eu.bias = ctx->f(L.up_b); eu.out16 = hbuf; eu.out32 = h32; eu.ldo = TF_FF;
+        sf_lin(ctx, EPI_RELU_F16, T, TF_FF, TF_D, x16, x32, TF_D, L.up, eu);
         EpiParams ed;
         ed.bias = ctx->f(L.dn_b); ed.resid = x32; ed.out32 = y; ed.ldo = TF_D;
-        gemm(s, EPI_RESID_F32, T, TF_D, TF_FF, hbuf, TF_FF, ctx->h(L.dn), TF_FF, ed);
+        sf_lin(ctx, EPI_RESID_F32, T, TF_D, TF_FF, hbuf, h32, TF_FF, L.dn, ed);
         layernorm_f16(s, y, T, TF_D, ctx->f(L.ln2_w), ctx->f(L.ln2_b), eps, x16, TF_D, nullptr, x32);
     }
 }
@@ -587,10 +781,10 @@ float * run_prediction(sortformer_context * ctx, int T) {
     sf::relu_f16(s, ctx->s_t32.as<float>(), (size_t) T * TF_D, r16);
     EpiParams e;
     e.bias = ctx->f(ctx->hid_b); e.out16 = h16; e.ldo = TF_D;
-    gemm(s, EPI_RELU_F16, T, TF_D, TF_D, r16, TF_D, ctx->h(ctx->hid), TF_D, e);
+    sf_lin(ctx, EPI_RELU_F16, T, TF_D, TF_D, r16, nullptr, TF_D, ctx->hid, e);
     EpiParams e2;
     e2.bias = ctx->f(ctx->spk_b); e2.out32 = pred; e2.ldo = N_SPK;
-    gemm(s, EPI_SIGMOID_F32, T, N_SPK, TF_D, h16, TF_D, ctx->h(ctx->spk), TF_D, e2);
+    sf_lin(ctx, EPI_SIGMOID_F32, T, N_SPK, TF_D, h16, nullptr, TF_D, ctx->spk, e2);
     return pred;
 }
 

@@ -1,0 +1,237 @@
+// Decode-row GEMM lab (M = 32 rows, f16 weights in the tiled [tile][kstep][1 KB] layout of
+// k_gemm_rows): times kernel variants as a hipGraph chain of NL launches over distinct weight
+// buffers (so every launch streams its weights from HBM), per shape.
+//   hipcc -O3 --offload-arch=gfx950 -std=c++17 tools/lab_gemv.hip -o /tmp/lab_gemv && /tmp/lab_gemv
+// Not part of the product: a measurement tool for the decode chain design.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+
+#define CK(x)                                                                              \
+    do {                                                                                   \
+        hipError_t e_ = (x);                                                               \
+        if (e_ != hipSuccess) {                                                            \
+            fprintf(stderr, "HIP %s at %d: %s\n", hipGetErrorString(e_), __LINE__, #x);     \
+            exit(1);                                                                       \
+        }                                                                                  \
+    } while (0)
+
+constexpr int M = 32;
+
+__global__ void k_fill(_Float16 * p, size_t n, uint32_t seed) {
+    for (size_t i = blockIdx.x * (size_t) blockDim.x + threadIdx.x; i < n; i += (size_t) gridDim.x * blockDim.x) {
+        uint32_t h = (uint32_t) i * 2654435761u ^ seed;
+        h ^= h >> 13; h *= 0x5bd1e995; h ^= h >> 15;
+        p[i] = (_Float16) (((int) (h & 1023) - 512) * (1.0f / 4096.0f));
+    }
+}
+
+// ---- variant 0: the product's k_gemm_rows (one 16-col tile per block, nw waves x J ksteps)
+template <int J, bool PART>
+__global__ __launch_bounds__(1024) void k_cur(int N, int K, const _Float16 * __restrict__ A,
+                                              const _Float16 * __restrict__ Wt, _Float16 * __restrict__ out,
+                                              float * __restrict__ part) {
+    __shared__ floatx4 red[16][2][64];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = blockDim.x >> 6;
+    const int tile = blockIdx.x, n0 = tile * 16;
+    const int nsteps = K >> 5;
+    const int ks0 = (blockIdx.y * nw + wave) * J;
+    const int nj = max(0, min(J, nsteps - ks0));
+    const half8 z8 = {0, 0, 0, 0, 0, 0, 0, 0};
+    const _Float16 * wp = Wt + ((size_t) tile * nsteps) * 512 + lane * 8;
+    half8 b[J], a[2][J];
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+        const half8 t = __builtin_nontemporal_load((const half8 *) (wp + (size_t) min(ks0 + j, nsteps - 1) * 512));
+        b[j] = j < nj ? t : z8;
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const _Float16 * ap = A + (size_t) (i * 16 + (lane & 15)) * K + 8 * (lane >> 4);
+#pragma unroll
+        for (int j = 0; j < J; ++j) {
+            const half8 t = *(const half8 *) (ap + min(ks0 + j, nsteps - 1) * 32);
+            a[i][j] = j < nj ? t : z8;
+        }
+    }
+    floatx4 acc[2] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
+#pragma unroll
+    for (int j = 0; j < J; ++j)
+#pragma unroll
+        for (int i = 0; i < 2; ++i) acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[i][j], b[j], acc[i], 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) red[wave][i][lane] = acc[i];
+    __syncthreads();
+    for (int o = tid; o < 2 * 256; o += blockDim.x) {
+        const int r = o >> 4, cc = o & 15;
+        const int i = r >> 4, rr = r & 15;
+        const int ln = 16 * (rr >> 2) + cc, e = rr & 3;
+        const float * rp = (const float *) &red[0][i][ln] + e;
+        float sum = rp[0];
+        for (int w = 1; w < nw; ++w) sum += rp[w * 2 * 64 * 4];
+        const int c = n0 + cc;
+        if (PART) part[((size_t) blockIdx.y * M + r) * N + c] = sum;
+        else out[(size_t) r * N + c] = (_Float16) sum;
+    }
+}
+
+// ---- variant 1: empty kernel of a given grid (launch / boundary floor)
+__global__ void k_empty(int * flag) {
+    if (flag && threadIdx.x == 0 && blockIdx.x == 0x7fffffff) flag[0] = 1;
+}
+
+// ---- variant 2: A slice staged once per block in LDS; 4 waves, wave w owns TPW column tiles of
+// the block's 4*TPW tiles over the block's KR k-steps; f32 partial [ks][M][N] (or f16 when KS == 1)
+template <int TPW, int KR>
+__global__ __launch_bounds__(256) void k_lds(int N, int K, const _Float16 * __restrict__ A,
+                                             const _Float16 * __restrict__ Wt, _Float16 * __restrict__ out,
+                                             float * __restrict__ part) {
+    // A slice: 32 rows x KR*32 halfs, stored as the MFMA fragments: [kstep][rowtile][lane] half8
+    __shared__ half8 as[KR][2][64];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int nsteps = K >> 5;
+    const int ks = blockIdx.y, k0 = ks * KR;
+    const int tile0 = blockIdx.x * 4 * TPW + wave * TPW;
+    const int ntiles = N >> 4;
+    half8 b[TPW][KR];
+#pragma unroll
+    for (int t = 0; t < TPW; ++t) {
+        const int tl = min(tile0 + t, ntiles - 1);
+        const _Float16 * wp = Wt + ((size_t) tl * nsteps + k0) * 512 + lane * 8;
+#pragma unroll
+        for (int j = 0; j < KR; ++j) b[t][j] = __builtin_nontemporal_load((const half8 *) (wp + (size_t) j * 512));
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    // cooperative A load: KR*2*64 half8 fragments over 256 threads
+    for (int f = tid; f < KR * 2 * 64; f += 256) {
+        const int j = f >> 7, i = (f >> 6) & 1, ln = f & 63;
+        as[j][i][ln] = *(const half8 *) (A + (size_t) (i * 16 + (ln & 15)) * K + (k0 + j) * 32 + 8 * (ln >> 4));
+    }
+    __syncthreads();
+    floatx4 acc[TPW][2];
+#pragma unroll
+    for (int t = 0; t < TPW; ++t) acc[t][0] = acc[t][1] = floatx4{0, 0, 0, 0};
+#pragma unroll
+    for (int j = 0; j < KR; ++j) {
+        const half8 a0 = as[j][0][lane], a1 = as[j][1][lane];
+#pragma unroll
+        for (int t = 0; t < TPW; ++t) {
+            acc[t][0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, b[t][j], acc[t][0], 0, 0, 0);
+            acc[t][1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1, b[t][j], acc[t][1], 0, 0, 0);
+        }
+    }
+#pragma unroll
+    for (int t = 0; t < TPW; ++t) {
+        const int c = (tile0 + t) * 16 + (lane & 15);
+        if (tile0 + t >= ntiles) continue;
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int r = i * 16 + 4 * (lane >> 4) + e;
+                if (gridDim.y > 1) part[((size_t) ks * M + r) * N + c] = acc[t][i][e];
+                else out[(size_t) r * N + c] = (_Float16) acc[t][i][e];
+            }
+    }
+}
+
+// split-K reduce to f16 (what a non-partial consumer would need)
+__global__ void k_reduce(int N, int KS, const float * __restrict__ part, _Float16 * __restrict__ out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= M * N) return;
+    float s = part[i];
+    for (int k = 1; k < KS; ++k) s += part[(size_t) k * M * N + i];
+    out[i] = (_Float16) s;
+}
+
+struct Shape {
+    const char * name;
+    int N, K;
+};
+
+int main(int argc, char ** argv) {
+    const int NL = 32, REPS = 10;
+    Shape shapes[] = {{"qkv", 3840, 1280}, {"o", 1280, 1280}, {"mlp0", 5120, 1280}, {"mlp1", 1280, 5120}};
+    hipStream_t s;
+    CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    _Float16 * A;
+    CK(hipMalloc(&A, (size_t) M * 5120 * 2));
+    k_fill<<<256, 256, 0, s>>>(A, (size_t) M * 5120, 7);
+    _Float16 * out;
+    float * part;
+    CK(hipMalloc(&out, (size_t) M * 5120 * 2));
+    CK(hipMalloc(&part, (size_t) 64 * M * 5120 * 4));
+    for (const Shape & sh : shapes) {
+        std::vector<_Float16 *> W(NL);
+        for (int l = 0; l < NL; ++l) {
+            CK(hipMalloc(&W[l], (size_t) sh.N * sh.K * 2));
+            k_fill<<<1024, 256, 0, s>>>(W[l], (size_t) sh.N * sh.K, 1000 + l);
+        }
+        CK(hipStreamSynchronize(s));
+        const double mb = (double) sh.N * sh.K * 2 / 1e6;
+        auto timeit = [&](const char * label, auto launch) {
+            hipGraph_t g;
+            hipGraphExec_t ex;
+            CK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+            for (int l = 0; l < NL; ++l) launch(l);
+            CK(hipStreamEndCapture(s, &g));
+            CK(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
+            for (int i = 0; i < 2; ++i) CK(hipGraphLaunch(ex, s));
+            hipEvent_t e0, e1;
+            CK(hipEventCreate(&e0));
+            CK(hipEventCreate(&e1));
+            CK(hipEventRecord(e0, s));
+            for (int i = 0; i < REPS; ++i) CK(hipGraphLaunch(ex, s));
+            CK(hipEventRecord(e1, s));
+            CK(hipEventSynchronize(e1));
+            float ms;
+            CK(hipEventElapsedTime(&ms, e0, e1));
+            const double us = ms * 1e3 / (REPS * NL);
+            printf("%-6s %-28s %7.2f us  %6.2f TB/s\n", sh.name, label, us, mb / us);
+            fflush(stdout);
+            CK(hipGraphExecDestroy(ex));
+            CK(hipGraphDestroy(g));
+        };
+        const int nsteps = sh.K / 32, tiles = sh.N / 16;
+        // current plans (rows_plan): full epilogue J = 2/4/8, partial J = 2/4 with KS
+        for (int J : {2, 4, 8}) {
+            const int KS = (nsteps + 16 * J - 1) / (16 * J);
+            const int per = (nsteps + KS - 1) / KS, nw = (per + J - 1) / J;
+            char lab[64];
+            snprintf(lab, sizeof lab, "cur J=%d KS=%d nw=%d", J, KS, nw);
+            timeit(lab, [&](int l) {
+                dim3 grid(tiles, KS);
+                if (J == 2) k_cur<2, true><<<grid, nw * 64, 0, s>>>(sh.N, sh.K, A, W[l], out, part);
+                if (J == 4) k_cur<4, true><<<grid, nw * 64, 0, s>>>(sh.N, sh.K, A, W[l], out, part);
+                if (J == 8) k_cur<8, true><<<grid, nw * 64, 0, s>>>(sh.N, sh.K, A, W[l], out, part);
+            });
+            if (J == 4) {
+                snprintf(lab, sizeof lab, "empty grid %dx%d", tiles, KS);
+                timeit(lab, [&](int) { k_empty<<<dim3(tiles, KS), nw * 64, 0, s>>>(nullptr); });
+            }
+        }
+#define LDS_VAR(TPW, KR)                                                                               \
+    if (nsteps % KR == 0 && tiles % (4 * TPW) == 0) {                                                  \
+        char lab[64];                                                                                  \
+        const int KS = nsteps / KR;                                                                    \
+        snprintf(lab, sizeof lab, "lds TPW=%d KR=%d grid %dx%d", TPW, KR, tiles / (4 * TPW), KS);       \
+        timeit(lab, [&](int l) {                                                                       \
+            k_lds<TPW, KR><<<dim3(tiles / (4 * TPW), KS), 256, 0, s>>>(sh.N, sh.K, A, W[l], out, part); \
+        });                                                                                            \
+    }
+        LDS_VAR(1, 4) LDS_VAR(1, 8) LDS_VAR(1, 10) LDS_VAR(1, 20) LDS_VAR(2, 4) LDS_VAR(2, 5) LDS_VAR(2, 8)
+        LDS_VAR(2, 10) LDS_VAR(4, 4) LDS_VAR(4, 5) LDS_VAR(1, 16) LDS_VAR(1, 32)
+        {
+            const int KS = 4;
+            timeit("reduce KS=4", [&](int) { k_reduce<<<(M * sh.N + 255) / 256, 256, 0, s>>>(sh.N, KS, part, out); });
+        }
+        for (auto p : W) CK(hipFree(p));
+    }
+    return 0;
+}
