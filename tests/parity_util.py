@@ -171,3 +171,31 @@ def check_cross_rows(w, st, arr, key, layer, name, n_rows=16):
         assert err.max() < 2e-2 * scale and err.mean() < 1e-3 * scale, (key, t, name, err.max(), err.mean(), scale)
         out[t] = float(err.max())
     return out
+
+
+def rttm_activity(rttm, n_frames, spk=4, frame=0.08):
+    """RTTM text -> [frame][speaker] activity (frames of 80 ms, the SortFormer output rate)"""
+    m = np.zeros((n_frames, spk), bool)
+    for line in rttm.splitlines():
+        f = line.split()
+        if len(f) < 8 or f[0] != "SPEAKER":
+            continue
+        s = int(f[7].rsplit("_", 1)[1])
+        a = int(round(float(f[3]) / frame))
+        b = int(round((float(f[3]) + float(f[4])) / frame))
+        m[a:min(b, n_frames), s] = True
+    return m
+
+
+def rttm_activity_diff(got_rttm, ref_rttm, ref_probs, floor_max, threshold=0.5, median=11):
+    """Speaker activity of two RTTMs compared frame by frame. A frame may differ only where the
+    reference's own probability is within 2x its noise floor of the threshold somewhere in the
+    median-filter window (a threshold crossing the reference itself makes under 1e-7 input noise).
+    Returns (frames that differ, mask of differing frames outside that band)."""
+    n = len(ref_probs)
+    got_m, ref_m = rttm_activity(got_rttm, n), rttm_activity(ref_rttm, n)
+    near = np.abs(np.asarray(ref_probs) - threshold) <= 2 * floor_max
+    near_w = np.zeros_like(near)
+    for s in range(-(median // 2), median // 2 + 1):
+        near_w |= np.roll(near, s, axis=0)
+    return int((got_m != ref_m).sum()), (got_m != ref_m) & ~near_w

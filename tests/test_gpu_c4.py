@@ -9,9 +9,12 @@ the RTTM.
 * free run: token ids, segments, token timestamps identical up to a near-tie bounded by the measured
   logit error of this soft_max context (parity_util, first window's prefill / step-1 logits);
 * teacher-forced onto the reference's per-window decoded tokens (parity_util.Forcer): the same
-  tokens, and every token's t_dtw, t0 and t1 EXACTLY the reference's;
+  tokens; t_dtw equal except at DTW path decisions the reference itself flips when its input is
+  perturbed by 1e-7 (make_golden_c4_floor.py: 27 of 3453 tokens in 4 runs, by <= 4 cs) -- each GPU
+  difference must be such a run, shifted the same way, by no more (_check_tdtw);
 * streaming diarization: per-feed frame counts identical, probabilities within 2x the reference's
-  own 1e-7-perturbation noise floor, RTTM text identical;
+  own 1e-7-perturbation noise floor, RTTM speaker activity frame by frame outside the reference's
+  threshold noise band;
 * alignment of the teacher-forced tokens with the GPU RTTM (libwhisper.so's C++ aligner): every
   word's speaker and every utterance identical to the reference pipeline's.
 """
@@ -23,7 +26,7 @@ import numpy as np
 import pytest
 
 import owk
-from parity_util import TIE_FACTOR, Forcer, compare_segments
+from parity_util import TIE_FACTOR, Forcer, compare_segments, rttm_activity_diff
 
 pytestmark = pytest.mark.gpu
 
@@ -82,6 +85,39 @@ def _logit_error(w, meta, arr, pcm):
 _free_run = {}  # test_configs4_transcription's result, aligned by test_configs4_stream_and_align
 
 
+def _runs(diffs):
+    """t_dtw differences [(token, got, want)] -> runs of consecutive tokens shifted alike: one DTW
+    path decision each (the path moves a stretch of tokens together)"""
+    runs = []
+    for i, a, b in diffs:
+        if runs and i == runs[-1][-1][0] + 1 and a - b == runs[-1][-1][1] - runs[-1][-1][2]:
+            runs[-1].append((i, a, b))
+        else:
+            runs.append([(i, a, b)])
+    return runs
+
+
+def _check_tdtw(meta, diffs, tag):
+    """t_dtw parity against the reference's own noise floor (make_golden_c4_floor.py: the reference on
+    the audio perturbed by 1e-7 relative noise). DTW picks its path by strict comparisons over the
+    alignment heads' attention (ref src/whisper.cpp:8837-8998); on near-uniform synthetic attention
+    some path decisions are ties far below any parity bar, and the reference itself flips them under
+    that noise. Every GPU difference must be one of those decisions: a run of tokens shifted alike
+    that overlaps (within 2 tokens) a run the perturbed reference shifts the same way, by no more
+    than the reference's own largest shift."""
+    fl = meta["results"]["tdtw_floor"]
+    floor_runs = _runs([tuple(d) for d in fl["diffs"]])
+    got_runs = _runs(diffs)
+    print(f"[c4] {tag}: t_dtw differs on {len(diffs)} tokens in {len(got_runs)} runs "
+          f"{[(r[0][0], len(r), r[0][1] - r[0][2]) for r in got_runs]}; the perturbed reference: "
+          f"{fl['n_diff']} tokens in {[(r[0][0], len(r), r[0][1] - r[0][2]) for r in floor_runs]}")
+    for r in got_runs:
+        lo, hi, sh = r[0][0], r[-1][0], r[0][1] - r[0][2]
+        assert abs(sh) <= fl["max_shift"], f"{tag}: t_dtw shift {sh} cs beyond the reference's {fl['max_shift']}"
+        assert any(f[0][0] - 2 <= hi and lo <= f[-1][0] + 2 and (f[0][1] - f[0][2]) * sh > 0 for f in floor_runs), \
+            f"{tag}: t_dtw run at tokens {lo}..{hi} (shift {sh}) is not a decision the reference flips itself"
+
+
 def _params(w, meta):
     return w.params(0, **meta["params"])
 
@@ -101,8 +137,8 @@ def test_configs4_transcription(c4, w4, test60):
     if g_ids == r_ids:  # no near-tie parting: the DTW timestamps of the free run are the reference's too
         diff = [(i, a[8], b[8]) for i, (a, b) in enumerate(zip([t for x in got for t in x["tokens"]],
                                                                 [t for x in want["segments"] for t in x["tokens"]])) if a[8] != b[8]]
-        print(f"[c4] free run: {len(g_ids)} tokens identical, t_dtw differs on {len(diff)}")
-        assert not diff, diff[:10]
+        print(f"[c4] free run: {len(g_ids)} tokens identical")
+        _check_tdtw(meta, diff, "free run")
     _free_run["segments"] = got
 
 
@@ -128,9 +164,8 @@ def test_configs4_dtw_teacher_forced(c4, w4, test60):
     g = [t[8] for s in got for t in s["tokens"]]
     r = [t[8] for s in want for t in s["tokens"]]
     diff = [(i, a, b) for i, (a, b) in enumerate(zip(g, r)) if a != b]
-    print(f"[c4] {len(r_ids)} tokens over {len(meta['results']['windows'])} windows; t_dtw differs on "
-          f"{len(diff)}: {diff[:6]}")
-    assert not diff, f"t_dtw differs: {diff[:10]}"
+    print(f"[c4] {len(r_ids)} tokens over {len(meta['results']['windows'])} windows")
+    _check_tdtw(meta, diff, "teacher-forced")
 
 
 def _stream(pcm, block):
@@ -156,20 +191,6 @@ def _stream(pcm, block):
     return np.concatenate(outs, 0), counts
 
 
-def _activity(rttm, n_frames, spk=4, frame=0.08):
-    """RTTM text -> [frame][speaker] activity (frames of 80 ms, the SortFormer output rate)"""
-    m = np.zeros((n_frames, spk), bool)
-    for line in rttm.splitlines():
-        f = line.split()
-        if len(f) < 8 or f[0] != "SPEAKER":
-            continue
-        s = int(f[7].rsplit("_", 1)[1])
-        a = int(round(float(f[3]) / frame))
-        b = int(round((float(f[3]) + float(f[4])) / frame))
-        m[a:min(b, n_frames), s] = True
-    return m
-
-
 def test_configs4_stream_and_align(c4, w4, test60):
     import sortformer as SF
 
@@ -184,13 +205,8 @@ def test_configs4_stream_and_align(c4, w4, test60):
     rttm = SF.to_rttm(probs, 0.5, 11, "audio")
     # RTTM: speaker activity frame by frame; a frame may differ only where the reference's own
     # probability is within 2x its noise floor of the threshold somewhere in the median window
-    got_m, ref_m = _activity(rttm, len(ref)), _activity(meta["results"]["rttm"], len(ref))
-    near = np.abs(ref - 0.5) <= 2 * fl["max"]
-    near_w = np.zeros_like(near)
-    for s in range(-5, 6):
-        near_w |= np.roll(near, s, axis=0)
-    bad = (got_m != ref_m) & ~near_w
-    print(f"[c4] RTTM activity: {int((got_m != ref_m).sum())} of {got_m.size} speaker-frames differ, "
+    n_diff, bad = rttm_activity_diff(rttm, meta["results"]["rttm"], ref, fl["max"])
+    print(f"[c4] RTTM activity: {n_diff} of {ref.size} speaker-frames differ, "
           f"{int(bad.sum())} outside the reference's threshold noise band")
     assert not bad.any(), np.argwhere(bad)[:10]
 

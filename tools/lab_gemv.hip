@@ -141,6 +141,26 @@ __global__ __launch_bounds__(256) void k_lds(int N, int K, const _Float16 * __re
     }
 }
 
+// the weight loads of k_lds<TPW, KR> with the same grid (so each block lands on the XCD the GEMM's
+// block of that index will), no compute: a prefetch of the GEMM's bytes into that XCD's L2
+template <int TPW, int KR>
+__global__ __launch_bounds__(256) void k_pf(int N, int K, const _Float16 * __restrict__ Wt, int * __restrict__ sink) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int nsteps = K >> 5;
+    const int k0 = blockIdx.y * KR;
+    const int tile0 = blockIdx.x * 4 * TPW + wave * TPW;
+    const int ntiles = N >> 4;
+    half8 acc = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int t = 0; t < TPW; ++t) {
+        const int tl = min(tile0 + t, ntiles - 1);
+        const _Float16 * wp = Wt + ((size_t) tl * nsteps + k0) * 512 + lane * 8;
+#pragma unroll
+        for (int j = 0; j < KR; ++j) acc += *(const half8 *) (wp + (size_t) j * 512);
+    }
+    if ((float) acc[0] == 12345.0f) sink[0] = 1;
+}
+
 // split-K reduce to f16 (what a non-partial consumer would need)
 __global__ void k_reduce(int N, int KS, const float * __restrict__ part, _Float16 * __restrict__ out) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -155,7 +175,10 @@ struct Shape {
     int N, K;
 };
 
+static int prefetch_lab();
+
 int main(int argc, char ** argv) {
+    if (argc > 1 && argv[1][0] == 'p') return prefetch_lab();
     const int NL = 32, REPS = 10;
     Shape shapes[] = {{"qkv", 3840, 1280}, {"o", 1280, 1280}, {"mlp0", 5120, 1280}, {"mlp1", 1280, 5120}};
     hipStream_t s;
@@ -231,6 +254,74 @@ int main(int argc, char ** argv) {
             const int KS = 4;
             timeit("reduce KS=4", [&](int) { k_reduce<<<(M * sh.N + 255) / 256, 256, 0, s>>>(sh.N, KS, part, out); });
         }
+        for (auto p : W) CK(hipFree(p));
+    }
+    return 0;
+}
+
+// Does a weight stream survive a kernel boundary in L2 / the Infinity Cache? Per shape, graph chains
+// of NL pairs: [pf(W_l) ; gemm(W_l)] against [pf(W_(l+NL/2)) ; gemm(W_l)] (prefetch of unrelated bytes),
+// plus gemm(W_l) twice back to back and pf alone.
+static int prefetch_lab() {
+    const int NL = 32, REPS = 10;
+    struct Sh { const char * name; int N, K; };
+    Sh shapes[] = {{"qkv", 3840, 1280}, {"o", 1280, 1280}, {"mlp0", 5120, 1280}, {"mlp1", 1280, 5120}};
+    hipStream_t s;
+    CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    _Float16 *A, *out;
+    float * part;
+    int * sink;
+    CK(hipMalloc(&A, (size_t) M * 5120 * 2));
+    CK(hipMalloc(&out, (size_t) M * 5120 * 2));
+    CK(hipMalloc(&part, (size_t) 64 * M * 5120 * 4));
+    CK(hipMalloc(&sink, 64));
+    k_fill<<<256, 256, 0, s>>>(A, (size_t) M * 5120, 7);
+    // a 512 MB buffer to sweep between replays (cold Infinity Cache)
+    _Float16 * big;
+    CK(hipMalloc(&big, (size_t) 256 << 20));
+    for (const Sh & sh : shapes) {
+        std::vector<_Float16 *> W(NL);
+        for (int l = 0; l < NL; ++l) {
+            CK(hipMalloc(&W[l], (size_t) sh.N * sh.K * 2));
+            k_fill<<<1024, 256, 0, s>>>(W[l], (size_t) sh.N * sh.K, 1000 + l);
+        }
+        CK(hipStreamSynchronize(s));
+        const int nsteps = sh.K / 32, tiles = sh.N / 16;
+        constexpr int TPW = 1, KR = 8;
+        const dim3 grid(tiles / (4 * TPW), nsteps / KR);
+        auto G = [&](int l) { k_lds<TPW, KR><<<grid, 256, 0, s>>>(sh.N, sh.K, A, W[l], out, part); };
+        auto P = [&](int l) { k_pf<TPW, KR><<<grid, 256, 0, s>>>(sh.N, sh.K, W[l], sink); };
+        auto timeit = [&](const char * label, auto body) {
+            hipGraph_t g;
+            hipGraphExec_t ex;
+            CK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+            for (int l = 0; l < NL; ++l) body(l);
+            CK(hipStreamEndCapture(s, &g));
+            CK(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
+            float tot = 0;
+            for (int i = 0; i < REPS + 1; ++i) {
+                CK(hipMemsetAsync(big, i, (size_t) 256 << 20, s));  // evict the Infinity Cache
+                hipEvent_t e0, e1;
+                CK(hipEventCreate(&e0));
+                CK(hipEventCreate(&e1));
+                CK(hipEventRecord(e0, s));
+                CK(hipGraphLaunch(ex, s));
+                CK(hipEventRecord(e1, s));
+                CK(hipEventSynchronize(e1));
+                float ms;
+                CK(hipEventElapsedTime(&ms, e0, e1));
+                if (i) tot += ms;
+            }
+            printf("%-6s %-34s %7.2f us per pair\n", sh.name, label, tot * 1e3 / (REPS * NL));
+            fflush(stdout);
+            CK(hipGraphExecDestroy(ex));
+            CK(hipGraphDestroy(g));
+        };
+        timeit("gemm alone", [&](int l) { G(l); });
+        timeit("pf alone", [&](int l) { P(l); });
+        timeit("pf(W_l) ; gemm(W_l)", [&](int l) { P(l); G(l); });
+        timeit("pf(W_other) ; gemm(W_l)", [&](int l) { P((l + NL / 2) % NL); G(l); });
+        timeit("gemm(W_l) ; gemm(W_l)", [&](int l) { G(l); G(l); });
         for (auto p : W) CK(hipFree(p));
     }
     return 0;
