@@ -501,7 +501,7 @@ uint64_t Engine::buffers_signature() const {
     uint64_t h = 1469598103934665603ull;
     for (const void * p : {d_x_.ptr, d_xn_.ptr, d_q_.ptr, d_ao_.ptr, d_h_.ptr, d_xl_.ptr, logits_.ptr, d_stg_.ptr,
                            q8a_.ptr, q8d_.ptr, d_xn32_.ptr, d_ao32_.ptr, d_xl32_.ptr, q16a_.ptr, q16d_.ptr,
-                           self_k_.ptr, self_v_.ptr, cross_k_.ptr, cross_v_.ptr, gws_part_.ptr, xsc_.ptr})
+                           self_k_.ptr, self_v_.ptr, cross_k_.ptr, cross_v_.ptr, gws_part_.ptr})
         h = (h ^ (uint64_t) (uintptr_t) p) * 1099511628211ull;
     return h;
 }
@@ -559,8 +559,6 @@ void Engine::decode(const std::vector<DecodeRow> & rows, const std::vector<int> 
                 q16d_.alloc(std::max(q16d_.bytes, kmax / 32 * mpad * 4));
             }
             logits_.alloc((size_t) C * nv * 4);
-            xsc_ld_ = (hp.n_audio_ctx + 63) / 64 * 64;
-            xsc_.alloc((size_t) C * hp.n_text_head * xsc_ld_ * 4);
         }
         dec_keys_cap_ = std::max(nk, std::max(dec_keys_cap_ * 2, 4096));
         clear_graphs();  // staging offsets and row buffers change: no captured graph stays valid
@@ -716,22 +714,10 @@ void Engine::launch_decode(const DecShape & sh) {
     const float kq_scale = powf(64.0f, -0.25f);
     const size_t self_stride = (size_t) cap_slots * kv_cells * d;
     const size_t cross_stride = (size_t) cap_slots * hp.n_audio_ctx * d;  // per layer (capacity)
-    // one_chunk cross attention of layer l: attn_cross_split (scores, then the F16 recurrence in
-    // half-heads spread evenly over the CUs; the outputs of k_attn_step bit for bit), tiled rows
-    // (prefills of >= 32 tokens) on k_attn_decoder
-    static const bool xsplit = !(getenv("OWK_XSPLIT") && atoi(getenv("OWK_XSPLIT")) == 0);
+    // one_chunk / tiled cross attention of layer l (soft_max rows: attn_decoder_softmax at the call site)
     auto cross_attn = [&](int l, const _Float16 * qv, _Float16 * o16, float * o32, int8_t * q8, float * q8d) {
-        const _Float16 * kl = cross_k_.as<_Float16>() + l * cross_stride;
-        const _Float16 * vl = cross_v_.as<_Float16>() + l * cross_stride;
-        if (xsplit && cross_oc) {
-            attn_cross_split(stream, qv, d, kl, vl, 64, T * 64, d_rc, R, H, kq_scale, T, xsc_.as<float>(), xsc_ld_, o16, d,
-                             o32, q8, q8d);
-            if (cross_tl) attn_decoder(stream, qv, d, kl, vl, 64, T * 64, d_rc, R, nullptr, H, kq_scale, T, o16, d, false,
-                                       true, o32, true, q8, q8d);
-        } else {
-            attn_decoder(stream, qv, d, kl, vl, 64, T * 64, d_rc, R, nullptr, H, kq_scale, T, o16, d, cross_oc, cross_tl,
-                         o32, true, q8, q8d);
-        }
+        attn_decoder(stream, qv, d, cross_k_.as<_Float16>() + l * cross_stride, cross_v_.as<_Float16>() + l * cross_stride,
+                     64, T * 64, d_rc, R, nullptr, H, kq_scale, T, o16, d, cross_oc, cross_tl, o32, true, q8, q8d);
     };
     // R <= 32 rows (F16 weights): each residual matmul (attn.out, cross_attn.out, mlp.2) writes
     // split-K partial tiles and resid_layernorm adds them with bias + residual and emits the next

@@ -169,8 +169,6 @@ private:
 
     // decoder workspace
     DevBuf d_x_, d_xn_, d_q_, d_ao_, d_h_, d_xl_;
-    DevBuf xsc_;  // cross-attention scores of attn_cross_split [rows][heads][xsc_ld_]
-    int xsc_ld_ = 0;
     DevBuf logits_, lg_probs_, lg_lp_;
     int dec_rows_cap_ = 0, dec_keys_cap_ = 0;
     PinnedBuf stg_;   // host image of the per-pass inputs

@@ -606,273 +606,6 @@ __global__ __launch_bounds__(64) void k_attn_step(const _Float16 * __restrict__ 
 }
 
 // ----------------------------------------------------------------------------------
-// Cross attention in two launches (round 3): k_attn_step's one_chunk result with its two HBM
-// streams split so that every CU carries the same bytes. k_attn_step runs one wave per
-// (row, head): 640 waves at 32 rows = 2.5 per CU, and a CU with 3 of them streams 1.2x the
-// average at the per-CU fetch ceiling (~25 GB/s, MI355X_MICROARCH ldsdma-fill), so the launch
-// ends with the 3-wave CUs (48.4 us for 246 MB, 5.1 TB/s).
-//   1. k_xattn_scores: one wave per (row, head, 64-key chunk): the K tile to LDS and the same
-//      f32 dot2 scores as k_attn_step, to sc[row * H + head][key]. The K half (123 MB at 32
-//      rows) in 15 360 short waves over every CU.
-//   2. k_xattn_vrec: the sequential part from the scores -- max-scan, (ms, vs), the F16
-//      recurrence over V. Work unit: half a (row, head) = 32 head dims (64 B of each V row).
-//      A block takes k = ceil(2 P / 256) consecutive half-units (P = rows x heads), one block
-//      per CU, so every CU streams k x 96 KB of V. A wave holds both halves of one (row, head)
-//      (lane = dim, as k_attn_step) or one half (lanes 32.. mirror 0..31 and emit nothing).
-// Scores, scan, exp and the per-key FMA order are k_attn_step's: the outputs are bit-identical.
-// ----------------------------------------------------------------------------------
-constexpr int XA_S_BYTES = AS_KC * 4;             // one chunk's scores
-constexpr int XA_WAVE_LDS = AS_NBUF * (AS_TILE + XA_S_BYTES);
-
-__global__ __launch_bounds__(256) void k_xattn_scores(const _Float16 * __restrict__ q, int ldq,
-                                                      const _Float16 * __restrict__ kb, int ld_kv, int hs,
-                                                      const AttnRow * __restrict__ rows, int H, int nchunks,
-                                                      int n_units, float scale, float * __restrict__ sc, int ldsc) {
-    __shared__ __attribute__((aligned(1024))) char smem[4 * AS_TILE];
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int u = blockIdx.x * 4 + w;
-    if (u >= n_units) return;
-    const int c = u % nchunks, p = u / nchunks;
-    const int r = p / H, h = p - r * H;
-    const AttnRow job = rows[r];
-    const int n = job.n_keys, base = c * AS_KC;
-    if (job.mode != 0 || base >= n) return;
-    const int nk = min(AS_KC, n - base);
-    const _Float16 * kh = kb + job.kv_base + (size_t) h * hs;
-    char * sK = smem + w * AS_TILE;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        const int kk = i * 8 + (lane >> 3);
-        const int key = min(base + kk, n - 1);
-        const int seg = (lane & 7) ^ (kk & 7);  // k_attn_step's swizzle
-        __builtin_amdgcn_global_load_lds((const void *) (kh + (size_t) key * ld_kv + seg * 8),
-                                         (lds_ptr_t) (sK + i * 1024), 16, 0, 2);
-    }
-    const half8 * qp = (const half8 *) (q + (size_t) job.q_row * ldq + h * 64);
-    half8 qv[8];
-#pragma unroll
-    for (int cc = 0; cc < 8; ++cc) qv[cc] = qp[cc];
-    wait_vmcnt<0>();
-    const char * kr = sK + lane * 128;
-    float part[8];
-    half8 krow[8];
-#pragma unroll
-    for (int cc = 0; cc < 8; ++cc) krow[cc] = *(const half8 *) (kr + ((cc ^ (lane & 7)) << 4));
-#pragma unroll
-    for (int cc = 0; cc < 8; ++cc) {
-        const half8 kv = krow[cc];
-        float a = 0.0f;
-#pragma unroll
-        for (int e = 0; e < 8; e += 2) {
-            const half2v k2 = {kv[e], kv[e + 1]}, q2 = {qv[cc][e], qv[cc][e + 1]};
-            a = __builtin_amdgcn_fdot2(k2, q2, a, false);
-        }
-        part[cc] = a;
-    }
-    const float a = ((part[0] + part[1]) + (part[2] + part[3])) + ((part[4] + part[5]) + (part[6] + part[7]));
-    if (lane < nk) sc[(size_t) p * ldsc + base + lane] = a * scale;
-}
-
-// one wave's (row, head) half-units: HALF = one 32-dim half (dim0 = 0 or 32), else all 64 dims
-template <bool HALF>
-__device__ __forceinline__ void xattn_vrec_wave(char * wl, const _Float16 * __restrict__ vh, int ld_kv,
-                                                const float * __restrict__ scp, int n, int n_zero_pad, int dim0,
-                                                float & acc_out, float & S_out) {
-    constexpr int PIECES = HALF ? 4 : 8;  // 1 KB V pieces per chunk
-    constexpr int PER = PIECES + 1;       // + the chunk's scores
-    constexpr int W = HALF ? 32 : 64;     // halves per V row in LDS
-    const int lane = threadIdx.x & 63;
-    const int nchunks = (n + AS_KC - 1) / AS_KC;
-    auto stage = [&](int b, int c) {
-        char * sV = wl + b * (AS_TILE + XA_S_BYTES);
-        char * sS = sV + AS_TILE;
-#pragma unroll
-        for (int i = 0; i < PIECES; ++i) {
-            const int kk = HALF ? i * 16 + (lane >> 2) : i * 8 + (lane >> 3);
-            const int key = min(c * AS_KC + kk, n - 1);
-            const int seg = HALF ? (lane & 3) : (lane & 7);
-            __builtin_amdgcn_global_load_lds((const void *) (vh + (size_t) key * ld_kv + dim0 + seg * 8),
-                                             (lds_ptr_t) (sV + i * 1024), 16, 0, 2);
-        }
-        __builtin_amdgcn_global_load_lds((const void *) (scp + min(c * AS_KC + lane, n - 1)), (lds_ptr_t) sS, 4, 0, 0);
-    };
-    float M = -INFINITY, S = 0.0f;
-    _Float16 acc = (_Float16) 0.0f;
-#pragma unroll
-    for (int c = 0; c < AS_NBUF; ++c)
-        if (c < nchunks) stage(c, c);
-    for (int c = 0; c < nchunks; ++c) {
-        const int ahead = min(AS_NBUF - 1, nchunks - 1 - c);
-        if (ahead == 2) wait_vmcnt<2 * PER>();
-        else if (ahead == 1) wait_vmcnt<PER>();
-        else wait_vmcnt<0>();
-        const char * sV = wl + (c % AS_NBUF) * (AS_TILE + XA_S_BYTES);
-        const float * sS = (const float *) (sV + AS_TILE);
-        const int base = c * AS_KC;
-        const int nk = min(AS_KC, n - base);
-        const float s = lane < nk ? sS[lane] : -INFINITY;
-        const float pm = wave_incl_max(s);
-        const float mex = fmaxf(wave_shr1(pm, M), M);
-        const bool nm = lane < nk && s > mex;
-        const float e = expf(nm ? mex - s : s - mex);
-        const float ms = nm ? e : 1.0f;
-        const float vs = nm ? 1.0f : e;
-        M = fmaxf(M, __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, pm), 63)));
-        const _Float16 * vcol = (const _Float16 *) sV + (lane & (W - 1));
-        const bool full = nk == AS_KC;
-        _Float16 vv[AS_KC];
-#pragma unroll
-        for (int kk = 0; kk < AS_KC; ++kk) vv[kk] = vcol[kk * W];
-        if (c + AS_NBUF < nchunks) {
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this buffer's reads are done
-            stage(c % AS_NBUF, c + AS_NBUF);
-        }
-        if (full && __builtin_amdgcn_ballot_w64(nm) == 0) {
-#pragma unroll
-            for (int kb = 0; kb < AS_KC; kb += AS_RLB) {
-                float vsb[AS_RLB];
-#pragma unroll
-                for (int j = 0; j < AS_RLB; ++j)
-                    vsb[j] = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, vs), kb + j));
-#pragma unroll
-                for (int j = 0; j < AS_RLB; ++j) {
-                    acc = (_Float16) fmaf((float) vv[kb + j], vsb[j], (float) acc);
-                    S = S + vsb[j];
-                }
-            }
-        } else if (full) {
-#pragma unroll
-            for (int kb = 0; kb < AS_KC; kb += AS_RLB / 2) {
-                float msb[AS_RLB / 2], vsb[AS_RLB / 2];
-#pragma unroll
-                for (int j = 0; j < AS_RLB / 2; ++j) {
-                    msb[j] = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, ms), kb + j));
-                    vsb[j] = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, vs), kb + j));
-                }
-#pragma unroll
-                for (int j = 0; j < AS_RLB / 2; ++j) {
-                    acc = (_Float16) ((float) acc * msb[j]);
-                    acc = (_Float16) fmaf((float) vv[kb + j], vsb[j], (float) acc);
-                    S = fmaf(S, msb[j], vsb[j]);
-                }
-            }
-        } else {
-#pragma unroll
-            for (int kb = 0; kb < AS_KC; kb += AS_RLB / 2) {
-                if (kb >= nk) break;
-                float msb[AS_RLB / 2], vsb[AS_RLB / 2];
-#pragma unroll
-                for (int j = 0; j < AS_RLB / 2; ++j) {
-                    msb[j] = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, ms), kb + j));
-                    vsb[j] = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, vs), kb + j));
-                }
-#pragma unroll
-                for (int j = 0; j < AS_RLB / 2; ++j) {
-                    if (kb + j < nk) {
-                        acc = (_Float16) ((float) acc * msb[j]);
-                        acc = (_Float16) fmaf((float) vv[kb + j], vsb[j], (float) acc);
-                        S = fmaf(S, msb[j], vsb[j]);
-                    }
-                }
-            }
-        }
-    }
-    for (int j = 0; j < n_zero_pad; ++j) {  // all-zero keys, as k_attn_step
-        if (0.0f > M) {
-            const float ms = expf(M - 0.0f);
-            M = 0.0f;
-            acc = (_Float16) ((float) acc * ms);
-            S = fmaf(S, ms, 1.0f);
-        } else {
-            S = fmaf(S, 1.0f, expf(0.0f - M));
-        }
-    }
-    acc_out = (float) acc;
-    S_out = S;
-}
-
-template <int NW>
-__global__ __launch_bounds__(NW * 64) void k_xattn_vrec(const _Float16 * __restrict__ vb, int ld_kv, int hs,
-                                                        const AttnRow * __restrict__ rows, int H, int n_half,
-                                                        int per_block, const float * __restrict__ sc, int ldsc,
-                                                        _Float16 * __restrict__ out, int ldo, float * __restrict__ out32,
-                                                        int8_t * __restrict__ q8, float * __restrict__ q8d) {
-    __shared__ __attribute__((aligned(1024))) char smem[NW * XA_WAVE_LDS];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    // this block's half-units [lo, hi): waves take a whole (row, head) where both halves are here
-    const int lo = blockIdx.x * per_block, hi = min(lo + per_block, n_half);
-    int pair = -1, cnt = 0;
-    for (int hu = lo, wi = 0; hu < hi; ++wi) {
-        const int c2 = ((hu & 1) == 0 && hu + 1 < hi) ? 2 : 1;
-        if (wi == wave) {
-            pair = hu;
-            cnt = c2;
-        }
-        hu += c2;
-    }
-    if (pair < 0) return;
-    const bool whole = cnt == 2;
-    const int half = pair & 1;
-    pair >>= 1;
-    const int r = pair / H, h = pair - r * H;
-    const AttnRow job = rows[r];
-    if (job.mode != 0) return;
-    const int dim = whole ? lane : half * 32 + (lane & 31);
-    const bool owner = whole || lane < 32;
-    auto emit = [&](float y) {
-        const size_t o = (size_t) job.q_row * ldo + h * 64 + dim;
-        if (owner) {
-            if (out32) out32[o] = y;
-            else out[o] = (_Float16) y;
-        }
-        if (q8) {  // the two 32-lane groups are the head's two Q8_0 blocks (k_attn_step's emit)
-            float m = fabsf(y);
-#pragma unroll
-            for (int sh = 16; sh > 0; sh >>= 1) m = fmaxf(m, __shfl_xor(m, sh, 32));
-            const float id = m != 0.0f ? 127.f / m : 0.0f;
-            if (owner) {
-                q8[o] = (int8_t) rintf(y * id);
-                if ((lane & 31) == 0) q8d[o >> 5] = m / 127.f;
-            }
-        }
-    };
-    const int n = job.n_keys;
-    if (n <= 0) {
-        emit(0.0f);
-        return;
-    }
-    const _Float16 * vh = vb + job.kv_base + (size_t) h * hs;
-    const float * scp = sc + (size_t) pair * ldsc;
-    char * wl = smem + wave * XA_WAVE_LDS;
-    float acc, S;
-    if (whole) xattn_vrec_wave<false>(wl, vh, ld_kv, scp, n, job.n_zero_pad, 0, acc, S);
-    else xattn_vrec_wave<true>(wl, vh, ld_kv, scp, n, job.n_zero_pad, half * 32, acc, S);
-    const float S_inv = S == 0.0f ? 0.0f : 1.0f / S;
-    emit(acc * S_inv);
-}
-
-void attn_cross_split(hipStream_t s, const _Float16 * q, int ldq, const _Float16 * kbase, const _Float16 * vbase,
-                      int ld_kv, int hs, const AttnRow * rows_dev, int n_rows, int H, float scale, int max_keys,
-                      float * scratch, int ldsc, _Float16 * out, int ldo, float * out32, int8_t * q8, float * q8d) {
-    if (n_rows <= 0) return;
-    if (max_keys > ldsc || ldsc % 64) throw std::runtime_error("attn_cross_split: score scratch too small");
-    const int nchunks = (max_keys + AS_KC - 1) / AS_KC;
-    const int P = n_rows * H, units = P * nchunks;
-    OWK_LAUNCH(k_xattn_scores, dim3((units + 3) / 4), dim3(256), 0, s, q, ldq, kbase, ld_kv, hs, rows_dev, H, nchunks,
-               units, scale, scratch, ldsc);
-    // half-units per block: an equal share per CU (one block per CU), at most 8 (6 waves of LDS)
-    const int n_half = 2 * P;
-    const int per = std::min(8, std::max(1, (n_half + 255) / 256));
-    const int nb = (n_half + per - 1) / per;
-    if (per <= 4)
-        OWK_LAUNCH(k_xattn_vrec<4>, dim3(nb), dim3(256), 0, s, vbase, ld_kv, hs, rows_dev, H, n_half, per, scratch, ldsc,
-                   out, ldo, out32, q8, q8d);
-    else
-        OWK_LAUNCH(k_xattn_vrec<6>, dim3(nb), dim3(384), 0, s, vbase, ld_kv, hs, rows_dev, H, n_half, per, scratch, ldsc,
-                   out, ldo, out32, q8, q8d);
-}
-
-// ----------------------------------------------------------------------------------
 // Decoder attention for rows on the tiled path (prefills of >= 32 tokens: F32
 // accumulator over tiles of 16 keys, ops.cpp:8417-8510). Block = 4 waves = 4 heads.
 // ----------------------------------------------------------------------------------

@@ -263,14 +263,6 @@ void attn_decoder(hipStream_t s, const _Float16 * q, int ldq, const _Float16 * k
                   int max_keys, _Float16 * out, int ldo, bool any_one_chunk, bool any_tiled, float * out32 = nullptr,
                   bool oc_listed = true,  // false: every one_chunk row is a contiguous cell run
                   int8_t * q8 = nullptr, float * q8d = nullptr);  // one_chunk rows: Q8_0 of the f32 output
-// the one_chunk rows (mode 0) of a cross-attention pass (no cell lists) as two launches with the same
-// outputs as attn_decoder: scores over every (row, head, 64-key chunk), then the F16 recurrence over
-// V in half-heads spread evenly over the CUs (k_attn.hip). scratch: [n_rows * H][ldsc] f32 scores,
-// ldsc >= max_keys, a multiple of 64. Tiled / soft_max rows are left to the other kernels.
-void attn_cross_split(hipStream_t s, const _Float16 * q, int ldq, const _Float16 * kbase, const _Float16 * vbase,
-                      int ld_kv, int hs, const AttnRow * rows_dev, int n_rows, int H, float scale, int max_keys,
-                      float * scratch, int ldsc, _Float16 * out, int ldo, float * out32 = nullptr,
-                      int8_t * q8 = nullptr, float * q8d = nullptr);
 // rows with mode 2 (flash_attn = false contexts): soft_max attention, F16 probabilities;
 // optional DTW capture of alignment-head probabilities cap[a][key][row] (amap: head -> a or -1)
 void attn_decoder_softmax(hipStream_t s, const _Float16 * q, int ldq, const _Float16 * kbase, const _Float16 * vbase,
@@ -278,7 +270,7 @@ void attn_decoder_softmax(hipStream_t s, const _Float16 * q, int ldq, const _Flo
                           int max_keys, _Float16 * out, int ldo, const int * amap, float * cap, int cap_rows,
                           float * out32 = nullptr);
 // test/bench hook: the one_chunk cross-attention kernels on contiguous head-major keys (ld 64):
-// which = 1 the one-wave k_attn_step (owk_debug_attn_cross calls attn_cross_split for 2)
+// which = 1 the one-wave k_attn_step
 void attn_cross_kernel(hipStream_t s, int which, const _Float16 * q, int ldq, const _Float16 * kbase,
                        const _Float16 * vbase, int hs, const AttnRow * rows_dev, int n_rows, int H, float scale,
                        _Float16 * out, int ldo);

@@ -1511,13 +1511,13 @@ int owk_debug_gemm_q5(int device, int M, int N, int K, const float * a, const ui
 }
 
 // one_chunk cross attention of R rows (row r over its own clip r: k, v [R][H][T][64] f16 head-major,
-// q [R][H*64]) with the one-wave k_attn_step (which = 1) or attn_cross_split (2); out [R][H*64] f16.
+// q [R][H*64]) with the one-wave k_attn_step (which = 1); out [R][H*64] f16.
 // iters > 0: also returns the mean device time per launch in microseconds (random q/k/v if the host
 // pointers are null); iters == 0 returns 0; -1 on error
 double owk_debug_attn_cross(int device, int which, int R, int H, int T, int n_zero_pad, float scale, const uint16_t * q,
                             const uint16_t * k, const uint16_t * v, uint16_t * out, int iters) {
     try {
-        if (R <= 0 || H <= 0 || T < 0 || n_zero_pad < 0 || (which != 1 && which != 2) || iters < 0)
+        if (R <= 0 || H <= 0 || T < 0 || n_zero_pad < 0 || which != 1 || iters < 0)
             throw std::runtime_error("bad arguments");
         OWK_HIP_CHECK(hipSetDevice(device));
         hipStream_t s;
@@ -1541,17 +1541,9 @@ double owk_debug_attn_cross(int device, int which, int R, int H, int T, int n_ze
         for (int r = 0; r < R; ++r) rows[r] = AttnRow{r, r * H * T * 64, T, -1, n_zero_pad, 0};
         drows.alloc(R * sizeof(AttnRow));
         OWK_HIP_CHECK(hipMemcpy(drows.ptr, rows.data(), R * sizeof(AttnRow), hipMemcpyHostToDevice));
-        const int ldsc = std::max(64, (T + 63) / 64 * 64);
-        DevBuf dsc;
-        dsc.alloc((size_t) R * H * ldsc * 4);
         auto run = [&] {
-            if (which == 2)
-                attn_cross_split(s, dq.as<_Float16>(), H * 64, dk.as<_Float16>(), dv.as<_Float16>(), 64, T * 64,
-                                 (const AttnRow *) drows.ptr, R, H, scale, T, dsc.as<float>(), ldsc, dout.as<_Float16>(),
-                                 H * 64);
-            else
-                attn_cross_kernel(s, which, dq.as<_Float16>(), H * 64, dk.as<_Float16>(), dv.as<_Float16>(), T * 64,
-                                  (const AttnRow *) drows.ptr, R, H, scale, dout.as<_Float16>(), H * 64);
+            attn_cross_kernel(s, which, dq.as<_Float16>(), H * 64, dk.as<_Float16>(), dv.as<_Float16>(), T * 64,
+                              (const AttnRow *) drows.ptr, R, H, scale, dout.as<_Float16>(), H * 64);
         };
         run();
         double us = 0.0;
