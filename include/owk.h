@@ -70,6 +70,7 @@ WHISPER_API const uint16_t * owk_debug_gelu_table(void);
 /* out[M][N] = A[M][K] . W[N][K]^T (f16 bits in, f32 out) through the engine's GEMM dispatch */
 WHISPER_API int owk_debug_gemm(int device, int M, int N, int K, const uint16_t * a, const uint16_t * w, float * out);
 // one large-tile epilogue mode through the 128x128 and 256x256 kernels on the same random operands: max |diff|
+// (mode | 0x800: the 8-phase 256x256 kernel instead of the 4-slot ring one)
 WHISPER_API double owk_debug_gemm_epi_diff(int device, int mode, int M, int N, int K, int d, int T);
 /* average microseconds per launch of `iters` back-to-back engine GEMMs (epilogue `mode`, zero data) */
 /* test hook (host only): the DTW alignment of captured alignment-head attention

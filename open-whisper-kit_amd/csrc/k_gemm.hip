@@ -600,6 +600,232 @@ __global__ __launch_bounds__(512, 2) void k_gemm_256(int M, int N, int K, const 
 }
 
 // ---------------------------------------------------------------------------------
+// 256x256 block tile with the CDNA guide's 8-phase schedule (round 3; cdna_hip_programming.md §5
+// "The 256^2 8-phase template"): K-tiles of 64, two LDS buffers of 64 KB (even / odd tiles), each
+// cut into four 16 KB parts of 128 rows x 64 k:
+//   A0 = A rows wr*128 + [0, 64) of both wave rows,   A1 = rows wr*128 + [64, 128),
+//   W0 = W rows wc*64 + [0, 32) of all wave columns,  W1 = rows wc*64 + [32, 64).
+// A wave (wr, wc) owns a 128 x 64 output block = four 64 x 32 quadrants; a K-tile is 4 phases, one
+// quadrant each (16 MFMAs over K = 64), reading the fragments it needs first:
+//   phase 1: A0 + W0 -> (A0, W0)   phase 2: W1 -> (A0, W1)   phase 3: A1 -> (A1, W1)   phase 4: -
+//   (A1, W0)
+// and staging one part of a later tile (2 global_load_lds of 16 B per thread): phases 1 / 2 stage W1 /
+// A1 of tile t+1, phases 3 / 4 stage A0 / W0 of tile t+2 -- each at least two phases after that part's
+// last read. Phase 4 ends with s_waitcnt vmcnt(4): the 4 loads of tile t+2 stay in flight, tile t+1 has
+// landed (read from the next phase on, behind two barriers). Per phase: ds_reads + staging, s_barrier,
+// lgkmcnt(0), 16 MFMAs under s_setprio(1), s_barrier; the two wave rows run one barrier apart (wave row 1
+// takes an extra s_barrier first, wave row 0 one at the end), so one row's MFMAs overlap the other's LDS
+// reads. 16-B chunk c of part row r is stored at chunk c ^ sw8(r): conflict-free ds_read_b128 for 16
+// consecutive rows (A) and for the permuted W rows of the C^T tiles. Output and epilogues as
+// k_gemm_256 (SWAP: C^T tiles, 16-byte vector epilogues).
+// ---------------------------------------------------------------------------------
+constexpr int G8_K = 64;
+constexpr int G8_PART = 128 * G8_K * 2;  // 16 KB
+constexpr int G8_BUF = 4 * G8_PART;      // 64 KB
+
+__device__ __forceinline__ int sw8(int r) {
+    return ((r >> 1) & 1) | ((((r >> 2) ^ (r >> 3)) & 1) << 1) | ((((r >> 3) ^ (r >> 4)) & 1) << 2);
+}
+
+template <int MODE, bool SWAP>
+__global__ __launch_bounds__(512, 1) void k_gemm_8p(int M, int N, int K, const _Float16 * __restrict__ A, int lda,
+                                                    const _Float16 * __restrict__ W, int ldw, EpiParams ep) {
+    __shared__ __attribute__((aligned(1024))) char smem[2 * G8_BUF];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wr = wave >> 2, wc = wave & 3;
+    const int nbn = (N + G2_N - 1) / G2_N;
+    const int nb = gridDim.x;
+    int bid = blockIdx.x;
+    {  // XCD-aware order, then the grouped tile order of k_gemm_256
+        const int xcd = bid & 7, q = nb >> 3, rr = nb & 7;
+        const int base = xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q;
+        bid = base + (bid >> 3);
+    }
+    int bm, bn;
+    tile_order(bid, nb, nbn, bm, bn);
+    const int m0 = bm * G2_M, n0 = bn * G2_N;
+
+    // staging: wave w fills part rows 16w .. 16w+15 of a part (2 x 1 KB pieces of 8 rows x 128 B);
+    // lane l: row 16w + 8i + (l >> 3), physical chunk l & 7 <- logical chunk (l & 7) ^ sw8(row)
+    const _Float16 * src[4][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int pr = wave * 16 + i * 8 + (lane >> 3);
+        const int ch = ((lane & 7) ^ sw8(pr)) * 8;
+        const int ra0 = (pr >> 6) * 128 + (pr & 63), ra1 = ra0 + 64;      // A0 / A1 part rows -> tile rows
+        const int rw0 = (pr >> 5) * 64 + (pr & 31), rw1 = rw0 + 32;       // W0 / W1
+        src[0][i] = A + (size_t) min(m0 + ra0, M - 1) * lda + ch;
+        src[1][i] = A + (size_t) min(m0 + ra1, M - 1) * lda + ch;
+        src[2][i] = W + (size_t) min(n0 + rw0, N - 1) * ldw + ch;
+        src[3][i] = W + (size_t) min(n0 + rw1, N - 1) * ldw + ch;
+    }
+    const int nt = K / G8_K;
+    // part p (0 A0, 1 A1, 2 W0, 3 W1) of tile t into buffer t & 1
+    auto stage = [&](int p, int t) {
+        char * dst = smem + (t & 1) * G8_BUF + p * G8_PART + wave * 2048;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const _Float16 * sp = p == 0 ? src[0][i] : p == 1 ? src[1][i] : p == 2 ? src[2][i] : src[3][i];
+            __builtin_amdgcn_global_load_lds((const void *) (sp + (size_t) t * G8_K), (lds_ptr_t) (dst + i * 1024), 16, 0, 0);
+        }
+    };
+
+    // fragment byte offsets inside a part: A frag i (of the wave's quadrant row) / W frag j, K half h
+    const int g = lane >> 4, l16 = lane & 15;
+    int offA[4], offW[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int pr = wr * 64 + i * 16 + l16;
+        offA[i] = pr * 128 + ((g ^ sw8(pr)) << 4);  // logical chunk g (+ 4 for the second K half)
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        // swap: W frag j row p = wc*64 + (j>>1)*32 + (p>>2)*8 + (j&1)*4 + (p&3) (k_gemm_256's permutation)
+        const int pr = SWAP ? wc * 32 + (l16 >> 2) * 8 + (j & 1) * 4 + (l16 & 3) : wc * 32 + (j & 1) * 16 + l16;
+        offW[j] = pr * 128 + ((g ^ sw8(pr)) << 4);
+    }
+    auto rdA = [&](const char * part, int i, int h) {  // chunk (h*4 + g) ^ sw8 = (g ^ sw8) ^ (h*4)
+        return *(const half8 *) (part + (offA[i] ^ (h << 6)));
+    };
+    auto rdW = [&](const char * part, int j, int h) { return *(const half8 *) (part + (offW[j] ^ (h << 6))); };
+
+    floatx4 acc[8][4];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+    // prologue: tile 0 whole, tile 1's A0 / W0; tile 0 landed everywhere
+    stage(0, 0);
+    stage(2, 0);
+    stage(3, 0);
+    stage(1, 0);
+    if (nt > 1) {
+        stage(0, 1);
+        stage(2, 1);
+        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    if (wr == 1) __builtin_amdgcn_s_barrier();  // the wave rows one barrier apart
+    __builtin_amdgcn_sched_barrier(0);
+
+    half8 fa[4][2], fw[4][2];
+    auto mma = [&](int i0, int j0) {  // quadrant rows i0..i0+3 (fa), columns j0, j0+1 (fw)
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    if (SWAP)
+                        acc[i0 + i][j0 + j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fw[j0 + j][h], fa[i][h], acc[i0 + i][j0 + j], 0, 0, 0);
+                    else
+                        acc[i0 + i][j0 + j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[i][h], fw[j0 + j][h], acc[i0 + i][j0 + j], 0, 0, 0);
+                }
+        __builtin_amdgcn_s_setprio(0);
+    };
+#define G8_SYNC_MMA(I0, J0)                                          \
+    __builtin_amdgcn_sched_barrier(0);                               \
+    __builtin_amdgcn_s_barrier();                                    \
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");               \
+    __builtin_amdgcn_sched_barrier(0);                               \
+    mma(I0, J0);                                                     \
+    __builtin_amdgcn_sched_barrier(0);                               \
+    __builtin_amdgcn_s_barrier();                                    \
+    __builtin_amdgcn_sched_barrier(0);
+
+    for (int t = 0; t < nt; ++t) {
+        const char * buf = smem + (t & 1) * G8_BUF;
+        // phase 1: A0 + W0 fragments; stage W1 of tile t+1
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int h = 0; h < 2; ++h) fa[i][h] = rdA(buf, i, h);
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int h = 0; h < 2; ++h) fw[j][h] = rdW(buf + 2 * G8_PART, j, h);
+        if (t + 1 < nt) stage(3, t + 1);
+        G8_SYNC_MMA(0, 0)
+        // phase 2: W1 fragments; stage A1 of tile t+1
+#pragma unroll
+        for (int j = 2; j < 4; ++j)
+#pragma unroll
+            for (int h = 0; h < 2; ++h) fw[j][h] = rdW(buf + 3 * G8_PART, j, h);
+        if (t + 1 < nt) stage(1, t + 1);
+        G8_SYNC_MMA(0, 2)
+        // phase 3: A1 fragments; stage A0 of tile t+2
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int h = 0; h < 2; ++h) fa[i][h] = rdA(buf + G8_PART, i, h);
+        if (t + 2 < nt) stage(0, t + 2);
+        G8_SYNC_MMA(4, 2)
+        // phase 4: no reads; stage W0 of tile t+2, then tile t+1 landed (t+2's 4 loads in flight)
+        if (t + 2 < nt) {
+            stage(2, t + 2);
+            asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        G8_SYNC_MMA(4, 0)
+    }
+#undef G8_SYNC_MMA
+    if (wr == 0) __builtin_amdgcn_s_barrier();  // every wave ends on the same barrier count
+
+    if (SWAP) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int r = m0 + wr * 128 + i * 16 + l16;
+            if (r >= M) continue;
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int c = n0 + wc * 64 + h * 32 + g * 8;
+                const float v[8] = {acc[i][2 * h][0], acc[i][2 * h][1], acc[i][2 * h][2], acc[i][2 * h][3],
+                                    acc[i][2 * h + 1][0], acc[i][2 * h + 1][1], acc[i][2 * h + 1][2], acc[i][2 * h + 1][3]};
+                if (c + 8 <= N) {
+                    epi_row8<MODE>(ep, r, c, v, ep.vec != 0);
+                } else {
+#pragma unroll
+                    for (int e = 0; e < 8; ++e)
+                        if (c + e < N) epi_store<MODE>(ep, r, c + e, v[e]);
+                }
+            }
+        }
+        return;
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int cl = n0 + wc * 64 + j * 16 + l16;
+            const int c = cl + ep.c_off;
+            const int r0 = m0 + wr * 128 + i * 16 + 4 * g;
+            if constexpr (MODE == EPI_QKV_ENC) {
+                const int d = ep.d;
+                if (c >= 2 * d && cl < N && r0 + 3 < M && ep.T % 4 == 0) {
+                    const int cc = c - 2 * d;
+                    const int clip = r0 / ep.T, t = r0 - clip * ep.T;
+                    const float bv = ep.bias2[cc];
+                    half4 hv;
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) hv[e] = (_Float16) (acc[i][j][e] + bv);
+                    *(half4 *) (ep.out16c + (((size_t) clip * (d >> 6) + (cc >> 6)) * 64 + (cc & 63)) * ep.Tpad + t) = hv;
+                    continue;
+                }
+            }
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int r = r0 + e;
+                if (r < M && cl < N) epi_store<MODE>(ep, r, c, acc[i][j][e]);
+            }
+        }
+}
+
+// ---------------------------------------------------------------------------------
 // Quantized large-tile GEMM (gemm_q16: encoder / cross-K/V matrices of Q5_0 / Q8_0 / Q4_0 models).
 // A = the Q8_0 integers of the activation rows and W = the weight integers, both as exact f16
 // values; each 32-wide K-step is one quantization block: its MFMA dot is an exact integer
@@ -1027,11 +1253,12 @@ template <int MODE> struct LaunchBig {
         OWK_LAUNCH(k_gemm_big<MODE>, dim3(nbm * nbn), dim3(256), 0, s, M, N, K, A, lda, W, ldw, ep);
     }
 };
-// 256x256 kernel selection: OWK_GEMM256 (default 1; 0 forces the 128x128 tile), overridden per
+// 256x256 kernel selection: OWK_GEMM256 (default 8 = k_gemm_8p; 1 the 4-slot ring k_gemm_256, 5 its
+// 5-slot variant, 0 forces the 128x128 tile), overridden per
 // thread by the debug hooks (gemm_set_256) so a hook never changes another thread's engine
-static thread_local int t_gemm256 = -1;  // -1: no override; 5: the 5-slot ring variant
+static thread_local int t_gemm256 = -1;  // -1: no override; 5: the 5-slot ring variant; 8: the 8-phase kernel
 static int gemm256_mode() {
-    static const int env = env_int("OWK_GEMM256", 1);
+    static const int env = env_int("OWK_GEMM256", 8);  // 8: the 8-phase kernel (round 3)
     return t_gemm256 >= 0 ? t_gemm256 : env;
 }
 template <int MODE> struct Launch256 {
@@ -1040,6 +1267,13 @@ template <int MODE> struct Launch256 {
         const int nbm = (M + G2_M - 1) / G2_M, nbn = (N + G2_N - 1) / G2_N;
         EpiParams e = ep;
         e.vec = epi_vec_ok(MODE, ep, N) ? 1 : 0;
+        if (gemm256_mode() == 8 && K % G8_K == 0) {  // the 8-phase schedule
+            if (MODE == EPI_QKV_ENC)
+                OWK_LAUNCH((k_gemm_8p<MODE, false>), dim3(nbm * nbn), dim3(512), 0, s, M, N, K, A, lda, W, ldw, e);
+            else
+                OWK_LAUNCH((k_gemm_8p<MODE, true>), dim3(nbm * nbn), dim3(512), 0, s, M, N, K, A, lda, W, ldw, e);
+            return;
+        }
         if (MODE == EPI_QKV_ENC) {
             // one launch of C tiles: the V columns need them (transposed image, 4 consecutive key
             // positions per lane), and splitting Q/K off as C^T tiles measured slower in all

@@ -1187,9 +1187,9 @@ __global__ static void k_fill_rand_f16(_Float16 * p, size_t n, uint32_t seed) {
 // mode bit 0x100: force the 128x128 large-GEMM kernel; bit 0x400: the 5-slot ring variant of the
 // 256x256 kernel; bit 0x200: random operands
 double owk_debug_gemm_bench(int device, int mode, int M, int N, int K, int iters) {
-    const bool force128 = mode & 0x100, rnd = mode & 0x200, ring5 = mode & 0x400;
+    const bool force128 = mode & 0x100, rnd = mode & 0x200, ring5 = mode & 0x400, p8 = mode & 0x800;
     mode &= 0xFF;
-    GemmOverride ov(force128 ? 0 : ring5 ? 5 : 1);
+    GemmOverride ov(force128 ? 0 : ring5 ? 5 : p8 ? 8 : 1);
     try {
         OWK_HIP_CHECK(hipSetDevice(device));
         hipStream_t s;
@@ -1577,6 +1577,8 @@ double owk_debug_attn_cross(int device, int which, int R, int H, int T, int n_ze
 // output the mode writes (f32 and f16 images), or -1 on error. d / T: EPI_QKV_ENC / EPI_KV_CROSS /
 // EPI_CONV2 shape parameters (N = 3d / 2d / d).
 double owk_debug_gemm_epi_diff(int device, int mode, int M, int N, int K, int d, int T) {
+    const int large = (mode & 0x800) ? 8 : 1;  // 0x800: the 8-phase kernel against the 128x128 one
+    mode &= 0xFF;
     try {
         OWK_HIP_CHECK(hipSetDevice(device));
         hipStream_t s;
@@ -1631,7 +1633,7 @@ double owk_debug_gemm_epi_diff(int device, int mode, int M, int N, int K, int d,
             ep.pos = pos.as<float>();
             ep.gelu_tab = gt.as<uint16_t>();
             if (mode == EPI_RESID_F32 || mode == EPI_HALF_RESID) ep.out32 = res[k].as<float>();  // in place, as the engine
-            GemmOverride ov(k == 0 ? 0 : 1);
+            GemmOverride ov(k == 0 ? 0 : large);
             gemm_f16(s, mode, M, N, K, da.as<_Float16>(), K, dw.as<_Float16>(), K, ep);
             OWK_HIP_CHECK(hipStreamSynchronize(s));
             out32[k].resize(n32);

@@ -117,8 +117,9 @@ _EPI_CASES = {
 }
 
 
+@pytest.mark.parametrize("kern", [0, 0x800], ids=["ring4", "8phase"])
 @pytest.mark.parametrize("case", sorted(_EPI_CASES))
-def test_gemm256_epilogue_matches_128(case):
+def test_gemm256_epilogue_matches_128(case, kern):
     """The 256x256 ring kernel computes C^T tiles and writes 8-column runs with 16-byte vector
     epilogues (k_gemm.hip epi_row8); the 128x128 kernel writes every element with epi_store.
     Same operands, bias, residual, positions and GELU table: every output must agree."""
@@ -127,8 +128,8 @@ def test_gemm256_epilogue_matches_128(case):
     L.owk_debug_gemm_epi_diff.restype = C.c_double
     L.owk_debug_gemm_epi_diff.argtypes = [C.c_int] * 7
     M = 3000 if T else 2304
-    diff = L.owk_debug_gemm_epi_diff(0, mode, M, N, 1280, d, T)
-    print(f"{case}: max|256 - 128| = {diff:.3g}")
+    diff = L.owk_debug_gemm_epi_diff(0, mode | kern, M, N, 1280, d, T)
+    print(f"{case} {kern:#x}: max|256 - 128| = {diff:.3g}")
     assert diff >= 0
     assert diff <= 1e-6, f"{case}: epilogues differ by {diff}"
 

@@ -47,7 +47,7 @@ def main():
     res = {}
     for rnd in range(3):
         for name, (M, N, K, epi) in SHAPES.items():
-            for kern, flag in (("256", 0), ("256r5", 0x400), ("128", 0x100), ("256zero", -0x200)):
+            for kern, flag in (("256", 0), ("8phase", 0x800), ("128", 0x100)):
                 mode = EPI[epi] | 0x200 | max(flag, 0) if flag >= 0 else EPI[epi]
                 us = L.owk_debug_gemm_bench(0, mode, M, N, K, 10)
                 res.setdefault((name, kern), []).append(us)
