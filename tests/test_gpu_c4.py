@@ -10,8 +10,8 @@ the RTTM.
   logit error of this soft_max context (parity_util, first window's prefill / step-1 logits);
 * teacher-forced onto the reference's per-window decoded tokens (parity_util.Forcer): the same
   tokens; t_dtw equal except at DTW path decisions the reference itself flips when its input is
-  perturbed by 1e-7 (make_golden_c4_floor.py: 27 of 3453 tokens in 4 runs, by <= 4 cs) -- each GPU
-  difference must be such a run, shifted the same way, by no more (_check_tdtw);
+  perturbed by 1e-7 (make_golden_c4_floor.py, three seeds: 27 / 100 / 75 of 3453 tokens in 2-7 runs,
+  by <= 4 cs) -- each GPU difference must be such a run, shifted the same way, by no more (_check_tdtw);
 * streaming diarization: per-feed frame counts identical, probabilities within 2x the reference's
   own 1e-7-perturbation noise floor, RTTM speaker activity frame by frame outside the reference's
   threshold noise band;
@@ -99,21 +99,23 @@ def _runs(diffs):
 
 def _check_tdtw(meta, diffs, tag):
     """t_dtw parity against the reference's own noise floor (make_golden_c4_floor.py: the reference on
-    the audio perturbed by 1e-7 relative noise). DTW picks its path by strict comparisons over the
-    alignment heads' attention (ref src/whisper.cpp:8837-8998); on near-uniform synthetic attention
-    some path decisions are ties far below any parity bar, and the reference itself flips them under
-    that noise. Every GPU difference must be one of those decisions: a run of tokens shifted alike
-    that overlaps (within 2 tokens) a run the perturbed reference shifts the same way, by no more
-    than the reference's own largest shift."""
-    fl = meta["results"]["tdtw_floor"]
-    floor_runs = _runs([tuple(d) for d in fl["diffs"]])
+    the audio perturbed by 1e-7 relative noise, three seeds). DTW picks its path by strict comparisons
+    over the alignment heads' attention (ref src/whisper.cpp:8837-8998); on near-uniform synthetic
+    attention some path decisions are ties far below any parity bar, and the reference itself flips
+    them under that noise (27 / 100 / 75 tokens by seed, in 2-7 runs). Every GPU difference must be
+    one of those decisions: a run of tokens shifted alike that overlaps (within 2 tokens) a run some
+    perturbed reference shifts the same way, by no more than the reference's own largest shift."""
+    seeds = meta["results"]["tdtw_floor_seeds"]
+    floor_runs = [r for sd in seeds for r in _runs([tuple(d) for d in sd["diffs"]])]
+    max_shift = max(sd["max_shift"] for sd in seeds)
     got_runs = _runs(diffs)
     print(f"[c4] {tag}: t_dtw differs on {len(diffs)} tokens in {len(got_runs)} runs "
-          f"{[(r[0][0], len(r), r[0][1] - r[0][2]) for r in got_runs]}; the perturbed reference: "
-          f"{fl['n_diff']} tokens in {[(r[0][0], len(r), r[0][1] - r[0][2]) for r in floor_runs]}")
+          f"{[(r[0][0], len(r), r[0][1] - r[0][2]) for r in got_runs]}; the perturbed reference (seeds "
+          f"{[sd['seed'] for sd in seeds]}): {[sd['n_diff'] for sd in seeds]} tokens, runs "
+          f"{sorted({(r[0][0], len(r), r[0][1] - r[0][2]) for r in floor_runs})}")
     for r in got_runs:
         lo, hi, sh = r[0][0], r[-1][0], r[0][1] - r[0][2]
-        assert abs(sh) <= fl["max_shift"], f"{tag}: t_dtw shift {sh} cs beyond the reference's {fl['max_shift']}"
+        assert abs(sh) <= max_shift, f"{tag}: t_dtw shift {sh} cs beyond the reference's {max_shift}"
         assert any(f[0][0] - 2 <= hi and lo <= f[-1][0] + 2 and (f[0][1] - f[0][2]) * sh > 0 for f in floor_runs), \
             f"{tag}: t_dtw run at tokens {lo}..{hi} (shift {sh}) is not a decision the reference flips itself"
 
