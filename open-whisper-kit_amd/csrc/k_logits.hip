@@ -463,7 +463,7 @@ constexpr size_t LG_REG_LDS = ((size_t) LG_ES * LG_THREADS + LG_TS + LG_E * LG_T
 void process_logits(hipStream_t s, float * logits, int n_vocab, const LogitJob * jobs_dev, int n_jobs,
                     const VocabInfo & vi, TokenOut * out_dev, float * logprobs_out, float * probs_out) {
     if (n_jobs <= 0) return;
-    static const bool reg = !(getenv("OWK_LOGITS_REG") && atoi(getenv("OWK_LOGITS_REG")) == 0);
+    static const bool reg = getenv("OWK_LOGITS_REG") && atoi(getenv("OWK_LOGITS_REG")) == 1;  // A/B pending
     if (reg && n_vocab <= LG_E * LG_THREADS && n_vocab - vi.beg <= LG_TS && vi.beg >= 0)
         OWK_LAUNCH(k_process_logits_reg, dim3(n_jobs), dim3(LG_THREADS), LG_REG_LDS, s, logits, n_vocab, jobs_dev, vi,
                    out_dev, logprobs_out, probs_out);
