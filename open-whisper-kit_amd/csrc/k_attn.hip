@@ -102,16 +102,27 @@ __global__ __launch_bounds__(256, 2) void k_attn_encoder(const _Float16 * __rest
             sc[t] = z;
         }
         float tmax = -INFINITY;
+        if ((kt + 1) * FA_KT <= T) {  // a full tile (every one but the last): no key mask
 #pragma unroll
-        for (int t = 0; t < 4; ++t)
+            for (int t = 0; t < 4; ++t)
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const int key = kt * FA_KT + t * 16 + 4 * g + e;
-                float v = sc[t][e] * scale2;
-                if (key >= T) v = -INFINITY;
-                sc[t][e] = v;
-                tmax = fmaxf(tmax, v);
-            }
+                for (int e = 0; e < 4; ++e) {
+                    const float v = sc[t][e] * scale2;
+                    sc[t][e] = v;
+                    tmax = fmaxf(tmax, v);
+                }
+        } else {
+#pragma unroll
+            for (int t = 0; t < 4; ++t)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int key = kt * FA_KT + t * 16 + 4 * g + e;
+                    float v = sc[t][e] * scale2;
+                    if (key >= T) v = -INFINITY;
+                    sc[t][e] = v;
+                    tmax = fmaxf(tmax, v);
+                }
+        }
         tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
         tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
         const float mnew = fmaxf(m, tmax);
