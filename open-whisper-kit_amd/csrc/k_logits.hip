@@ -300,176 +300,11 @@ void nosp_probs(hipStream_t s, const float * row0, int n_vocab, const int2 * req
     OWK_LAUNCH(k_nosp, dim3(n), dim3(LG_THREADS), 0, s, row0, n_vocab, req_dev, rmx, stride, nosp, out_dev);
 }
 
-// The same processing with the row on chip (round 3): thread t owns elements t + k * LG_THREADS,
-// k < LG_E; slots k < LG_ES live in LDS ([k][t], 144 KB), the rest in registers, so the six sweeps
-// of k_process_logits read the chip instead of the 207 KB row from L2 each time; the row is loaded
-// once and its final state (temperature, masks, suppress list, timestamp rule) written back once.
-// Every loop visits a thread's elements in k_process_logits' order and every reduction is the same
-// block reduction: the results are k_process_logits' bit for bit. The suppress list goes through an
-// LDS bitmap, the timestamp sum through the timestamp range staged in LDS in that kernel's partition.
-constexpr int LG_E = 52;   // 52 x 1024 >= 51 866, the largest Whisper vocabulary
-constexpr int LG_ES = 36;  // slots in LDS (36 x 4 KB); 16 in registers
-constexpr int LG_TS = 1536;
-__global__ __launch_bounds__(LG_THREADS) void k_process_logits_reg(float * __restrict__ logits, int n_vocab,
-                                                                  const LogitJob * __restrict__ jobs, VocabInfo vi,
-                                                                  TokenOut * __restrict__ outv,
-                                                                  float * __restrict__ lp_out,
-                                                                  float * __restrict__ pr_out) {
-    extern __shared__ float lsm[];
-    float * sl = lsm;                                  // [LG_ES][LG_THREADS]
-    float * tsl = sl + LG_ES * LG_THREADS;             // [LG_TS]
-    uint32_t * sup = (uint32_t *) (tsl + LG_TS);       // [LG_E * LG_THREADS / 32]
-    __shared__ float redf[LG_WAVES];
-    __shared__ double redd[LG_WAVES];
-    __shared__ int redi[LG_WAVES];
-    __shared__ int apply_ts_rule;
-    const LogitJob job = jobs[blockIdx.x];
-    float * L = logits + (size_t) job.row * n_vocab;
-    const int f = job.flags;
-    const int tid = threadIdx.x;
-    TokenOut res;
-    res.nosp_prob = 0.0f;
-    float v[LG_E - LG_ES];
-    // fn(i, x) over this thread's elements i < n_vocab in ascending order (x by reference)
-    auto visit = [&](auto && fn) {
-        for (int k = 0; k < LG_ES; ++k) {
-            const int i = tid + k * LG_THREADS;
-            if (i < n_vocab) fn(i, sl[k * LG_THREADS + tid]);
-        }
-#pragma unroll
-        for (int k = LG_ES; k < LG_E; ++k) {
-            const int i = tid + k * LG_THREADS;
-            if (i < n_vocab) fn(i, v[k - LG_ES]);
-        }
-    };
-    for (int k = 0; k < LG_ES; ++k) {
-        const int i = tid + k * LG_THREADS;
-        sl[k * LG_THREADS + tid] = i < n_vocab ? L[i] : -INFINITY;
-    }
-#pragma unroll
-    for (int k = LG_ES; k < LG_E; ++k) {
-        const int i = tid + k * LG_THREADS;
-        v[k - LG_ES] = i < n_vocab ? L[i] : -INFINITY;
-    }
-    for (int w = tid; w < LG_E * LG_THREADS / 32; w += LG_THREADS) sup[w] = 0u;
-    __syncthreads();
-    for (int j = tid; j < vi.n_suppress; j += LG_THREADS) {
-        const int t = vi.suppress_list[j];
-        atomicOr(&sup[t >> 5], 1u << (t & 31));
-    }
-
-    // no_speech probability of the raw logits (whisper.cpp:7186-7196)
-    if (f & LF_NEED_NOSP) {
-        float mx = -INFINITY;
-        visit([&](int, float & x) { mx = fmaxf(mx, x); });
-        mx = block_max(mx, redf);
-        double s = 0.0;
-        visit([&](int, float & x) {
-            if (x > -INFINITY) s += (double) expf(x - mx);
-        });
-        s = block_sum(s, redd);
-        const float lse = logf((float) s) + mx;
-        res.nosp_prob = expf(L[vi.nosp] - lse);
-    }
-    __syncthreads();  // the suppress bitmap is complete
-
-    // temperature + suppression masks (whisper.cpp:6200-6330), then the suppress list
-    visit([&](int i, float & x) {
-        float y = x;
-        if (job.temperature > 0.0f) y /= job.temperature;
-        if (masked(i, f, job.ts_min, vi)) y = -INFINITY;
-        if ((sup[i >> 5] >> (i & 31)) & 1u) y = -INFINITY;
-        x = y;
-    });
-
-    // log_softmax (whisper_compute_logprobs, 6137-6157)
-    float mx = -INFINITY;
-    visit([&](int, float & x) { mx = fmaxf(mx, x); });
-    mx = block_max(mx, redf);
-    double s = 0.0;
-    visit([&](int, float & x) {
-        if (x > -INFINITY) s += (double) expf(x - mx);
-    });
-    s = block_sum(s, redd);
-    const float lse = logf((float) s) + mx;
-
-    // timestamp mass vs best text token (6337-6361)
-    float ts_max = -INFINITY, tx_max = -INFINITY;
-    visit([&](int i, float & x) {
-        const float lp = x > -INFINITY ? x - lse : -INFINITY;
-        if (i >= vi.beg) {
-            ts_max = fmaxf(ts_max, lp);
-            tsl[i - vi.beg] = lp;
-        } else {
-            tx_max = fmaxf(tx_max, lp);
-        }
-    });
-    ts_max = block_max(ts_max, redf);  // its barriers also publish tsl
-    tx_max = block_max(tx_max, redf);
-    double ts_sum = 0.0;
-    for (int i = tid; i < n_vocab - vi.beg; i += LG_THREADS) {  // k_process_logits' partition of the range
-        const float lp = tsl[i];
-        if (lp > -INFINITY) ts_sum += (double) expf(lp - ts_max);
-    }
-    ts_sum = block_sum(ts_sum, redd);
-    if (tid == 0) {
-        const float ts_lp = ts_sum > 0.0 ? logf((float) ts_sum) + ts_max : -INFINITY;
-        apply_ts_rule = ts_lp > tx_max;
-    }
-    __syncthreads();
-    const bool ts_rule = apply_ts_rule;
-
-    // probs + greedy pick (whisper_compute_probs 6159-6171, whisper_sample_token 6460-6517); the
-    // processed row goes back to the logits buffer
-    float best = -1.0f;
-    int best_i = 0x7fffffff;
-    float tbest = -1.0f;
-    int tbest_i = 0x7fffffff;
-    double ts_psum = 0.0;
-    visit([&](int i, float & x) {
-        if (ts_rule && i < vi.beg) x = -INFINITY;
-        L[i] = x;
-        const float lp = x > -INFINITY ? x - lse : -INFINITY;
-        const float p = x == -INFINITY ? 0.0f : expf(lp);
-        if (lp_out) lp_out[(size_t) blockIdx.x * n_vocab + i] = lp;
-        if (pr_out) pr_out[(size_t) blockIdx.x * n_vocab + i] = p;
-        if (p > best) { best = p; best_i = i; }
-        if (i >= vi.beg) {
-            ts_psum += (double) p;
-            if (p > tbest) { tbest = p; tbest_i = i; }
-        }
-    });
-    block_argmax(best, best_i, redf, redi);
-    block_argmax(tbest, tbest_i, redf, redi);
-    ts_psum = block_sum(ts_psum, redd);
-    if (tid == 0) {
-        res.id = best > 0.0f ? best_i : 0;
-        res.p = best > 0.0f ? best : 0.0f;
-        res.plog = L[res.id] > -INFINITY ? L[res.id] - lse : -INFINITY;
-        res.tid = tbest > 0.0f ? tbest_i : 0;
-        const double max_ts = tbest > 0.0f ? (double) tbest : 0.0;
-        res.pt = (float) (max_ts / (ts_psum + 1e-10));
-        res.ptsum = (float) ts_psum;
-        if (res.id >= vi.beg) {
-            res.tid = res.id;
-            res.pt = res.p;
-        }
-        res.pad_ = 0.0f;
-        outv[blockIdx.x] = res;
-    }
-}
-constexpr size_t LG_REG_LDS = ((size_t) LG_ES * LG_THREADS + LG_TS + LG_E * LG_THREADS / 32) * 4;
-
 void process_logits(hipStream_t s, float * logits, int n_vocab, const LogitJob * jobs_dev, int n_jobs,
                     const VocabInfo & vi, TokenOut * out_dev, float * logprobs_out, float * probs_out) {
     if (n_jobs <= 0) return;
-    static const bool reg = getenv("OWK_LOGITS_REG") && atoi(getenv("OWK_LOGITS_REG")) == 1;  // A/B pending
-    if (reg && n_vocab <= LG_E * LG_THREADS && n_vocab - vi.beg <= LG_TS && vi.beg >= 0)
-        OWK_LAUNCH(k_process_logits_reg, dim3(n_jobs), dim3(LG_THREADS), LG_REG_LDS, s, logits, n_vocab, jobs_dev, vi,
-                   out_dev, logprobs_out, probs_out);
-    else
-        OWK_LAUNCH(k_process_logits, dim3(n_jobs), dim3(LG_THREADS), 0, s, logits, n_vocab, jobs_dev, vi, out_dev,
-                   logprobs_out, probs_out);
+    OWK_LAUNCH(k_process_logits, dim3(n_jobs), dim3(LG_THREADS), 0, s, logits, n_vocab, jobs_dev, vi, out_dev,
+                       logprobs_out, probs_out);
 }
 
 } // namespace owk
