@@ -70,7 +70,8 @@ WHISPER_API const uint16_t * owk_debug_gelu_table(void);
 /* out[M][N] = A[M][K] . W[N][K]^T (f16 bits in, f32 out) through the engine's GEMM dispatch */
 WHISPER_API int owk_debug_gemm(int device, int M, int N, int K, const uint16_t * a, const uint16_t * w, float * out);
 // one large-tile epilogue mode through the 128x128 and 256x256 kernels on the same random operands: max |diff|
-// (mode | 0x800: the 8-phase 256x256 kernel instead of the 4-slot ring one)
+// (mode | 0x800: the 8-phase 256x256 kernel instead of the 4-slot ring one; | 0x1000 / 0x2000: the 64x64 /
+// 32x32 ring tile of mid-size GEMMs against the 128x128 tile)
 WHISPER_API double owk_debug_gemm_epi_diff(int device, int mode, int M, int N, int K, int d, int T);
 /* average microseconds per launch of `iters` back-to-back engine GEMMs (epilogue `mode`, zero data) */
 /* test hook (host only): the DTW alignment of captured alignment-head attention
@@ -108,6 +109,7 @@ WHISPER_API int owk_debug_gemm_quant2(int device, int fmt, int M, int N, int K, 
  * row dequantization of the token embedding (deq [N][K], may be NULL); 0 on success */
 WHISPER_API int owk_debug_kquant(int fmt, int N, int K, const uint8_t * w_blocks, uint16_t * wi, float * dwt, float * deq);
 /* mode | 0x100: force the 128x128 large-GEMM kernel; | 0x400: 5-slot ring variant of the 256x256 kernel;
+ * | 0x800: the 8-phase 256x256 kernel; | 0x1000 / 0x2000: the 64x64 / 32x32 ring tile;
  * | 0x200: uniform random operands (else zeros) */
 WHISPER_API double owk_debug_gemm_bench(int device, int mode, int M, int N, int K, int iters);
 /* the decoder's per-layer matmul + residual/LayerNorm chain (no attention) of a large-v3-shaped model,

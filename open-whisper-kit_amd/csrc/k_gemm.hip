@@ -356,6 +356,120 @@ __global__ __launch_bounds__(256, 2) void k_gemm_big(int M, int N, int K, const 
 }
 
 // ---------------------------------------------------------------------------------
+// 64x64 block tile for mid-size GEMMs whose 128x128 grid leaves most CUs idle (SortFormer
+// chunk passes: M = a few hundred rows, N = 192..2048; small Whisper models at one clip).
+// Those launches are latency-bound: k_gemm_big keeps one 64-deep K stage in flight, so every
+// stage pays a full load round trip (M 400 x N 512 x K 512: 16 blocks, 19 us). Here K advances
+// in 32-deep steps through an 8-slot LDS ring (slot = 64 x 32 f16 of A + of W = 8 KB, 64 KB in
+// all, two blocks per CU) with 7 steps in flight: top of step j: s_waitcnt vmcnt (this wave's
+// step-j DMA landed, later steps stay in flight) -> s_barrier (every wave's step-j DMA landed,
+// every wave done with step j-1) -> issue step j+7 into step j-1's slot -> 4 MFMAs per wave.
+// 4 waves (2 x 2) of 32 x 32. Same MFMA sequence per output as k_gemm_big (32-deep K steps in
+// ascending order): bit-identical results. LDS image as k_gemm_256 (64-B rows, 16-B chunk c of
+// row r at c ^ ((r >> 2) & 3), swizzle applied on the global source address).
+// ---------------------------------------------------------------------------------
+constexpr int GM_K = 32, GM_SLOTS = 8;
+
+// TM = 64: 4 waves (2 x 2) of 32 x 32; TM = 32 (twice the blocks of a narrow grid, for launches
+// whose 64x64 grid still leaves CUs idle): 2 waves of 16 x 32. TM * 4 threads: thread t stages row
+// t >> 2 of A and of W.
+template <int MODE, int TM>
+__global__ __launch_bounds__(TM * 4) void k_gemm_mid(int M, int N, int K, const _Float16 * __restrict__ A, int lda,
+                                                    const _Float16 * __restrict__ W, int ldw, EpiParams ep) {
+    constexpr int AHEAD = GM_SLOTS - 1;  // steps in flight beyond the one being computed
+    constexpr int OP = TM * GM_K * 2;    // one operand of one K-step
+    constexpr int WR = TM / 32;          // 16-row MFMA tiles per wave
+    __shared__ __attribute__((aligned(1024))) char smem[GM_SLOTS * 2 * OP];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = TM == 64 ? wave >> 1 : wave, wn = TM == 64 ? wave & 1 : 0;
+
+    const int nbn = (N + TM - 1) / TM;
+    const int nb = gridDim.x;
+    int bid = blockIdx.x;
+    {  // XCD-aware order (k_gemm_big): a contiguous run of tiles per XCD
+        const int xcd = bid & 7, q = nb >> 3, rr = nb & 7;
+        const int base = xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q;
+        bid = base + (bid >> 3);
+    }
+    const int bm = bid / nbn, bn = bid - bm * nbn;
+    const int m0 = bm * TM, n0 = bn * TM;
+
+    // staging: thread t carries row t >> 2, 16-B chunk t & 3 of A and of W; wave w's 64 lanes
+    // write rows 16w .. 16w+15 lane-linearly (1 KB)
+    const int srow = tid >> 2;
+    const int sch = ((lane & 3) ^ ((srow >> 2) & 3)) * 8;
+    const _Float16 * ga = A + (size_t) min(m0 + srow, M - 1) * lda + sch;
+    const _Float16 * gw = W + (size_t) min(n0 + srow, N - 1) * ldw + sch;
+    auto stage = [&](int slot, int k0) {
+        char * sA = smem + slot * 2 * OP + wave * 1024;
+        __builtin_amdgcn_global_load_lds((const void *) (ga + k0), (lds_ptr_t) sA, 16, 0, 0);
+        __builtin_amdgcn_global_load_lds((const void *) (gw + k0), (lds_ptr_t) (sA + OP), 16, 0, 0);
+    };
+
+    const int g = lane >> 4, l16 = lane & 15;
+    int offA[WR], offB[2];
+#pragma unroll
+    for (int i = 0; i < WR; ++i) {
+        const int ra = wm * 16 * WR + i * 16 + l16;
+        offA[i] = ra * 64 + ((g ^ ((ra >> 2) & 3)) << 4);
+    }
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const int rb = wn * 32 + j * 16 + l16;
+        offB[j] = OP + rb * 64 + ((g ^ ((rb >> 2) & 3)) << 4);
+    }
+    floatx4 acc[WR][2];
+#pragma unroll
+    for (int i = 0; i < WR; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+    const int nk = K / GM_K;
+#pragma unroll
+    for (int i = 0; i < AHEAD; ++i)
+        if (i < nk) stage(i, i * GM_K);
+    int slot = 0;
+    for (int j = 0; j < nk; ++j) {
+        // 2 loads per step per thread: steps j+1 .. j+later (issued) may stay in flight
+        const int later = min(AHEAD - 1, nk - 1 - j);
+        switch (later) {
+            case 6: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
+            case 5: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
+            case 4: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+            case 3: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+            case 2: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+            case 1: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+            default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+        }
+        __builtin_amdgcn_s_barrier();
+        if (j + AHEAD < nk) stage(slot == 0 ? GM_SLOTS - 1 : slot - 1, (j + AHEAD) * GM_K);  // step j-1's slot
+        const char * sA = smem + slot * 2 * OP;
+        half8 a[WR], b[2];
+#pragma unroll
+        for (int i = 0; i < WR; ++i) a[i] = *(const half8 *) (sA + offA[i]);
+#pragma unroll
+        for (int i = 0; i < 2; ++i) b[i] = *(const half8 *) (sA + offB[i]);
+#pragma unroll
+        for (int i = 0; i < WR; ++i)
+#pragma unroll
+            for (int jj = 0; jj < 2; ++jj)
+                acc[i][jj] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[i], b[jj], acc[i][jj], 0, 0, 0);
+        slot = slot + 1 == GM_SLOTS ? 0 : slot + 1;
+    }
+
+#pragma unroll
+    for (int i = 0; i < WR; ++i)
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj) {
+            const int c = n0 + wn * 32 + jj * 16 + l16;
+            const int r0 = m0 + wm * 16 * WR + i * 16 + 4 * g;
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+                if (r0 + e < M && c < N) epi_store<MODE>(ep, r0 + e, c, acc[i][jj][e]);
+        }
+}
+
+// ---------------------------------------------------------------------------------
 // 256x256 block tile for the large encoder / cross-KV GEMMs (M = clips x 1500 rows).
 // 8 waves (2 in M x 4 in N), each 128x64 of the output = 8 x 4 MFMA 16x16x32 tiles
 // (128 accumulators). K advances in 32-deep steps through a 4-slot LDS ring
@@ -1253,6 +1367,18 @@ template <int MODE> struct LaunchBig {
         OWK_LAUNCH(k_gemm_big<MODE>, dim3(nbm * nbn), dim3(256), 0, s, M, N, K, A, lda, W, ldw, ep);
     }
 };
+static int mid_tile(int M, int N);
+template <int MODE> struct LaunchMid {
+    static void run(hipStream_t s, int M, int N, int K, const _Float16 * A, int lda, const _Float16 * W, int ldw,
+                    const EpiParams & ep) {
+        if (mid_tile(M, N) == 32)
+            OWK_LAUNCH((k_gemm_mid<MODE, 32>), dim3(((M + 31) / 32) * ((N + 31) / 32)), dim3(128), 0, s, M, N, K, A, lda, W,
+                       ldw, ep);
+        else
+            OWK_LAUNCH((k_gemm_mid<MODE, 64>), dim3(((M + 63) / 64) * ((N + 63) / 64)), dim3(256), 0, s, M, N, K, A, lda, W,
+                       ldw, ep);
+    }
+};
 // 256x256 kernel selection: OWK_GEMM256 (default 8 = k_gemm_8p; 1 the 4-slot ring k_gemm_256, 5 its
 // 5-slot variant, 0 forces the 128x128 tile), overridden per
 // thread by the debug hooks (gemm_set_256) so a hook never changes another thread's engine
@@ -1976,12 +2102,33 @@ int gemm_set_256(int on) {
     t_gemm256 = on;
     return prev;
 }
-static bool use_256(int M, int N, int K) { return gemm256_mode() && M >= 2048 && N >= 1024 && K % G2_K == 0; }
+static bool use_256(int M, int N, int K) {
+    const int m = gemm256_mode();
+    return m && m != GEMM_MID_FORCED && M >= 2048 && N >= 1024 && K % G2_K == 0;
+}
+// the 64x64 ring tile where the 128x128 grid would not give every CU a block (OWK_GEMM_MID=0 or
+// the override 0 keep the 128x128 tile; the override GEMM_MID_FORCED takes the 64x64 tile always)
+static bool use_mid(int M, int N) {
+    const int m = gemm256_mode();
+    if (m == 0) return false;
+    if (m == GEMM_MID_FORCED || m == GEMM_MID32_FORCED) return true;
+    static const int env = env_int("OWK_GEMM_MID", 1);
+    return env && ((M + GB_M - 1) / GB_M) * ((N + GB_N - 1) / GB_N) < 256;
+}
+// tile edge of the ring kernel: 32 where the 64x64 grid would still leave CUs idle (SortFormer chunk
+// shapes at M = 413, tests/test_gpu_kernels.py::test_gemm_mid_speed: 32x32 4.6-15.7 us against 64x64
+// 6.2-21.7 us, N = 2048 included, whose 64x64 grid is 224 blocks; profiles/r03h_gemm_mid_speed.txt)
+static int mid_tile(int M, int N) {
+    const int m = gemm256_mode();
+    if (m == GEMM_MID_FORCED || m == GEMM_MID32_FORCED) return m == GEMM_MID32_FORCED ? 32 : 64;
+    return ((M + 63) / 64) * ((N + 63) / 64) < 256 ? 32 : 64;
+}
 
 void gemm_f16(hipStream_t s, int mode, int M, int N, int K, const _Float16 * A, int lda, const _Float16 * W, int ldw,
               const EpiParams & ep) {
     check_shape(M, N, K, lda, ldw, GB_K);
     if (use_256(M, N, K)) dispatch_mode<Launch256>(mode, s, M, N, K, A, lda, W, ldw, ep);
+    else if (use_mid(M, N)) dispatch_mode<LaunchMid>(mode, s, M, N, K, A, lda, W, ldw, ep);
     else dispatch_mode<LaunchBig>(mode, s, M, N, K, A, lda, W, ldw, ep);
 }
 

@@ -60,8 +60,11 @@ struct EpiParams {
 void gemm_f16(hipStream_t s, int mode, int M, int N, int K, const _Float16 * A, int lda,
               const _Float16 * W, int ldw, const EpiParams & ep);
 // skinny (decode steps, M <= 64): split-K across the waves of a block, LDS reduction
-// this thread's 256x256-kernel override (-1 none, 0 force 128x128, 1 on, 5 the 5-slot ring);
+// this thread's 256x256-kernel override (-1 none, 0 force 128x128, 1 on, 5 the 5-slot ring, 8 the
+// 8-phase kernel, GEMM_MID_FORCED / GEMM_MID32_FORCED the 64x64 / 32x32 ring tile for every shape
+// below the 256x256 path);
 // returns the previous override (debug hooks restore it with GemmOverride)
+constexpr int GEMM_MID_FORCED = 16, GEMM_MID32_FORCED = 17;
 int gemm_set_256(int on);
 struct GemmOverride {
     int prev;

@@ -1185,11 +1185,12 @@ __global__ static void k_fill_rand_f16(_Float16 * p, size_t n, uint32_t seed) {
 }
 
 // mode bit 0x100: force the 128x128 large-GEMM kernel; bit 0x400: the 5-slot ring variant of the
-// 256x256 kernel; bit 0x200: random operands
+// 256x256 kernel; 0x800: the 8-phase kernel; 0x1000 / 0x2000: the 64x64 / 32x32 ring tile; bit 0x200:
+// random operands
 double owk_debug_gemm_bench(int device, int mode, int M, int N, int K, int iters) {
-    const bool force128 = mode & 0x100, rnd = mode & 0x200, ring5 = mode & 0x400, p8 = mode & 0x800;
+    const bool force128 = mode & 0x100, rnd = mode & 0x200, ring5 = mode & 0x400, p8 = mode & 0x800, mid = mode & 0x1000, mid32 = mode & 0x2000;
     mode &= 0xFF;
-    GemmOverride ov(force128 ? 0 : ring5 ? 5 : p8 ? 8 : 1);
+    GemmOverride ov(force128 ? 0 : ring5 ? 5 : p8 ? 8 : mid ? GEMM_MID_FORCED : mid32 ? GEMM_MID32_FORCED : 1);
     try {
         OWK_HIP_CHECK(hipSetDevice(device));
         hipStream_t s;
@@ -1577,7 +1578,8 @@ double owk_debug_attn_cross(int device, int which, int R, int H, int T, int n_ze
 // output the mode writes (f32 and f16 images), or -1 on error. d / T: EPI_QKV_ENC / EPI_KV_CROSS /
 // EPI_CONV2 shape parameters (N = 3d / 2d / d).
 double owk_debug_gemm_epi_diff(int device, int mode, int M, int N, int K, int d, int T) {
-    const int large = (mode & 0x800) ? 8 : 1;  // 0x800: the 8-phase kernel against the 128x128 one
+    // 0x800: the 8-phase kernel against the 128x128 one; 0x1000 / 0x2000: the 64x64 / 32x32 ring tile
+    const int large = (mode & 0x800) ? 8 : (mode & 0x1000) ? GEMM_MID_FORCED : (mode & 0x2000) ? GEMM_MID32_FORCED : 1;
     mode &= 0xFF;
     try {
         OWK_HIP_CHECK(hipSetDevice(device));

@@ -133,3 +133,39 @@ def test_gemm256_epilogue_matches_128(case, kern):
     assert diff >= 0
     assert diff <= 1e-6, f"{case}: epilogues differ by {diff}"
 
+
+@pytest.mark.parametrize("kern", [0x1000, 0x2000], ids=["mid64", "mid32"])
+@pytest.mark.parametrize("case", sorted(_EPI_CASES))
+def test_gemm_mid_matches_128(case, kern):
+    """The 64x64 ring tile (k_gemm_mid: mid-size GEMMs, e.g. SortFormer chunk passes) runs the same
+    MFMA sequence per output as the 128x128 tile: every epilogue output must be bit-identical.
+    Ragged M (not a multiple of 64) and N (f16_ragged) exercise the edge tiles."""
+    mode, N, d, T = _EPI_CASES[case]
+    L = owk.load()
+    L.owk_debug_gemm_epi_diff.restype = C.c_double
+    L.owk_debug_gemm_epi_diff.argtypes = [C.c_int] * 7
+    M = 1500 if T else 413
+    diff = L.owk_debug_gemm_epi_diff(0, mode | kern, M, N, 512, d, T)
+    print(f"{case} {kern:#x}: max|mid - 128| = {diff:.3g}")
+    assert diff == 0, f"{case}: epilogues differ by {diff}"
+
+
+def test_gemm_mid_speed():
+    """Device time of the SortFormer chunk-pass GEMM shapes (M = 413 rows) through the 64x64 ring
+    tile and the 128x128 tile, printed for the record; the ring tile must not be slower."""
+    L = owk.load()
+    L.owk_debug_gemm_bench.restype = C.c_double
+    L.owk_debug_gemm_bench.argtypes = [C.c_int] * 6
+    worse = []
+    for mode, N, K in ((9, 1536, 512), (10, 2048, 512), (11, 512, 2048), (2, 512, 512), (9, 192, 512),
+                       (12, 768, 192), (2, 192, 768)):
+        t_mid = min(L.owk_debug_gemm_bench(0, mode | 0x1000 | 0x200, 413, N, K, 50) for _ in range(3))
+        t_32 = min(L.owk_debug_gemm_bench(0, mode | 0x2000 | 0x200, 413, N, K, 50) for _ in range(3))
+        t_big = min(L.owk_debug_gemm_bench(0, mode | 0x100 | 0x200, 413, N, K, 50) for _ in range(3))
+        print(f"M=413 N={N} K={K} mode {mode}: 64x64 ring {t_mid:.2f} us, 32x32 ring {t_32:.2f} us, "
+              f"128x128 {t_big:.2f} us")
+        assert t_mid > 0 and t_32 > 0 and t_big > 0
+        t_mid = min(t_mid, t_32)
+        if t_mid > 1.1 * t_big:
+            worse.append((N, K))
+    assert not worse, worse
