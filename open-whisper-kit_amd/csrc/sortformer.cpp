@@ -250,7 +250,7 @@ struct sortformer_context {
     bool quant = false; // any linear quantized: producers also keep their f32 outputs
 
     // position-embedding cache (ref:140-142, 1127-1136): f16 table of the current n_pos
-    int pos_n = 0;
+    int pos_T = 0;  // positions pos_T-1 .. -(pos_T-1) in pos16 / pos32
     DevBuf pos16;
 
     // scratch (grown on demand)
@@ -604,31 +604,36 @@ int run_preenc(sortformer_context * ctx, const float * mel, int ld, int c0, int 
 }
 
 // NeMo relative positions T-1 .. -(T-1), interleaved sin/cos (ref:1050-1066), as F16 (the
-// activation rounding of linear_pos's F16 mul_mat); cached per n_pos like the reference
-void ensure_pos(sortformer_context * ctx, int T) {
-    const int n_pos = 2 * T - 1, d = ctx->d_model;
-    if (ctx->pos_n == n_pos) return;
-    std::vector<uint16_t> pe((size_t) n_pos * d);
-    std::vector<float> pe32((size_t) n_pos * d);  // quantized linear_pos: the f32 table is its operand
-    const int half = d / 2;
-    for (int p = 0; p < n_pos; ++p) {
-        const float pos = (float) (T - 1 - p);
-        for (int j = 0; j < half; ++j) {
-            const float freq = 1.0f / powf(10000.0f, (2.0f * j) / (float) d);
-            const float angle = pos * freq;
-            pe32[(size_t) p * d + 2 * j] = sinf(angle);
-            pe32[(size_t) p * d + 2 * j + 1] = cosf(angle);
+// activation rounding of linear_pos's F16 mul_mat). A row depends only on its position, so one table
+// for the longest T seen (rounded up to 64) serves every shorter T as a contiguous row range: returns
+// the row of position T-1. (The reference rebuilds it per n_pos; here a streaming pass whose length
+// changes no longer recomputes 0.4 M transcendentals on the host and waits for the upload.)
+int ensure_pos(sortformer_context * ctx, int T) {
+    if (T > ctx->pos_T) {
+        const int Tc = (T + 63) / 64 * 64, n_pos = 2 * Tc - 1, d = ctx->d_model;
+        std::vector<uint16_t> pe((size_t) n_pos * d);
+        std::vector<float> pe32((size_t) n_pos * d);  // quantized linear_pos: the f32 table is its operand
+        const int half = d / 2;
+        for (int p = 0; p < n_pos; ++p) {
+            const float pos = (float) (Tc - 1 - p);
+            for (int j = 0; j < half; ++j) {
+                const float freq = 1.0f / powf(10000.0f, (2.0f * j) / (float) d);
+                const float angle = pos * freq;
+                pe32[(size_t) p * d + 2 * j] = sinf(angle);
+                pe32[(size_t) p * d + 2 * j + 1] = cosf(angle);
+            }
         }
+        for (size_t i = 0; i < pe.size(); ++i) pe[i] = f32_to_f16_host(pe32[i]);
+        _Float16 * dst = grow<_Float16>(ctx->pos16, pe.size());
+        OWK_HIP_CHECK(hipMemcpyAsync(dst, pe.data(), pe.size() * 2, hipMemcpyHostToDevice, ctx->stream));
+        if (ctx->quant) {
+            float * d32 = grow<float>(ctx->pos32, pe32.size());
+            OWK_HIP_CHECK(hipMemcpyAsync(d32, pe32.data(), pe32.size() * 4, hipMemcpyHostToDevice, ctx->stream));
+        }
+        OWK_HIP_CHECK(hipStreamSynchronize(ctx->stream));  // pe is a host temporary
+        ctx->pos_T = Tc;
     }
-    for (size_t i = 0; i < pe.size(); ++i) pe[i] = f32_to_f16_host(pe32[i]);
-    _Float16 * dst = grow<_Float16>(ctx->pos16, pe.size());
-    OWK_HIP_CHECK(hipMemcpyAsync(dst, pe.data(), pe.size() * 2, hipMemcpyHostToDevice, ctx->stream));
-    if (ctx->quant) {
-        float * d32 = grow<float>(ctx->pos32, pe32.size());
-        OWK_HIP_CHECK(hipMemcpyAsync(d32, pe32.data(), pe32.size() * 4, hipMemcpyHostToDevice, ctx->stream));
-    }
-    OWK_HIP_CHECK(hipStreamSynchronize(ctx->stream));  // pe is a host temporary
-    ctx->pos_n = n_pos;
+    return ctx->pos_T - T;
 }
 
 // independent sequences stacked along the rows of one buffer: (first row, length). Row-wise
@@ -654,7 +659,7 @@ float * run_conformer(sortformer_context * ctx, float * x, const Segs & segs, in
     _Float16 * ao = grow<_Float16>(ctx->s_ao, (size_t) T * d);
     float * cv = grow<float>(ctx->s_cv, (size_t) T * 2 * d);
     _Float16 * g = grow<_Float16>(ctx->s_g, (size_t) T * d);
-    ensure_pos(ctx, Tmax);
+    const size_t p0 = (size_t) ensure_pos(ctx, Tmax) * d;  // table row of position Tmax-1
     const float eps = 1e-5f;
     for (int il = 0; il <= last; ++il) {
         const ConfLayer & L = ctx->conf[il];
@@ -680,7 +685,7 @@ float * run_conformer(sortformer_context * ctx, float * x, const Segs & segs, in
             sf_lin(ctx, EPI_BIAS_F32, T, 3 * d, d, xn, xn32, d, L.qkv, e);
             EpiParams ep;
             ep.out32 = P; ep.ldo = d;
-            sf_lin(ctx, EPI_F32, 2 * Tmax - 1, d, d, ctx->pos16.as<_Float16>(), L.pos.quant() ? ctx->pos32.as<float>() : nullptr,
+            sf_lin(ctx, EPI_F32, 2 * Tmax - 1, d, d, ctx->pos16.as<_Float16>() + p0, L.pos.quant() ? ctx->pos32.as<float>() + p0 : nullptr,
                    d, L.pos, ep);
             // positions Tb-1 .. -(Tb-1) of a shorter sequence are rows Tmax-Tb .. of the table
             float * ao32 = f32_for(ctx, L.out, ctx->s_ao32, (size_t) T * d);
