@@ -228,12 +228,16 @@ void to_f16(hipStream_t s, const float * x, size_t n, _Float16 * out) {
 // ---------------------------------------------------------------------------------
 // attention (ref:1170-1235 relative-position MHSA, ref:1470-1503 transformer MHA)
 //
-// One block per (head, 16 query rows). Keys stream through LDS in tiles of 64; the score
-// rows [16][T] stay in LDS for the softmax and the P.V pass. The relative-position term
-// uses the Transformer-XL shift in closed form: row i, key j reads P[T-1-i+j] (the
-// pad/roll/view of ref:1203-1216), so the 64 keys of a tile need 79 consecutive P rows.
+// One block per (head, 8 query rows): 8 heads x T/8 blocks fill the chip at chunk-pass lengths
+// (T ~ 400), where 16-row blocks left every CU a single block and no latency hiding. Keys stream
+// through LDS in tiles of 64; each tile's global loads are issued into registers one tile ahead
+// (they fly while the current tile is computed). The score rows [8][T] stay in LDS for the softmax
+// and the P.V pass (whose V tiles are prefetched the same way, the first one under the softmax).
+// The relative-position term uses the Transformer-XL shift in closed form: row i, key j reads
+// P[T-1-i+j] (the pad/roll/view of ref:1203-1216), so the 64 keys of a tile need 71 consecutive
+// P rows. Per-output arithmetic is independent of the tiling (same sums in the same order).
 // ---------------------------------------------------------------------------------
-constexpr int AQ = 16;   // query rows per block
+constexpr int AQ = 8;    // query rows per block
 constexpr int AKT = 64;  // keys per tile
 
 template <int DH, bool REL>
@@ -243,44 +247,76 @@ __global__ __launch_bounds__(256) void k_sf_attn(const float * __restrict__ qkv,
                                                  float * __restrict__ out32, int Tpad) {
     extern __shared__ float smem[];
     constexpr int LDK = DH + 4;
+    constexpr int TPQ = 256 / AQ;                   // threads per query row
+    constexpr int KPT = AKT * DH / 256;             // K / V tile floats per thread
+    constexpr int PR = AQ - 1 + AKT;                // P rows per tile
+    constexpr int PPT = (PR * DH + 255) / 256;      // P tile floats per thread
     float * S = smem;                       // [AQ][Tpad]
     float * Ks = S + AQ * Tpad;             // [AKT][LDK]
-    float * Ps = Ks + AKT * LDK;            // [AQ - 1 + AKT][LDK]
+    float * Ps = Ks + AKT * LDK;            // [PR][LDK]
+    float * Qv = Ps + PR * LDK;             // [AQ][DH] Q + pos_bias_v (REL; LDS keeps the VGPRs for prefetch)
     const int h = blockIdx.x, q0 = blockIdx.y * AQ, tid = threadIdx.x;
     const int ldp = H * DH;
-    const int qi = tid >> 4, kk = tid & 15;
+    const int qi = tid / TPQ, kk = tid % TPQ;
     const int qrow = min(q0 + qi, T - 1);
 
-    float qu[DH], qv[REL ? DH : 1];
+    float kreg[KPT], preg[REL ? PPT : 1];
+    auto load_kv = [&](int j0, int col) {
+#pragma unroll
+        for (int u = 0; u < KPT; ++u) {
+            const int i = tid + 256 * u, r = i / DH, d = i - r * DH, j = j0 + r;
+            kreg[u] = j < T ? qkv[(size_t) j * ldq + col + h * DH + d] : 0.0f;
+        }
+    };
+    auto store_kv = [&]() {
+#pragma unroll
+        for (int u = 0; u < KPT; ++u) {
+            const int i = tid + 256 * u, r = i / DH, d = i - r * DH;
+            Ks[r * LDK + d] = kreg[u];
+        }
+    };
+    auto load_p = [&](int j0) {
+        const int pbase = T - 1 - (q0 + AQ - 1) + j0;
+#pragma unroll
+        for (int u = 0; u < PPT; ++u) {
+            const int i = tid + 256 * u, r = i / DH, d = i - r * DH, p = pbase + r;
+            preg[u] = (i < PR * DH && p >= 0 && p < 2 * T - 1) ? P[(size_t) p * ldp + h * DH + d] : 0.0f;
+        }
+    };
+    auto store_p = [&]() {
+#pragma unroll
+        for (int u = 0; u < PPT; ++u) {
+            const int i = tid + 256 * u, r = i / DH, d = i - r * DH;
+            if (i < PR * DH) Ps[r * LDK + d] = preg[u];
+        }
+    };
+
+    load_kv(0, kcol);
+    if constexpr (REL) load_p(0);
+    float qu[DH];
 #pragma unroll
     for (int d = 0; d < DH; ++d) {
         const float q = qkv[(size_t) qrow * ldq + h * DH + d];
-        if (REL) {
-            qu[d] = q + ub[h * DH + d];  // Q_u = Q + pos_bias_u (ggml_add, ref:1185)
-            qv[d] = q + vb[h * DH + d];
-        } else {
-            qu[d] = q;
-        }
+        qu[d] = REL ? q + ub[h * DH + d] : q;  // Q_u = Q + pos_bias_u (ggml_add, ref:1185)
     }
+    if constexpr (REL)
+        for (int i = tid; i < AQ * DH; i += 256) {
+            const int r = i / DH, d = i - r * DH;
+            Qv[i] = qkv[(size_t) min(q0 + r, T - 1) * ldq + h * DH + d] + vb[h * DH + d];
+        }
 
     for (int j0 = 0; j0 < T; j0 += AKT) {
-        for (int i = tid; i < AKT * DH; i += 256) {
-            const int r = i / DH, d = i - r * DH;
-            const int j = j0 + r;
-            Ks[r * LDK + d] = j < T ? qkv[(size_t) j * ldq + kcol + h * DH + d] : 0.0f;
-        }
-        const int pbase = T - 1 - (q0 + AQ - 1) + j0;
-        if (REL) {
-            for (int i = tid; i < (AQ - 1 + AKT) * DH; i += 256) {
-                const int r = i / DH, d = i - r * DH;
-                const int p = pbase + r;
-                Ps[r * LDK + d] = (p >= 0 && p < 2 * T - 1) ? P[(size_t) p * ldp + h * DH + d] : 0.0f;
-            }
-        }
+        __syncthreads();  // every thread done with the previous tile
+        store_kv();
+        if constexpr (REL) store_p();
         __syncthreads();
-#pragma unroll
-        for (int rr = 0; rr < AKT / 16; ++rr) {
-            const int kj = kk + 16 * rr;
+        if (j0 + AKT < T) {  // next tile in flight during this one
+            load_kv(j0 + AKT, kcol);
+            if constexpr (REL) load_p(j0 + AKT);
+        }
+#pragma unroll 1
+        for (int rr = 0; rr < AKT / TPQ; ++rr) {  // (unrolled, the LDS reads of both keys were hoisted: 256+ VGPRs)
+            const int kj = kk + TPQ * rr;
             const int j = j0 + kj;
             const float * kr = Ks + kj * LDK;
             float ac = 0.0f;
@@ -289,8 +325,9 @@ __global__ __launch_bounds__(256) void k_sf_attn(const float * __restrict__ qkv,
             float s;
             if (REL) {
                 const float * pr = Ps + ((AQ - 1 - qi) + kj) * LDK;
+                const float * qv = Qv + qi * DH;
                 float bd = 0.0f;
-#pragma unroll
+#pragma unroll 16
                 for (int d = 0; d < DH; ++d) bd += qv[d] * pr[d];
                 s = (ac + bd) * sc;  // ggml_add(ac, bd) then ggml_scale (ref:1222-1223)
             } else {
@@ -298,8 +335,9 @@ __global__ __launch_bounds__(256) void k_sf_attn(const float * __restrict__ qkv,
             }
             if (j < T) S[qi * Tpad + j] = s;
         }
-        __syncthreads();
     }
+    load_kv(0, vcol);  // the first V tile flies under the softmax
+    __syncthreads();
 
     // softmax per row (ggml_compute_forward_soft_max_f32: max, expf, double sum, * (float)(1/sum))
     const int lane = tid & 63, wave = tid >> 6;
@@ -320,21 +358,18 @@ __global__ __launch_bounds__(256) void k_sf_attn(const float * __restrict__ qkv,
         const float inv = (float) (1.0 / sum);
         for (int j = lane; j < T; j += 64) row[j] *= inv;
     }
-    __syncthreads();
 
     // out = P . V (ggml_mul_mat(attn, V), f32)
     constexpr int NOUT = (AQ * DH + 255) / 256;
     float acc[NOUT];
 #pragma unroll
     for (int m = 0; m < NOUT; ++m) acc[m] = 0.0f;
-    float * Vs = Ks;
+    const float * Vs = Ks;
     for (int j0 = 0; j0 < T; j0 += AKT) {
-        for (int i = tid; i < AKT * DH; i += 256) {
-            const int r = i / DH, d = i - r * DH;
-            const int j = j0 + r;
-            Vs[r * LDK + d] = j < T ? qkv[(size_t) j * ldq + vcol + h * DH + d] : 0.0f;
-        }
+        __syncthreads();  // softmax rows final / previous V tile consumed
+        store_kv();
         __syncthreads();
+        if (j0 + AKT < T) load_kv(j0 + AKT, vcol);
         const int nk = min(AKT, T - j0);
 #pragma unroll
         for (int m = 0; m < NOUT; ++m) {
@@ -347,7 +382,6 @@ __global__ __launch_bounds__(256) void k_sf_attn(const float * __restrict__ qkv,
                 acc[m] = a;
             }
         }
-        __syncthreads();
     }
 #pragma unroll
     for (int m = 0; m < NOUT; ++m) {
@@ -366,8 +400,8 @@ template <int DH, bool REL>
 static void launch_attn(hipStream_t s, const float * qkv, int ldq, int kcol, int vcol, int T, int H, const float * u,
                         const float * v, const float * P, float sc, _Float16 * out, float * out32) {
     const int Tpad = (T + AKT - 1) / AKT * AKT;
-    const size_t lds = ((size_t) AQ * Tpad + (size_t) AKT * (DH + 4) + (REL ? (size_t) (AQ - 1 + AKT) * (DH + 4) : 0)) *
-                       sizeof(float);
+    const size_t lds = ((size_t) AQ * Tpad + (size_t) AKT * (DH + 4) +
+                        (REL ? (size_t) (AQ - 1 + AKT) * (DH + 4) + (size_t) AQ * DH : 0)) * sizeof(float);
     if (lds > 160 * 1024) throw std::runtime_error("sf::attention: T too large for the LDS score tile");
     OWK_LAUNCH((k_sf_attn<DH, REL>), dim3(H, (T + AQ - 1) / AQ), dim3(256), lds, s, qkv, ldq, kcol, vcol, T, H,
                        u, v, P, sc, out, out32, Tpad);
