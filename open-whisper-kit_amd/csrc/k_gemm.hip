@@ -1531,11 +1531,60 @@ __global__ __launch_bounds__(256) void k_quantize_q8_f16(const TA * __restrict__
     }
 }
 
+// the same with 8 consecutive elements per lane (one 16/32-byte load, one 16-byte store; four lanes
+// per block, amax over the quad): the per-element version moved 2.3 TB/s (f32 rows, 163 us for the
+// 48000 x 1280 encoder operand, profiles/r03g_q5_kernel_stats.txt)
+template <typename TA>
+__global__ __launch_bounds__(256) void k_quantize_q8_f16_v8(const TA * __restrict__ A, int lda, int M, int K,
+                                                            _Float16 * __restrict__ q, float * __restrict__ dat, int mpad) {
+    const int nb = K >> 5;
+    const size_t total = (size_t) M * nb * 4;  // quads of 8 elements
+    const int sub = threadIdx.x & 3;
+    for (size_t i = (size_t) blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (size_t) gridDim.x * blockDim.x) {
+        const size_t blk = i >> 2;
+        const int r = (int) (blk / nb), b = (int) (blk - (size_t) r * nb);
+        const TA * src = A + (size_t) r * lda + b * 32 + sub * 8;
+        float x[8];
+        if constexpr (sizeof(TA) == 4) {
+            const float4 u = ((const float4 *) src)[0], v = ((const float4 *) src)[1];
+            x[0] = u.x; x[1] = u.y; x[2] = u.z; x[3] = u.w; x[4] = v.x; x[5] = v.y; x[6] = v.z; x[7] = v.w;
+        } else {
+            const half8 h = *(const half8 *) src;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) x[e] = (float) h[e];
+        }
+        float am = 0.0f;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) am = fmaxf(am, fabsf(x[e]));
+        am = fmaxf(am, __shfl_xor(am, 1, 64));
+        am = fmaxf(am, __shfl_xor(am, 2, 64));
+        const float dd = am / 127.f;
+        const float id = am != 0.0f ? 127.f / am : 0.0f;
+        half8 o;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] = (_Float16) (float) (int) (int8_t) rintf(x[e] * id);
+        *(half8 *) (q + (size_t) r * K + b * 32 + sub * 8) = o;
+        if (sub == 0) {
+            const int t = r & 127;
+            const int pr = (r & ~127) | (t & 64) | ((t & 15) << 2) | ((t >> 4) & 3);
+            dat[(size_t) b * mpad + pr] = (float) (_Float16) dd;
+        }
+    }
+}
+
 void quantize_q8_f16(hipStream_t s, const float * A32, const _Float16 * A16, int lda, int M, int K, _Float16 * q16,
                      float * dat, int mpad) {
     if (M <= 0) return;
     if (K % 32 || mpad < (M + 127) / 128 * 128) throw std::runtime_error("quantize_q8_f16: shape");
     const size_t blocks = (size_t) M * (K / 32);
+    if (lda % 8 == 0 && ((uintptr_t) (A32 ? (const void *) A32 : (const void *) A16) & 31) == 0 && ((uintptr_t) q16 & 15) == 0) {
+        const int grid = (int) std::min<size_t>((blocks * 4 + 255) / 256, 65536);
+        if (A32)
+            OWK_LAUNCH(k_quantize_q8_f16_v8<float>, dim3(grid), dim3(256), 0, s, A32, lda, M, K, q16, dat, mpad);
+        else
+            OWK_LAUNCH(k_quantize_q8_f16_v8<_Float16>, dim3(grid), dim3(256), 0, s, A16, lda, M, K, q16, dat, mpad);
+        return;
+    }
     const int grid = (int) std::min<size_t>((blocks * 32 + 255) / 256, 65536);
     if (A32)
         OWK_LAUNCH(k_quantize_q8_f16<float>, dim3(grid), dim3(256), 0, s, A32, lda, M, K, q16, dat, mpad);
