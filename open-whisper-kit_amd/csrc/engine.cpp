@@ -1046,8 +1046,12 @@ void Engine::step_post(const StepPost & post, const std::vector<LogitJob> & jobs
                 lg_lp_.alloc((size_t) n * nv * 4);
                 lp = lg_lp_.as<float>();
             }
+            bool any_nosp = false;
+            for (const LogitJob & j : jobs) any_nosp |= (j.flags & 256) != 0;  // LF_NEED_NOSP
+            lg_ws_.alloc(process_logits_ws_bytes(n));
             owk::process_logits(stream, logits_.as<float>(), nv, (const LogitJob *) (dv + o_jobs), n, vi,
-                                (TokenOut *) (post_out_d_.as<char>() + r_tok), lp, pr);
+                                (TokenOut *) (post_out_d_.as<char>() + r_tok), lp, pr, any_nosp, lg_ws_.ptr,
+                                lg_ws_.bytes);
             if (pr) OWK_HIP_CHECK(hipMemcpyAsync(probs_host, pr, (size_t) n * nv * 4, hipMemcpyDeviceToHost, stream));
             if (lp) OWK_HIP_CHECK(hipMemcpyAsync(logprobs_host, lp, (size_t) n * nv * 4, hipMemcpyDeviceToHost, stream));
         }

@@ -169,7 +169,7 @@ private:
 
     // decoder workspace
     DevBuf d_x_, d_xn_, d_q_, d_ao_, d_h_, d_xl_;
-    DevBuf logits_, lg_probs_, lg_lp_;
+    DevBuf logits_, lg_probs_, lg_lp_, lg_ws_;
     int dec_rows_cap_ = 0, dec_keys_cap_ = 0;
     PinnedBuf stg_;   // host image of the per-pass inputs
     DevBuf d_stg_;    // its device copy (fixed sections, see stage_layout)

@@ -300,11 +300,263 @@ void nosp_probs(hipStream_t s, const float * row0, int n_vocab, const int2 * req
     OWK_LAUNCH(k_nosp, dim3(n), dim3(LG_THREADS), 0, s, row0, n_vocab, req_dev, rmx, stride, nosp, out_dev);
 }
 
+// ---------------------------------------------------------------------------------
+// The same processing with every row split over LGS_B blocks (decode passes: 32 rows were 32 blocks
+// on 256 CUs, each sweeping a 207 KB row six times at one CU's fetch rate: 63 us per pass). Five
+// launches, each a short sweep of row / LGS_B, with per-block partials combined in fixed block order:
+//   mask    temperature + masks + suppress list (in place); block maxima of the row, of its
+//           timestamp range and of its text range
+//   sum     M = max of the block maxima; block double sum of exp(L - M)
+//   ts      (one block per row) lse = log(sum) + M; the timestamp-mass rule of 6337-6361 over the
+//           timestamp range; its decision and lse to the row record
+//   pick    the decision applied (text logits -inf, in place); logprobs / probs; block first-max of p,
+//           of the timestamp p, block double sum of the timestamp p
+//   final   the greedy record of whisper_sample_token from the partials
+// max(L_i - lse) = fl(max(L_i) - lse) (rounding is monotonic), so the range maxima of the masked
+// logits give the reference's ts_max / tx_max; argmax with first-index ties is order-independent;
+// the double sums differ from the one-block order only below double precision. Rows that need the
+// no-speech probability of the raw logits (prefill passes) take k_process_logits.
+// ---------------------------------------------------------------------------------
+constexpr int LGS_B = 16, LGS_T = 256, LGS_W = LGS_T / 64;
+struct LgPart {
+    float m, tsl, txl, best, tbest;
+    int best_i, tbest_i, pad;
+    double s, ts_psum;
+};
+struct LgRow {
+    float lse;
+    int apply;
+};
+
+template <int NW> __device__ __forceinline__ float bmax(float v, float * red) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    float r = red[0];
+    for (int i = 1; i < NW; ++i) r = fmaxf(r, red[i]);
+    return r;
+}
+template <int NW> __device__ __forceinline__ double bsum(double v, double * red) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    double r = 0.0;
+    for (int i = 0; i < NW; ++i) r += red[i];
+    return r;
+}
+template <int NW> __device__ __forceinline__ void bargmax(float & v, int & idx, float * redv, int * redi) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const float ov = __shfl_xor(v, o, 64);
+        const int oi = __shfl_xor(idx, o, 64);
+        if (ov > v || (ov == v && oi < idx)) { v = ov; idx = oi; }
+    }
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) { redv[threadIdx.x >> 6] = v; redi[threadIdx.x >> 6] = idx; }
+    __syncthreads();
+    v = redv[0]; idx = redi[0];
+    for (int i = 1; i < NW; ++i)
+        if (redv[i] > v || (redv[i] == v && redi[i] < idx)) { v = redv[i]; idx = redi[i]; }
+}
+
+__device__ __forceinline__ void lgs_range(int n_vocab, int b, int & i0, int & i1) {
+    const int per = (n_vocab + LGS_B - 1) / LGS_B;
+    i0 = b * per;
+    i1 = min(n_vocab, i0 + per);
+}
+
+__global__ __launch_bounds__(LGS_T) void k_lgs_mask(float * __restrict__ logits, int n_vocab,
+                                                    const LogitJob * __restrict__ jobs, VocabInfo vi,
+                                                    LgPart * __restrict__ part) {
+    __shared__ float red[LGS_W];
+    const int jb = blockIdx.x / LGS_B, b = blockIdx.x % LGS_B;
+    const LogitJob job = jobs[jb];
+    float * L = logits + (size_t) job.row * n_vocab;
+    int i0, i1;
+    lgs_range(n_vocab, b, i0, i1);
+    for (int i = i0 + threadIdx.x; i < i1; i += LGS_T) {
+        float v = L[i];
+        if (job.temperature > 0.0f) v /= job.temperature;
+        if (masked(i, job.flags, job.ts_min, vi)) v = -INFINITY;
+        L[i] = v;
+    }
+    __syncthreads();
+    for (int j = threadIdx.x; j < vi.n_suppress; j += LGS_T) {
+        const int t = vi.suppress_list[j];
+        if (t >= i0 && t < i1) L[t] = -INFINITY;
+    }
+    __syncthreads();
+    float m = -INFINITY, ts = -INFINITY, tx = -INFINITY;
+    for (int i = i0 + threadIdx.x; i < i1; i += LGS_T) {
+        const float v = L[i];
+        m = fmaxf(m, v);
+        if (i >= vi.beg) ts = fmaxf(ts, v); else tx = fmaxf(tx, v);
+    }
+    m = bmax<LGS_W>(m, red);
+    ts = bmax<LGS_W>(ts, red);
+    tx = bmax<LGS_W>(tx, red);
+    if (threadIdx.x == 0) {
+        LgPart & p = part[blockIdx.x];
+        p.m = m;
+        p.tsl = ts;
+        p.txl = tx;
+    }
+}
+
+__global__ __launch_bounds__(LGS_T) void k_lgs_sum(const float * __restrict__ logits, int n_vocab,
+                                                   const LogitJob * __restrict__ jobs, LgPart * __restrict__ part) {
+    __shared__ double red[LGS_W];
+    const int jb = blockIdx.x / LGS_B, b = blockIdx.x % LGS_B;
+    const float * L = logits + (size_t) jobs[jb].row * n_vocab;
+    const LgPart * rp = part + (size_t) jb * LGS_B;
+    float M = rp[0].m;
+    for (int k = 1; k < LGS_B; ++k) M = fmaxf(M, rp[k].m);
+    int i0, i1;
+    lgs_range(n_vocab, b, i0, i1);
+    double s = 0.0;
+    for (int i = i0 + threadIdx.x; i < i1; i += LGS_T)
+        if (L[i] > -INFINITY) s += (double) expf(L[i] - M);
+    s = bsum<LGS_W>(s, red);
+    if (threadIdx.x == 0) part[blockIdx.x].s = s;
+}
+
+__global__ __launch_bounds__(LGS_T) void k_lgs_ts(const float * __restrict__ logits, int n_vocab,
+                                                  const LogitJob * __restrict__ jobs, VocabInfo vi,
+                                                  const LgPart * __restrict__ part, LgRow * __restrict__ rows) {
+    __shared__ double red[LGS_W];
+    const int jb = blockIdx.x;
+    const float * L = logits + (size_t) jobs[jb].row * n_vocab;
+    const LgPart * rp = part + (size_t) jb * LGS_B;
+    float M = rp[0].m, tsl = rp[0].tsl, txl = rp[0].txl;
+    double S = rp[0].s;
+    for (int k = 1; k < LGS_B; ++k) {
+        M = fmaxf(M, rp[k].m);
+        tsl = fmaxf(tsl, rp[k].tsl);
+        txl = fmaxf(txl, rp[k].txl);
+        S += rp[k].s;
+    }
+    const float lse = logf((float) S) + M;
+    const float ts_max = tsl > -INFINITY ? tsl - lse : -INFINITY;
+    const float tx_max = txl > -INFINITY ? txl - lse : -INFINITY;
+    double ts_sum = 0.0;
+    for (int i = vi.beg + threadIdx.x; i < n_vocab; i += LGS_T) {
+        const float lp = L[i] > -INFINITY ? L[i] - lse : -INFINITY;
+        if (lp > -INFINITY) ts_sum += (double) expf(lp - ts_max);
+    }
+    ts_sum = bsum<LGS_W>(ts_sum, red);
+    if (threadIdx.x == 0) {
+        const float ts_lp = ts_sum > 0.0 ? logf((float) ts_sum) + ts_max : -INFINITY;
+        rows[jb].lse = lse;
+        rows[jb].apply = ts_lp > tx_max;
+    }
+}
+
+__global__ __launch_bounds__(LGS_T) void k_lgs_pick(float * __restrict__ logits, int n_vocab,
+                                                    const LogitJob * __restrict__ jobs, VocabInfo vi,
+                                                    const LgRow * __restrict__ rows, LgPart * __restrict__ part,
+                                                    float * __restrict__ lp_out, float * __restrict__ pr_out) {
+    __shared__ float redf[LGS_W];
+    __shared__ int redi[LGS_W];
+    __shared__ double redd[LGS_W];
+    const int jb = blockIdx.x / LGS_B, b = blockIdx.x % LGS_B;
+    float * L = logits + (size_t) jobs[jb].row * n_vocab;
+    const LgRow row = rows[jb];
+    int i0, i1;
+    lgs_range(n_vocab, b, i0, i1);
+    float best = -1.0f, tbest = -1.0f;
+    int best_i = 0x7fffffff, tbest_i = 0x7fffffff;
+    double ts_psum = 0.0;
+    for (int i = i0 + threadIdx.x; i < i1; i += LGS_T) {
+        float v = L[i];
+        if (row.apply && i < vi.beg) {
+            v = -INFINITY;
+            L[i] = v;
+        }
+        const float lp = v > -INFINITY ? v - row.lse : -INFINITY;
+        const float p = v == -INFINITY ? 0.0f : expf(lp);
+        if (lp_out) lp_out[(size_t) jb * n_vocab + i] = lp;
+        if (pr_out) pr_out[(size_t) jb * n_vocab + i] = p;
+        if (p > best) { best = p; best_i = i; }
+        if (i >= vi.beg) {
+            ts_psum += (double) p;
+            if (p > tbest) { tbest = p; tbest_i = i; }
+        }
+    }
+    bargmax<LGS_W>(best, best_i, redf, redi);
+    bargmax<LGS_W>(tbest, tbest_i, redf, redi);
+    ts_psum = bsum<LGS_W>(ts_psum, redd);
+    if (threadIdx.x == 0) {
+        LgPart & p = part[blockIdx.x];
+        p.best = best;
+        p.best_i = best_i;
+        p.tbest = tbest;
+        p.tbest_i = tbest_i;
+        p.ts_psum = ts_psum;
+    }
+}
+
+__global__ void k_lgs_final(const float * __restrict__ logits, int n_vocab, const LogitJob * __restrict__ jobs,
+                            VocabInfo vi, const LgRow * __restrict__ rows, const LgPart * __restrict__ part,
+                            TokenOut * __restrict__ outv) {
+    const int jb = blockIdx.x;
+    const LgPart * rp = part + (size_t) jb * LGS_B;
+    float best = rp[0].best, tbest = rp[0].tbest;
+    int best_i = rp[0].best_i, tbest_i = rp[0].tbest_i;
+    double ts_psum = rp[0].ts_psum;
+    for (int k = 1; k < LGS_B; ++k) {
+        if (rp[k].best > best || (rp[k].best == best && rp[k].best_i < best_i)) { best = rp[k].best; best_i = rp[k].best_i; }
+        if (rp[k].tbest > tbest || (rp[k].tbest == tbest && rp[k].tbest_i < tbest_i)) {
+            tbest = rp[k].tbest;
+            tbest_i = rp[k].tbest_i;
+        }
+        ts_psum += rp[k].ts_psum;
+    }
+    const float * L = logits + (size_t) jobs[jb].row * n_vocab;
+    const float lse = rows[jb].lse;
+    TokenOut res;
+    res.nosp_prob = 0.0f;
+    res.id = best > 0.0f ? best_i : 0;
+    res.p = best > 0.0f ? best : 0.0f;
+    res.plog = L[res.id] > -INFINITY ? L[res.id] - lse : -INFINITY;
+    res.tid = tbest > 0.0f ? tbest_i : 0;
+    const double max_ts = tbest > 0.0f ? (double) tbest : 0.0;
+    res.pt = (float) (max_ts / (ts_psum + 1e-10));
+    res.ptsum = (float) ts_psum;
+    if (res.id >= vi.beg) {
+        res.tid = res.id;
+        res.pt = res.p;
+    }
+    res.pad_ = 0.0f;
+    outv[jb] = res;
+}
+
+size_t process_logits_ws_bytes(int n_jobs) {
+    return (size_t) n_jobs * LGS_B * sizeof(LgPart) + (size_t) n_jobs * sizeof(LgRow) + 64;
+}
+
 void process_logits(hipStream_t s, float * logits, int n_vocab, const LogitJob * jobs_dev, int n_jobs,
-                    const VocabInfo & vi, TokenOut * out_dev, float * logprobs_out, float * probs_out) {
+                    const VocabInfo & vi, TokenOut * out_dev, float * logprobs_out, float * probs_out, bool any_nosp,
+                    void * ws, size_t ws_bytes) {
     if (n_jobs <= 0) return;
-    OWK_LAUNCH(k_process_logits, dim3(n_jobs), dim3(LG_THREADS), 0, s, logits, n_vocab, jobs_dev, vi, out_dev,
-                       logprobs_out, probs_out);
+    // (turbo bench, interleaved on one box: 3819-3844 one block per row, 3897-3916 split;
+    // profiles/r03l_ab_logits_split_turbo.txt)
+    if (any_nosp || !ws || ws_bytes < process_logits_ws_bytes(n_jobs)) {
+        OWK_LAUNCH(k_process_logits, dim3(n_jobs), dim3(LG_THREADS), 0, s, logits, n_vocab, jobs_dev, vi, out_dev,
+                   logprobs_out, probs_out);
+        return;
+    }
+    LgPart * part = (LgPart *) ws;
+    LgRow * rows = (LgRow *) (part + (size_t) n_jobs * LGS_B);
+    const dim3 g(n_jobs * LGS_B);
+    OWK_LAUNCH(k_lgs_mask, g, dim3(LGS_T), 0, s, logits, n_vocab, jobs_dev, vi, part);
+    OWK_LAUNCH(k_lgs_sum, g, dim3(LGS_T), 0, s, logits, n_vocab, jobs_dev, part);
+    OWK_LAUNCH(k_lgs_ts, dim3(n_jobs), dim3(LGS_T), 0, s, logits, n_vocab, jobs_dev, vi, part, rows);
+    OWK_LAUNCH(k_lgs_pick, g, dim3(LGS_T), 0, s, logits, n_vocab, jobs_dev, vi, rows, part, logprobs_out, probs_out);
+    OWK_LAUNCH(k_lgs_final, dim3(n_jobs), dim3(1), 0, s, logits, n_vocab, jobs_dev, vi, rows, part, out_dev);
 }
 
 } // namespace owk

@@ -310,9 +310,13 @@ void rowmax_update(hipStream_t s, const float * logits, int n_vocab, const int4 
                    int stride);
 void nosp_probs(hipStream_t s, const float * row0, int n_vocab, const int2 * req_dev, int n, const float * rmx,
                 int stride, int nosp, float * out_dev);
-// processes logits in place (filters applied), writes logprobs/probs when requested
+// processes logits in place (filters applied), writes logprobs/probs when requested. With a workspace of
+// process_logits_ws_bytes(n_jobs) and no job needing the raw no-speech probability (any_nosp false),
+// every row is split over several blocks (k_logits.hip); else one block per row.
+size_t process_logits_ws_bytes(int n_jobs);
 void process_logits(hipStream_t s, float * logits, int n_vocab, const LogitJob * jobs_dev, int n_jobs,
-                    const VocabInfo & vi, TokenOut * out_dev, float * logprobs_out, float * probs_out);
+                    const VocabInfo & vi, TokenOut * out_dev, float * logprobs_out, float * probs_out,
+                    bool any_nosp = true, void * ws = nullptr, size_t ws_bytes = 0);
 
 // Silero VAD (k_vad.hip). Weights as the kernels read them: F16 conv weights transposed
 // to [(ic * K + k)][OC] (im2col row order), W_ih transposed to [128][512], W_hh row-major.
