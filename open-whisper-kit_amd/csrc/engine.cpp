@@ -185,7 +185,8 @@ void Engine::compute_mel(const std::vector<int> & slots, const std::vector<const
     OWK_HIP_CHECK(hipMemcpyAsync(mel_jobs_.ptr, jobs.data(), sizeof(MelJob) * n, hipMemcpyHostToDevice, stream));
     {
         ProfScope ps(prof, stream, "mel");
-        mel_spectrogram(stream, mel_jobs_.as<MelJob>(), n, max_frames, m->mel_filters, n_mel, m->twiddle, m->hann);
+        mel_spectrogram(stream, mel_jobs_.as<MelJob>(), n, max_frames, m->mel_filters, m->mel_rng, n_mel, m->twiddle,
+                        m->hann);
         mel_normalize(stream, mel_jobs_.as<MelJob>(), n, n_mel);
     }
     sync();  // pcm host buffers may go away after return

@@ -349,63 +349,92 @@ void embed_tokens_q5(hipStream_t s, const Q5W & te, const float * pe, const int 
 // Log-mel spectrogram (ref whisper.cpp:3104-3260). Per frame: reflect-padded samples
 // times the periodic Hann window (float product, as the reference), 201-bin DFT of
 // the 400-sample frame evaluated in double (the reference's float radix-2/DFT FFT is
-// a rounding of this), power, mel projection summed in double, log10(max(., 1e-10)).
+// a rounding of the exact value; so is this, at double precision), power, mel projection
+// summed in double, log10(max(., 1e-10)).
 // Frames past n_samples/160 hold only zero padding -> log10(1e-10) = -10 exactly.
-// One block per (frame, clip).
+// One block per (MEL_FPB frames, clip).
 // ----------------------------------------------------------------------------------
+constexpr int MEL_FPB = 4;  // frames per block
 __global__ __launch_bounds__(256) void k_mel(const MelJob * __restrict__ jobs, const float * __restrict__ filters,
-                                             int n_mel, const float * __restrict__ hann,
+                                             const int * __restrict__ rng, int n_mel, const float * __restrict__ hann,
                                              const double * __restrict__ tw) {
     const MelJob job = jobs[blockIdx.y];
-    const int f = blockIdx.x;
-    if (f >= job.n_len) return;
     const int n = job.n_samples;
     const int n_w = n + 200;  // samples after the 200-sample reflect pad
     const int n_compute = min(n_w / 160 + 1, job.n_len);
     float * mel = job.mel;
-    if (f >= n_compute) {
-        for (int m = threadIdx.x; m < n_mel; m += blockDim.x) mel[(size_t) m * job.n_len + f] = -10.0f;
-        return;
-    }
     __shared__ double frame[400];
     __shared__ double power[201];
-    __shared__ double stw[800];  // cos / sin table in LDS: the DFT loop reads it 800 times per bin
-    for (int j = threadIdx.x; j < 800; j += blockDim.x) stw[j] = tw[j];
-    const int off = f * 160;
-    for (int j = threadIdx.x; j < 400; j += blockDim.x) {
-        const int p = off + j;  // index into the padded signal
-        float v = 0.0f;
-        if (p < n_w) {
-            v = p < 200 ? job.pcm[200 - p] : job.pcm[p - 200];
+    __shared__ double stw[800];  // cos / sin table in LDS (loaded once per MEL_FPB frames)
+    __shared__ double ysub[800];  // the 16 x 25 sub-DFT outputs (re, im)
+    if (blockIdx.x * MEL_FPB < n_compute)
+        for (int j = threadIdx.x; j < 800; j += blockDim.x) stw[j] = tw[j];
+    for (int fi = 0; fi < MEL_FPB; ++fi) {
+        const int f = blockIdx.x * MEL_FPB + fi;
+        if (f >= job.n_len) return;
+        if (f >= n_compute) {
+            for (int m = threadIdx.x; m < n_mel; m += blockDim.x) mel[(size_t) m * job.n_len + f] = -10.0f;
+            continue;
         }
-        frame[j] = (double) (hann[j] * v);
-    }
-    __syncthreads();
-    for (int k = threadIdx.x; k < 201; k += blockDim.x) {
-        double re = 0.0, im = 0.0;
-        int idx = 0;
-        for (int j = 0; j < 400; ++j) {
-            const double x = frame[j];
-            re += x * stw[idx];
-            im -= x * stw[400 + idx];
-            idx += k;
-            if (idx >= 400) idx -= 400;
+        __syncthreads();  // the previous frame's LDS reads are done
+        const int off = f * 160;
+        for (int j = threadIdx.x; j < 400; j += blockDim.x) {
+            const int p = off + j;  // index into the padded signal
+            float v = 0.0f;
+            if (p < n_w) {
+                v = p < 200 ? job.pcm[200 - p] : job.pcm[p - 200];
+            }
+            frame[j] = (double) (hann[j] * v);
         }
-        power[k] = re * re + im * im;
-    }
-    __syncthreads();
-    for (int m = threadIdx.x; m < n_mel; m += blockDim.x) {
-        const float * fr = filters + (size_t) m * 201;
-        double sum = 0.0;
-        for (int k = 0; k < 201; ++k) sum += power[k] * (double) fr[k];
-        mel[(size_t) m * job.n_len + f] = (float) log10(fmax(sum, 1e-10));
+        __syncthreads();
+        // the 400-point DFT as 16 x 25 (Cooley-Tukey, j = 16a + b): Y_b[r] = sum_a x[16a+b] W25^(ar) for
+        // the 16 residues b, then X[k] = sum_b W400^(bk) Y_b[k mod 25] -- 33 K double FMAs per frame
+        // instead of the direct sum's 160 K, the same exact-value target (twiddles from the 400 table:
+        // W25^m = W400^(16m))
+        for (int t = threadIdx.x; t < 400; t += blockDim.x) {
+            const int b = t / 25, r = t - b * 25;
+            double yr = 0.0, yi = 0.0;
+            int idx = 0;  // 16 * (a * r mod 25)
+            for (int a = 0; a < 25; ++a) {
+                const double x = frame[16 * a + b];
+                yr += x * stw[idx];
+                yi -= x * stw[400 + idx];
+                idx += 16 * r;
+                if (idx >= 400) idx -= 400;
+            }
+            ysub[2 * t] = yr;
+            ysub[2 * t + 1] = yi;
+        }
+        __syncthreads();
+        for (int k = threadIdx.x; k < 201; k += blockDim.x) {
+            const int r = k % 25;
+            double re = 0.0, im = 0.0;
+            int idx = 0;  // b * k mod 400
+            for (int b = 0; b < 16; ++b) {
+                const double c = stw[idx], sn = stw[400 + idx];
+                const double yr = ysub[2 * (b * 25 + r)], yi = ysub[2 * (b * 25 + r) + 1];
+                re += c * yr + sn * yi;
+                im += c * yi - sn * yr;
+                idx += k;
+                if (idx >= 400) idx -= 400;
+            }
+            power[k] = re * re + im * im;
+        }
+        __syncthreads();
+        for (int m = threadIdx.x; m < n_mel; m += blockDim.x) {
+            const float * fr = filters + (size_t) m * 201;
+            double sum = 0.0;
+            for (int k = rng[2 * m], k1 = rng[2 * m + 1]; k < k1; ++k) sum += power[k] * (double) fr[k];
+            mel[(size_t) m * job.n_len + f] = (float) log10(fmax(sum, 1e-10));
+        }
     }
 }
 
 void mel_spectrogram(hipStream_t s, const MelJob * jobs_dev, int n_jobs, int max_frames, const float * filters,
-                     int n_mel, const double * twiddle, const float * hann) {
+                     const int * filter_rng, int n_mel, const double * twiddle, const float * hann) {
     if (n_jobs <= 0 || max_frames <= 0) return;
-    OWK_LAUNCH(k_mel, dim3(max_frames, n_jobs), dim3(256), 0, s, jobs_dev, filters, n_mel, hann, twiddle);
+    OWK_LAUNCH(k_mel, dim3((max_frames + MEL_FPB - 1) / MEL_FPB, n_jobs), dim3(256), 0, s, jobs_dev, filters, filter_rng,
+               n_mel, hann, twiddle);
 }
 
 // global max over the whole (padded) clip, clamp to max-8, (x+4)/4 (whisper.cpp:3228-3244)

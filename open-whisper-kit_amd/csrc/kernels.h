@@ -219,7 +219,8 @@ struct MelJob {
 // twiddle: cos[400] then sin[400] (double); hann: periodic window [400] (float, host-computed
 // exactly as whisper_global_cache::fill_hann_window, whisper.cpp:3023-3031)
 void mel_spectrogram(hipStream_t s, const MelJob * jobs_dev, int n_jobs, int max_frames,
-                     const float * filters, int n_mel, const double * twiddle, const float * hann);
+                     const float * filters, const int * filter_rng, int n_mel, const double * twiddle,
+                     const float * hann);
 // per-job max, clamp to max-8, (x+4)/4 (ref whisper.cpp:3228-3244)
 void mel_normalize(hipStream_t s, const MelJob * jobs_dev, int n_jobs, int n_mel);
 

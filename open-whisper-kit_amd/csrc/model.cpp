@@ -397,6 +397,8 @@ Model * load_model(whisper_model_loader * loader, int device, std::string & err)
     const size_t o_filt = reserve(m->filters.size() * 4);
     const size_t o_tw = reserve(800 * 8);
     const size_t o_hann = reserve(400 * 4);
+    const int n_filt = (int) (m->filters.size() / 201);
+    const size_t o_rng = reserve((size_t) n_filt * 2 * 4);
 
     m->blob.alloc(off);
     OWK_HIP_CHECK(hipMemset(m->blob.ptr, 0, off));
@@ -450,6 +452,18 @@ Model * load_model(whisper_model_loader * loader, int device, std::string & err)
         std::vector<float> hann(400);
         for (int i = 0; i < 400; ++i) hann[i] = (float) (0.5 * (1.0 - cosf((float) ((2.0 * M_PI * i) / (400 + 0)))));
         up(o_hann, hann.data(), hann.size() * 4);
+        // each mel filter's nonzero bin range [lo, hi): the projection skips the zero weights around it
+        // (power * 0 adds an exact 0 to the double sum, so the result is unchanged)
+        std::vector<int> rng((size_t) n_filt * 2);
+        for (int f = 0; f < n_filt; ++f) {
+            const float * fr = m->filters.data() + (size_t) f * 201;
+            int lo = 0, hi = 201;
+            while (lo < hi && fr[lo] == 0.0f) ++lo;
+            while (hi > lo && fr[hi - 1] == 0.0f) --hi;
+            rng[2 * f] = lo;
+            rng[2 * f + 1] = hi;
+        }
+        up(o_rng, rng.data(), rng.size() * 4);
     }
 
     auto F = [&](const std::string & n) { return (const float *) (base + place.at(n)); };
@@ -718,6 +732,7 @@ Model * load_model(whisper_model_loader * loader, int device, std::string & err)
     m->mel_filters = (const float *) (base + o_filt);
     m->twiddle = (const double *) (base + o_tw);
     m->hann = (const float *) (base + o_hann);
+    m->mel_rng = (const int *) (base + o_rng);
     return m.release();
 }
 

@@ -101,6 +101,7 @@ struct Model {
     // device constants
     const uint16_t * gelu_tab = nullptr;  // 65536 f16 entries
     const float * mel_filters = nullptr;  // [n_mel][201]
+    const int * mel_rng = nullptr;        // [n_mel][2]: nonzero bin range [lo, hi) of each filter
     const double * twiddle = nullptr;     // cos[400], sin[400]
     const float * hann = nullptr;         // [400]
     int device = 0;
