@@ -1301,6 +1301,66 @@ __global__ __launch_bounds__(GR_MAXW * 64) void k_gemm_rows(int M, int N, int K,
     }
 }
 
+// k_gemm_rows with NT column tiles per block (KS = 1, full epilogues): every wave loads its activation
+// fragments once and runs them against NT weight tiles, so the activation rows are read from L2 once per
+// NT tiles instead of once per tile (the logits GEMM: 3242 tiles x 10 waves x 8 KB = 265 MB of L2
+// reads for 133 MB of weights). Per output the same MFMA chain and the same fixed wave order as
+// k_gemm_rows: bit-identical.
+template <int MODE, int MT, int J, int NT>
+__global__ __launch_bounds__(GR_MAXW * 64) void k_gemm_rows_nt(int M, int N, int K, const _Float16 * __restrict__ A,
+                                                               int lda, const _Float16 * __restrict__ Wt, EpiParams ep) {
+    __shared__ floatx4 red[GR_MAXW][NT][MT][64];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = blockDim.x >> 6;
+    const int ntiles = (N + 15) >> 4, t0 = blockIdx.x * NT;
+    const int nsteps = K >> 5;
+    const int ks0 = wave * J;
+    const int nj = max(0, min(J, nsteps - ks0));
+    const half8 z8 = {0, 0, 0, 0, 0, 0, 0, 0};
+    half8 b[NT][J], a[MT][J];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+        const _Float16 * wp = Wt + ((size_t) min(t0 + t, ntiles - 1) * nsteps) * 512 + lane * 8;
+#pragma unroll
+        for (int j = 0; j < J; ++j) {
+            const half8 v = __builtin_nontemporal_load((const half8 *) (wp + (size_t) min(ks0 + j, nsteps - 1) * 512));
+            b[t][j] = j < nj ? v : z8;
+        }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int i = 0; i < MT; ++i) {
+        const _Float16 * ap = A + (size_t) min(i * 16 + (lane & 15), M - 1) * lda + 8 * (lane >> 4);
+#pragma unroll
+        for (int j = 0; j < J; ++j) {
+            const half8 v = *(const half8 *) (ap + min(ks0 + j, nsteps - 1) * 32);
+            a[i][j] = j < nj ? v : z8;
+        }
+    }
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+        floatx4 acc[MT];
+#pragma unroll
+        for (int i = 0; i < MT; ++i) acc[i] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int j = 0; j < J; ++j)
+#pragma unroll
+            for (int i = 0; i < MT; ++i) acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[i][j], b[t][j], acc[i], 0, 0, 0);
+#pragma unroll
+        for (int i = 0; i < MT; ++i) red[wave][t][i][lane] = acc[i];
+    }
+    __syncthreads();
+    for (int o = tid; o < NT * MT * 256; o += blockDim.x) {
+        const int t = o / (MT * 256), q = o - t * (MT * 256);
+        const int r = q >> 4, cc = q & 15;
+        const int i = r >> 4, rr = r & 15;
+        const int ln = 16 * (rr >> 2) + cc, e = rr & 3;
+        float sum = ((const float *) &red[0][t][i][ln])[e];
+        for (int w = 1; w < nw; ++w) sum += ((const float *) &red[w][t][i][ln])[e];
+        const int c = (t0 + t) * 16 + cc;
+        if (r < M && c < N) epi_store<MODE>(ep, r, c, sum);
+    }
+}
+
 template <int MODE, int MT>
 __global__ __launch_bounds__(MT * 64) void k_gemm_rows_reduce(int M, int N, int KS, const float * __restrict__ part,
                                                               EpiParams ep) {
@@ -1456,6 +1516,24 @@ template <int MODE> struct LaunchRows {
         }
         const dim3 grid(tiles, pl.KS);
         const bool one = M <= 16;
+        // full-epilogue launches take 2 column tiles per block: the logits GEMM 47.7 -> 37.0 us for
+        // 32 x 51866 x 1280 (tools/logits_gemm_bench.py, profiles/r03n_logits_gemm_nt.txt; 4 tiles: 37.3 us,
+        // and slower at 8 rows), MLP0 7.76 -> 5.98 us in isolation; large-v3 bench 998-1007 -> 1022-1026
+        // with QKV / cross-Q / MLP0 / logits all on it (profiles/r03n_ab_rows_nt_all.txt).
+        // OWK_ROWS_NT / OWK_ROWS_NT_MIN_N: tuning sweeps (tools/rows_nt_sweep.py)
+        static const int nt_env = env_int("OWK_ROWS_NT", 0), nt_min_n = env_int("OWK_ROWS_NT_MIN_N", 1);
+        const int nt = nt_env ? nt_env : 2;
+        if (MODE != EPI_PARTIAL && pl.KS == 1 && N >= nt_min_n && (nt == 2 || nt == 4) && pl.J == 4) {
+            const dim3 g((tiles + nt - 1) / nt);
+            if (nt == 2) {
+                if (one) OWK_LAUNCH((k_gemm_rows_nt<MODE, 1, 4, 2>), g, dim3(pl.nw * 64), 0, s, M, N, K, A, lda, Wt, ep);
+                else OWK_LAUNCH((k_gemm_rows_nt<MODE, 2, 4, 2>), g, dim3(pl.nw * 64), 0, s, M, N, K, A, lda, Wt, ep);
+            } else {
+                if (one) OWK_LAUNCH((k_gemm_rows_nt<MODE, 1, 4, 4>), g, dim3(pl.nw * 64), 0, s, M, N, K, A, lda, Wt, ep);
+                else OWK_LAUNCH((k_gemm_rows_nt<MODE, 2, 4, 4>), g, dim3(pl.nw * 64), 0, s, M, N, K, A, lda, Wt, ep);
+            }
+            return;
+        }
         switch (pl.J) {
             case 2: one ? go<1, 2>(s, grid, pl.nw, M, N, K, A, lda, Wt, ep, part)
                         : go<2, 2>(s, grid, pl.nw, M, N, K, A, lda, Wt, ep, part); break;
