@@ -1308,12 +1308,13 @@ __global__ __launch_bounds__(GR_MAXW * 64) void k_gemm_rows(int M, int N, int K,
 // k_gemm_rows: bit-identical.
 template <int MODE, int MT, int J, int NT>
 __global__ __launch_bounds__(GR_MAXW * 64) void k_gemm_rows_nt(int M, int N, int K, const _Float16 * __restrict__ A,
-                                                               int lda, const _Float16 * __restrict__ Wt, EpiParams ep) {
+                                                               int lda, const _Float16 * __restrict__ Wt, EpiParams ep,
+                                                               float * __restrict__ part) {
     __shared__ floatx4 red[GR_MAXW][NT][MT][64];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = blockDim.x >> 6;
     const int ntiles = (N + 15) >> 4, t0 = blockIdx.x * NT;
     const int nsteps = K >> 5;
-    const int ks0 = wave * J;
+    const int ks0 = (blockIdx.y * nw + wave) * J;  // EPI_PARTIAL: k split blockIdx.y
     const int nj = max(0, min(J, nsteps - ks0));
     const half8 z8 = {0, 0, 0, 0, 0, 0, 0, 0};
     half8 b[NT][J], a[MT][J];
@@ -1357,7 +1358,12 @@ __global__ __launch_bounds__(GR_MAXW * 64) void k_gemm_rows_nt(int M, int N, int
         float sum = ((const float *) &red[0][t][i][ln])[e];
         for (int w = 1; w < nw; ++w) sum += ((const float *) &red[w][t][i][ln])[e];
         const int c = (t0 + t) * 16 + cc;
-        if (r < M && c < N) epi_store<MODE>(ep, r, c, sum);
+        if (r < M && c < N) {
+            if constexpr (MODE == EPI_PARTIAL)
+                part[((size_t) blockIdx.y * M + r) * N + c] = sum;  // row-major [ks][M][N] for resid_layernorm
+            else
+                epi_store<MODE>(ep, r, c, sum);
+        }
     }
 }
 
@@ -1523,15 +1529,21 @@ template <int MODE> struct LaunchRows {
         // OWK_ROWS_NT / OWK_ROWS_NT_MIN_N: tuning sweeps (tools/rows_nt_sweep.py)
         static const int nt_env = env_int("OWK_ROWS_NT", 0), nt_min_n = env_int("OWK_ROWS_NT_MIN_N", 1);
         const int nt = nt_env ? nt_env : 2;
-        if (MODE != EPI_PARTIAL && pl.KS == 1 && N >= nt_min_n && (nt == 2 || nt == 4) && pl.J == 4) {
-            const dim3 g((tiles + nt - 1) / nt);
+        // OWK_ROWS_NT_PARTIAL=1: also the split-K partial launches and J = 2 plans (A/B pending)
+        static const bool nt_wide = env_int("OWK_ROWS_NT_PARTIAL", 0) != 0;
+        const bool fits = MODE == EPI_PARTIAL ? nt_wide : pl.KS == 1 && (pl.J == 4 || nt_wide);
+        if (fits && N >= nt_min_n && (nt == 2 || nt == 4) && (pl.J == 4 || pl.J == 2)) {
+            const dim3 g((tiles + nt - 1) / nt, pl.KS);
+#define OWK_ROWS_NT_GO(MT_, J_, NT_) \
+    OWK_LAUNCH((k_gemm_rows_nt<MODE, MT_, J_, NT_>), g, dim3(pl.nw * 64), 0, s, M, N, K, A, lda, Wt, ep, part)
             if (nt == 2) {
-                if (one) OWK_LAUNCH((k_gemm_rows_nt<MODE, 1, 4, 2>), g, dim3(pl.nw * 64), 0, s, M, N, K, A, lda, Wt, ep);
-                else OWK_LAUNCH((k_gemm_rows_nt<MODE, 2, 4, 2>), g, dim3(pl.nw * 64), 0, s, M, N, K, A, lda, Wt, ep);
+                if (pl.J == 4) { if (one) OWK_ROWS_NT_GO(1, 4, 2); else OWK_ROWS_NT_GO(2, 4, 2); }
+                else { if (one) OWK_ROWS_NT_GO(1, 2, 2); else OWK_ROWS_NT_GO(2, 2, 2); }
             } else {
-                if (one) OWK_LAUNCH((k_gemm_rows_nt<MODE, 1, 4, 4>), g, dim3(pl.nw * 64), 0, s, M, N, K, A, lda, Wt, ep);
-                else OWK_LAUNCH((k_gemm_rows_nt<MODE, 2, 4, 4>), g, dim3(pl.nw * 64), 0, s, M, N, K, A, lda, Wt, ep);
+                if (pl.J == 4) { if (one) OWK_ROWS_NT_GO(1, 4, 4); else OWK_ROWS_NT_GO(2, 4, 4); }
+                else { if (one) OWK_ROWS_NT_GO(1, 2, 4); else OWK_ROWS_NT_GO(2, 2, 4); }
             }
+#undef OWK_ROWS_NT_GO
             return;
         }
         switch (pl.J) {
