@@ -67,6 +67,10 @@ WHISPER_API int owk_debug_enc(struct whisper_context * ctx, struct whisper_state
 WHISPER_API int owk_debug_cross(struct whisper_context * ctx, struct whisper_state * st, int slot, int layer,
                                 uint16_t * k, uint16_t * v);
 WHISPER_API const uint16_t * owk_debug_gelu_table(void);
+/* test hook (host only): whisper_tokenize on the vocabulary of the model file at path_model (only
+ * its header, mel filters and vocabulary are read). Returns the token count (written to out when
+ * it fits cap), -count when it does not, INT32_MIN when the file cannot be parsed. */
+WHISPER_API int owk_debug_tokenize(const char * path_model, const char * text, int * out, int cap);
 /* out[M][N] = A[M][K] . W[N][K]^T (f16 bits in, f32 out) through the engine's GEMM dispatch */
 WHISPER_API int owk_debug_gemm(int device, int M, int N, int K, const uint16_t * a, const uint16_t * w, float * out);
 // one large-tile epilogue mode through the 128x128 and 256x256 kernels on the same random operands: max |diff|

@@ -16,6 +16,7 @@
 #include <cstring>
 #include <memory>
 #include <mutex>
+#include <regex>
 
 namespace owk {
 
@@ -186,7 +187,7 @@ struct HostTensor {
 
 } // namespace
 
-Model * load_model(whisper_model_loader * loader, int device, std::string & err) {
+Model * load_model(whisper_model_loader * loader, int device, std::string & err, bool vocab_only) {
     Reader r{loader};
     auto m = std::make_unique<Model>();
     m->device = device;
@@ -296,6 +297,7 @@ Model * load_model(whisper_model_loader * loader, int device, std::string & err)
         }
     }
     if (!r.ok) { err = "truncated vocab"; return nullptr; }
+    if (vocab_only) return m.release();
 
     // tensors
     const auto specs = expected_tensors(hp);
@@ -734,6 +736,45 @@ Model * load_model(whisper_model_loader * loader, int device, std::string & err)
     m->hann = (const float *) (base + o_hann);
     m->mel_rng = (const int *) (base + o_rng);
     return m.release();
+}
+
+std::vector<int> tokenize_text(const Vocab & v, const std::string & text) {
+    // words: the GPT-2 pre-tokenizer regex in std::regex form, matched in the classic "C" locale
+    // (bytes >= 0x80 are neither alpha nor digit), exactly as ref whisper.cpp:3276-3288
+    std::vector<std::string> words;
+    {
+        std::string str = text;
+        static const std::regex re(
+            R"('s|'t|'re|'ve|'m|'ll|'d| ?[[:alpha:]]+| ?[[:digit:]]+| ?[^\s[:alpha:][:digit:]]+|\s+(?!\S)|\s+)");
+        std::smatch m;
+        while (std::regex_search(str, m, re)) {
+            for (auto x : m) words.push_back(x);
+            str = m.suffix();
+        }
+    }
+    // each word: repeatedly the longest vocabulary entry starting at i; a byte no entry starts
+    // with is dropped with the reference's "unknown token" error
+    std::vector<int> res;
+    for (const auto & w : words) {
+        const int n = (int) w.size();
+        for (int i = 0; i < n;) {
+            int j = n;
+            for (; j > i; --j) {
+                auto it = v.token_to_id.find(w.substr(i, j - i));
+                if (it != v.token_to_id.end()) {
+                    res.push_back(it->second);
+                    break;
+                }
+            }
+            if (j > i) {
+                i = j;
+            } else {
+                log_msg(GGML_LOG_LEVEL_ERROR, "unknown token\n");
+                ++i;
+            }
+        }
+    }
+    return res;
 }
 
 } // namespace owk

@@ -109,7 +109,12 @@ struct Model {
 
 // parse a ggml-bin model through a whisper_model_loader and upload it to `device`.
 // Returns nullptr (after logging) on malformed input, like whisper_model_load.
-Model * load_model(whisper_model_loader * loader, int device, std::string & err);
+// vocab_only: stop after the header, mel filters and vocabulary (host only, no device touched)
+Model * load_model(whisper_model_loader * loader, int device, std::string & err, bool vocab_only = false);
+
+// whisper_tokenize's algorithm on a vocabulary (regex word split + greedy longest match,
+// ref whisper.cpp:3272-3320)
+std::vector<int> tokenize_text(const Vocab & v, const std::string & text);
 
 void log_msg(ggml_log_level level, const char * fmt, ...) __attribute__((format(printf, 2, 3)));
 

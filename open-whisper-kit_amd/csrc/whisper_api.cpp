@@ -8,6 +8,7 @@
 #include <cstring>
 #include <fstream>
 #include <map>
+#include <mutex>
 #include <regex>
 #include <thread>
 
@@ -516,42 +517,10 @@ int whisper_decode(struct whisper_context * ctx, const whisper_token * tokens, i
 }
 
 // ---------------------------------------------------------------------------------
-// tokenizer (greedy longest match over regex-split words, ref 3272-3320)
+// tokenizer (tokenize_text: greedy longest match over regex-split words, ref 3272-3320)
 // ---------------------------------------------------------------------------------
 int whisper_tokenize(struct whisper_context * ctx, const char * text, whisper_token * tokens, int n_max_tokens) {
-    const Vocab & v = ctx->model->vocab;
-    std::vector<std::string> words;
-    {
-        std::string str = text;
-        const std::regex re(R"('s|'t|'re|'ve|'m|'ll|'d| ?[[:alpha:]]+| ?[[:digit:]]+| ?[^\s[:alpha:][:digit:]]+|\s+(?!\S)|\s+)");
-        std::smatch m;
-        while (std::regex_search(str, m, re)) {
-            for (auto x : m) words.push_back(x);
-            str = m.suffix();
-        }
-    }
-    std::vector<whisper_token> res;
-    for (const auto & w : words) {
-        if (w.empty()) continue;
-        int i = 0;
-        const int n = (int) w.size();
-        while (i < n) {
-            bool found = false;
-            for (int j = n; j > i; --j) {
-                auto it = v.token_to_id.find(w.substr(i, j - i));
-                if (it != v.token_to_id.end()) {
-                    res.push_back(it->second);
-                    i = j;
-                    found = true;
-                    break;
-                }
-            }
-            if (!found) {
-                log_msg(GGML_LOG_LEVEL_ERROR, "unknown token\n");
-                ++i;
-            }
-        }
-    }
+    const std::vector<int> res = tokenize_text(ctx->model->vocab, text);
     if (n_max_tokens < (int) res.size()) {
         if (n_max_tokens > 0)
             log_msg(GGML_LOG_LEVEL_ERROR, "%s: too many resulting tokens: %d (max %d)\n", __func__, (int) res.size(),
@@ -1113,6 +1082,46 @@ int owk_debug_cross(struct whisper_context * ctx, struct whisper_state * st, int
     const int n = st->eng->n_ctx() * ctx->model->hp.n_text_state;
     if (k && v) st->eng->download_cross(slot, layer, k, v);
     return n;
+}
+
+// host-only: whisper_tokenize over the vocabulary of a model file (header, mel filters and vocab
+// parsed by the product loader, no weights, no device)
+int owk_debug_tokenize(const char * path_model, const char * text, int * out, int cap) {
+    // the parsed vocabulary of the last file is kept (tests tokenize thousands of strings)
+    static std::mutex mu;
+    static std::string cached_path;
+    static std::unique_ptr<Model> cached;
+    try {
+        std::lock_guard<std::mutex> lock(mu);
+        if (!cached || cached_path != path_model) {
+            cached.reset();
+            std::ifstream fin(path_model, std::ios::binary);
+            if (!fin) return INT32_MIN;
+            whisper_model_loader loader = {};
+            loader.context = &fin;
+            loader.read = [](void * c, void * o, size_t n) {
+                auto * f = (std::ifstream *) c;
+                f->read((char *) o, n);
+                return (size_t) f->gcount();
+            };
+            loader.eof = [](void * c) { return ((std::ifstream *) c)->eof(); };
+            loader.close = [](void *) {};
+            std::string err;
+            cached.reset(load_model(&loader, 0, err, true));
+            if (!cached) {
+                log_msg(GGML_LOG_LEVEL_ERROR, "owk_debug_tokenize: %s\n", err.c_str());
+                return INT32_MIN;
+            }
+            cached_path = path_model;
+        }
+        const std::vector<int> res = tokenize_text(cached->vocab, text);
+        if (cap < (int) res.size()) return -(int) res.size();
+        std::copy(res.begin(), res.end(), out);
+        return (int) res.size();
+    } catch (const std::exception & ex) {
+        log_msg(GGML_LOG_LEVEL_ERROR, "owk_debug_tokenize: %s\n", ex.what());
+        return INT32_MIN;
+    }
 }
 
 const uint16_t * owk_debug_gelu_table(void) { return gelu_table_host().data(); }

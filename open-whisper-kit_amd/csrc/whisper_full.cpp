@@ -431,15 +431,18 @@ struct Clip {
 
     void on_encoded() {
         st->n_encode++;
-        if (p.abort_callback && p.abort_callback(p.abort_callback_user_data)) {
-            log_msg(GGML_LOG_LEVEL_ERROR, "whisper_full_with_state: failed to encode\n");
-            fail(-6);
-            return;
-        }
         if (phase == Phase::LANG_WAIT_ENC) {
+            // the language probe encodes through whisper_encode_with_state: no abort check
+            // (ref whisper.cpp:3918, 4047)
             rows.assign(1, CallToken{vocab().sot, 0, 0, true});
             st->kv.seq_rm(0, 0, -1);
             phase = Phase::LANG_WAIT_DEC;
+            return;
+        }
+        // whisper_encode_internal's last act: the abort check (ref whisper.cpp:2455 -> 7055-7058)
+        if (p.abort_callback && p.abort_callback(p.abort_callback_user_data)) {
+            log_msg(GGML_LOG_LEVEL_ERROR, "whisper_full_with_state: failed to encode\n");
+            fail(-6);
             return;
         }
         if (seek > seek_start && seek + 500 >= seek_end) {
@@ -1052,7 +1055,11 @@ int full_batch(whisper_context * ctx, whisper_state ** states, const whisper_ful
             if (nt == 1) { st->t_decode_us += dt; st->n_decode++; }
             else if (nt < 16) { st->t_batchd_us += dt; st->n_batchd += nt; }
             else { st->t_prompt_us += dt; st->n_prompt += nt; }
-            if (c->p.abort_callback && c->p.abort_callback(c->p.abort_callback_user_data)) {
+            // whisper_decode_internal's abort check (ref whisper.cpp:2977) for the prompt and step
+            // decodes of whisper_full (7181, 7493); the language probe and the DTW re-decode pass
+            // no callback (4047, 8891)
+            if (c->phase != Phase::LANG_WAIT_DEC && c->phase != Phase::WAIT_DTW && c->p.abort_callback &&
+                c->p.abort_callback(c->p.abort_callback_user_data)) {
                 c->fail(c->phase == Phase::WAIT_PREFILL ? -8 : -9);
                 continue;
             }

@@ -210,7 +210,101 @@ float * ref_logits(void * vctx) { return whisper_get_logits((whisper_context *) 
 static std::string g_vad_path;
 void ref_set_vad(const char * path) { g_vad_path = path ? path : ""; }
 
+// whisper_full_params fields beyond ref_full_cfg (the SDK / CLI branches: whisper.cpp:6944-6979
+// initial prompt, 6990-6996 translate, 7035-7052 progress / encoder_begin, 7626-7760 segments,
+// 6077-6128 wrap, 6213-6250 suppress_regex / nst / tdrz) and a recorder of every callback the
+// reference invokes, in order.
+struct ref_full_ext {
+    const char * initial_prompt;
+    int   carry_initial_prompt;
+    int   translate;
+    int   max_len;
+    int   split_on_word;
+    int   tdrz_enable;
+    int   offset_ms;
+    int   duration_ms;
+    const char * suppress_regex;
+    int   n_max_text_ctx;       // 0 = default
+    int   print_special;
+    int   callbacks;            // 1: install the recording callbacks (log: ref_cb_log)
+    int   cancel_at_progress;   // > 0: CallbackBridge semantics -- the progress callback whose value is
+                                // >= this sets shouldCancel, the abort callback returns it (-1 = never)
+    int   enc_begin_false_at;   // > 0: encoder_begin_callback returns false on this call
+    int   tdrz_boost;           // logits_filter: solm := 1000 when finite and n_tokens % 5 == 2
+    float max_initial_ts;       // < 0: default
+    int   suppress_blank;       // < 0: default
+    int   detect_language;
+};
+
+// callback log: (kind, a, b) triples. kind 1 progress (value, n_segments), 2 encoder_begin (call #,
+// returned), 3 abort checks (consecutive calls folded: count, last returned), 4 new_segment (n_new,
+// n_segments), 5 new_segment segment text follows in g_cb_text
+static std::vector<int> g_cb_log;
+static std::vector<std::string> g_cb_text;
+static int g_cb_enc_calls = 0, g_cb_enc_false_at = 0, g_cb_cancel_at = -1;
+static bool g_cb_cancel = false;
+
+static void cb_push(int k, int a, int b) {
+    g_cb_log.push_back(k); g_cb_log.push_back(a); g_cb_log.push_back(b);
+}
+static void ref_cb_progress(whisper_context *, whisper_state * st, int progress, void *) {
+    cb_push(1, progress, (int) st->result_all.size());
+    if (g_cb_cancel_at >= 0 && progress >= g_cb_cancel_at) g_cb_cancel = true;
+}
+static bool ref_cb_enc_begin(whisper_context *, whisper_state *, void *) {
+    ++g_cb_enc_calls;
+    const bool ret = g_cb_enc_calls != g_cb_enc_false_at;
+    cb_push(2, g_cb_enc_calls, ret ? 1 : 0);
+    return ret;
+}
+static bool ref_cb_abort(void *) {
+    const int n = (int) g_cb_log.size();
+    if (n >= 3 && g_cb_log[n - 3] == 3 && g_cb_log[n - 1] == (g_cb_cancel ? 1 : 0)) {
+        g_cb_log[n - 2]++;
+    } else {
+        cb_push(3, 1, g_cb_cancel ? 1 : 0);
+    }
+    return g_cb_cancel;
+}
+// as the Swift CallbackBridge reads it: the last n_new segments of the context's default state
+static void ref_cb_new_segment(whisper_context * ctx, whisper_state * st, int n_new, void *) {
+    const int total = (int) st->result_all.size();
+    cb_push(4, n_new, total);
+    for (int i = std::max(0, total - n_new); i < total; ++i) {
+        g_cb_text.push_back(std::to_string(st->result_all[i].t0) + "|" + std::to_string(st->result_all[i].t1) + "|" +
+                            st->result_all[i].text);
+    }
+    (void) ctx;
+}
+static void ref_tdrz_boost_cb(struct whisper_context * ctx, struct whisper_state *, const whisper_token_data *,
+                              int n_tokens, float * logits, void *) {
+    const int solm = whisper_token_solm(ctx);
+    if (n_tokens % 5 == 2 && logits[solm] > -INFINITY) logits[solm] = 1000.0f;
+}
+
+int ref_cb_log(int * out, int cap) {
+    if (out) std::copy(g_cb_log.begin(), g_cb_log.begin() + std::min<size_t>(cap, g_cb_log.size()), out);
+    return (int) g_cb_log.size();
+}
+int ref_cb_n_text() { return (int) g_cb_text.size(); }
+const char * ref_cb_text(int i) { return i >= 0 && i < (int) g_cb_text.size() ? g_cb_text[i].c_str() : nullptr; }
+
+// whisper_tokenize as the reference runs it (whisper.cpp:3272-3320, 3957-3973)
+int ref_tokenize(void * vctx, const char * text, int * out, int cap) {
+    return whisper_tokenize((whisper_context *) vctx, text, out, cap);
+}
+
+static int ref_full_impl(void * vctx, const float * pcm, int n, const ref_full_cfg * cfg, const ref_full_ext * ext);
+
 int ref_full(void * vctx, const float * pcm, int n, const ref_full_cfg * cfg) {
+    return ref_full_impl(vctx, pcm, n, cfg, nullptr);
+}
+
+int ref_full_ex(void * vctx, const float * pcm, int n, const ref_full_cfg * cfg, const ref_full_ext * ext) {
+    return ref_full_impl(vctx, pcm, n, cfg, ext);
+}
+
+static int ref_full_impl(void * vctx, const float * pcm, int n, const ref_full_cfg * cfg, const ref_full_ext * ext) {
     auto * ctx = (whisper_context *) vctx;
     auto p = whisper_full_default_params(cfg->strategy == 1 ? WHISPER_SAMPLING_BEAM_SEARCH
                                                             : WHISPER_SAMPLING_GREEDY);
@@ -244,6 +338,33 @@ int ref_full(void * vctx, const float * pcm, int n, const ref_full_cfg * cfg) {
     if (!g_vad_path.empty()) {
         p.vad = true;
         p.vad_model_path = g_vad_path.c_str();
+    }
+    g_cb_log.clear(); g_cb_text.clear();
+    g_cb_enc_calls = 0; g_cb_enc_false_at = 0; g_cb_cancel_at = -1; g_cb_cancel = false;
+    if (ext) {
+        p.initial_prompt       = ext->initial_prompt;
+        p.carry_initial_prompt = ext->carry_initial_prompt != 0;
+        p.translate            = ext->translate != 0;
+        p.max_len              = ext->max_len;
+        p.split_on_word        = ext->split_on_word != 0;
+        p.tdrz_enable          = ext->tdrz_enable != 0;
+        p.offset_ms            = ext->offset_ms;
+        p.duration_ms          = ext->duration_ms;
+        p.suppress_regex       = ext->suppress_regex;
+        p.print_special        = ext->print_special != 0;
+        p.detect_language      = ext->detect_language != 0;
+        if (ext->n_max_text_ctx > 0) p.n_max_text_ctx = ext->n_max_text_ctx;
+        if (ext->max_initial_ts >= 0.0f) p.max_initial_ts = ext->max_initial_ts;
+        if (ext->suppress_blank >= 0) p.suppress_blank = ext->suppress_blank != 0;
+        if (ext->tdrz_boost) p.logits_filter_callback = ref_tdrz_boost_cb;
+        if (ext->callbacks) {
+            g_cb_enc_false_at = ext->enc_begin_false_at;
+            g_cb_cancel_at = ext->cancel_at_progress;
+            p.progress_callback = ref_cb_progress;
+            p.encoder_begin_callback = ref_cb_enc_begin;
+            p.abort_callback = ref_cb_abort;
+            p.new_segment_callback = ref_cb_new_segment;
+        }
     }
     if (cfg->n_processors > 1) return whisper_full_parallel(ctx, p, pcm, n, cfg->n_processors);
     return whisper_full(ctx, p, pcm, n);

@@ -24,6 +24,37 @@ class RefFullCfg(C.Structure):
                 ("record_topk", C.c_int), ("audio_ctx", C.c_int), ("n_processors", C.c_int)]
 
 
+class RefFullExt(C.Structure):  # ref_probe.cpp ref_full_ext
+    _fields_ = [("initial_prompt", C.c_char_p), ("carry_initial_prompt", C.c_int), ("translate", C.c_int),
+                ("max_len", C.c_int), ("split_on_word", C.c_int), ("tdrz_enable", C.c_int), ("offset_ms", C.c_int),
+                ("duration_ms", C.c_int), ("suppress_regex", C.c_char_p), ("n_max_text_ctx", C.c_int),
+                ("print_special", C.c_int), ("callbacks", C.c_int), ("cancel_at_progress", C.c_int),
+                ("enc_begin_false_at", C.c_int), ("tdrz_boost", C.c_int), ("max_initial_ts", C.c_float),
+                ("suppress_blank", C.c_int), ("detect_language", C.c_int)]
+
+
+EXT_DEFAULTS = dict(initial_prompt=None, carry_initial_prompt=False, translate=False, max_len=0, split_on_word=False,
+                    tdrz_enable=False, offset_ms=0, duration_ms=0, suppress_regex=None, n_max_text_ctx=0,
+                    print_special=False, callbacks=False, cancel_at_progress=-1, enc_begin_false_at=0,
+                    tdrz_boost=False, max_initial_ts=-1.0, suppress_blank=-1, detect_language=False)
+
+
+def make_ext(**kw):
+    v = dict(EXT_DEFAULTS)
+    for k in kw:
+        if k not in v:
+            raise KeyError(k)
+    v.update(kw)
+    e = RefFullExt()
+    for k, x in v.items():
+        if isinstance(x, str):
+            x = x.encode("utf-8", "surrogateescape")
+        elif isinstance(x, bool):
+            x = int(x)
+        setattr(e, k, x)
+    return e
+
+
 class RefTokenData(C.Structure):
     _fields_ = [("id", C.c_int32), ("tid", C.c_int32), ("p", C.c_float), ("plog", C.c_float), ("pt", C.c_float),
                 ("ptsum", C.c_float), ("t0", C.c_int64), ("t1", C.c_int64), ("t_dtw", C.c_int64),
@@ -61,6 +92,13 @@ def lib():
         L.ref_logits.restype = fp
         L.ref_logits.argtypes = [vp]
         L.ref_full.argtypes = [vp, fp, ip, C.POINTER(RefFullCfg)]
+        L.ref_full_ex.argtypes = [vp, fp, ip, C.POINTER(RefFullCfg), C.POINTER(RefFullExt)]
+        L.ref_cb_log.argtypes = [C.POINTER(ip), ip]
+        L.ref_cb_text.restype = C.c_char_p
+        L.ref_cb_text.argtypes = [ip]
+        L.ref_tokenize.argtypes = [vp, C.c_char_p, C.POINTER(ip), ip]
+        L.whisper_full_get_segment_speaker_turn_next.restype = C.c_bool
+        L.whisper_full_get_segment_speaker_turn_next.argtypes = [vp, ip]
         L.ref_record_get.argtypes = [C.POINTER(ip), C.POINTER(ip), C.POINTER(ip), fp, C.POINTER(ip)]
         L.ref_timings.argtypes = [vp] + [C.POINTER(C.c_double)] * 6 + [C.POINTER(ip)]
         L.whisper_full_n_segments.argtypes = [vp]
@@ -145,6 +183,55 @@ class Ref:
         pcm = np.ascontiguousarray(pcm, np.float32)
         ret = self.L.ref_full(self.ctx, fptr(pcm), len(pcm), C.byref(cfg))
         return ret, self.segments(dtw=self.dtw)
+
+    def full_ex(self, pcm, ext: dict, **kw):
+        """ref_full with the whisper_full_params fields of ref_full_ext (initial_prompt, translate,
+        max_len, tdrz, offsets, suppress_regex, callbacks ...). Returns (ret, segments, callback log)."""
+        full_kw = {k: v for k, v in kw.items()}
+        cfg_fields = dict(strategy=0, n_threads=8, best_of=5, beam_size=5, temperature=0.0, temperature_inc=0.2,
+                          no_timestamps=False, max_tokens=0, suppress_eot=False, token_timestamps=False,
+                          no_context=True, single_segment=False, language="en", suppress_nst=False,
+                          length_penalty=-1.0, record_topk=False, audio_ctx=0, n_processors=1)
+        for k in full_kw:
+            if k not in cfg_fields:
+                raise KeyError(k)
+        cfg_fields.update(full_kw)
+        c = cfg_fields
+        cfg = RefFullCfg(c["strategy"], c["n_threads"], c["best_of"], c["beam_size"], c["temperature"],
+                         c["temperature_inc"], int(c["no_timestamps"]), c["max_tokens"], int(c["suppress_eot"]),
+                         int(c["token_timestamps"]), int(c["no_context"]), int(c["single_segment"]),
+                         c["language"].encode() if c["language"] else None, int(c["suppress_nst"]),
+                         c["length_penalty"], int(c["record_topk"]), int(c["audio_ctx"]), int(c["n_processors"]))
+        e = make_ext(**ext)
+        pcm = np.ascontiguousarray(pcm, np.float32)
+        ret = self.L.ref_full_ex(self.ctx, fptr(pcm), len(pcm), C.byref(cfg), C.byref(e))
+        segs = self.segments(dtw=self.dtw)
+        for i, s in enumerate(segs):
+            s["speaker_turn_next"] = bool(self.L.whisper_full_get_segment_speaker_turn_next(self.ctx, i))
+        return ret, segs, self.cb_log()
+
+    def cb_log(self):
+        n = self.L.ref_cb_log(None, 0)
+        buf = (C.c_int * max(n, 1))()
+        self.L.ref_cb_log(buf, n)
+        ev = [tuple(buf[i:i + 3]) for i in range(0, n, 3)]
+        texts = []
+        i = 0
+        while True:
+            t = self.L.ref_cb_text(i)
+            if t is None:
+                break
+            texts.append(t.decode("utf-8", "surrogateescape"))
+            i += 1
+        return {"events": [list(x) for x in ev], "texts": texts}
+
+    def tokenize(self, text: bytes):
+        n = self.L.ref_tokenize(self.ctx, text, None, 0)
+        n = -n if n < 0 else n
+        buf = (C.c_int * max(n, 1))()
+        m = self.L.ref_tokenize(self.ctx, text, buf, n)
+        assert m == n, (m, n)
+        return list(buf[:n])
 
     def dtw_data(self):
         """Alignment-head attention of the last DTW re-decode, flat [head][n_audio_ctx][n_tok]."""
