@@ -27,7 +27,7 @@ dispatches themselves (hipExtLaunchKernel start/stop events: the first bracketed
 the last one's end, the timestamps rocprofv3 reports, no hipEventRecord marker packets in the
 interval). `roofline` reports the class with the largest such device time, its average launch time
 and, for the cross-check, the same kernel's average from the committed rocprofv3 --kernel-trace
---stats summary of this command (profiles/, ROCPROF_STATS).
+--stats summary of this command (profiles/, PROFILES[model]).
 
 cpu_baseline: the reference ggml CPU path (oracle/_ref/libwhisper_ref.so, compiled from the
 reference sources by oracle/ref/Makefile) runs ONE clip of the same workload on this host's
@@ -52,40 +52,61 @@ CLIP_SAMPLES = 480000     # 30 s at 16 kHz
 MFMA_CLASSES = {"gemm_enc", "gemm_cross", "gemm_conv", "gemm_dec_big", "gemm_logits_big", "attn_encoder"}
 MAX_TOKENS = 219          # completion at i >= max_tokens -> 220 tokens per clip
 TOP_CLASSES = 3           # classes re-timed alone for the roofline
-# kernels of each class (mangled-name patterns, for the PMC traffic lookup): the decode-row GEMM
-# epilogue 7 (EPI_F32) is the logits matmul, every other decode-row launch is gemm_dec
+# kernels of each class (mangled-name patterns, for the rocprof / PMC lookups). Decode-row GEMMs:
+# epilogue 7 (EPI_F32) is the logits matmul, every other epilogue is gemm_dec; the quantized models'
+# decode-row GEMMs are k_gemm_q5_rows (every block format). Large GEMMs: epilogue 5 (EPI_KV_CROSS) is
+# gemm_cross, 3 (EPI_CONV2) gemm_conv, the encoder's QKV / O / MLP0 / MLP1 epilogues 0, 1, 2, 4
+# gemm_enc (conv1 shares epilogue 1 with MLP0: 2 launches of 66 per step)
+_BIG = r"(?:k_gemm_8p|k_gemm_256|k_gemm_big|k_gemm_q16|k_gemm_q5_big)"
 CLASS_KERNELS = {
     "attn_cross": r"k_attn_stepILb0ELb1E",
     "attn_self": r"k_attn_stepILb[01]ELb0E",
-    "attn_encoder": r"k_attn_encoderE",
-    "gemm_dec": r"k_gemm_rowsILi(?!7E)\d+E|k_gemm_rows_reduceILi(?!7E)\d+E",
-    "gemm_logits": r"k_gemm_rowsILi7E",
+    "attn_encoder": r"k_attn_encoder(?:_sm)?E",
+    "gemm_dec": r"k_gemm_rows(?:_nt|_ln)?ILi(?!7E)\d+E|k_gemm_rows_reduceILi(?!7E)\d+E|k_gemm_q5_rowsILi(?!7E)\d+E",
+    "gemm_logits": r"k_gemm_rows(?:_nt)?ILi7E|k_gemm_q5_rowsILi7E",
     "layernorm": r"k_layernorm_f16|k_resid_layernorm",
-    "gemm_enc": r"k_gemm_256|k_gemm_bigILi[0-6]E",
+    "gemm_enc": _BIG + r"ILi[0124]E",
+    "gemm_cross": _BIG + r"ILi5E",
+    "gemm_conv": _BIG + r"ILi3E",
 }
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "pmc_fetch_summary.txt")
-# rocprofv3 --kernel-trace --stats summary of `python bench.py` on this tree (tools/gpu_round.sh ->
-# tools/prof_summary.py), committed per round
-ROCPROF_STATS = os.path.join(ROOT, "profiles", "r03_bench_kernel_stats.txt")
+# committed profiles of `python bench.py --model M` on this tree, per model (tools/gpu_profiles.sh):
+# rocprofv3 --kernel-trace --stats summary (tools/prof_summary.py) and the PMC FETCH_SIZE pass
+# (tools/pmc_summary.py). A model without its own files reports null cross-checks.
+PROFILES = {
+    "large-v3": ("profiles/r04_bench_kernel_stats.txt", "profiles/r04_pmc_fetch_summary.txt"),
+    "large-v3-turbo": ("profiles/r04_turbo_kernel_stats.txt", "profiles/r04_turbo_pmc_fetch_summary.txt"),
+    "large-v3-q5_0": ("profiles/r04_q5_kernel_stats.txt", "profiles/r04_q5_pmc_fetch_summary.txt"),
+}
 # human-readable kernel of each class (the mangled names CLASS_KERNELS matches)
 CLASS_KERNEL_NAME = {"attn_cross": "owk::k_attn_step<false, true> (one_chunk cross attention, k_attn.hip)",
-                     "attn_self": "owk::k_attn_step<*, false>", "gemm_dec": "owk::k_gemm_rows<mode, MT, J>",
-                     "gemm_enc": "owk::k_gemm_256<mode, 4, swap>", "attn_encoder": "owk::k_attn_encoder",
-                     "layernorm": "owk::k_resid_layernorm / k_layernorm_f16", "gemm_logits": "owk::k_gemm_rows<7, MT, J>"}
+                     "attn_self": "owk::k_attn_step<*, false>",
+                     "gemm_dec": "owk::k_gemm_rows_ln / k_gemm_rows / k_gemm_rows_nt <mode != 7> (F16), k_gemm_q5_rows (quantized)",
+                     "gemm_enc": "owk::k_gemm_8p<mode, swap> (F16), k_gemm_q16<mode> (quantized)",
+                     "gemm_cross": "owk::k_gemm_8p<5, swap> (F16), k_gemm_q16<5> (quantized)",
+                     "attn_encoder": "owk::k_attn_encoder",
+                     "layernorm": "owk::k_resid_layernorm / k_layernorm_f16",
+                     "gemm_logits": "owk::k_gemm_rows_nt<7, MT, J, NT> (F16), k_gemm_q5_rows<7> (quantized)"}
 
 
-def pmc_traffic(cls):
+def profile_files(model):
+    """(rocprof stats, PMC summary) paths for `model`, each None when not committed."""
+    st, pmc = PROFILES.get(model, (None, None))
+    ok = lambda p: os.path.join(ROOT, p) if p and os.path.exists(os.path.join(ROOT, p)) else None
+    return ok(st), ok(pmc)
+
+
+def pmc_traffic(cls, path):
     """HBM bytes per launch of `cls` from the committed rocprofv3 --pmc FETCH_SIZE pass of this
-    command (tools/gpu_pmc.sh -> profiles/pmc_fetch_summary.txt): the FETCH_SIZE total of the
-    class's kernels over their dispatch count. FETCH_SIZE is in KB and on gfx950 counts half the
-    bytes of wide streaming reads (MI355X_MICROARCH.md, HBM): x 1024 x 2."""
+    command (tools/gpu_profiles.sh -> PROFILES[model][1]): the FETCH_SIZE total of the class's
+    kernels over their dispatch count. FETCH_SIZE is in KB and on gfx950 counts half the bytes of
+    wide streaming reads (MI355X_MICROARCH.md, HBM): x 1024 x 2."""
     import re
 
     pat = CLASS_KERNELS.get(cls)
-    if not pat or not os.path.exists(PMC_SUMMARY):
+    if not pat or not path:
         return None
     tot, n = 0.0, 0
-    for line in open(PMC_SUMMARY):
+    for line in open(path):
         parts = line.split(None, 3)
         if len(parts) == 4 and parts[0].isdigit() and re.search(pat, parts[3]):
             n += int(parts[0])
@@ -93,14 +114,13 @@ def pmc_traffic(cls):
     return round(tot / n * 1024 * 2) if n else None
 
 
-def rocprof_avg_ms(cls, path=None):
+def rocprof_avg_ms(cls, path):
     """Average launch duration (ms) of the class's kernels in the committed rocprofv3 stats summary
     (calls-weighted over the matching kernels), or None."""
     import re
 
-    path = path or ROCPROF_STATS
     pat = CLASS_KERNELS.get(cls)
-    if not pat or not os.path.exists(path):
+    if not pat or not path:
         return None
     tot, n = 0.0, 0
     for line in open(path):
@@ -296,9 +316,10 @@ class GpuRunner:
         return base, parity
 
 
-def roofline(classes, ms_per_step, alone=None):
+def roofline(classes, ms_per_step, alone=None, model="large-v3"):
     """`roofline` of the class with the largest device time; `alone` = {class: record} of the top
     classes each timed in a step where only its launches carry events (preferred when given)."""
+    stats_path, pmc_path = profile_files(model)
     src = alone or classes
     dom = max(src, key=lambda c: src[c]["ms"])
     d = src[dom]
@@ -311,8 +332,8 @@ def roofline(classes, ms_per_step, alone=None):
         ach = d["bytes"] / (d["ms"] * 1e-3) / 1e9
         roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                 "frac": round(ach / PEAK_HBM_GBS, 4), "traffic": None}
-    roof["traffic"] = pmc_traffic(dom)
-    roof["traffic_unit"] = "bytes/launch (PMC FETCH_SIZE x2, profiles/pmc_fetch_summary.txt)"
+    roof["traffic"] = pmc_traffic(dom, pmc_path)
+    roof["traffic_unit"] = ("bytes/launch (PMC FETCH_SIZE x2, " + os.path.relpath(pmc_path, ROOT) + ")") if pmc_path else None
     roof["kernel_class"] = dom
     roof["kernel"] = CLASS_KERNEL_NAME.get(dom, dom)
     roof["measured"] = ("HIP events bound to this class's kernel dispatches on the engine stream "
@@ -323,9 +344,9 @@ def roofline(classes, ms_per_step, alone=None):
     if alone and dom in classes:
         roof["avg_launch_ms_marker_events"] = round(classes[dom]["ms"] / max(1, classes[dom]["launches"]), 5)
     roof["launches"] = d["launches"]
-    rp = rocprof_avg_ms(dom)
+    rp = rocprof_avg_ms(dom, stats_path)
     roof["rocprof_avg_launch_ms"] = rp
-    roof["rocprof_stats"] = os.path.relpath(ROCPROF_STATS, ROOT) if rp is not None else None
+    roof["rocprof_stats"] = os.path.relpath(stats_path, ROOT) if rp is not None else None
     roof["events_vs_rocprof"] = round(avg_ms / rp, 4) if rp else None
     roof["phases"] = phase_fractions(classes, ms_per_step)
     return roof
@@ -383,7 +404,7 @@ def main(argv=None, runner=None):
                 continue
             v = dict(got[c])
             alone[c] = v
-        roof = roofline(classes, 1e3 * dt / args.steps, alone or None)
+        roof = roofline(classes, 1e3 * dt / args.steps, alone or None, args.model)
         if rank == 0:
             for c, v in alone.items():
                 log(f"[bench] alone {c:16s} {v['ms']:10.2f} ms  launches {v['launches']:7d}  "

@@ -74,8 +74,8 @@ WHISPER_API int owk_debug_tokenize(const char * path_model, const char * text, i
 /* out[M][N] = A[M][K] . W[N][K]^T (f16 bits in, f32 out) through the engine's GEMM dispatch */
 WHISPER_API int owk_debug_gemm(int device, int M, int N, int K, const uint16_t * a, const uint16_t * w, float * out);
 // one large-tile epilogue mode through the 128x128 and 256x256 kernels on the same random operands: max |diff|
-// (mode | 0x800: the 8-phase 256x256 kernel instead of the 4-slot ring one; | 0x1000 / 0x2000: the 64x64 /
-// 32x32 ring tile of mid-size GEMMs against the 128x128 tile)
+// (mode alone or | 0x800: the 8-phase 256x256 kernel; | 0x1000 / 0x2000: the 64x64 / 32x32 ring tile of
+// mid-size GEMMs against the 128x128 tile)
 WHISPER_API double owk_debug_gemm_epi_diff(int device, int mode, int M, int N, int K, int d, int T);
 /* average microseconds per launch of `iters` back-to-back engine GEMMs (epilogue `mode`, zero data) */
 /* test hook (host only): the DTW alignment of captured alignment-head attention
@@ -112,14 +112,20 @@ WHISPER_API int owk_debug_gemm_quant2(int device, int fmt, int M, int N, int K, 
  * expansion the GEMMs run on (wi [N][kx] f16 bits, dwt [kx/32][N] f32; either may be NULL) and the f32
  * row dequantization of the token embedding (deq [N][K], may be NULL); 0 on success */
 WHISPER_API int owk_debug_kquant(int fmt, int N, int K, const uint8_t * w_blocks, uint16_t * wi, float * dwt, float * deq);
-/* mode | 0x100: force the 128x128 large-GEMM kernel; | 0x400: 5-slot ring variant of the 256x256 kernel;
- * | 0x800: the 8-phase 256x256 kernel; | 0x1000 / 0x2000: the 64x64 / 32x32 ring tile;
+/* mode | 0x100: force the 128x128 large-GEMM kernel; (default, or | 0x800) the 8-phase 256x256 kernel; | 0x1000 / 0x2000: the 64x64 / 32x32 ring tile;
  * | 0x200: uniform random operands (else zeros) */
 WHISPER_API double owk_debug_gemm_bench(int device, int mode, int M, int N, int K, int iters);
 /* the decoder's per-layer matmul + residual/LayerNorm chain (no attention) of a large-v3-shaped model,
  * R rows, distinct random weights per layer, one captured hipGraph: device microseconds per layer */
 WHISPER_API double owk_debug_decode_chain(int device, int R, int n_layers, int iters);
 
+/* test hook: the decoder's LayerNorm-prologue GEMM (M <= 32 rows, K <= 1280) against layernorm + GEMM, EPI_F16
+ * with bias b (may be NULL), f16 bits out [M][N]; with w2 / resid (may be NULL): the whole-K residual epilogue of
+ * an [N][4N] matmul against split-K partials + resid_layernorm, f32 [M][N] each (out_resid_* may be NULL) */
+WHISPER_API int owk_debug_gemm_rows_ln(int device, int M, int N, int K, const float * x, const float * lnw,
+                                       const float * lnb, const float * b, const uint16_t * w, uint16_t * out_fused,
+                                       uint16_t * out_ref, const uint16_t * w2, const float * resid,
+                                       float * out_resid_full, float * out_resid_split);
 /* library identity: 1 when the gfx950 HIP code object is present and a device is usable */
 WHISPER_API int owk_device_ok(int device);
 WHISPER_API const char * owk_build_info(void);

@@ -720,37 +720,38 @@ void Engine::launch_decode(const DecShape & sh) {
         attn_decoder(stream, qv, d, cross_k_.as<_Float16>() + l * cross_stride, cross_v_.as<_Float16>() + l * cross_stride,
                      64, T * 64, d_rc, R, nullptr, H, kq_scale, T, o16, d, cross_oc, cross_tl, o32, true, q8, q8d);
     };
-    // R <= 32 rows (F16 weights): each residual matmul (attn.out, cross_attn.out, mlp.2) writes
-    // split-K partial tiles and resid_layernorm adds them with bias + residual and emits the next
-    // LayerNorm's f16 rows (one launch where a full-epilogue GEMM plus a LayerNorm were). Round 2
-    // measured the alternatives slower and removed them (profiles/r02e_ab.txt: LayerNorm inside
-    // the consumer GEMM 846 RTF, statistics-producing residual GEMMs 806, against 923; two row
-    // groups on two streams 744). soft_max rows (flash_attn = false) and DTW captures run the
-    // soft_max attention launches inside the same chain. Larger passes use the full-epilogue
-    // GEMMs and separate LayerNorms.
-    const bool fused = R <= 32 && !q5;
+    // R <= 32 rows (F16 weights), 8 launches per layer: every matmul whose input is a LayerNorm output
+    // (attn QKV, cross_attn.query, mlp.0) runs that LayerNorm in its prologue from the f32 residual
+    // stream (gemm_rows_ln), and every residual matmul (attn.out, cross_attn.out, mlp.2) adds its bias
+    // and the residual in its epilogue over the whole K in one block (EPI_RESID_F32, in place on x).
+    // Round 4: replaces split-K partial tiles + a resid_layernorm launch per residual matmul (11
+    // launches per layer); measured alternatives of earlier rounds (profiles/r02e_ab.txt, the round-3
+    // ticket finish in tools/lab_gemv.hip) lost on the launch boundary or the in-launch seam. soft_max
+    // rows (flash_attn = false) and DTW captures run the soft_max attention launches inside the same
+    // chain. Larger passes use the full-epilogue GEMMs and separate LayerNorms.
+    const bool fused = R <= 32 && !q5 && gemm_rows_ln_applies(R, 4 * hp.n_text_state, hp.n_text_state);
 
     auto fused_rows = [&]() {
         hipStream_t s = stream;
         float * x = d_x_.as<float>();
-        _Float16 * xn = d_xn_.as<_Float16>();
         _Float16 * qb = d_q_.as<_Float16>();
         _Float16 * aob = d_ao_.as<_Float16>();
         _Float16 * hr = d_h_.as<_Float16>();
         const int n = R;
-        auto gemm_rows = [&](int mode, int N, int K, const _Float16 * A, const _Float16 * Wt, const EpiParams & ep) {
-            ProfScope ps(prof, s, "gemm_dec", 2.0 * n * (double) N * K, 2.0 * ((double) n * K + (double) N * K));
-            gemm(s, mode, n, N, K, A, K, nullptr, K, ep, &gws_, Wt);
+        // algorithmic bytes: the weights once, the activation rows once (f32 for the LayerNorm prologue)
+        auto gemm_ln = [&](int mode, int N, const float * lnw, const float * lnb, const _Float16 * Wt,
+                           const EpiParams & ep) {
+            ProfScope ps(prof, s, "gemm_dec", 2.0 * n * (double) N * d, 2.0 * (double) N * d + 4.0 * n * d);
+            gemm_rows_ln(s, mode, n, N, d, x, lnw, lnb, hp.eps, Wt, ep);
         };
-        // residual matmul as partial tiles + resid_layernorm (lnw null: residual only). (Round 3
-        // measured the finish inside the matmul launch -- write-through partials, an agent-scope
-        // ticket, the last blocks polling the arrivals and doing the rows -- slower: the per-layer
-        // chain 51.6 -> 58.1 us, tools/chain_sweep.py; the tail costs more than the boundary.)
-        auto resid_ln = [&](const _Float16 * A, const _Float16 * Wt, int K, const float * bias, const float * lnw,
-                            const float * lnb) {
-            gemm_rows(EPI_PARTIAL, d, K, A, Wt, EpiParams());
-            ProfScope ps(prof, s, "layernorm");
-            resid_layernorm(s, n, d, gemm_partial_splits(K), gws_.partial, bias, x, lnw, lnb, hp.eps, xn, d);
+        auto resid = [&](const _Float16 * A, const _Float16 * Wt, int K, const float * bias) {
+            ProfScope ps(prof, s, "gemm_dec", 2.0 * n * (double) d * K, 2.0 * ((double) n * K + (double) d * K));
+            EpiParams ep;
+            ep.bias = bias;
+            ep.resid = x;
+            ep.out32 = x;
+            ep.ldo = d;
+            gemm(s, EPI_RESID_F32, n, d, K, A, K, nullptr, K, ep, &gws_, Wt);
         };
         for (int l = 0; l < hp.n_text_layer; ++l) {
             const DecLayerW & L = m->dec[l];
@@ -768,9 +769,7 @@ void Engine::launch_decode(const DecShape & sh) {
                 ep.d = d;
                 ep.row_off = d_rowoff;
                 ep.Tpad = kv_cells * 64;
-                // the attn_ln output: the previous layer's resid_layernorm (layer 0: the LayerNorm
-                // launch before the chain)
-                gemm_rows(EPI_QKV_DEC, 3 * d, d, xn, L.t_qkv, ep);
+                gemm_ln(EPI_QKV_DEC, 3 * d, L.attn_ln_w, L.attn_ln_b, L.t_qkv, ep);
             }
             {
                 ProfScope ps(prof, s, "attn_self");
@@ -780,13 +779,13 @@ void Engine::launch_decode(const DecShape & sh) {
                     attn_decoder_softmax(s, qb, d, Kl, Vl, 64, kv_cells * 64, d_rs, n, d_keys, H, 1.0f, max_keys, aob,
                                          d, nullptr, nullptr, 0, nullptr);
             }
-            resid_ln(aob, L.t_o, d, L.b_o, L.cross_ln_w, L.cross_ln_b);
+            resid(aob, L.t_o, d, L.b_o);
             {
                 EpiParams ep;
                 ep.bias = L.cb_q;
                 ep.out16 = qb;
                 ep.ldo = d;
-                gemm_rows(EPI_F16, d, d, xn, L.t_cq, ep);
+                gemm_ln(EPI_F16, d, L.cross_ln_w, L.cross_ln_b, L.t_cq, ep);
             }
             {
                 ProfScope ps(prof, s, "attn_cross", 4.0 * n * (double) n_ctx_pad * d, 2.0 * 2.0 * n * (double) T * d);
@@ -797,17 +796,16 @@ void Engine::launch_decode(const DecShape & sh) {
                                          kq_scale, T, aob, d, sh.capture ? amap_.as<int>() + l * H : nullptr,
                                          sh.capture ? cap_.as<float>() : nullptr, R, nullptr);
             }
-            resid_ln(aob, L.t_co, d, L.cb_o, L.mlp_ln_w, L.mlp_ln_b);
+            resid(aob, L.t_co, d, L.cb_o);
             {
                 EpiParams ep;
                 ep.bias = L.b_mlp0;
                 ep.gelu_tab = m->gelu_tab;
                 ep.out16 = hr;
                 ep.ldo = 4 * d;
-                gemm_rows(EPI_GELU_F16, 4 * d, d, xn, L.t_mlp0, ep);
+                gemm_ln(EPI_GELU_F16, 4 * d, L.mlp_ln_w, L.mlp_ln_b, L.t_mlp0, ep);
             }
-            const DecLayerW * nx = l + 1 < hp.n_text_layer ? &m->dec[l + 1] : nullptr;
-            resid_ln(hr, L.t_mlp1, 4 * d, L.b_mlp1, nx ? nx->attn_ln_w : nullptr, nx ? nx->attn_ln_b : nullptr);
+            resid(hr, L.t_mlp1, 4 * d, L.b_mlp1);
         }
     };
     auto resid_full = [&](const _Float16 * A, const float * A32, const _Float16 * W, const _Float16 * Wt,
@@ -824,10 +822,7 @@ void Engine::launch_decode(const DecShape & sh) {
         layernorm_f16(stream, d_x_.as<float>(), R, d, w, b, hp.eps, d_xn_.as<_Float16>(), d, nullptr, xn32, q8a(),
                       q8d());
     };
-    if (fused) {
-        ln(m->dec[0].attn_ln_w, m->dec[0].attn_ln_b);  // layer 0's attn_ln of the embeddings
-        fused_rows();
-    }
+    if (fused) fused_rows();
     // quantized decode passes of <= 32 rows (the bench's greedy steps): the residual matmuls (attn.out,
     // cross_attn.out, mlp.2) write split-K partial tiles and resid_layernorm adds them to the residual
     // stream with bias and emits the next LayerNorm as f16 AND as Q8_0 rows (the next GEMM's operand):

@@ -869,12 +869,9 @@ void attn_decoder_softmax(hipStream_t s, const _Float16 * q, int ldq, const _Flo
                           float * out32) {
     if (n_rows <= 0) return;
     if (max_keys > SM_MAX_KEYS) throw std::runtime_error("attn_decoder_softmax: too many keys");
-    // outputs do not depend on the width (k_attn_softmax); OWK_SM_WIDE=0 keeps 256 threads (tests)
-    static const bool wide_ok = [] {
-        const char * v = getenv("OWK_SM_WIDE");
-        return !(v && atoi(v) == 0);
-    }();
-    if (wide_ok && n_rows * H <= 128)
+    // outputs do not depend on the width (k_attn_softmax): 1024 threads when the pass has few
+    // (row, head) blocks (configs[4]'s one-row steps), 256 otherwise
+    if (n_rows * H <= 128)
         OWK_LAUNCH(k_attn_softmax<1024>, dim3(H, n_rows), dim3(1024), 0, s, q, ldq, kbase, vbase, ld_kv, hs, rows_dev,
                            key_idx, scale, out, ldo, amap, cap, cap_rows, out32);
     else

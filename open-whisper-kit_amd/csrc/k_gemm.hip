@@ -365,7 +365,7 @@ __global__ __launch_bounds__(256, 2) void k_gemm_big(int M, int N, int K, const 
 // step-j DMA landed, later steps stay in flight) -> s_barrier (every wave's step-j DMA landed,
 // every wave done with step j-1) -> issue step j+7 into step j-1's slot -> 4 MFMAs per wave.
 // 4 waves (2 x 2) of 32 x 32. Same MFMA sequence per output as k_gemm_big (32-deep K steps in
-// ascending order): bit-identical results. LDS image as k_gemm_256 (64-B rows, 16-B chunk c of
+// ascending order): bit-identical results. LDS image: 64-B rows, 16-B chunk c of
 // row r at c ^ ((r >> 2) & 3), swizzle applied on the global source address).
 // ---------------------------------------------------------------------------------
 constexpr int GM_K = 32, GM_SLOTS = 8;
@@ -470,24 +470,14 @@ __global__ __launch_bounds__(TM * 4) void k_gemm_mid(int M, int N, int K, const 
 }
 
 // ---------------------------------------------------------------------------------
-// 256x256 block tile for the large encoder / cross-KV GEMMs (M = clips x 1500 rows).
-// 8 waves (2 in M x 4 in N), each 128x64 of the output = 8 x 4 MFMA 16x16x32 tiles
-// (128 accumulators). K advances in 32-deep steps through a 4-slot LDS ring
-// (slot = 256 x 32 f16 of A + of W = 32 KB, 128 KB in all, one block per CU):
-//   top of step j: s_waitcnt vmcnt(4) (this wave's step-j DMA landed; step j+1's 4
-//   global_load_lds stay in flight) -> s_barrier (every wave's step-j DMA landed, and
-//   every wave is done reading step j-2's slot) -> issue step j+2 into that slot ->
-//   read fragments + 32 MFMAs of step j.
-// Two K-steps stay in flight across every barrier (the "pipelining across barriers"
-// rule of the CDNA guide: counted vmcnt, raw s_barrier, one __shared__ array), so the
-// loop never drains the DMA queue. LDS image: 64-B rows (32 f16), 16-B chunk c of row r
-// stored at chunk c ^ ((r >> 2) & 3) -- the swizzle is applied to the global source
-// address of each lane (global_load_lds writes lane-linear), and the ds_read_b128 of 16
-// consecutive rows then hits 16 distinct 16-B bank groups.
+// 256x256 block tiles for the large encoder / cross-KV GEMMs (M = clips x 1500 rows): k_gemm_8p below
+// (and the quantized k_gemm_q16 with 128-row tiles). Round 2's 4/5-slot ring version (32-deep K-steps,
+// two in flight across each barrier) was superseded by the 8-phase schedule (profiles/
+// r03s6_gemm_8phase_vs_ring.txt: 8-17 % faster on every encoder shape) and removed in round 4.
+// LDS images use 16-B chunks XOR-swizzled by row so the ds_read_b128 of 16 consecutive rows hit 16
+// distinct bank groups.
 // ---------------------------------------------------------------------------------
 constexpr int G2_M = 256, G2_N = 256, G2_K = 32;
-constexpr int G2_OP = G2_M * G2_K * 2;     // 16 KB: one operand of one K-step
-constexpr int G2_SLOT = 2 * G2_OP;         // 32 KB
 
 // Tile of the (XCD-remapped, so per-XCD contiguous) index t: groups of TO_GM row panels swept column
 // by column, so the ~32 tiles an XCD runs at once cover 8 row panels x 4 column panels -- A and W
@@ -511,208 +501,6 @@ __device__ __forceinline__ void tile_order(int t, int ntiles, int nbn, int & bm,
     bn = r / gm;
 }
 
-template <int MODE, int G2_SLOTS, bool SWAP = true>
-__global__ __launch_bounds__(512, 2) void k_gemm_256(int M, int N, int K, const _Float16 * __restrict__ A, int lda,
-                                                     const _Float16 * __restrict__ W, int ldw, EpiParams ep) {
-    // G2_SLOTS ring slots: G2_SLOTS - 2 K-steps stay in flight past every barrier
-    static_assert(G2_SLOTS == 4 || G2_SLOTS == 5, "ring depth");
-    constexpr int AHEAD = G2_SLOTS - 2;  // steps issued beyond the one being computed
-    constexpr int SLOT = G2_SLOT;
-    __shared__ __attribute__((aligned(1024))) char smem[G2_SLOTS * SLOT];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int wr = wave >> 2, wc = wave & 3;
-
-    const int nbn = (N + G2_N - 1) / G2_N;
-    const int nb = gridDim.x;
-    int bid = blockIdx.x;
-    {  // XCD-aware order: a run of consecutive tiles (one A row panel) per XCD
-        const int xcd = bid & 7, q = nb >> 3, rr = nb & 7;
-        const int base = xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q;
-        bid = base + (bid >> 3);
-    }
-    int bm, bn;
-    tile_order(bid, nb, nbn, bm, bn);
-    const int m0 = bm * G2_M, n0 = bn * G2_N;
-
-    // Output layout. Q/K-type tiles ("swap": every mode except the V tiles of EPI_QKV_ENC) compute
-    // C^T = W . A^T: the W fragment is the MFMA's A operand, so a lane's accumulator elements run
-    // along N -- with the W rows permuted (offB below), lane (g, l16) of row tile i holds columns
-    // wc*64 + g*8 + (0..7) and + 32 + (0..7) of row wr*128 + i*16 + l16: two 8-column runs, stored
-    // by epi_row8 as 16-byte vectors. V tiles of EPI_QKV_ENC keep C = A . W^T (4 consecutive rows
-    // per lane = 4 consecutive key positions of the transposed V image).
-    // (a compile-time choice: a runtime one made hipcc drain the DMA queue at the branch joins,
-    // 8x slower; EPI_QKV_ENC launches its V columns separately with SWAP = false, ep.c_off = 2d)
-    constexpr bool swap = SWAP;
-
-    // staging: wave w issues row groups 2w, 2w+1 (16 rows x 64 B each) of A and of W. A rows are
-    // stored with 16-B chunk c at c ^ ((r >> 2) & 3); W rows at c ^ wsw(r), which keeps both W
-    // fragment row orders (16 consecutive rows, or the permuted rows of swap tiles) conflict-free
-    auto wsw = [](int r) { return ((r >> 2) ^ (r >> 3)) & 3; };
-    const int srow0 = wave * 32 + (lane >> 2);
-    const _Float16 * ga[2];
-    const _Float16 * gw[2];
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-        const int row = srow0 + i * 16;
-        ga[i] = A + (size_t) min(m0 + row, M - 1) * lda + ((lane & 3) ^ ((row >> 2) & 3)) * 8;
-        gw[i] = W + (size_t) min(n0 + row, N - 1) * ldw + ((lane & 3) ^ wsw(row)) * 8;
-    }
-    auto stage = [&](int slot, int k0) {
-        char * sA = smem + slot * SLOT + wave * 2048;
-        char * sB = sA + G2_OP;
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            __builtin_amdgcn_global_load_lds((const void *) (ga[i] + k0), (lds_ptr_t) (sA + i * 1024), 16, 0, 0);
-            __builtin_amdgcn_global_load_lds((const void *) (gw[i] + k0), (lds_ptr_t) (sB + i * 1024), 16, 0, 0);
-        }
-    };
-
-    floatx4 acc[8][4];
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
-
-    // fragment addresses (byte offsets inside an operand image): row r, logical chunk g
-    const int g = lane >> 4, l16 = lane & 15;
-    int offA[8], offB[4];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        const int r = wr * 128 + i * 16 + l16;
-        offA[i] = r * 64 + ((g ^ ((r >> 2) & 3)) << 4);
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        // swap: fragment j's row p = W row wc*64 + (j>>1)*32 + (p>>2)*8 + (j&1)*4 + (p&3), so that
-        // accumulator element e of lane group g is column wc*64 + (j>>1)*32 + g*8 + (j&1)*4 + e
-        const int r = swap ? wc * 64 + (j >> 1) * 32 + (l16 >> 2) * 8 + (j & 1) * 4 + (l16 & 3) : wc * 64 + j * 16 + l16;
-        offB[j] = r * 64 + ((g ^ wsw(r)) << 4);
-    }
-
-    const int nk = K / G2_K;
-    // waits for step `next` while steps next+1 .. next+AHEAD-1 (those issued) stay in flight
-    auto wait_step = [&](int next) {
-        const int later = min(AHEAD - 1, nk - 1 - next);
-        if (later >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-        else if (later == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    };
-    // prologue: steps 0 .. AHEAD-1 in flight, step 0 landed, step AHEAD issued, first fragments read
-#pragma unroll
-    for (int i = 0; i < AHEAD; ++i)
-        if (i < nk) stage(i, i * G2_K);
-    wait_step(0);
-    __builtin_amdgcn_s_barrier();
-    if (AHEAD < nk) stage(AHEAD, AHEAD * G2_K);
-    half8 b[4], a[2];
-#pragma unroll
-    for (int t = 0; t < 4; ++t) b[t] = *(const half8 *) (smem + G2_OP + offB[t]);
-    a[0] = *(const half8 *) (smem + offA[0]);
-    a[1] = *(const half8 *) (smem + offA[1]);
-    // step j = 4 groups of 8 MFMAs (2 row tiles x 4 column tiles); the fragments of the next
-    // group -- across the step boundary: of step j+1, after its DMA wait + barrier -- are read
-    // before the current group's MFMAs are issued, so LDS latency hides behind them
-    int slot = 0;
-    for (int j = 0; j < nk; ++j) {
-        const char * sA = smem + slot * SLOT;
-        const int nslot = slot + 1 == G2_SLOTS ? 0 : slot + 1;
-        half8 bn[4], an[2];
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            if (g < 3) {
-                an[0] = *(const half8 *) (sA + offA[2 * g + 2]);
-                an[1] = *(const half8 *) (sA + offA[2 * g + 3]);
-            } else if (j + 1 < nk) {
-                // step j+1 landed for every wave (this wave: counted vmcnt; all: barrier), and
-                // every wave is done with step j-1's slot: restage it with step j+1+AHEAD
-                wait_step(j + 1);
-                __builtin_amdgcn_s_barrier();
-                if (j + 1 + AHEAD < nk) {
-                    const int fs = slot == 0 ? G2_SLOTS - 1 : slot - 1;  // (j - 1) mod G2_SLOTS
-                    stage(fs, (j + 1 + AHEAD) * G2_K);
-                }
-                const char * nA = smem + nslot * SLOT;
-#pragma unroll
-                for (int t = 0; t < 4; ++t) bn[t] = *(const half8 *) (nA + G2_OP + offB[t]);
-                an[0] = *(const half8 *) (nA + offA[0]);
-                an[1] = *(const half8 *) (nA + offA[1]);
-            }
-            // keep the order: next fragments' ds_reads issued, then this group's MFMAs (the
-            // scheduler would otherwise consume each read right after issuing it)
-            __builtin_amdgcn_sched_barrier(0);
-            if (swap) {
-#pragma unroll
-                for (int i = 0; i < 2; ++i)
-#pragma unroll
-                    for (int t = 0; t < 4; ++t)
-                        acc[2 * g + i][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(b[t], a[i], acc[2 * g + i][t], 0, 0, 0);
-            } else {
-#pragma unroll
-                for (int i = 0; i < 2; ++i)
-#pragma unroll
-                    for (int t = 0; t < 4; ++t)
-                        acc[2 * g + i][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[i], b[t], acc[2 * g + i][t], 0, 0, 0);
-            }
-            __builtin_amdgcn_sched_barrier(0);
-            a[0] = an[0];
-            a[1] = an[1];
-        }
-#pragma unroll
-        for (int t = 0; t < 4; ++t) b[t] = bn[t];
-        slot = nslot;
-    }
-
-    if (swap) {
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            const int r = m0 + wr * 128 + i * 16 + l16;
-            if (r >= M) continue;
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                const int c = n0 + wc * 64 + h * 32 + g * 8;
-                const float v[8] = {acc[i][2 * h][0], acc[i][2 * h][1], acc[i][2 * h][2], acc[i][2 * h][3],
-                                    acc[i][2 * h + 1][0], acc[i][2 * h + 1][1], acc[i][2 * h + 1][2], acc[i][2 * h + 1][3]};
-                if (c + 8 <= N) {
-                    epi_row8<MODE>(ep, r, c, v, ep.vec != 0);
-                } else {
-#pragma unroll
-                    for (int e = 0; e < 8; ++e)
-                        if (c + e < N) epi_store<MODE>(ep, r, c + e, v[e]);
-                }
-            }
-        }
-        return;
-    }
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int cl = n0 + wc * 64 + j * 16 + l16;  // launch column; c: the epilogue's column
-            const int c = cl + ep.c_off;
-            const int r0 = m0 + wr * 128 + i * 16 + 4 * g;
-            if constexpr (MODE == EPI_QKV_ENC) {
-                // V columns -> the transposed [clip][head][dim][Tpad] image: a lane's 4 rows are 4
-                // consecutive t of one clip (T % 4 == 0, r0 % 4 == 0): one 8-byte store
-                const int d = ep.d;
-                if (c >= 2 * d && cl < N && r0 + 3 < M && ep.T % 4 == 0) {
-                    const int cc = c - 2 * d;
-                    const int clip = r0 / ep.T, t = r0 - clip * ep.T;
-                    const float bv = ep.bias2[cc];
-                    half4 hv;
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) hv[e] = (_Float16) (acc[i][j][e] + bv);
-                    *(half4 *) (ep.out16c + (((size_t) clip * (d >> 6) + (cc >> 6)) * 64 + (cc & 63)) * ep.Tpad + t) = hv;
-                    continue;
-                }
-            }
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const int r = r0 + e;
-                if (r < M && cl < N) epi_store<MODE>(ep, r, c, acc[i][j][e]);
-            }
-        }
-}
-
 // ---------------------------------------------------------------------------------
 // 256x256 block tile with the CDNA guide's 8-phase schedule (round 3; cdna_hip_programming.md §5
 // "The 256^2 8-phase template"): K-tiles of 64, two LDS buffers of 64 KB (even / odd tiles), each
@@ -731,7 +519,7 @@ __global__ __launch_bounds__(512, 2) void k_gemm_256(int M, int N, int K, const 
 // takes an extra s_barrier first, wave row 0 one at the end), so one row's MFMAs overlap the other's LDS
 // reads. 16-B chunk c of part row r is stored at chunk c ^ sw8(r): conflict-free ds_read_b128 for 16
 // consecutive rows (A) and for the permuted W rows of the C^T tiles. Output and epilogues as
-// k_gemm_256 (SWAP: C^T tiles, 16-byte vector epilogues).
+// round 2's ring kernel (SWAP: C^T tiles, 16-byte vector epilogues).
 // ---------------------------------------------------------------------------------
 constexpr int G8_K = 64;
 constexpr int G8_PART = 128 * G8_K * 2;  // 16 KB
@@ -750,7 +538,7 @@ __global__ __launch_bounds__(512, 1) void k_gemm_8p(int M, int N, int K, const _
     const int nbn = (N + G2_N - 1) / G2_N;
     const int nb = gridDim.x;
     int bid = blockIdx.x;
-    {  // XCD-aware order, then the grouped tile order of k_gemm_256
+    {  // XCD-aware order, then the grouped tile order (tile_order)
         const int xcd = bid & 7, q = nb >> 3, rr = nb & 7;
         const int base = xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q;
         bid = base + (bid >> 3);
@@ -794,7 +582,7 @@ __global__ __launch_bounds__(512, 1) void k_gemm_8p(int M, int N, int K, const _
     }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-        // swap: W frag j row p = wc*64 + (j>>1)*32 + (p>>2)*8 + (j&1)*4 + (p&3) (k_gemm_256's permutation)
+        // swap: W frag j row p = wc*64 + (j>>1)*32 + (p>>2)*8 + (j&1)*4 + (p&3) (the C^T tiles' row permutation)
         const int pr = SWAP ? wc * 32 + (l16 >> 2) * 8 + (j & 1) * 4 + (l16 & 3) : wc * 32 + (j & 1) * 16 + l16;
         offW[j] = pr * 128 + ((g ^ sw8(pr)) << 4);
     }
@@ -946,7 +734,7 @@ __global__ __launch_bounds__(512, 1) void k_gemm_8p(int M, int N, int K, const _
 // (|sum| <= 32 * 127 * 16 < 2^24) that enters the f32 accumulator as
 // acc = fma(dot, d_w * d_a, acc) -- ggml_vec_dot_q5_0_q8_0's per-block term (the f32 product of the
 // two f16 scales, fused multiply-add). Block 128 x 256, 8 waves of 64 x 64 (acc 64 registers: the
-// per-block scaling needs the room a 256-row tile does not leave), the ring of k_gemm_256 (4 slots,
+// per-block scaling needs the room a 256-row tile does not leave), a ring of 32-deep K-steps (4 slots,
 // two K-steps in flight across each barrier, counted vmcnt) carrying 128 A rows, 256 W rows and the
 // step's 128 + 256 scales (da / dw block-major; da rows permuted so a lane's 4 rows are one float4).
 // Output: C^T tiles (lane = 16 consecutive columns of one row), epi_row8 vector epilogues.
@@ -967,7 +755,7 @@ __global__ __launch_bounds__(512, 2) void k_gemm_q16(int M, int N, int K, const 
     const int nbn = (N + G2_N - 1) / G2_N;
     const int nbt = gridDim.x;
     int bid = blockIdx.x;
-    {  // XCD-aware order (k_gemm_256)
+    {  // XCD-aware order
         const int xcd = bid & 7, q = nbt >> 3, rr = nbt & 7;
         const int base = xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q;
         bid = base + (bid >> 3);
@@ -1367,6 +1155,178 @@ __global__ __launch_bounds__(GR_MAXW * 64) void k_gemm_rows_nt(int M, int N, int
     }
 }
 
+// k_gemm_rows_nt with the decoder's LayerNorm in the prologue (F16 weights, M <= 32 rows, K = the
+// LayerNorm width, one k split): A = f16(LayerNorm(x)) of the residual stream x [M][K] f32 -- what a
+// separate resid_layernorm launch wrote as f16 rows before (ggml_norm + mul + add, ref whisper.cpp:
+// 2528-2536, 2638-2646, 2750-2758). The waves of a block cover all K / 32 k-steps between them: each
+// loads its k range of x for every row (the f32 values its MFMA A fragments are made of), the row
+// statistics are combined over the waves in LDS in fixed wave order (mean = the f32 of the double sum
+// / N; variance = the double sum of the f32-rounded centred squares / N, scale = 1 / sqrtf(var + eps),
+// as resid_layernorm / ggml_norm, ops.cpp:3578-3623), and every lane forms its fragments in registers:
+// no LDS image of the rows, no extra launch. The weight tiles are requested right after the x slices,
+// so the statistics are computed while the weights stream in.
+constexpr int GRL_MAXW = 10;  // waves per block: K <= GRL_MAXW * J * 32
+template <int MODE, int MT, int J, int NT>
+__global__ __launch_bounds__(GRL_MAXW * 64) void k_gemm_rows_ln(int M, int N, int K, const float * __restrict__ x,
+                                                               const float * __restrict__ lnw,
+                                                               const float * __restrict__ lnb, float eps,
+                                                               const _Float16 * __restrict__ Wt, EpiParams ep) {
+    __shared__ floatx4 red[GRL_MAXW][NT][MT][64];
+    __shared__ double rs[2][GRL_MAXW][MT * 16];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = blockDim.x >> 6;
+    const int ntiles = (N + 15) >> 4, t0 = blockIdx.x * NT;
+    const int nsteps = K >> 5;
+    const int ks0 = wave * J;
+    const int nj = max(0, min(J, nsteps - ks0));
+    const int cl = 8 * (lane >> 4);  // this lane's 8 columns inside a 32-wide k-step
+    // x slices of this wave: rows i*16 + (lane & 15), columns (ks0 + j) * 32 + cl .. + 7
+    float4 xv[MT][J][2];
+#pragma unroll
+    for (int i = 0; i < MT; ++i) {
+        const float * xr = x + (size_t) min(i * 16 + (lane & 15), M - 1) * K + cl;
+#pragma unroll
+        for (int j = 0; j < J; ++j) {
+            const float4 * p = (const float4 *) (xr + min(ks0 + j, nsteps - 1) * 32);
+            xv[i][j][0] = p[0];
+            xv[i][j][1] = p[1];
+        }
+    }
+    half8 b[NT][J];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+        const _Float16 * wp = Wt + ((size_t) min(t0 + t, ntiles - 1) * nsteps) * 512 + lane * 8;
+#pragma unroll
+        for (int j = 0; j < J; ++j)
+            b[t][j] = __builtin_nontemporal_load((const half8 *) (wp + (size_t) min(ks0 + j, nsteps - 1) * 512));
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    const half8 z8 = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int j = 0; j < J; ++j)
+            if (j >= nj) b[t][j] = z8;
+
+    // row sums: this lane's 8 columns x nj k-steps, then the 4 lanes of a row, then the waves
+    auto lane_group_sum = [&](double v) {
+        v += __shfl_xor(v, 16);
+        v += __shfl_xor(v, 32);
+        return v;
+    };
+    float mean[MT], scale[MT];
+#pragma unroll
+    for (int i = 0; i < MT; ++i) {
+        double s = 0.0;
+#pragma unroll
+        for (int j = 0; j < J; ++j) {
+            if (j < nj) {
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const float4 v = xv[i][j][h];
+                    s += ((double) v.x + (double) v.y) + ((double) v.z + (double) v.w);
+                }
+            }
+        }
+        s = lane_group_sum(s);
+        if (lane < 16) rs[0][wave][i * 16 + lane] = s;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < MT; ++i) {
+        double s = 0.0;
+        for (int w = 0; w < nw; ++w) s += rs[0][w][i * 16 + (lane & 15)];
+        mean[i] = (float) s / (float) K;
+        double v = 0.0;
+#pragma unroll
+        for (int j = 0; j < J; ++j) {
+            if (j < nj) {
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const float4 q = xv[i][j][h];
+                    const float tx = q.x - mean[i], ty = q.y - mean[i], tz = q.z - mean[i], tw = q.w - mean[i];
+                    v += ((double) (tx * tx) + (double) (ty * ty)) + ((double) (tz * tz) + (double) (tw * tw));
+                }
+            }
+        }
+        v = lane_group_sum(v);
+        if (lane < 16) rs[1][wave][i * 16 + lane] = v;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < MT; ++i) {
+        double v = 0.0;
+        for (int w = 0; w < nw; ++w) v += rs[1][w][i * 16 + (lane & 15)];
+        const float var = (float) (v / (double) K);
+        scale[i] = 1.0f / sqrtf(var + eps);
+    }
+    // A fragments: f16((x - mean) * scale * w + b), the reference's separate roundings
+    half8 a[MT][J];
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+        const int c = min(ks0 + j, nsteps - 1) * 32 + cl;
+        const float4 w0 = *(const float4 *) (lnw + c), w1 = *(const float4 *) (lnw + c + 4);
+        const float4 b0 = *(const float4 *) (lnb + c), b1 = *(const float4 *) (lnb + c + 4);
+        const float wv[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+        const float bv[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+#pragma unroll
+        for (int i = 0; i < MT; ++i) {
+            const float xs[8] = {xv[i][j][0].x, xv[i][j][0].y, xv[i][j][0].z, xv[i][j][0].w,
+                                 xv[i][j][1].x, xv[i][j][1].y, xv[i][j][1].z, xv[i][j][1].w};
+            half8 h;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) h[e] = (_Float16) ((xs[e] - mean[i]) * scale[i] * wv[e] + bv[e]);
+            a[i][j] = j < nj ? h : z8;
+        }
+    }
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+        floatx4 acc[MT];
+#pragma unroll
+        for (int i = 0; i < MT; ++i) acc[i] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int j = 0; j < J; ++j)
+#pragma unroll
+            for (int i = 0; i < MT; ++i) acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[i][j], b[t][j], acc[i], 0, 0, 0);
+#pragma unroll
+        for (int i = 0; i < MT; ++i) red[wave][t][i][lane] = acc[i];
+    }
+    __syncthreads();
+    for (int o = tid; o < NT * MT * 256; o += blockDim.x) {
+        const int t = o / (MT * 256), q = o - t * (MT * 256);
+        const int r = q >> 4, cc = q & 15;
+        const int i = r >> 4, rr = r & 15;
+        const int ln = 16 * (rr >> 2) + cc, e = rr & 3;
+        float sum = ((const float *) &red[0][t][i][ln])[e];
+        for (int w = 1; w < nw; ++w) sum += ((const float *) &red[w][t][i][ln])[e];
+        const int c = (t0 + t) * 16 + cc;
+        if (r < M && c < N) epi_store<MODE>(ep, r, c, sum);
+    }
+}
+
+template <int MODE> struct LaunchRowsLn {
+    static void run(hipStream_t s, int M, int N, int K, const float * x, const float * lnw, const float * lnb, float eps,
+                    const _Float16 * Wt, const EpiParams & ep) {
+        const int nsteps = K / 32;
+        const int J = nsteps <= 2 * GRL_MAXW ? 2 : 4;
+        const int nw = (nsteps + J - 1) / J;
+        const int tiles = (N + 15) / 16;
+        // two column tiles per block where that still gives >= 128 blocks (QKV, MLP0); one otherwise
+        const int nt = (tiles + 1) / 2 >= 128 ? 2 : 1;
+        const dim3 g((tiles + nt - 1) / nt);
+        const bool one = M <= 16;
+#define OWK_ROWS_LN_GO(MT_, J_, NT_) \
+    OWK_LAUNCH((k_gemm_rows_ln<MODE, MT_, J_, NT_>), g, dim3(nw * 64), 0, s, M, N, K, x, lnw, lnb, eps, Wt, ep)
+        if (J == 4) {
+            if (nt == 2) { if (one) OWK_ROWS_LN_GO(1, 4, 2); else OWK_ROWS_LN_GO(2, 4, 2); }
+            else { if (one) OWK_ROWS_LN_GO(1, 4, 1); else OWK_ROWS_LN_GO(2, 4, 1); }
+        } else {
+            if (nt == 2) { if (one) OWK_ROWS_LN_GO(1, 2, 2); else OWK_ROWS_LN_GO(2, 2, 2); }
+            else { if (one) OWK_ROWS_LN_GO(1, 2, 1); else OWK_ROWS_LN_GO(2, 2, 1); }
+        }
+#undef OWK_ROWS_LN_GO
+    }
+};
+
 template <int MODE, int MT>
 __global__ __launch_bounds__(MT * 64) void k_gemm_rows_reduce(int M, int N, int KS, const float * __restrict__ part,
                                                               EpiParams ep) {
@@ -1386,22 +1346,17 @@ __global__ __launch_bounds__(MT * 64) void k_gemm_rows_reduce(int M, int N, int 
 struct RowsPlan {
     int J, nw, KS;
 };
-static int env_int(const char * name, int dflt) {
-    const char * v = getenv(name);
-    return v && *v ? atoi(v) : dflt;
-}
 // partial (EPI_PARTIAL) launches split K for free (resid_layernorm adds the splits), so
 // they take shorter k ranges per wave and twice the blocks; full-epilogue launches avoid
 // a second (reduce) launch unless K is very long (tools/gemm_sweep.py measurements)
 static RowsPlan rows_plan(int K, bool partial) {
     const int nsteps = K / 32;
     RowsPlan p;
+    // full epilogues take the whole K in one block up to 160 k-steps (K = 5120, the MLP's second
+    // matmul: J = 10 x 16 waves), so no reduce launch follows
     if (partial) p.J = nsteps <= 64 ? 2 : 4;
-    else p.J = nsteps <= 32 ? 2 : nsteps <= 64 ? 4 : 8;
-    static const int j_over = env_int("OWK_GR_J", 0), ks_over = env_int("OWK_GR_KS", 0);  // tuning sweeps
-    if (j_over == 2 || j_over == 4 || j_over == 8) p.J = j_over;
+    else p.J = nsteps <= 32 ? 2 : nsteps <= 64 ? 4 : nsteps <= 128 ? 8 : 10;
     p.KS = (nsteps + GR_MAXW * p.J - 1) / (GR_MAXW * p.J);
-    if (ks_over > p.KS && ks_over <= nsteps / p.J) p.KS = ks_over;
     const int per = (nsteps + p.KS - 1) / p.KS;
     p.nw = (per + p.J - 1) / p.J;
     return p;
@@ -1445,38 +1400,23 @@ template <int MODE> struct LaunchMid {
                        ldw, ep);
     }
 };
-// 256x256 kernel selection: OWK_GEMM256 (default 8 = k_gemm_8p; 1 the 4-slot ring k_gemm_256, 5 its
-// 5-slot variant, 0 forces the 128x128 tile), overridden per
-// thread by the debug hooks (gemm_set_256) so a hook never changes another thread's engine
-static thread_local int t_gemm256 = -1;  // -1: no override; 5: the 5-slot ring variant; 8: the 8-phase kernel
-static int gemm256_mode() {
-    static const int env = env_int("OWK_GEMM256", 8);  // 8: the 8-phase kernel (round 3)
-    return t_gemm256 >= 0 ? t_gemm256 : env;
-}
+// 256x256 kernel: the 8-phase k_gemm_8p (K % 64 == 0; other shapes take the 128x128 tile). The
+// debug hooks override the choice per thread (gemm_set_256: 0 = the 128x128 tile, GEMM_MID_FORCED /
+// GEMM_MID32_FORCED = the ring tiles for every shape) so a hook never changes another thread's engine
+static thread_local int t_gemm256 = -1;  // -1: no override
+static int gemm256_mode() { return t_gemm256 >= 0 ? t_gemm256 : 8; }
 template <int MODE> struct Launch256 {
     static void run(hipStream_t s, int M, int N, int K, const _Float16 * A, int lda, const _Float16 * W, int ldw,
                     const EpiParams & ep) {
         const int nbm = (M + G2_M - 1) / G2_M, nbn = (N + G2_N - 1) / G2_N;
         EpiParams e = ep;
         e.vec = epi_vec_ok(MODE, ep, N) ? 1 : 0;
-        if (gemm256_mode() == 8 && K % G8_K == 0) {  // the 8-phase schedule
-            if (MODE == EPI_QKV_ENC)
-                OWK_LAUNCH((k_gemm_8p<MODE, false>), dim3(nbm * nbn), dim3(512), 0, s, M, N, K, A, lda, W, ldw, e);
-            else
-                OWK_LAUNCH((k_gemm_8p<MODE, true>), dim3(nbm * nbn), dim3(512), 0, s, M, N, K, A, lda, W, ldw, e);
-            return;
-        }
-        if (MODE == EPI_QKV_ENC) {
-            // one launch of C tiles: the V columns need them (transposed image, 4 consecutive key
-            // positions per lane), and splitting Q/K off as C^T tiles measured slower in all
-            // (605 + 241 us against 623 us: two tails and A read twice; profiles/r02n_mfma_util.txt)
-            OWK_LAUNCH((k_gemm_256<MODE, 4, false>), dim3(nbm * nbn), dim3(512), 0, s, M, N, K, A, lda, W, ldw, e);
-            return;
-        }
-        if (gemm256_mode() == 5)
-            OWK_LAUNCH((k_gemm_256<MODE, 5>), dim3(nbm * nbn), dim3(512), 0, s, M, N, K, A, lda, W, ldw, e);
+        // EPI_QKV_ENC: C tiles (its V columns are written transposed, 4 consecutive key positions per
+        // lane); every other epilogue: C^T tiles with 16-byte vector stores
+        if (MODE == EPI_QKV_ENC)
+            OWK_LAUNCH((k_gemm_8p<MODE, false>), dim3(nbm * nbn), dim3(512), 0, s, M, N, K, A, lda, W, ldw, e);
         else
-            OWK_LAUNCH((k_gemm_256<MODE, 4>), dim3(nbm * nbn), dim3(512), 0, s, M, N, K, A, lda, W, ldw, e);
+            OWK_LAUNCH((k_gemm_8p<MODE, true>), dim3(nbm * nbn), dim3(512), 0, s, M, N, K, A, lda, W, ldw, e);
     }
 };
 template <int MODE> struct Launch256Q {
@@ -1522,27 +1462,18 @@ template <int MODE> struct LaunchRows {
         }
         const dim3 grid(tiles, pl.KS);
         const bool one = M <= 16;
-        // full-epilogue launches take 2 column tiles per block: the logits GEMM 47.7 -> 37.0 us for
-        // 32 x 51866 x 1280 (tools/logits_gemm_bench.py, profiles/r03n_logits_gemm_nt.txt; 4 tiles: 37.3 us,
-        // and slower at 8 rows), MLP0 7.76 -> 5.98 us in isolation; large-v3 bench 998-1007 -> 1022-1026
-        // with QKV / cross-Q / MLP0 / logits all on it (profiles/r03n_ab_rows_nt_all.txt).
-        // OWK_ROWS_NT / OWK_ROWS_NT_MIN_N: tuning sweeps (tools/rows_nt_sweep.py)
-        static const int nt_env = env_int("OWK_ROWS_NT", 0), nt_min_n = env_int("OWK_ROWS_NT_MIN_N", 1);
-        const int nt = nt_env ? nt_env : 2;
-        // OWK_ROWS_NT_PARTIAL=1: also the split-K partial launches and J = 2 plans (A/B pending)
-        static const bool nt_wide = env_int("OWK_ROWS_NT_PARTIAL", 0) != 0;
-        const bool fits = MODE == EPI_PARTIAL ? nt_wide : pl.KS == 1 && (pl.J == 4 || nt_wide);
-        if (fits && N >= nt_min_n && (nt == 2 || nt == 4) && (pl.J == 4 || pl.J == 2)) {
-            const dim3 g((tiles + nt - 1) / nt, pl.KS);
-#define OWK_ROWS_NT_GO(MT_, J_, NT_) \
-    OWK_LAUNCH((k_gemm_rows_nt<MODE, MT_, J_, NT_>), g, dim3(pl.nw * 64), 0, s, M, N, K, A, lda, Wt, ep, part)
-            if (nt == 2) {
-                if (pl.J == 4) { if (one) OWK_ROWS_NT_GO(1, 4, 2); else OWK_ROWS_NT_GO(2, 4, 2); }
-                else { if (one) OWK_ROWS_NT_GO(1, 2, 2); else OWK_ROWS_NT_GO(2, 2, 2); }
-            } else {
-                if (pl.J == 4) { if (one) OWK_ROWS_NT_GO(1, 4, 4); else OWK_ROWS_NT_GO(2, 4, 4); }
-                else { if (one) OWK_ROWS_NT_GO(1, 2, 4); else OWK_ROWS_NT_GO(2, 2, 4); }
-            }
+        // full-epilogue launches with many column tiles take 2 per block (a wave's activation
+        // fragments serve both): the logits GEMM 47.7 -> 37.0 us for 32 x 51866 x 1280
+        // (profiles/r03n_logits_gemm_nt.txt), MLP0 9.7 -> 8.0 us; where halving the grid would leave
+        // fewer than 128 blocks (cross-Q, attn.out: N = 1280 -> 40 blocks) one tile per block is faster
+        // (r04: cross-Q 7.1 us with 2, 5.7 with 1); split-K partial launches measured slower with 2
+        // (r04b A/B, large-v3 RTF 1017 vs 1026)
+        if (MODE != EPI_PARTIAL && pl.KS == 1 && (pl.J == 4 || pl.J == 2) && (tiles + 1) / 2 >= 128) {
+            const dim3 g((tiles + 1) / 2, 1);
+#define OWK_ROWS_NT_GO(MT_, J_) \
+    OWK_LAUNCH((k_gemm_rows_nt<MODE, MT_, J_, 2>), g, dim3(pl.nw * 64), 0, s, M, N, K, A, lda, Wt, ep, part)
+            if (pl.J == 4) { if (one) OWK_ROWS_NT_GO(1, 4); else OWK_ROWS_NT_GO(2, 4); }
+            else { if (one) OWK_ROWS_NT_GO(1, 2); else OWK_ROWS_NT_GO(2, 2); }
 #undef OWK_ROWS_NT_GO
             return;
         }
@@ -1553,6 +1484,8 @@ template <int MODE> struct LaunchRows {
                         : go<2, 4>(s, grid, pl.nw, M, N, K, A, lda, Wt, ep, part); break;
             case 8: one ? go<1, 8>(s, grid, pl.nw, M, N, K, A, lda, Wt, ep, part)
                         : go<2, 8>(s, grid, pl.nw, M, N, K, A, lda, Wt, ep, part); break;
+            case 10: one ? go<1, 10>(s, grid, pl.nw, M, N, K, A, lda, Wt, ep, part)
+                         : go<2, 10>(s, grid, pl.nw, M, N, K, A, lda, Wt, ep, part); break;
             default: throw std::runtime_error("gemm_rows: no kernel for this plan");
         }
     }
@@ -2243,16 +2176,15 @@ int gemm_set_256(int on) {
 }
 static bool use_256(int M, int N, int K) {
     const int m = gemm256_mode();
-    return m && m != GEMM_MID_FORCED && M >= 2048 && N >= 1024 && K % G2_K == 0;
+    return m && m != GEMM_MID_FORCED && m != GEMM_MID32_FORCED && M >= 2048 && N >= 1024 && K % G8_K == 0;
 }
-// the 64x64 ring tile where the 128x128 grid would not give every CU a block (OWK_GEMM_MID=0 or
-// the override 0 keep the 128x128 tile; the override GEMM_MID_FORCED takes the 64x64 tile always)
+// the 64x64 ring tile where the 128x128 grid would not give every CU a block (the override 0 keeps
+// the 128x128 tile; the overrides GEMM_MID_FORCED / GEMM_MID32_FORCED take a ring tile always)
 static bool use_mid(int M, int N) {
     const int m = gemm256_mode();
     if (m == 0) return false;
     if (m == GEMM_MID_FORCED || m == GEMM_MID32_FORCED) return true;
-    static const int env = env_int("OWK_GEMM_MID", 1);
-    return env && ((M + GB_M - 1) / GB_M) * ((N + GB_N - 1) / GB_N) < 256;
+    return ((M + GB_M - 1) / GB_M) * ((N + GB_N - 1) / GB_N) < 256;
 }
 // tile edge of the ring kernel: 32 where the 64x64 grid would still leave CUs idle (SortFormer chunk
 // shapes at M = 413, tests/test_gpu_kernels.py::test_gemm_mid_speed: 32x32 4.6-15.7 us against 64x64
@@ -2309,6 +2241,21 @@ size_t gemm_ws_floats(int N, int K) {
 }
 size_t gemm_partial_floats(int N, int K) { return (size_t) rows_plan(K, true).KS * ((N + 15) / 16) * 2 * 64 * 4; }
 int gemm_partial_splits(int K) { return rows_plan(K, true).KS; }
+
+bool gemm_rows_ln_applies(int M, int N, int K) {
+    return M >= 1 && M <= 32 && K % 32 == 0 && K % 8 == 0 && N % 16 == 0 && K / 32 <= GRL_MAXW * 4;
+}
+
+void gemm_rows_ln(hipStream_t s, int mode, int M, int N, int K, const float * x, const float * lnw, const float * lnb,
+                  float eps, const _Float16 * Wt, const EpiParams & ep) {
+    if (!gemm_rows_ln_applies(M, N, K) || !Wt || !x || !lnw || !lnb) throw std::runtime_error("gemm_rows_ln: unsupported shape");
+    switch (mode) {
+        case EPI_F16: LaunchRowsLn<EPI_F16>::run(s, M, N, K, x, lnw, lnb, eps, Wt, ep); break;
+        case EPI_GELU_F16: LaunchRowsLn<EPI_GELU_F16>::run(s, M, N, K, x, lnw, lnb, eps, Wt, ep); break;
+        case EPI_QKV_DEC: LaunchRowsLn<EPI_QKV_DEC>::run(s, M, N, K, x, lnw, lnb, eps, Wt, ep); break;
+        default: throw std::runtime_error("gemm_rows_ln: epilogue not instantiated");
+    }
+}
 
 void gemm(hipStream_t s, int mode, int M, int N, int K, const _Float16 * A, int lda, const _Float16 * W, int ldw,
           const EpiParams & ep, const GemmWs * ws, const _Float16 * Wt) {

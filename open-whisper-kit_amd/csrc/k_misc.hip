@@ -111,7 +111,8 @@ __global__ __launch_bounds__(256) void k_layernorm_f16(const float * __restrict_
 // row's partial loads are spread over 4 waves instead of one); the LayerNorm statistics are
 // the same double sums as ln_row_regs (exact for a row of f32 values; the variance sum
 // differs from the one-wave order only below double precision).
-constexpr int RL_V4 = 2;  // float4 per thread -> N <= 2048
+constexpr int RL_V4 = 2;     // float4 per thread -> N <= 2048
+constexpr int RL_KSMAX = 4;  // k splits (gemm_partial_splits <= 3, q5_partial_splits <= 4)
 
 __device__ __forceinline__ double block_sum_d(double v, double * red) {
     v = wave_sum_d(v);
@@ -133,19 +134,40 @@ __global__ __launch_bounds__(256) void k_resid_layernorm(int M, int N, int KS, c
     const int row = blockIdx.x;
     const int n4 = N >> 2;
     float4 * xr = (float4 *) (x + (size_t) row * N);
+    // every load of the block is issued before the first add (the k splits, bias, residual and the
+    // LayerNorm gains): one memory round trip instead of one per split (a runtime split loop waits
+    // on each load before the next is issued)
+    const float4 z4 = float4{0.f, 0.f, 0.f, 0.f};
+    // branch-free: indices clamped into the row / the last split, unused values discarded below
+    const float4 * p4 = (const float4 *) part;
+    const float4 * w4 = (const float4 *) (w ? w : bias);
+    const float4 * b4 = (const float4 *) (w ? b : bias);
+    float4 pv[RL_V4][RL_KSMAX], bv[RL_V4], rv[RL_V4], wv[RL_V4], lbv[RL_V4];
+#pragma unroll
+    for (int j = 0; j < RL_V4; ++j) {
+        const int i = min(t + 256 * j, n4 - 1);
+#pragma unroll
+        for (int ks = 0; ks < RL_KSMAX; ++ks) pv[j][ks] = p4[((size_t) min(ks, KS - 1) * M + row) * n4 + i];
+        bv[j] = ((const float4 *) bias)[i];
+        rv[j] = xr[i];
+        wv[j] = w4[i];
+        lbv[j] = b4[i];
+    }
     float4 xv[RL_V4];
 #pragma unroll
     for (int j = 0; j < RL_V4; ++j) {
         const int i = t + 256 * j;
-        float4 r = float4{0.f, 0.f, 0.f, 0.f};
+        float4 r = z4;
         if (i < n4) {
-            float4 a = ((const float4 *) (part + (size_t) row * N))[i];
-            for (int ks = 1; ks < KS; ++ks) {
-                const float4 p = ((const float4 *) (part + ((size_t) ks * M + row) * N))[i];
-                a.x += p.x; a.y += p.y; a.z += p.z; a.w += p.w;
+            float4 a = pv[j][0];  // the splits in k order, as before
+#pragma unroll
+            for (int ks = 1; ks < RL_KSMAX; ++ks) {
+                if (ks < KS) {
+                    const float4 q = pv[j][ks];
+                    a.x += q.x; a.y += q.y; a.z += q.z; a.w += q.w;
+                }
             }
-            const float4 bb = ((const float4 *) bias)[i];
-            const float4 res = xr[i];
+            const float4 bb = bv[j], res = rv[j];
             r.x = res.x + (a.x + bb.x);
             r.y = res.y + (a.y + bb.y);
             r.z = res.z + (a.z + bb.z);
@@ -177,7 +199,7 @@ __global__ __launch_bounds__(256) void k_resid_layernorm(int M, int N, int KS, c
     for (int j = 0; j < RL_V4; ++j) {
         const int i = t + 256 * j;
         if (i < n4) {
-            const float4 ww = ((const float4 *) w)[i], bb = ((const float4 *) b)[i];
+            const float4 ww = wv[j], bb = lbv[j];
             float4 y;
             y.x = (xv[j].x - mean) * scale * ww.x + bb.x;
             y.y = (xv[j].y - mean) * scale * ww.y + bb.y;
@@ -211,7 +233,8 @@ __global__ __launch_bounds__(256) void k_resid_layernorm(int M, int N, int KS, c
 void resid_layernorm(hipStream_t s, int M, int N, int ks, const float * part, const float * bias, float * x,
                      const float * lnw, const float * lnb, float eps, _Float16 * xn, int ldo, int8_t * q8, float * q8d) {
     if (M <= 0) return;
-    if (M > 32 || N % 16 != 0 || N > 4 * 256 * RL_V4) throw std::runtime_error("resid_layernorm: unsupported shape");
+    if (M > 32 || N % 16 != 0 || N > 4 * 256 * RL_V4 || ks < 1 || ks > RL_KSMAX)
+        throw std::runtime_error("resid_layernorm: unsupported shape");
     if (q8 && (N % 32 != 0 || !q8d)) throw std::runtime_error("resid_layernorm: Q8_0 output needs N % 32 == 0");
     // (a one-wave-per-row variant measured slower: 159 -> 249 ms per step, the row's split partials
     // are too many serial loads for one wave, profiles/r02e_ab.txt)

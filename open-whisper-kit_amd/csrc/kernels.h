@@ -60,9 +60,8 @@ struct EpiParams {
 void gemm_f16(hipStream_t s, int mode, int M, int N, int K, const _Float16 * A, int lda,
               const _Float16 * W, int ldw, const EpiParams & ep);
 // skinny (decode steps, M <= 64): split-K across the waves of a block, LDS reduction
-// this thread's 256x256-kernel override (-1 none, 0 force 128x128, 1 on, 5 the 5-slot ring, 8 the
-// 8-phase kernel, GEMM_MID_FORCED / GEMM_MID32_FORCED the 64x64 / 32x32 ring tile for every shape
-// below the 256x256 path);
+// this thread's large-GEMM override (-1 none, 0 force 128x128, 8 the 8-phase 256x256 kernel (the
+// default), GEMM_MID_FORCED / GEMM_MID32_FORCED the 64x64 / 32x32 ring tile for every shape);
 // returns the previous override (debug hooks restore it with GemmOverride)
 constexpr int GEMM_MID_FORCED = 16, GEMM_MID32_FORCED = 17;
 int gemm_set_256(int on);
@@ -88,6 +87,12 @@ int gemm_partial_splits(int K);            // its k splits (rows of partial tile
 void resid_layernorm(hipStream_t s, int M, int N, int ks, const float * part, const float * bias, float * x,
                      const float * lnw, const float * lnb, float eps, _Float16 * xn, int ldo,
                      int8_t * q8 = nullptr, float * q8d = nullptr);
+// decode-row GEMM whose A operand is f16(LayerNorm(x)) of the f32 residual stream x [M][K] (lnw / lnb
+// the LayerNorm gain / bias [K]): the LayerNorm runs in the GEMM's prologue (M <= 32, K <= 1280,
+// epilogues EPI_F16 / EPI_GELU_F16 / EPI_QKV_DEC); Wt the tiled weight copy
+bool gemm_rows_ln_applies(int M, int N, int K);
+void gemm_rows_ln(hipStream_t s, int mode, int M, int N, int K, const float * x, const float * lnw, const float * lnb,
+                  float eps, const _Float16 * Wt, const EpiParams & ep);
 // dispatch on M: <= 32 rows decode-row GEMM (needs the tiled copy Wt), <= 64 skinny,
 // else 128x128 tiles (row-major W)
 void gemm(hipStream_t s, int mode, int M, int N, int K, const _Float16 * A, int lda,

@@ -779,15 +779,16 @@ int whisper_full_parallel(struct whisper_context * ctx, struct whisper_full_para
         ps[i].progress_callback_user_data = nullptr;
     }
     int ret = 0;
+    // the states of this call (the context's default state and the fresh ones), locked in address
+    // order like owk_full_batch, and held through the merge below (it writes ctx->state's results
+    // and timings); the context lock while the shared recorder is on
+    std::vector<whisper_state *> held(states);
+    std::sort(held.begin(), held.end());
+    std::vector<std::unique_lock<std::mutex>> locks;
+    std::unique_lock<std::mutex> ctx_lock(ctx->mu, std::defer_lock);
+    if (ctx->prof.on) ctx_lock.lock();
+    for (whisper_state * st : held) locks.emplace_back(st->mu);
     try {
-        // the states of this call (the context's default state and the fresh ones), locked in
-        // address order like owk_full_batch; the context lock while the shared recorder is on
-        std::vector<whisper_state *> held(states);
-        std::sort(held.begin(), held.end());
-        std::vector<std::unique_lock<std::mutex>> locks;
-        std::unique_lock<std::mutex> ctx_lock(ctx->mu, std::defer_lock);
-        if (ctx->prof.on) ctx_lock.lock();
-        for (whisper_state * st : held) locks.emplace_back(st->mu);
         ret = full_batch(ctx, states.data(), ps.data(), nullptr, ptr.data(), ns.data(), n_processors);
     } catch (const std::exception & e) {
         log_msg(GGML_LOG_LEVEL_ERROR, "whisper_full_parallel: %s\n", e.what());
@@ -815,12 +816,13 @@ int whisper_full_parallel(struct whisper_context * ctx, struct whisper_full_para
         ctx->state->n_decode += s->n_decode;
         ctx->state->n_batchd += s->n_batchd;
         ctx->state->n_prompt += s->n_prompt;
-        whisper_free_state(s);
     }
     ctx->state->t_mel_us /= n_processors;
     ctx->state->t_sample_us /= n_processors;
     ctx->state->t_encode_us /= n_processors;
     ctx->state->t_decode_us /= n_processors;
+    locks.clear();  // release before freeing the helper states (their mutexes die with them)
+    for (int i = 1; i < n_processors; ++i) whisper_free_state(states[i]);
     return ret;
 }
 
@@ -1193,13 +1195,12 @@ __global__ static void k_fill_rand_f16(_Float16 * p, size_t n, uint32_t seed) {
     }
 }
 
-// mode bit 0x100: force the 128x128 large-GEMM kernel; bit 0x400: the 5-slot ring variant of the
-// 256x256 kernel; 0x800: the 8-phase kernel; 0x1000 / 0x2000: the 64x64 / 32x32 ring tile; bit 0x200:
-// random operands
+// mode bit 0x100: force the 128x128 large-GEMM kernel; 0x800 (the default): the 8-phase 256x256 kernel;
+// 0x1000 / 0x2000: the 64x64 / 32x32 ring tile; bit 0x200: random operands
 double owk_debug_gemm_bench(int device, int mode, int M, int N, int K, int iters) {
-    const bool force128 = mode & 0x100, rnd = mode & 0x200, ring5 = mode & 0x400, p8 = mode & 0x800, mid = mode & 0x1000, mid32 = mode & 0x2000;
+    const bool force128 = mode & 0x100, rnd = mode & 0x200, mid = mode & 0x1000, mid32 = mode & 0x2000;
     mode &= 0xFF;
-    GemmOverride ov(force128 ? 0 : ring5 ? 5 : p8 ? 8 : mid ? GEMM_MID_FORCED : mid32 ? GEMM_MID32_FORCED : 1);
+    GemmOverride ov(force128 ? 0 : mid ? GEMM_MID_FORCED : mid32 ? GEMM_MID32_FORCED : 8);
     try {
         OWK_HIP_CHECK(hipSetDevice(device));
         hipStream_t s;
@@ -1588,7 +1589,7 @@ double owk_debug_attn_cross(int device, int which, int R, int H, int T, int n_ze
 // EPI_CONV2 shape parameters (N = 3d / 2d / d).
 double owk_debug_gemm_epi_diff(int device, int mode, int M, int N, int K, int d, int T) {
     // 0x800: the 8-phase kernel against the 128x128 one; 0x1000 / 0x2000: the 64x64 / 32x32 ring tile
-    const int large = (mode & 0x800) ? 8 : (mode & 0x1000) ? GEMM_MID_FORCED : (mode & 0x2000) ? GEMM_MID32_FORCED : 1;
+    const int large = (mode & 0x1000) ? GEMM_MID_FORCED : (mode & 0x2000) ? GEMM_MID32_FORCED : 8;
     mode &= 0xFF;
     try {
         OWK_HIP_CHECK(hipSetDevice(device));
@@ -1699,6 +1700,89 @@ int owk_debug_gemm(int device, int M, int N, int K, const uint16_t * a, const ui
         OWK_HIP_CHECK(hipStreamDestroy(s));
     } catch (const std::exception & ex) {
         log_msg(GGML_LOG_LEVEL_ERROR, "owk_debug_gemm: %s\n", ex.what());
+        return -1;
+    }
+    return 0;
+}
+
+// The decoder's LayerNorm-prologue GEMM (gemm_rows_ln) against the two-launch form it replaces
+// (layernorm_f16 -> f16 rows -> decode-row GEMM), EPI_F16 with bias b (may be null) and scale 1:
+// x [M][K] f32, lnw / lnb [K], w [N][K] f16 bits; out_fused / out_ref [M][N] f16 bits. Also the
+// residual epilogue over the whole K (EPI_RESID_F32 with K = 4 N, the mlp.2 shape) against the
+// split-K partial + resid_layernorm finish: resid [M][N] f32 in, out_resid_* [M][N] f32 (may be null).
+int owk_debug_gemm_rows_ln(int device, int M, int N, int K, const float * x, const float * lnw, const float * lnb,
+                           const float * b, const uint16_t * w, uint16_t * out_fused, uint16_t * out_ref,
+                           const uint16_t * w2, const float * resid, float * out_resid_full, float * out_resid_split) {
+    try {
+        OWK_HIP_CHECK(hipSetDevice(device));
+        hipStream_t s;
+        OWK_HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+        DevBuf dx, dlw, dlb, db, dw, dwt, dxn, o1, o2, part;
+        dx.alloc((size_t) M * K * 4);
+        dlw.alloc((size_t) K * 4);
+        dlb.alloc((size_t) K * 4);
+        db.alloc((size_t) N * 4);
+        dw.alloc((size_t) N * K * 2);
+        dwt.alloc(tiled_weight_elems(N, K) * 2);
+        dxn.alloc((size_t) M * K * 2);
+        o1.alloc((size_t) M * N * 2);
+        o2.alloc((size_t) M * N * 2);
+        OWK_HIP_CHECK(hipMemcpy(dx.ptr, x, (size_t) M * K * 4, hipMemcpyHostToDevice));
+        OWK_HIP_CHECK(hipMemcpy(dlw.ptr, lnw, (size_t) K * 4, hipMemcpyHostToDevice));
+        OWK_HIP_CHECK(hipMemcpy(dlb.ptr, lnb, (size_t) K * 4, hipMemcpyHostToDevice));
+        if (b) OWK_HIP_CHECK(hipMemcpy(db.ptr, b, (size_t) N * 4, hipMemcpyHostToDevice));
+        OWK_HIP_CHECK(hipMemcpy(dw.ptr, w, (size_t) N * K * 2, hipMemcpyHostToDevice));
+        tile_weights(s, dw.as<_Float16>(), N, K, dwt.as<_Float16>());
+        EpiParams ep;
+        ep.bias = b ? db.as<float>() : nullptr;
+        ep.ldo = N;
+        ep.out16 = o1.as<_Float16>();
+        gemm_rows_ln(s, EPI_F16, M, N, K, dx.as<float>(), dlw.as<float>(), dlb.as<float>(), 1e-5f, dwt.as<_Float16>(), ep);
+        layernorm_f16(s, dx.as<float>(), M, K, dlw.as<float>(), dlb.as<float>(), 1e-5f, dxn.as<_Float16>(), K, nullptr,
+                      nullptr, nullptr, nullptr);
+        ep.out16 = o2.as<_Float16>();
+        GemmWs ws;
+        const size_t fl = std::max(gemm_ws_floats(N, K), gemm_partial_floats(N, 4 * N));
+        part.alloc(std::max<size_t>(fl, 1) * 4);
+        ws.partial = part.as<float>();
+        ws.partial_floats = fl;
+        gemm(s, EPI_F16, M, N, K, dxn.as<_Float16>(), K, dw.as<_Float16>(), K, ep, &ws, dwt.as<_Float16>());
+        if (w2 && resid) {
+            // mlp.2 shape: [M][4N] f16 activations (the LayerNorm rows of x reused as data) x [N][4N]
+            const int K2 = 4 * N;
+            DevBuf dw2, dw2t, da2, r1, r2;
+            dw2.alloc((size_t) N * K2 * 2);
+            dw2t.alloc(tiled_weight_elems(N, K2) * 2);
+            da2.alloc((size_t) M * K2 * 2);
+            r1.alloc((size_t) M * N * 4);
+            r2.alloc((size_t) M * N * 4);
+            OWK_HIP_CHECK(hipMemcpy(dw2.ptr, w2, (size_t) N * K2 * 2, hipMemcpyHostToDevice));
+            tile_weights(s, dw2.as<_Float16>(), N, K2, dw2t.as<_Float16>());
+            std::vector<uint16_t> a2((size_t) M * K2);
+            for (size_t i = 0; i < a2.size(); ++i) a2[i] = w2[(i * 7919) % ((size_t) N * K2)];
+            OWK_HIP_CHECK(hipMemcpy(da2.ptr, a2.data(), a2.size() * 2, hipMemcpyHostToDevice));
+            OWK_HIP_CHECK(hipMemcpy(r1.ptr, resid, (size_t) M * N * 4, hipMemcpyHostToDevice));
+            OWK_HIP_CHECK(hipMemcpy(r2.ptr, resid, (size_t) M * N * 4, hipMemcpyHostToDevice));
+            EpiParams e2;
+            e2.bias = db.as<float>();
+            e2.resid = r1.as<float>();
+            e2.out32 = r1.as<float>();
+            e2.ldo = N;
+            gemm(s, EPI_RESID_F32, M, N, K2, da2.as<_Float16>(), K2, dw2.as<_Float16>(), K2, e2, &ws, dw2t.as<_Float16>());
+            EpiParams e3;
+            gemm(s, EPI_PARTIAL, M, N, K2, da2.as<_Float16>(), K2, nullptr, K2, e3, &ws, dw2t.as<_Float16>());
+            resid_layernorm(s, M, N, gemm_partial_splits(K2), ws.partial, db.as<float>(), r2.as<float>(), nullptr,
+                            nullptr, 1e-5f, nullptr, N);
+            OWK_HIP_CHECK(hipStreamSynchronize(s));
+            if (out_resid_full) OWK_HIP_CHECK(hipMemcpy(out_resid_full, r1.ptr, (size_t) M * N * 4, hipMemcpyDeviceToHost));
+            if (out_resid_split) OWK_HIP_CHECK(hipMemcpy(out_resid_split, r2.ptr, (size_t) M * N * 4, hipMemcpyDeviceToHost));
+        }
+        OWK_HIP_CHECK(hipStreamSynchronize(s));
+        OWK_HIP_CHECK(hipMemcpy(out_fused, o1.ptr, (size_t) M * N * 2, hipMemcpyDeviceToHost));
+        OWK_HIP_CHECK(hipMemcpy(out_ref, o2.ptr, (size_t) M * N * 2, hipMemcpyDeviceToHost));
+        OWK_HIP_CHECK(hipStreamDestroy(s));
+    } catch (const std::exception & ex) {
+        log_msg(GGML_LOG_LEVEL_ERROR, "owk_debug_gemm_rows_ln: %s\n", ex.what());
         return -1;
     }
     return 0;

@@ -173,3 +173,28 @@ def test_align_matches_restatement(seed):
     assert got["text"] == exp["text"]
     segs_sorted = sorted(segs, key=lambda s: s[1])
     assert owk.rttm_generate(segs_sorted, "f") == ref.rttm_generate(segs_sorted, "f")
+
+
+# --- the configs[4] pipeline's own input: 3,453 words x the reference's 3-speaker stream RTTM ------
+@pytest.mark.parametrize("variant", ["default", "nosmooth", "fill", "smooth5"])
+def test_align_c4_reference_pipeline(variant):
+    """libwhisper.so's aligner on the reference configs[4] pipeline's words and 2 s-stream RTTM
+    (tests/golden/c4_golden.json; make_golden_c4.py / make_golden_c4_align.py) with each AlignmentOptions
+    variant: word speakers, utterances and text identical to the reference pipeline's."""
+    import json
+    import os
+
+    meta = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "c4_golden.json")))
+    words = [tuple(w) for w in meta["results"]["words"]]
+    segs = owk.rttm_parse(meta["results"]["rttm"])
+    if variant == "default":
+        opt, exp = {}, meta["results"]["aligned"]
+    else:
+        v = meta["results"]["aligned_variants"][variant]
+        opt, exp = v["options"], v
+    got = owk.align(words, segs, **opt)
+    assert spk(got) == exp["speakers"]
+    assert [(u["speaker"], u["words"][0], len(u["words"])) for u in got["segments"]] == [tuple(u) for u in exp["utterances"]]
+    assert got["text"] == exp["text"]
+    if variant in ("nosmooth", "fill"):
+        assert len({s for s in exp["speakers"] if s}) >= 3 and len(exp["utterances"]) >= 10
