@@ -118,6 +118,10 @@ WHISPER_API double owk_debug_gemm_bench(int device, int mode, int M, int N, int 
 /* the decoder's per-layer matmul + residual/LayerNorm chain (no attention) of a large-v3-shaped model,
  * R rows, distinct random weights per layer, one captured hipGraph: device microseconds per layer */
 WHISPER_API double owk_debug_decode_chain(int device, int R, int n_layers, int iters);
+/* the same with the chain's form chosen by `variant` (whisper_api.cpp: 0 round-3 split-K + resid_layernorm,
+ * 1 LayerNorm-prologue consumers + whole-K residual epilogues, 2 = 1 without the prologue statistics
+ * (timing only), 3 / 4 mixed) */
+WHISPER_API double owk_debug_decode_chain2(int device, int R, int n_layers, int iters, int variant);
 
 /* test hook: the decoder's LayerNorm-prologue GEMM (M <= 32 rows, K <= 1280) against layernorm + GEMM, EPI_F16
  * with bias b (may be NULL), f16 bits out [M][N]; with w2 / resid (may be NULL): the whole-K residual epilogue of

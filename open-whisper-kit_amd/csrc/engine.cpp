@@ -502,7 +502,7 @@ uint64_t Engine::buffers_signature() const {
     uint64_t h = 1469598103934665603ull;
     for (const void * p : {d_x_.ptr, d_xn_.ptr, d_q_.ptr, d_ao_.ptr, d_h_.ptr, d_xl_.ptr, logits_.ptr, d_stg_.ptr,
                            q8a_.ptr, q8d_.ptr, d_xn32_.ptr, d_ao32_.ptr, d_xl32_.ptr, q16a_.ptr, q16d_.ptr,
-                           self_k_.ptr, self_v_.ptr, cross_k_.ptr, cross_v_.ptr, gws_part_.ptr})
+                           self_k_.ptr, self_v_.ptr, cross_k_.ptr, cross_v_.ptr, gws_part_.ptr, sm_ws_.ptr})
         h = (h ^ (uint64_t) (uintptr_t) p) * 1099511628211ull;
     return h;
 }
@@ -627,6 +627,10 @@ void Engine::decode(const std::vector<DecodeRow> & rows, const std::vector<int> 
     if (sh.self_oc && sh.max_keys > attn_max_listed_keys()) throw std::runtime_error("decode: too many self-attention keys");
     if (sh.self_tl && sh.max_keys > attn_max_tiled_keys()) throw std::runtime_error("decode: too many self-attention keys");
 
+    if ((sh.self_sm || sh.cross_sm) && sm_ws_.bytes < attn_softmax_ws_floats(dec_rows_cap_, hp.n_text_head) * 4) {
+        sync();  // soft_max rows: the key-split attention workspace for the row capacity
+        sm_ws_.alloc(attn_softmax_ws_floats(dec_rows_cap_, hp.n_text_head) * 4);
+    }
     if (capture) {
         if (!n_ah_ || !amap_.ptr) throw std::runtime_error("decode: capture without alignment heads");
         if (!sh.cross_sm) throw std::runtime_error("decode: capture needs soft_max cross attention (flash_attn = false)");
@@ -688,6 +692,8 @@ void Engine::launch_decode(const DecShape & sh) {
     const int max_keys = sh.max_keys;
     const bool self_oc = sh.self_oc, self_tl = sh.self_tl, cross_oc = sh.cross_oc, cross_tl = sh.cross_tl;
 
+    auto sm_ws = [&]() { return sm_ws_.as<float>(); };
+    auto sm_ws_floats = [&]() { return sm_ws_.bytes / 4; };
     const bool q5 = m->q5;
     // A32: the f32 activation a Q5_0 GEMM quantizes (null: the f16 A is exact, e.g. GELU output)
     // a_q8: the A operand's Q8_0 rows are already in q8a_ / q8d_ (Q5_0 models; written by the
@@ -720,41 +726,69 @@ void Engine::launch_decode(const DecShape & sh) {
         attn_decoder(stream, qv, d, cross_k_.as<_Float16>() + l * cross_stride, cross_v_.as<_Float16>() + l * cross_stride,
                      64, T * 64, d_rc, R, nullptr, H, kq_scale, T, o16, d, cross_oc, cross_tl, o32, true, q8, q8d);
     };
-    // R <= 32 rows (F16 weights), 8 launches per layer: every matmul whose input is a LayerNorm output
-    // (attn QKV, cross_attn.query, mlp.0) runs that LayerNorm in its prologue from the f32 residual
-    // stream (gemm_rows_ln), and every residual matmul (attn.out, cross_attn.out, mlp.2) adds its bias
-    // and the residual in its epilogue over the whole K in one block (EPI_RESID_F32, in place on x).
-    // Round 4: replaces split-K partial tiles + a resid_layernorm launch per residual matmul (11
-    // launches per layer); measured alternatives of earlier rounds (profiles/r02e_ab.txt, the round-3
-    // ticket finish in tools/lab_gemv.hip) lost on the launch boundary or the in-launch seam. soft_max
-    // rows (flash_attn = false) and DTW captures run the soft_max attention launches inside the same
-    // chain. Larger passes use the full-epilogue GEMMs and separate LayerNorms.
-    const bool fused = R <= 32 && !q5 && gemm_rows_ln_applies(R, 4 * hp.n_text_state, hp.n_text_state);
+    // R <= 32 rows (F16 weights): the per-layer chain of decode-row GEMMs. Each residual matmul site
+    // (attn.out, cross_attn.out, mlp.2) is either
+    //   split: split-K partial tiles + resid_layernorm, which adds bias + residual and writes the next
+    //          LayerNorm's f16 rows for the next matmul (2 launches), or
+    //   whole-K: one launch adding bias + residual in its epilogue (EPI_RESID_F32, in place on x); the
+    //          next matmul then runs the LayerNorm in its own prologue (gemm_rows_ln).
+    // Whole-K saves a launch per site but every block of the consumer recomputes the row statistics
+    // from the f32 rows: it pays at few rows (configs[4]'s one-row steps) and not at 32
+    // (tools/chain_ab.py). Earlier measured alternatives (profiles/r02e_ab.txt,
+    // the round-3 ticket finish) lost on the launch boundary or the in-launch seam. soft_max rows
+    // (flash_attn = false) and DTW captures run the soft_max attention launches inside the same chain.
+    // Larger passes use the full-epilogue GEMMs and separate LayerNorms.
+    const bool fused = R <= 32 && !q5;
+    const bool whole_k = fused && R <= kRowsLnMaxRows && gemm_rows_ln_applies(R, 4 * hp.n_text_state, hp.n_text_state);
 
     auto fused_rows = [&]() {
         hipStream_t s = stream;
         float * x = d_x_.as<float>();
+        _Float16 * xn = d_xn_.as<_Float16>();
         _Float16 * qb = d_q_.as<_Float16>();
         _Float16 * aob = d_ao_.as<_Float16>();
         _Float16 * hr = d_h_.as<_Float16>();
         const int n = R;
-        // algorithmic bytes: the weights once, the activation rows once (f32 for the LayerNorm prologue)
-        auto gemm_ln = [&](int mode, int N, const float * lnw, const float * lnb, const _Float16 * Wt,
-                           const EpiParams & ep) {
-            ProfScope ps(prof, s, "gemm_dec", 2.0 * n * (double) N * d, 2.0 * (double) N * d + 4.0 * n * d);
-            gemm_rows_ln(s, mode, n, N, d, x, lnw, lnb, hp.eps, Wt, ep);
+        // consumer of a LayerNorm (QKV, cross-Q, mlp.0): from the f16 rows the split producer wrote, or
+        // with the LayerNorm in its prologue; algorithmic bytes: weights + activation rows once
+        auto consumer = [&](int mode, int N, const float * lnw, const float * lnb, const _Float16 * Wt,
+                            const EpiParams & ep) {
+            if (whole_k) {
+                ProfScope ps(prof, s, "gemm_dec", 2.0 * n * (double) N * d, 2.0 * (double) N * d + 4.0 * n * d);
+                gemm_rows_ln(s, mode, n, N, d, x, lnw, lnb, hp.eps, Wt, ep);
+            } else {
+                ProfScope ps(prof, s, "gemm_dec", 2.0 * n * (double) N * d, 2.0 * ((double) n * d + (double) N * d));
+                gemm(s, mode, n, N, d, xn, d, nullptr, d, ep, &gws_, Wt);
+            }
         };
-        auto resid = [&](const _Float16 * A, const _Float16 * Wt, int K, const float * bias) {
-            ProfScope ps(prof, s, "gemm_dec", 2.0 * n * (double) d * K, 2.0 * ((double) n * K + (double) d * K));
-            EpiParams ep;
-            ep.bias = bias;
-            ep.resid = x;
-            ep.out32 = x;
-            ep.ldo = d;
-            gemm(s, EPI_RESID_F32, n, d, K, A, K, nullptr, K, ep, &gws_, Wt);
+        // residual matmul; lnw / lnb: the LayerNorm of the next consumer (null after the last layer)
+        auto resid = [&](const _Float16 * A, const _Float16 * Wt, int K, const float * bias, const float * lnw,
+                         const float * lnb) {
+            if (whole_k) {
+                ProfScope ps(prof, s, "gemm_dec", 2.0 * n * (double) d * K, 2.0 * ((double) n * K + (double) d * K));
+                EpiParams ep;
+                ep.bias = bias;
+                ep.resid = x;
+                ep.out32 = x;
+                ep.ldo = d;
+                gemm(s, EPI_RESID_F32, n, d, K, A, K, nullptr, K, ep, &gws_, Wt);
+                return;
+            }
+            {
+                ProfScope ps(prof, s, "gemm_dec", 2.0 * n * (double) d * K, 2.0 * ((double) n * K + (double) d * K));
+                gemm(s, EPI_PARTIAL, n, d, K, A, K, nullptr, K, EpiParams(), &gws_, Wt);
+            }
+            ProfScope ps(prof, s, "layernorm");
+            resid_layernorm(s, n, d, gemm_partial_splits(K), gws_.partial, bias, x, lnw, lnb, hp.eps, xn, d);
         };
+        if (!whole_k) {  // layer 0's attn_ln of the embeddings
+            ProfScope ps(prof, s, "layernorm");
+            layernorm_f16(s, x, n, d, m->dec[0].attn_ln_w, m->dec[0].attn_ln_b, hp.eps, xn, d, nullptr, nullptr,
+                          nullptr, nullptr);
+        }
         for (int l = 0; l < hp.n_text_layer; ++l) {
             const DecLayerW & L = m->dec[l];
+            const DecLayerW * nx = l + 1 < hp.n_text_layer ? &m->dec[l + 1] : nullptr;
             _Float16 * Kl = self_k_.as<_Float16>() + l * self_stride;
             _Float16 * Vl = self_v_.as<_Float16>() + l * self_stride;
             {
@@ -769,7 +803,7 @@ void Engine::launch_decode(const DecShape & sh) {
                 ep.d = d;
                 ep.row_off = d_rowoff;
                 ep.Tpad = kv_cells * 64;
-                gemm_ln(EPI_QKV_DEC, 3 * d, L.attn_ln_w, L.attn_ln_b, L.t_qkv, ep);
+                consumer(EPI_QKV_DEC, 3 * d, L.attn_ln_w, L.attn_ln_b, L.t_qkv, ep);
             }
             {
                 ProfScope ps(prof, s, "attn_self");
@@ -777,15 +811,15 @@ void Engine::launch_decode(const DecShape & sh) {
                              self_oc, self_tl, nullptr, sh.self_list, nullptr, nullptr);
                 if (sh.self_sm)  // flash_attn = false rows: masked soft_max (scale 1; Q, K pre-scaled)
                     attn_decoder_softmax(s, qb, d, Kl, Vl, 64, kv_cells * 64, d_rs, n, d_keys, H, 1.0f, max_keys, aob,
-                                         d, nullptr, nullptr, 0, nullptr);
+                                         d, nullptr, nullptr, 0, nullptr, sm_ws(), sm_ws_floats());
             }
-            resid(aob, L.t_o, d, L.b_o);
+            resid(aob, L.t_o, d, L.b_o, L.cross_ln_w, L.cross_ln_b);
             {
                 EpiParams ep;
                 ep.bias = L.cb_q;
                 ep.out16 = qb;
                 ep.ldo = d;
-                gemm_ln(EPI_F16, d, L.cross_ln_w, L.cross_ln_b, L.t_cq, ep);
+                consumer(EPI_F16, d, L.cross_ln_w, L.cross_ln_b, L.t_cq, ep);
             }
             {
                 ProfScope ps(prof, s, "attn_cross", 4.0 * n * (double) n_ctx_pad * d, 2.0 * 2.0 * n * (double) T * d);
@@ -794,18 +828,18 @@ void Engine::launch_decode(const DecShape & sh) {
                     attn_decoder_softmax(s, qb, d, cross_k_.as<_Float16>() + l * cross_stride,
                                          cross_v_.as<_Float16>() + l * cross_stride, 64, T * 64, d_rc, n, nullptr, H,
                                          kq_scale, T, aob, d, sh.capture ? amap_.as<int>() + l * H : nullptr,
-                                         sh.capture ? cap_.as<float>() : nullptr, R, nullptr);
+                                         sh.capture ? cap_.as<float>() : nullptr, R, nullptr, sm_ws(), sm_ws_floats());
             }
-            resid(aob, L.t_co, d, L.cb_o);
+            resid(aob, L.t_co, d, L.cb_o, L.mlp_ln_w, L.mlp_ln_b);
             {
                 EpiParams ep;
                 ep.bias = L.b_mlp0;
                 ep.gelu_tab = m->gelu_tab;
                 ep.out16 = hr;
                 ep.ldo = 4 * d;
-                gemm_ln(EPI_GELU_F16, 4 * d, L.mlp_ln_w, L.mlp_ln_b, L.t_mlp0, ep);
+                consumer(EPI_GELU_F16, 4 * d, L.mlp_ln_w, L.mlp_ln_b, L.t_mlp0, ep);
             }
-            resid(hr, L.t_mlp1, 4 * d, L.b_mlp1);
+            resid(hr, L.t_mlp1, 4 * d, L.b_mlp1, nx ? nx->attn_ln_w : nullptr, nx ? nx->attn_ln_b : nullptr);
         }
     };
     auto resid_full = [&](const _Float16 * A, const float * A32, const _Float16 * W, const _Float16 * Wt,
@@ -918,7 +952,7 @@ void Engine::launch_decode(const DecShape & sh) {
             if (sh.self_sm)  // masked soft_max with scale 1 (Q, K pre-scaled; whisper.cpp:2614-2628)
                 attn_decoder_softmax(stream, d_q_.as<_Float16>(), d, Kl, Vl, 64, kv_cells * 64, d_rs, R, d_keys, H, 1.0f,
                                      max_keys,
-                                     d_ao_.as<_Float16>(), d, nullptr, nullptr, 0, ao32);
+                                     d_ao_.as<_Float16>(), d, nullptr, nullptr, 0, ao32, sm_ws(), sm_ws_floats());
         }
         resid_full(d_ao_.as<_Float16>(), ao32, L.w_o, L.t_o, L.q_o, d, L.b_o, fq_self);
         ln(L.cross_ln_w, L.cross_ln_b);
@@ -938,7 +972,7 @@ void Engine::launch_decode(const DecShape & sh) {
                 attn_decoder_softmax(stream, d_q_.as<_Float16>(), d, cross_k_.as<_Float16>() + l * cross_stride,
                                      cross_v_.as<_Float16>() + l * cross_stride, 64, T * 64, d_rc, R, nullptr, H, kq_scale, T,
                                      d_ao_.as<_Float16>(), d, sh.capture ? amap_.as<int>() + l * H : nullptr,
-                                     sh.capture ? cap_.as<float>() : nullptr, R, ao32);
+                                     sh.capture ? cap_.as<float>() : nullptr, R, ao32, sm_ws(), sm_ws_floats());
         }
         resid_full(d_ao_.as<_Float16>(), ao32, L.cw_o, L.t_co, L.q_co, d, L.cb_o, fq_cross);
         ln(L.mlp_ln_w, L.mlp_ln_b);

@@ -11,6 +11,10 @@
 
 namespace owk {
 
+// decode passes of at most this many rows run the whole-K residual + LayerNorm-prologue chain
+// (engine.cpp launch_decode); larger passes the split-K + resid_layernorm chain
+constexpr int kRowsLnMaxRows = 8;
+
 // per-kernel-class HIP-event timing + algorithmic work counters
 // eager launches with an event pair around each kernel-class launch on the engine stream; with a
 // class selection (owk_prof_select) only the selected classes carry events: the host then stays
@@ -192,6 +196,7 @@ private:
     float * q8d() { return m->q5 && !m->kq ? q8d_.as<float>() : nullptr; }
     DevBuf e_xn32_, e_ao32_, d_xn32_, d_ao32_, d_xl32_;
 
+    DevBuf sm_ws_;       // key-split soft_max attention workspace (flash_attn = false passes)
     DevBuf amap_, cap_;  // DTW: head map [L][H], captured probabilities [n_ah][T][cap_rows_]
     int n_ah_ = 0, cap_rows_ = 0;
 

@@ -863,12 +863,156 @@ __global__ __launch_bounds__(NT) void k_attn_softmax(const _Float16 * __restrict
     }
 }
 
+// The same soft_max attention with every (row, head) spread over ceil(n / SMS_CK) blocks: a block per 128
+// keys computes their scores (A), every chunk block then recomputes the row's exact max and double sum
+// from the stored scores -- the same per-thread residues (mod 256) and wave trees as k_attn_softmax, so
+// probabilities (and DTW captures) are bit-identical to it -- and the P.V partial of its keys (B); a
+// third launch adds the chunk partials in chunk order (C). One (row, head) in one block reads 384 KB
+// of K / V through one CU (configs[4]'s one-row steps: 20 blocks on 256 CUs, ~25 us per cross pass);
+// spread over 12 blocks per head it streams at the chip's rate. Workspace per (row, head): scores
+// [SM_MAX_KEYS] f32, chunk maxima [SMS_MAXC], partials [SMS_MAXC][64] (attn_softmax_ws_floats).
+constexpr int SMS_CK = 128;
+constexpr int SMS_MAXC = SM_MAX_KEYS / SMS_CK;
+constexpr int SMS_PER_RH = SM_MAX_KEYS + SMS_MAXC + SMS_MAXC * 64;
+
+__global__ __launch_bounds__(SMS_CK) void k_sm_split_scores(const _Float16 * __restrict__ q, int ldq,
+                                                            const _Float16 * __restrict__ kb, int ld_kv, int hs,
+                                                            const AttnRow * __restrict__ rows,
+                                                            const int * __restrict__ key_idx, float scale, int H,
+                                                            float * __restrict__ ws) {
+    __shared__ float redf[SMS_CK / 64];
+    const AttnRow job = rows[blockIdx.y];
+    if (job.mode != 2) return;
+    const int h = blockIdx.x % H, c = blockIdx.x / H;
+    const int n = job.n_keys;
+    if (c * SMS_CK >= n) return;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    float * w = ws + ((size_t) blockIdx.y * H + h) * SMS_PER_RH;
+    const int * list = job.key_list >= 0 ? key_idx + job.key_list : nullptr;
+    const _Float16 * kh = kb + job.kv_base + (size_t) h * hs;
+    const _Float16 * qr = q + (size_t) job.q_row * ldq + h * 64;
+    const int i = c * SMS_CK + tid;
+    float s = -INFINITY;
+    if (i < n) {
+        const int cell = list ? list[i] : i;
+        const half8 * kr = (const half8 *) (kh + (size_t) cell * ld_kv);
+        float part[8];
+#pragma unroll
+        for (int cc = 0; cc < 8; ++cc) {
+            const half8 kv = kr[cc];
+            const half8 qv = ((const half8 *) qr)[cc];
+            float a = 0.0f;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) a = fmaf((float) kv[e], (float) qv[e], a);
+            part[cc] = a;
+        }
+        s = (((part[0] + part[1]) + (part[2] + part[3])) + ((part[4] + part[5]) + (part[6] + part[7]))) * scale;
+        w[i] = s;
+    }
+    float mx = s;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+    if (lane == 0) redf[wave] = mx;
+    __syncthreads();
+    if (tid == 0) w[SM_MAX_KEYS + c] = fmaxf(redf[0], redf[1]);
+}
+
+__global__ __launch_bounds__(256) void k_sm_split_pv(const _Float16 * __restrict__ vb, int ld_kv, int hs,
+                                                     const AttnRow * __restrict__ rows, const int * __restrict__ key_idx,
+                                                     int H, const int * __restrict__ amap, float * __restrict__ cap,
+                                                     int cap_rows, float * __restrict__ ws) {
+    __shared__ _Float16 p16[SMS_CK];
+    __shared__ double redd[4];
+    __shared__ float red[32][64];
+    const AttnRow job = rows[blockIdx.y];
+    if (job.mode != 2) return;
+    const int h = blockIdx.x % H, c = blockIdx.x / H;
+    const int n = job.n_keys;
+    if (c * SMS_CK >= n) return;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    float * w = ws + ((size_t) blockIdx.y * H + h) * SMS_PER_RH;
+    const int nc = (n + SMS_CK - 1) / SMS_CK;
+    float mx = w[SM_MAX_KEYS];
+    for (int k = 1; k < nc; ++k) mx = fmaxf(mx, w[SM_MAX_KEYS + k]);
+    // k_attn_softmax's sum: thread t < 256 over keys t + 256 j, each exp as its (float) sp, then the trees
+    double sum = 0.0;
+    for (int i = tid; i < n; i += 256) sum += (double) expf(w[i] - mx);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o, 64);
+    if (lane == 0) redd[wave] = sum;
+    __syncthreads();
+    const float inv = (float) (1.0 / ((redd[0] + redd[1]) + (redd[2] + redd[3])));
+    const int i0 = c * SMS_CK, nk = min(SMS_CK, n - i0);
+    const int a = amap ? amap[h] : -1;
+    if (tid < nk) {
+        const float p = expf(w[i0 + tid] - mx) * inv;
+        p16[tid] = (_Float16) p;
+        if (a >= 0) cap[((size_t) a * n + i0 + tid) * cap_rows + job.q_row] = p;
+    }
+    __syncthreads();
+    // P . V over this chunk: 32 groups of 8 threads (16 bytes of a V row each), keys g + 32 u in order
+    const int * list = job.key_list >= 0 ? key_idx + job.key_list : nullptr;
+    const _Float16 * vh = vb + job.kv_base + (size_t) h * hs;
+    const int g = tid >> 3, seg = tid & 7;
+    half8 vv[SMS_CK / 32];
+#pragma unroll
+    for (int u = 0; u < SMS_CK / 32; ++u) {
+        const int k = min(g + 32 * u, nk - 1);
+        const int cell = list ? list[i0 + k] : i0 + k;
+        vv[u] = *(const half8 *) (vh + (size_t) cell * ld_kv + seg * 8);
+    }
+    float acc[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] = 0.0f;
+#pragma unroll
+    for (int u = 0; u < SMS_CK / 32; ++u) {
+        const int k = g + 32 * u;
+        const float pp = k < nk ? (float) p16[k] : 0.0f;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[e] = fmaf(pp, (float) vv[u][e], acc[e]);
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) red[g][seg * 8 + e] = acc[e];
+    __syncthreads();
+    if (tid < 64) {
+        float r = 0.0f;
+        for (int gg = 0; gg < 32; ++gg) r += red[gg][tid];
+        w[SM_MAX_KEYS + SMS_MAXC + c * 64 + tid] = r;
+    }
+}
+
+__global__ __launch_bounds__(64) void k_sm_split_combine(const AttnRow * __restrict__ rows, int H,
+                                                         const float * __restrict__ ws, _Float16 * __restrict__ out,
+                                                         int ldo, float * __restrict__ out32) {
+    const AttnRow job = rows[blockIdx.y];
+    if (job.mode != 2) return;
+    const int h = blockIdx.x, d = threadIdx.x;
+    const float * w = ws + ((size_t) blockIdx.y * H + h) * SMS_PER_RH + SM_MAX_KEYS + SMS_MAXC;
+    const int nc = (job.n_keys + SMS_CK - 1) / SMS_CK;
+    float r = 0.0f;
+    for (int c = 0; c < nc; ++c) r += w[c * 64 + d];
+    if (out32) out32[(size_t) job.q_row * ldo + h * 64 + d] = r;
+    else out[(size_t) job.q_row * ldo + h * 64 + d] = (_Float16) r;
+}
+
+size_t attn_softmax_ws_floats(int n_rows, int H) { return (size_t) n_rows * H * SMS_PER_RH; }
+
 void attn_decoder_softmax(hipStream_t s, const _Float16 * q, int ldq, const _Float16 * kbase, const _Float16 * vbase,
                           int ld_kv, int hs, const AttnRow * rows_dev, int n_rows, const int * key_idx, int H, float scale,
                           int max_keys, _Float16 * out, int ldo, const int * amap, float * cap, int cap_rows,
-                          float * out32) {
+                          float * out32, float * ws, size_t ws_floats) {
     if (n_rows <= 0) return;
     if (max_keys > SM_MAX_KEYS) throw std::runtime_error("attn_decoder_softmax: too many keys");
+    if (ws) {  // key-split form (every pass that has the workspace: a row's bits do not depend on its pass)
+        if (ws_floats < attn_softmax_ws_floats(n_rows, H)) throw std::runtime_error("attn_decoder_softmax: workspace");
+        const int nc = (max_keys + SMS_CK - 1) / SMS_CK;
+        OWK_LAUNCH(k_sm_split_scores, dim3(H * nc, n_rows), dim3(SMS_CK), 0, s, q, ldq, kbase, ld_kv, hs, rows_dev,
+                   key_idx, scale, H, ws);
+        OWK_LAUNCH(k_sm_split_pv, dim3(H * nc, n_rows), dim3(256), 0, s, vbase, ld_kv, hs, rows_dev, key_idx, H, amap,
+                   cap, cap_rows, ws);
+        OWK_LAUNCH(k_sm_split_combine, dim3(H, n_rows), dim3(64), 0, s, rows_dev, H, ws, out, ldo, out32);
+        return;
+    }
     // outputs do not depend on the width (k_attn_softmax): 1024 threads when the pass has few
     // (row, head) blocks (configs[4]'s one-row steps), 256 otherwise
     if (n_rows * H <= 128)

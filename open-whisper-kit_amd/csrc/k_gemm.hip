@@ -1166,7 +1166,7 @@ __global__ __launch_bounds__(GR_MAXW * 64) void k_gemm_rows_nt(int M, int N, int
 // no LDS image of the rows, no extra launch. The weight tiles are requested right after the x slices,
 // so the statistics are computed while the weights stream in.
 constexpr int GRL_MAXW = 10;  // waves per block: K <= GRL_MAXW * J * 32
-template <int MODE, int MT, int J, int NT>
+template <int MODE, int MT, int J, int NT, bool STATS = true>
 __global__ __launch_bounds__(GRL_MAXW * 64) void k_gemm_rows_ln(int M, int N, int K, const float * __restrict__ x,
                                                                const float * __restrict__ lnw,
                                                                const float * __restrict__ lnb, float eps,
@@ -1215,6 +1215,9 @@ __global__ __launch_bounds__(GRL_MAXW * 64) void k_gemm_rows_ln(int M, int N, in
     };
     float mean[MT], scale[MT];
 #pragma unroll
+    for (int i = 0; i < MT; ++i) mean[i] = 0.0f, scale[i] = 1.0f;
+    if constexpr (STATS) {
+#pragma unroll
     for (int i = 0; i < MT; ++i) {
         double s = 0.0;
 #pragma unroll
@@ -1258,6 +1261,7 @@ __global__ __launch_bounds__(GRL_MAXW * 64) void k_gemm_rows_ln(int M, int N, in
         for (int w = 0; w < nw; ++w) v += rs[1][w][i * 16 + (lane & 15)];
         const float var = (float) (v / (double) K);
         scale[i] = 1.0f / sqrtf(var + eps);
+    }
     }
     // A fragments: f16((x - mean) * scale * w + b), the reference's separate roundings
     half8 a[MT][J];
@@ -1303,7 +1307,7 @@ __global__ __launch_bounds__(GRL_MAXW * 64) void k_gemm_rows_ln(int M, int N, in
     }
 }
 
-template <int MODE> struct LaunchRowsLn {
+template <int MODE, bool STATS = true> struct LaunchRowsLn {
     static void run(hipStream_t s, int M, int N, int K, const float * x, const float * lnw, const float * lnb, float eps,
                     const _Float16 * Wt, const EpiParams & ep) {
         const int nsteps = K / 32;
@@ -1315,7 +1319,7 @@ template <int MODE> struct LaunchRowsLn {
         const dim3 g((tiles + nt - 1) / nt);
         const bool one = M <= 16;
 #define OWK_ROWS_LN_GO(MT_, J_, NT_) \
-    OWK_LAUNCH((k_gemm_rows_ln<MODE, MT_, J_, NT_>), g, dim3(nw * 64), 0, s, M, N, K, x, lnw, lnb, eps, Wt, ep)
+    OWK_LAUNCH((k_gemm_rows_ln<MODE, MT_, J_, NT_, STATS>), g, dim3(nw * 64), 0, s, M, N, K, x, lnw, lnb, eps, Wt, ep)
         if (J == 4) {
             if (nt == 2) { if (one) OWK_ROWS_LN_GO(1, 4, 2); else OWK_ROWS_LN_GO(2, 4, 2); }
             else { if (one) OWK_ROWS_LN_GO(1, 4, 1); else OWK_ROWS_LN_GO(2, 4, 1); }
@@ -2247,8 +2251,16 @@ bool gemm_rows_ln_applies(int M, int N, int K) {
 }
 
 void gemm_rows_ln(hipStream_t s, int mode, int M, int N, int K, const float * x, const float * lnw, const float * lnb,
-                  float eps, const _Float16 * Wt, const EpiParams & ep) {
+                  float eps, const _Float16 * Wt, const EpiParams & ep, bool debug_no_stats) {
     if (!gemm_rows_ln_applies(M, N, K) || !Wt || !x || !lnw || !lnb) throw std::runtime_error("gemm_rows_ln: unsupported shape");
+    if (debug_no_stats) {  // timing experiments only: the LayerNorm statistics skipped (mean 0, scale 1)
+        switch (mode) {
+            case EPI_F16: LaunchRowsLn<EPI_F16, false>::run(s, M, N, K, x, lnw, lnb, eps, Wt, ep); return;
+            case EPI_GELU_F16: LaunchRowsLn<EPI_GELU_F16, false>::run(s, M, N, K, x, lnw, lnb, eps, Wt, ep); return;
+            case EPI_QKV_DEC: LaunchRowsLn<EPI_QKV_DEC, false>::run(s, M, N, K, x, lnw, lnb, eps, Wt, ep); return;
+            default: throw std::runtime_error("gemm_rows_ln: epilogue not instantiated");
+        }
+    }
     switch (mode) {
         case EPI_F16: LaunchRowsLn<EPI_F16>::run(s, M, N, K, x, lnw, lnb, eps, Wt, ep); break;
         case EPI_GELU_F16: LaunchRowsLn<EPI_GELU_F16>::run(s, M, N, K, x, lnw, lnb, eps, Wt, ep); break;

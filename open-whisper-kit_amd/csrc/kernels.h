@@ -92,7 +92,7 @@ void resid_layernorm(hipStream_t s, int M, int N, int ks, const float * part, co
 // epilogues EPI_F16 / EPI_GELU_F16 / EPI_QKV_DEC); Wt the tiled weight copy
 bool gemm_rows_ln_applies(int M, int N, int K);
 void gemm_rows_ln(hipStream_t s, int mode, int M, int N, int K, const float * x, const float * lnw, const float * lnb,
-                  float eps, const _Float16 * Wt, const EpiParams & ep);
+                  float eps, const _Float16 * Wt, const EpiParams & ep, bool debug_no_stats = false);
 // dispatch on M: <= 32 rows decode-row GEMM (needs the tiled copy Wt), <= 64 skinny,
 // else 128x128 tiles (row-major W)
 void gemm(hipStream_t s, int mode, int M, int N, int K, const _Float16 * A, int lda,
@@ -277,7 +277,10 @@ void attn_decoder(hipStream_t s, const _Float16 * q, int ldq, const _Float16 * k
 void attn_decoder_softmax(hipStream_t s, const _Float16 * q, int ldq, const _Float16 * kbase, const _Float16 * vbase,
                           int ld_kv, int hs, const AttnRow * rows_dev, int n_rows, const int * key_idx, int H, float scale,
                           int max_keys, _Float16 * out, int ldo, const int * amap, float * cap, int cap_rows,
-                          float * out32 = nullptr);
+                          float * out32 = nullptr, float * ws = nullptr, size_t ws_floats = 0);
+// workspace of the key-split soft_max form (ws non-null above): every (row, head) over ceil(keys / 128)
+// blocks, probabilities bit-identical to the one-block kernel, P.V partials added in chunk order
+size_t attn_softmax_ws_floats(int n_rows, int H);
 // test/bench hook: the one_chunk cross-attention kernels on contiguous head-major keys (ld 64):
 // which = 1 the one-wave k_attn_step
 void attn_cross_kernel(hipStream_t s, int which, const _Float16 * q, int ldq, const _Float16 * kbase,

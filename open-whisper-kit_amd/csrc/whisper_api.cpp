@@ -1265,6 +1265,14 @@ double owk_debug_gemm_bench(int device, int mode, int M, int N, int K, int iters
 // weights per layer (1.47 GB: every replay streams them from HBM as a decode step does), the whole
 // chain captured in one hipGraph; returns device microseconds per layer (events around replays).
 double owk_debug_decode_chain(int device, int R, int n_layers, int iters) {
+    return owk_debug_decode_chain2(device, R, n_layers, iters, 0);
+}
+
+// variant 0: split-K partial residual matmuls + resid_layernorm, consumers read the f16 LayerNorm rows
+// (the round-3 chain); 1: LayerNorm in the consumer prologue (gemm_rows_ln) + whole-K residual epilogues;
+// 2: as 1 with the prologue statistics skipped (timing only); 3: as 1 but mlp.2 split-K + resid_layernorm
+// and the next QKV from its f16 rows; 4: as 0 but attn.out / cross_attn.out whole-K + LN prologue consumers
+double owk_debug_decode_chain2(int device, int R, int n_layers, int iters, int variant) {
     try {
         OWK_HIP_CHECK(hipSetDevice(device));
         if (R < 1 || R > 32 || n_layers < 1) throw std::runtime_error("bad shape");
@@ -1303,11 +1311,32 @@ double owk_debug_decode_chain(int device, int R, int n_layers, int iters) {
         GemmWs ws;
         ws.partial = part.as<float>();
         ws.partial_floats = fl;
+        // site 0 attn.out, 1 cross_attn.out, 2 mlp.2: split (partial + resid_layernorm) or whole-K
+        auto split_site = [&](int site) {
+            if (variant == 0) return true;
+            if (variant == 3) return site == 2;
+            if (variant == 4) return site == 2;
+            return false;
+        };
+        // consumer c (0 QKV, 1 cross-Q, 2 mlp.0) takes the LayerNorm in its prologue unless its producer
+        // (c = 0: the previous mlp.2, 1: attn.out, 2: cross_attn.out) finished the rows with resid_layernorm
+        auto ln_prologue = [&](int c) { return !split_site(c == 0 ? 2 : c - 1); };
         auto resid = [&](int site, const _Float16 * A, const _Float16 * Wt, int K) {
-            (void) site;
-            gemm(s, EPI_PARTIAL, R, d, K, A, K, nullptr, K, EpiParams(), &ws, Wt);
-            resid_layernorm(s, R, d, gemm_partial_splits(K), ws.partial, bias.as<float>(), x.as<float>(), lnw.as<float>(),
-                            lnb.as<float>(), 1e-5f, xn.as<_Float16>(), d);
+            if (split_site(site)) {
+                gemm(s, EPI_PARTIAL, R, d, K, A, K, nullptr, K, EpiParams(), &ws, Wt);
+                resid_layernorm(s, R, d, gemm_partial_splits(K), ws.partial, bias.as<float>(), x.as<float>(), lnw.as<float>(),
+                                lnb.as<float>(), 1e-5f, xn.as<_Float16>(), d);
+            } else {
+                EpiParams e;
+                e.bias = bias.as<float>(); e.resid = x.as<float>(); e.out32 = x.as<float>(); e.ldo = d;
+                gemm(s, EPI_RESID_F32, R, d, K, A, K, nullptr, K, e, &ws, Wt);
+            }
+        };
+        auto consumer = [&](int c, int mode, int N, const _Float16 * Wt, const EpiParams & e) {
+            if (ln_prologue(c))
+                gemm_rows_ln(s, mode, R, N, d, x.as<float>(), lnw.as<float>(), lnb.as<float>(), 1e-5f, Wt, e, variant == 2);
+            else
+                gemm(s, mode, R, N, d, xn.as<_Float16>(), d, nullptr, d, e, &ws, Wt);
         };
         auto chain = [&]() {
             for (int l = 0; l < n_layers; ++l) {
@@ -1316,16 +1345,16 @@ double owk_debug_decode_chain(int device, int R, int n_layers, int iters) {
                 e1.bias = bias.as<float>(); e1.bias2 = bias.as<float>(); e1.scale = 0.35f;
                 e1.out16 = q.as<_Float16>(); e1.ldo = d; e1.out16b = kc.as<_Float16>(); e1.out16c = vc.as<_Float16>();
                 e1.d = d; e1.row_off = rowoff.as<int64_t>(); e1.Tpad = cells * 64;
-                gemm(s, EPI_QKV_DEC, R, 3 * d, d, xn.as<_Float16>(), d, nullptr, d, e1, &ws, L.qkv.as<_Float16>());
-                resid(3 * l, ao.as<_Float16>(), L.o.as<_Float16>(), d);
+                consumer(0, EPI_QKV_DEC, 3 * d, L.qkv.as<_Float16>(), e1);
+                resid(0, ao.as<_Float16>(), L.o.as<_Float16>(), d);
                 EpiParams e2;
                 e2.bias = bias.as<float>(); e2.out16 = q.as<_Float16>(); e2.ldo = d;
-                gemm(s, EPI_F16, R, d, d, xn.as<_Float16>(), d, nullptr, d, e2, &ws, L.cq.as<_Float16>());
-                resid(3 * l + 1, ao.as<_Float16>(), L.co.as<_Float16>(), d);
+                consumer(1, EPI_F16, d, L.cq.as<_Float16>(), e2);
+                resid(1, ao.as<_Float16>(), L.co.as<_Float16>(), d);
                 EpiParams e3;
                 e3.bias = bias4.as<float>(); e3.gelu_tab = gt.as<uint16_t>(); e3.out16 = h.as<_Float16>(); e3.ldo = 4 * d;
-                gemm(s, EPI_GELU_F16, R, 4 * d, d, xn.as<_Float16>(), d, nullptr, d, e3, &ws, L.m0.as<_Float16>());
-                resid(3 * l + 2, h.as<_Float16>(), L.m1.as<_Float16>(), 4 * d);
+                consumer(2, EPI_GELU_F16, 4 * d, L.m0.as<_Float16>(), e3);
+                resid(2, h.as<_Float16>(), L.m1.as<_Float16>(), 4 * d);
             }
         };
         OWK_HIP_CHECK(hipStreamSynchronize(s));

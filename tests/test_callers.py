@@ -103,7 +103,9 @@ def test_whisper_cli_configs0(case, model_path, tmp_path):
     for gs, rs in zip(got_segs, ref_segs):
         assert [(t["id"], t["text"], t["offsets"]) for t in gs["tokens"]] == \
                [(t["id"], t["text"], t["offsets"]) for t in rs["tokens"]]
-        assert max(abs(a["p"] - b["p"]) for a, b in zip(gs["tokens"], rs["tokens"])) <= 1e-3
+        # whisper-cli prints p with 3 decimals: a probability within the parity bar of the reference's
+        # can round to the neighbouring printed value (one unit of the last digit)
+        assert max(abs(a["p"] - b["p"]) for a, b in zip(gs["tokens"], rs["tokens"])) <= 1e-3 + 1e-9
     assert doc["result"] == want["json"]["result"]
 
 
