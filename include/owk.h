@@ -130,6 +130,9 @@ WHISPER_API int owk_debug_gemm_rows_ln(int device, int M, int N, int K, const fl
                                        const float * lnb, const float * b, const uint16_t * w, uint16_t * out_fused,
                                        uint16_t * out_ref, const uint16_t * w2, const float * resid,
                                        float * out_resid_full, float * out_resid_split);
+/* test hook: decode passes of at most n rows run the whole-K decoder chain (0 = never; bit-identical to the
+ * split-K chain by construction); returns the previous limit */
+WHISPER_API int owk_debug_set_whole_k_rows(int n);
 /* library identity: 1 when the gfx950 HIP code object is present and a device is usable */
 WHISPER_API int owk_device_ok(int device);
 WHISPER_API const char * owk_build_info(void);

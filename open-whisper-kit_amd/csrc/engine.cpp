@@ -1,5 +1,7 @@
 // Batch-major device engine (see engine.h).
 #include "engine.h"
+
+#include <atomic>
 #include "kquant.h"
 
 #include <algorithm>
@@ -122,6 +124,10 @@ Engine::~Engine() {
     for (auto * b : mel_) delete b;
     if (stream) (void) hipStreamDestroy(stream);
 }
+
+static std::atomic<int> g_whole_k_rows{kWholeKRowsDefault};
+int whole_k_rows() { return g_whole_k_rows.load(std::memory_order_relaxed); }
+int set_whole_k_rows(int n) { return g_whole_k_rows.exchange(n); }
 
 void Engine::sync() { OWK_HIP_CHECK(hipStreamSynchronize(stream)); }
 
@@ -650,10 +656,12 @@ void Engine::decode(const std::vector<DecodeRow> & rows, const std::vector<int> 
         graphs_sig_ = sig;
     }
     const uint64_t key = (uint64_t) R | ((uint64_t) n_logit_rows << 20) | ((uint64_t) sh.self_oc << 40) |
+                         ((uint64_t) (R <= whole_k_rows()) << 47) |
                          ((uint64_t) sh.self_tl << 41) | ((uint64_t) sh.cross_oc << 42) | ((uint64_t) sh.cross_tl << 43) |
                          ((uint64_t) sh.self_sm << 44) | ((uint64_t) sh.cross_sm << 45) |
-                         ((uint64_t) sh.self_list << 46) | ((uint64_t) T << 48);  // T: head stride baked in
-    auto it = graphs_.find(key);
+                         ((uint64_t) sh.self_list << 46) | ((uint64_t) T << 48) |  // T: head stride baked in
+                         // soft_max self rows: the key-split grid has one block per 128 keys of the longest row
+                         ((uint64_t) (sh.self_sm ? std::min(15, (sh.max_keys + 127) / 128 - 1) : 0) << 60);    auto it = graphs_.find(key);
     if (it == graphs_.end()) {
         if (graphs_.size() >= 64) clear_graphs();
         hipGraph_t g = nullptr;
@@ -730,16 +738,19 @@ void Engine::launch_decode(const DecShape & sh) {
     // (attn.out, cross_attn.out, mlp.2) is either
     //   split: split-K partial tiles + resid_layernorm, which adds bias + residual and writes the next
     //          LayerNorm's f16 rows for the next matmul (2 launches), or
-    //   whole-K: one launch adding bias + residual in its epilogue (EPI_RESID_F32, in place on x); the
-    //          next matmul then runs the LayerNorm in its own prologue (gemm_rows_ln).
+    //   whole-K (passes of <= whole_k_rows() rows): one launch (gemm_rows_res) adding the same partial
+    //          sums in the same order, bias and residual; the next matmul runs the LayerNorm in its
+    //          prologue (gemm_rows_lnx) with the statistics in the order of the kernel it replaces --
+    //          bit-identical to the split chain, so a clip's result does not depend on its pass size.
     // Whole-K saves a launch per site but every block of the consumer recomputes the row statistics
-    // from the f32 rows: it pays at few rows (configs[4]'s one-row steps) and not at 32
-    // (tools/chain_ab.py). Earlier measured alternatives (profiles/r02e_ab.txt,
+    // from the f32 rows, and the exact split-order reduction costs more than the launch it saves:
+    // 36.8 vs 32.5 us per layer at 1 row, 48.3 vs 36.3 at 8 (profiles/r04h_chain_ab.txt), so it is off
+    // by default (whole_k_rows() = 0) and kept as a verified alternative. Earlier measured alternatives (profiles/r02e_ab.txt,
     // the round-3 ticket finish) lost on the launch boundary or the in-launch seam. soft_max rows
     // (flash_attn = false) and DTW captures run the soft_max attention launches inside the same chain.
     // Larger passes use the full-epilogue GEMMs and separate LayerNorms.
     const bool fused = R <= 32 && !q5;
-    const bool whole_k = fused && R <= kRowsLnMaxRows && gemm_rows_ln_applies(R, 4 * hp.n_text_state, hp.n_text_state);
+    const bool whole_k = fused && R <= whole_k_rows() && gemm_rows_exact_applies(R, hp.n_text_state);
 
     auto fused_rows = [&]() {
         hipStream_t s = stream;
@@ -751,11 +762,12 @@ void Engine::launch_decode(const DecShape & sh) {
         const int n = R;
         // consumer of a LayerNorm (QKV, cross-Q, mlp.0): from the f16 rows the split producer wrote, or
         // with the LayerNorm in its prologue; algorithmic bytes: weights + activation rows once
+        // order: 1 for layer 0's attn_ln (layernorm_f16's statistics), 0 after a residual site (resid_layernorm's)
         auto consumer = [&](int mode, int N, const float * lnw, const float * lnb, const _Float16 * Wt,
-                            const EpiParams & ep) {
+                            const EpiParams & ep, int order) {
             if (whole_k) {
                 ProfScope ps(prof, s, "gemm_dec", 2.0 * n * (double) N * d, 2.0 * (double) N * d + 4.0 * n * d);
-                gemm_rows_ln(s, mode, n, N, d, x, lnw, lnb, hp.eps, Wt, ep);
+                gemm_rows_lnx(s, mode, order, n, N, d, x, lnw, lnb, hp.eps, Wt, ep);
             } else {
                 ProfScope ps(prof, s, "gemm_dec", 2.0 * n * (double) N * d, 2.0 * ((double) n * d + (double) N * d));
                 gemm(s, mode, n, N, d, xn, d, nullptr, d, ep, &gws_, Wt);
@@ -766,12 +778,7 @@ void Engine::launch_decode(const DecShape & sh) {
                          const float * lnb) {
             if (whole_k) {
                 ProfScope ps(prof, s, "gemm_dec", 2.0 * n * (double) d * K, 2.0 * ((double) n * K + (double) d * K));
-                EpiParams ep;
-                ep.bias = bias;
-                ep.resid = x;
-                ep.out32 = x;
-                ep.ldo = d;
-                gemm(s, EPI_RESID_F32, n, d, K, A, K, nullptr, K, ep, &gws_, Wt);
+                gemm_rows_res(s, n, d, K, A, Wt, bias, x);
                 return;
             }
             {
@@ -803,7 +810,7 @@ void Engine::launch_decode(const DecShape & sh) {
                 ep.d = d;
                 ep.row_off = d_rowoff;
                 ep.Tpad = kv_cells * 64;
-                consumer(EPI_QKV_DEC, 3 * d, L.attn_ln_w, L.attn_ln_b, L.t_qkv, ep);
+                consumer(EPI_QKV_DEC, 3 * d, L.attn_ln_w, L.attn_ln_b, L.t_qkv, ep, l == 0 ? 1 : 0);
             }
             {
                 ProfScope ps(prof, s, "attn_self");
@@ -819,7 +826,7 @@ void Engine::launch_decode(const DecShape & sh) {
                 ep.bias = L.cb_q;
                 ep.out16 = qb;
                 ep.ldo = d;
-                consumer(EPI_F16, d, L.cross_ln_w, L.cross_ln_b, L.t_cq, ep);
+                consumer(EPI_F16, d, L.cross_ln_w, L.cross_ln_b, L.t_cq, ep, 0);
             }
             {
                 ProfScope ps(prof, s, "attn_cross", 4.0 * n * (double) n_ctx_pad * d, 2.0 * 2.0 * n * (double) T * d);
@@ -837,7 +844,7 @@ void Engine::launch_decode(const DecShape & sh) {
                 ep.gelu_tab = m->gelu_tab;
                 ep.out16 = hr;
                 ep.ldo = 4 * d;
-                consumer(EPI_GELU_F16, 4 * d, L.mlp_ln_w, L.mlp_ln_b, L.t_mlp0, ep);
+                consumer(EPI_GELU_F16, 4 * d, L.mlp_ln_w, L.mlp_ln_b, L.t_mlp0, ep, 0);
             }
             resid(hr, L.t_mlp1, 4 * d, L.b_mlp1, nx ? nx->attn_ln_w : nullptr, nx ? nx->attn_ln_b : nullptr);
         }

@@ -11,9 +11,13 @@
 
 namespace owk {
 
-// decode passes of at most this many rows run the whole-K residual + LayerNorm-prologue chain
-// (engine.cpp launch_decode); larger passes the split-K + resid_layernorm chain
-constexpr int kRowsLnMaxRows = 8;
+// decode passes of at most whole_k_rows() rows run the whole-K residual + LayerNorm-prologue chain
+// (engine.cpp launch_decode; bit-identical to the split chain), larger passes the split-K +
+// resid_layernorm chain. Default 0: the whole-K chain measured slower at every row count
+// (tools/chain_ab.py, profiles/r04h_chain_ab.txt); the test hook keeps it verified bit-identical.
+constexpr int kWholeKRowsDefault = 0;
+int whole_k_rows();           // the current limit (kWholeKRowsDefault unless a test hook changed it)
+int set_whole_k_rows(int n);  // test hook (owk_debug_set_whole_k_rows); returns the previous limit
 
 // per-kernel-class HIP-event timing + algorithmic work counters
 // eager launches with an event pair around each kernel-class launch on the engine stream; with a

@@ -1307,6 +1307,233 @@ __global__ __launch_bounds__(GRL_MAXW * 64) void k_gemm_rows_ln(int M, int N, in
     }
 }
 
+// ---------------------------------------------------------------------------------
+// Whole-K forms of the decoder's chain for passes of <= 16 rows that reproduce the split chain BIT FOR
+// BIT (a clip's result must not depend on how many rows share its decode pass):
+//   k_gemm_rows_res: the residual matmul (attn.out, cross_attn.out, mlp.2) in one launch. Its waves
+//     play the split-K plan's (k split y, wave w) roles -- same k-steps, same MFMA chains -- and the
+//     epilogue adds the wave partials of each split in wave order, the splits in split order, then
+//     bias and residual: exactly the EPI_PARTIAL launch + resid_layernorm's x update.
+//   k_gemm_rows_lnx: the next matmul with the LayerNorm in its prologue, its statistics formed in the
+//     order of the kernel that wrote the f16 rows in the split chain (ORDER 0: resid_layernorm's 256
+//     threads x 2 float4 and its wave trees; ORDER 1: layernorm_f16's wave per row, 8 float4 per lane,
+//     every lane its own butterfly sum) from per-float4 pair sums exchanged in LDS, and the GEMM's
+//     waves, k-steps and MFMA chains those of the full-epilogue decode-row plan (rows_plan).
+// ---------------------------------------------------------------------------------
+constexpr int LNX_MAX_ROWS = 16, LNX_MAX4 = 320;  // rows per pass, float4 per row (d <= 1280)
+
+template <int J, int KS>
+__global__ __launch_bounds__(GR_MAXW * 64) void k_gemm_rows_res(int M, int N, int K, const _Float16 * __restrict__ A,
+                                                                const _Float16 * __restrict__ Wt,
+                                                                const float * __restrict__ bias, float * __restrict__ x) {
+    __shared__ floatx4 red[KS][GR_MAXW][64];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = blockDim.x >> 6;
+    const int tile = blockIdx.x, n0 = tile * 16;
+    const int nsteps = K >> 5;
+    const half8 z8 = {0, 0, 0, 0, 0, 0, 0, 0};
+    const _Float16 * wp = Wt + ((size_t) tile * nsteps) * 512 + lane * 8;
+    half8 b[KS][J], a[KS][J];
+#pragma unroll
+    for (int y = 0; y < KS; ++y)
+#pragma unroll
+        for (int j = 0; j < J; ++j) {
+            const int ks = (y * nw + wave) * J + j;
+            const half8 t = __builtin_nontemporal_load((const half8 *) (wp + (size_t) min(ks, nsteps - 1) * 512));
+            b[y][j] = ks < nsteps ? t : z8;
+        }
+    __builtin_amdgcn_sched_barrier(0);
+    const _Float16 * ap = A + (size_t) min(lane & 15, M - 1) * K + 8 * (lane >> 4);
+#pragma unroll
+    for (int y = 0; y < KS; ++y)
+#pragma unroll
+        for (int j = 0; j < J; ++j) {
+            const int ks = (y * nw + wave) * J + j;
+            const half8 t = *(const half8 *) (ap + min(ks, nsteps - 1) * 32);
+            a[y][j] = ks < nsteps ? t : z8;
+        }
+#pragma unroll
+    for (int y = 0; y < KS; ++y) {
+        floatx4 acc = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int j = 0; j < J; ++j) acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[y][j], b[y][j], acc, 0, 0, 0);
+        red[y][wave][lane] = acc;
+    }
+    __syncthreads();
+    for (int o = tid; o < 256; o += blockDim.x) {
+        const int r = o >> 4, cc = o & 15;
+        const int ln = 16 * (r >> 2) + cc, e = r & 3;
+        float a_sum = 0.0f;
+#pragma unroll
+        for (int y = 0; y < KS; ++y) {
+            float sy = ((const float *) &red[y][0][ln])[e];
+            for (int w = 1; w < nw; ++w) sy += ((const float *) &red[y][w][ln])[e];
+            a_sum = y == 0 ? sy : a_sum + sy;
+        }
+        const int c = n0 + cc;
+        if (r < M && c < N) {
+            const size_t oi = (size_t) r * N + c;
+            x[oi] = x[oi] + (a_sum + bias[c]);
+        }
+    }
+}
+
+__device__ __forceinline__ double pair_sum_d(const float4 v) {
+    return ((double) v.x + (double) v.y) + ((double) v.z + (double) v.w);
+}
+__device__ __forceinline__ double pair_sq_d(const float4 v, float m) {
+    const float tx = v.x - m, ty = v.y - m, tz = v.z - m, tw = v.w - m;
+    return ((double) (tx * tx) + (double) (ty * ty)) + ((double) (tz * tz) + (double) (tw * tw));
+}
+__device__ __forceinline__ double wave_bfly_sum_d(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+template <int MODE, int J, int NT, int ORDER>
+__global__ __launch_bounds__(GR_MAXW * 64) void k_gemm_rows_lnx(int M, int N, int K, const float * __restrict__ x,
+                                                                const float * __restrict__ lnw,
+                                                                const float * __restrict__ lnb, float eps,
+                                                                const _Float16 * __restrict__ Wt, EpiParams ep) {
+    __shared__ floatx4 red[GR_MAXW][NT][64];
+    __shared__ double pd[LNX_MAX_ROWS][LNX_MAX4];
+    __shared__ double rs[LNX_MAX_ROWS][4];
+    __shared__ float mrow[LNX_MAX_ROWS][64], srow[LNX_MAX_ROWS][64];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = blockDim.x >> 6;
+    const int ntiles = (N + 15) >> 4, t0 = blockIdx.x * NT;
+    const int nsteps = K >> 5, n4 = K >> 2;
+    const int ks0 = wave * J;
+    const int nj = max(0, min(J, nsteps - ks0));
+    const int g = lane >> 4, row = lane & 15;
+    const bool own = row < M;  // lanes of clamped rows only read
+    float4 xv[J][2];
+    {
+        const float * xr = x + (size_t) min(row, M - 1) * K + 8 * g;
+#pragma unroll
+        for (int j = 0; j < J; ++j) {
+            const float4 * p = (const float4 *) (xr + min(ks0 + j, nsteps - 1) * 32);
+            xv[j][0] = p[0];
+            xv[j][1] = p[1];
+        }
+    }
+    half8 b[NT][J];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+        const _Float16 * wp = Wt + ((size_t) min(t0 + t, ntiles - 1) * nsteps) * 512 + lane * 8;
+#pragma unroll
+        for (int j = 0; j < J; ++j)
+            b[t][j] = __builtin_nontemporal_load((const half8 *) (wp + (size_t) min(ks0 + j, nsteps - 1) * 512));
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    // float4 index of (j, h) in the row: k-step * 8 + 2 g + h
+    auto f4 = [&](int j, int h) { return (ks0 + j) * 8 + 2 * g + h; };
+    // 1. pair sums of every float4 of the rows
+#pragma unroll
+    for (int j = 0; j < J; ++j)
+        if (j < nj && own)
+#pragma unroll
+            for (int h = 0; h < 2; ++h) pd[row][f4(j, h)] = pair_sum_d(xv[j][h]);
+    __syncthreads();
+    // 2. the mean, in the partition of the split chain's LayerNorm kernel
+    if constexpr (ORDER == 0) {
+        for (int task = wave; task < M * 4; task += nw) {
+            const int r = task >> 2, vw = task & 3, t = vw * 64 + lane;
+            double s = 0.0;
+            s += t < n4 ? pd[r][t] : 0.0;
+            s += t + 256 < n4 ? pd[r][t + 256] : 0.0;
+            s = wave_bfly_sum_d(s);
+            if (lane == 0) rs[r][vw] = s;
+        }
+    } else {
+        for (int r = wave; r < M; r += nw) {
+            double s = 0.0;
+#pragma unroll
+            for (int jj = 0; jj < 8; ++jj) s += lane + 64 * jj < n4 ? pd[r][lane + 64 * jj] : 0.0;
+            s = wave_bfly_sum_d(s);
+            mrow[r][lane] = (float) s / (float) K;
+        }
+    }
+    __syncthreads();
+    float mean_r = 0.0f;
+    if constexpr (ORDER == 0)
+        mean_r = (float) ((rs[min(row, M - 1)][0] + rs[min(row, M - 1)][1]) +
+                          (rs[min(row, M - 1)][2] + rs[min(row, M - 1)][3])) / (float) K;
+    auto mean_of = [&](int i) { return ORDER == 0 ? mean_r : mrow[min(row, M - 1)][i & 63]; };
+    // 3. centred squares (f32 difference and square, as the LayerNorm kernels), same partitions
+#pragma unroll
+    for (int j = 0; j < J; ++j)
+        if (j < nj && own)
+#pragma unroll
+            for (int h = 0; h < 2; ++h) pd[row][f4(j, h)] = pair_sq_d(xv[j][h], mean_of(f4(j, h)));
+    __syncthreads();
+    if constexpr (ORDER == 0) {
+        for (int task = wave; task < M * 4; task += nw) {
+            const int r = task >> 2, vw = task & 3, t = vw * 64 + lane;
+            double v = 0.0;
+            if (t < n4) v += pd[r][t];
+            if (t + 256 < n4) v += pd[r][t + 256];
+            v = wave_bfly_sum_d(v);
+            if (lane == 0) rs[r][vw] = v;
+        }
+    } else {
+        for (int r = wave; r < M; r += nw) {
+            double v = 0.0;
+#pragma unroll
+            for (int jj = 0; jj < 8; ++jj)
+                if (lane + 64 * jj < n4) v += pd[r][lane + 64 * jj];
+            v = wave_bfly_sum_d(v);
+            srow[r][lane] = 1.0f / sqrtf((float) (v / (double) K) + eps);
+        }
+    }
+    __syncthreads();
+    float scale_r = 0.0f;
+    if constexpr (ORDER == 0) {
+        const int rr = min(row, M - 1);
+        const float var = (float) (((rs[rr][0] + rs[rr][1]) + (rs[rr][2] + rs[rr][3])) / (double) K);
+        scale_r = 1.0f / sqrtf(var + eps);
+    }
+    auto scale_of = [&](int i) { return ORDER == 0 ? scale_r : srow[min(row, M - 1)][i & 63]; };
+    // 4. A fragments f16((x - mean) * scale * w + b)
+    const half8 z8 = {0, 0, 0, 0, 0, 0, 0, 0};
+    half8 a[J];
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+        const int c = min(ks0 + j, nsteps - 1) * 32 + 8 * g;
+        const float4 w0 = *(const float4 *) (lnw + c), w1 = *(const float4 *) (lnw + c + 4);
+        const float4 b0 = *(const float4 *) (lnb + c), b1 = *(const float4 *) (lnb + c + 4);
+        const float wv[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+        const float bv[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+        const float xs[8] = {xv[j][0].x, xv[j][0].y, xv[j][0].z, xv[j][0].w, xv[j][1].x, xv[j][1].y, xv[j][1].z, xv[j][1].w};
+        half8 hv;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const int i = f4(j, e >> 2);
+            hv[e] = (_Float16) ((xs[e] - mean_of(i)) * scale_of(i) * wv[e] + bv[e]);
+        }
+        a[j] = j < nj ? hv : z8;
+        if (j >= nj)
+#pragma unroll
+            for (int t = 0; t < NT; ++t) b[t][j] = z8;
+    }
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+        floatx4 acc = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int j = 0; j < J; ++j) acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[j], b[t][j], acc, 0, 0, 0);
+        red[wave][t][lane] = acc;
+    }
+    __syncthreads();
+    for (int o = tid; o < NT * 256; o += blockDim.x) {
+        const int t = o >> 8, q = o & 255;
+        const int r = q >> 4, cc = q & 15;
+        const int ln = 16 * (r >> 2) + cc, e = r & 3;
+        float sum = ((const float *) &red[0][t][ln])[e];
+        for (int w = 1; w < nw; ++w) sum += ((const float *) &red[w][t][ln])[e];
+        const int c = (t0 + t) * 16 + cc;
+        if (r < M && c < N) epi_store<MODE>(ep, r, c, sum);
+    }
+}
+
 template <int MODE, bool STATS = true> struct LaunchRowsLn {
     static void run(hipStream_t s, int M, int N, int K, const float * x, const float * lnw, const float * lnb, float eps,
                     const _Float16 * Wt, const EpiParams & ep) {
@@ -2245,6 +2472,57 @@ size_t gemm_ws_floats(int N, int K) {
 }
 size_t gemm_partial_floats(int N, int K) { return (size_t) rows_plan(K, true).KS * ((N + 15) / 16) * 2 * 64 * 4; }
 int gemm_partial_splits(int K) { return rows_plan(K, true).KS; }
+
+bool gemm_rows_exact_applies(int M, int d) {
+    if (M < 1 || M > LNX_MAX_ROWS || d % 32 || d / 4 > LNX_MAX4) return false;
+    const RowsPlan pf = rows_plan(d, false), pr = rows_plan(4 * d, true), po = rows_plan(d, true);
+    return pf.KS == 1 && (pf.J == 2 || pf.J == 4) && pr.KS <= 3 && po.KS <= 3;
+}
+
+void gemm_rows_res(hipStream_t s, int M, int N, int K, const _Float16 * A, const _Float16 * Wt, const float * bias,
+                   float * x) {
+    const RowsPlan p = rows_plan(K, true);
+    if (M < 1 || M > 16 || N % 16 || K % 32 || p.KS > 3 || !Wt || !A || !bias || !x)
+        throw std::runtime_error("gemm_rows_res: unsupported shape");
+    const dim3 g((N + 15) / 16);
+#define OWK_RES_GO(J_, KS_) OWK_LAUNCH((k_gemm_rows_res<J_, KS_>), g, dim3(p.nw * 64), 0, s, M, N, K, A, Wt, bias, x)
+    if (p.J == 2) {
+        if (p.KS == 1) OWK_RES_GO(2, 1); else if (p.KS == 2) OWK_RES_GO(2, 2); else OWK_RES_GO(2, 3);
+    } else {
+        if (p.KS == 1) OWK_RES_GO(4, 1); else if (p.KS == 2) OWK_RES_GO(4, 2); else OWK_RES_GO(4, 3);
+    }
+#undef OWK_RES_GO
+}
+
+template <int MODE> static void launch_lnx(hipStream_t s, int order, int M, int N, int K, const float * x, const float * lnw,
+                                           const float * lnb, float eps, const _Float16 * Wt, const EpiParams & ep) {
+    const RowsPlan p = rows_plan(K, false);
+    const int tiles = (N + 15) / 16;
+    // column tiles per block as the split chain's full-epilogue dispatch (LaunchRows): no effect on bits
+    const int nt = (p.J == 4 || p.J == 2) && (tiles + 1) / 2 >= 128 ? 2 : 1;
+    const dim3 g((tiles + nt - 1) / nt);
+#define OWK_LNX_GO(J_, NT_, O_) \
+    OWK_LAUNCH((k_gemm_rows_lnx<MODE, J_, NT_, O_>), g, dim3(p.nw * 64), 0, s, M, N, K, x, lnw, lnb, eps, Wt, ep)
+    if (p.J == 4) {
+        if (nt == 2) { if (order) OWK_LNX_GO(4, 2, 1); else OWK_LNX_GO(4, 2, 0); }
+        else { if (order) OWK_LNX_GO(4, 1, 1); else OWK_LNX_GO(4, 1, 0); }
+    } else {
+        if (nt == 2) { if (order) OWK_LNX_GO(2, 2, 1); else OWK_LNX_GO(2, 2, 0); }
+        else { if (order) OWK_LNX_GO(2, 1, 1); else OWK_LNX_GO(2, 1, 0); }
+    }
+#undef OWK_LNX_GO
+}
+
+void gemm_rows_lnx(hipStream_t s, int mode, int order, int M, int N, int K, const float * x, const float * lnw,
+                   const float * lnb, float eps, const _Float16 * Wt, const EpiParams & ep) {
+    if (!gemm_rows_exact_applies(M, K) || N % 16 || !Wt || !x || !lnw || !lnb) throw std::runtime_error("gemm_rows_lnx: unsupported shape");
+    switch (mode) {
+        case EPI_F16: launch_lnx<EPI_F16>(s, order, M, N, K, x, lnw, lnb, eps, Wt, ep); break;
+        case EPI_GELU_F16: launch_lnx<EPI_GELU_F16>(s, order, M, N, K, x, lnw, lnb, eps, Wt, ep); break;
+        case EPI_QKV_DEC: launch_lnx<EPI_QKV_DEC>(s, order, M, N, K, x, lnw, lnb, eps, Wt, ep); break;
+        default: throw std::runtime_error("gemm_rows_lnx: epilogue not instantiated");
+    }
+}
 
 bool gemm_rows_ln_applies(int M, int N, int K) {
     return M >= 1 && M <= 32 && K % 32 == 0 && K % 8 == 0 && N % 16 == 0 && K / 32 <= GRL_MAXW * 4;

@@ -90,6 +90,14 @@ void resid_layernorm(hipStream_t s, int M, int N, int ks, const float * part, co
 // decode-row GEMM whose A operand is f16(LayerNorm(x)) of the f32 residual stream x [M][K] (lnw / lnb
 // the LayerNorm gain / bias [K]): the LayerNorm runs in the GEMM's prologue (M <= 32, K <= 1280,
 // epilogues EPI_F16 / EPI_GELU_F16 / EPI_QKV_DEC); Wt the tiled weight copy
+// the bit-exact whole-K chain of passes with <= 16 rows (k_gemm.hip): residual matmul in one launch
+// (x += A W^T + bias, the split-K partials + resid_layernorm's order) and the LayerNorm-prologue matmul
+// (order 0: the statistics of resid_layernorm, 1: of layernorm_f16 -- the kernel whose f16 rows it replaces)
+bool gemm_rows_exact_applies(int M, int d);
+void gemm_rows_res(hipStream_t s, int M, int N, int K, const _Float16 * A, const _Float16 * Wt, const float * bias,
+                   float * x);
+void gemm_rows_lnx(hipStream_t s, int mode, int order, int M, int N, int K, const float * x, const float * lnw,
+                   const float * lnb, float eps, const _Float16 * Wt, const EpiParams & ep);
 bool gemm_rows_ln_applies(int M, int N, int K);
 void gemm_rows_ln(hipStream_t s, int mode, int M, int N, int K, const float * x, const float * lnw, const float * lnb,
                   float eps, const _Float16 * Wt, const EpiParams & ep, bool debug_no_stats = false);

@@ -1271,7 +1271,8 @@ double owk_debug_decode_chain(int device, int R, int n_layers, int iters) {
 // variant 0: split-K partial residual matmuls + resid_layernorm, consumers read the f16 LayerNorm rows
 // (the round-3 chain); 1: LayerNorm in the consumer prologue (gemm_rows_ln) + whole-K residual epilogues;
 // 2: as 1 with the prologue statistics skipped (timing only); 3: as 1 but mlp.2 split-K + resid_layernorm
-// and the next QKV from its f16 rows; 4: as 0 but attn.out / cross_attn.out whole-K + LN prologue consumers
+// and the next QKV from its f16 rows; 4: as 0 but attn.out / cross_attn.out whole-K + LN prologue consumers;
+// 5: the bit-exact whole-K chain the engine runs at <= whole_k_rows() rows (gemm_rows_res + gemm_rows_lnx)
 double owk_debug_decode_chain2(int device, int R, int n_layers, int iters, int variant) {
     try {
         OWK_HIP_CHECK(hipSetDevice(device));
@@ -1321,8 +1322,11 @@ double owk_debug_decode_chain2(int device, int R, int n_layers, int iters, int v
         // consumer c (0 QKV, 1 cross-Q, 2 mlp.0) takes the LayerNorm in its prologue unless its producer
         // (c = 0: the previous mlp.2, 1: attn.out, 2: cross_attn.out) finished the rows with resid_layernorm
         auto ln_prologue = [&](int c) { return !split_site(c == 0 ? 2 : c - 1); };
+        if (variant == 5 && !gemm_rows_exact_applies(R, d)) throw std::runtime_error("variant 5: too many rows");
         auto resid = [&](int site, const _Float16 * A, const _Float16 * Wt, int K) {
-            if (split_site(site)) {
+            if (variant == 5) {
+                gemm_rows_res(s, R, d, K, A, Wt, bias.as<float>(), x.as<float>());
+            } else if (split_site(site)) {
                 gemm(s, EPI_PARTIAL, R, d, K, A, K, nullptr, K, EpiParams(), &ws, Wt);
                 resid_layernorm(s, R, d, gemm_partial_splits(K), ws.partial, bias.as<float>(), x.as<float>(), lnw.as<float>(),
                                 lnb.as<float>(), 1e-5f, xn.as<_Float16>(), d);
@@ -1333,7 +1337,9 @@ double owk_debug_decode_chain2(int device, int R, int n_layers, int iters, int v
             }
         };
         auto consumer = [&](int c, int mode, int N, const _Float16 * Wt, const EpiParams & e) {
-            if (ln_prologue(c))
+            if (variant == 5)
+                gemm_rows_lnx(s, mode, 0, R, N, d, x.as<float>(), lnw.as<float>(), lnb.as<float>(), 1e-5f, Wt, e);
+            else if (ln_prologue(c))
                 gemm_rows_ln(s, mode, R, N, d, x.as<float>(), lnw.as<float>(), lnb.as<float>(), 1e-5f, Wt, e, variant == 2);
             else
                 gemm(s, mode, R, N, d, xn.as<_Float16>(), d, nullptr, d, e, &ws, Wt);
@@ -1816,5 +1822,9 @@ int owk_debug_gemm_rows_ln(int device, int M, int N, int K, const float * x, con
     }
     return 0;
 }
+
+// test hook: decode passes of at most n rows take the whole-K chain (engine.cpp; 0 = never); returns
+// the previous limit. Both chains must give the same bits (tests/test_gpu_kernels.py).
+int owk_debug_set_whole_k_rows(int n) { return set_whole_k_rows(n); }
 
 }  // extern "C"

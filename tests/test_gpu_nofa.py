@@ -152,3 +152,25 @@ def test_dtw_timestamps(nofa, model_path, clips, model, clip):
     else:
         assert all(abs(a - b) <= 20 and a >= 0 and b >= 0 for _, a, b in diff), f"t_dtw differs: {diff[:10]}"
         assert len(diff) <= 0.05 * len(r_dtw), f"t_dtw differs on {len(diff)}/{len(r_dtw)} tokens: {diff[:10]}"
+
+
+def test_dtw_with_reduced_audio_ctx_fails_cleanly(nofa, model_path, clips):
+    """DTW timestamps with audio_ctx below the window (ref whisper.cpp:8850 asserts n_frames <= 2 *
+    n_audio_ctx: the reference aborts the process): the engine returns an error code from
+    whisper_full (timestamps.cpp's guard) instead of reading past the captured attention, logs why,
+    and the context and a new state keep working (the same call at full width succeeds afterwards)."""
+    meta, _ = nofa
+    owk.quiet()
+    w = whisper_nofa(model_path, meta, "tiny.en")
+    st = w.new_state()
+    # no timestamp tokens: the window's seek_delta stays 3000 frames > 2 x 384
+    p = w.params(0, language="en", temperature_inc=0.0, audio_ctx=384, no_timestamps=True)
+    del owk.errors[:]
+    ret = w.full(st, clips["synth30"], p)
+    assert ret != 0, "DTW over a window longer than 2 x audio_ctx frames must fail"
+    assert any("n_frames" in e and "n_audio_ctx" in e for e in owk.errors), owk.errors[-5:]
+    st2 = w.new_state()
+    want = meta["results"]["tiny.en/synth30/full/greedy_dtw"]
+    p2 = w.params(0, language="en", temperature_inc=0.0, no_timestamps=want["no_timestamps"])
+    assert w.full(st2, clips["synth30"], p2) == want["ret"]
+    assert w.segments(st2), "the context must still decode after the failed call"

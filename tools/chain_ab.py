@@ -11,6 +11,6 @@ L = owk.load()
 f = L.owk_debug_decode_chain2
 f.restype = C.c_double
 f.argtypes = [C.c_int] * 5
-for R in (32, 1):
-    for v in (0, 1, 2, 3, 4, 0, 1):
+for R in (32, 16, 8, 4, 1):
+    for v in ((0, 1, 0, 1) if R > 16 else (0, 5, 1, 0, 5)):
         print(f"R={R} variant {v}: {f(0, R, 8, 40, v):.2f} us per layer", flush=True)

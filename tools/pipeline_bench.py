@@ -168,6 +168,8 @@ def main():
     ap.add_argument("--mode", choices=["both", "chunked", "sequential"], default="both")
     ap.add_argument("--serial", dest="concurrent", action="store_false",
                     help="sequential mode: diarize after the transcription instead of beside it")
+    ap.add_argument("--whole-k-rows", type=int, default=None,
+                    help="A/B: decode passes of at most this many rows take the whole-K chain (engine default if unset)")
     args = ap.parse_args()
     cache = os.environ.get("OWK_MODEL_CACHE", "/tmp/owk_models")
     model = S.ensure_model("large-v3", cache_dir=cache)
@@ -179,6 +181,10 @@ def main():
     pcm = S.synth_audio(n, 5)
 
     owk.quiet()
+    if args.whole_k_rows is not None:
+        import ctypes as C
+        owk.load().owk_debug_set_whole_k_rows.argtypes = [C.c_int]
+        owk.load().owk_debug_set_whole_k_rows(args.whole_k_rows)
     w = owk.Whisper(model, flash_attn=False, dtw_preset=AHEADS_LARGE_V3)
     sf = SF.Sortformer(sf_path)
     import ctypes as C
