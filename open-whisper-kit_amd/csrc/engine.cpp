@@ -649,43 +649,55 @@ void Engine::decode(const std::vector<DecodeRow> & rows, const std::vector<int> 
         launch_decode(sh);
         return;
     }
-    // replay a captured graph of the whole decoder pass (one launch instead of ~10 per layer)
+    // replay captured graphs of the decoder pass (one launch instead of ~10 per layer)
     const uint64_t sig = buffers_signature();
     if (sig != graphs_sig_) {
         clear_graphs();
         graphs_sig_ = sig;
     }
-    const uint64_t key = (uint64_t) R | ((uint64_t) n_logit_rows << 20) | ((uint64_t) sh.self_oc << 40) |
-                         ((uint64_t) (R <= whole_k_rows()) << 47) |
-                         ((uint64_t) sh.self_tl << 41) | ((uint64_t) sh.cross_oc << 42) | ((uint64_t) sh.cross_tl << 43) |
-                         ((uint64_t) sh.self_sm << 44) | ((uint64_t) sh.cross_sm << 45) |
-                         ((uint64_t) sh.self_list << 46) | ((uint64_t) T << 48) |  // T: head stride baked in
-                         // soft_max self rows: the key-split grid has one block per 128 keys of the longest row
-                         ((uint64_t) (sh.self_sm ? std::min(15, (sh.max_keys + 127) / 128 - 1) : 0) << 60);    auto it = graphs_.find(key);
-    if (it == graphs_.end()) {
-        if (graphs_.size() >= 64) clear_graphs();
-        hipGraph_t g = nullptr;
-        OWK_HIP_CHECK(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal));
-        try {
-            launch_decode(sh);
-        } catch (...) {
-            (void) hipStreamEndCapture(stream, &g);
-            if (g) (void) hipGraphDestroy(g);
-            throw;
-        }
-        OWK_HIP_CHECK(hipStreamEndCapture(stream, &g));
-        hipGraphExec_t ex = nullptr;
-        const hipError_t e = hipGraphInstantiate(&ex, g, nullptr, nullptr, 0);
-        (void) hipGraphDestroy(g);
-        OWK_HIP_CHECK(e);
-        it = graphs_.emplace(key, ex).first;
+    // bits 0-19 R, 20-39 n_logit_rows, 40-47 flags,
+    // 48-58 T (the cross head stride baked in), 60-63 the soft_max self-attention chunk count
+    const uint64_t shape = ((uint64_t) sh.self_oc << 40) | ((uint64_t) sh.self_tl << 41) |
+                           ((uint64_t) sh.cross_oc << 42) | ((uint64_t) sh.cross_tl << 43) |
+                           ((uint64_t) sh.self_sm << 44) | ((uint64_t) sh.cross_sm << 45) |
+                           ((uint64_t) sh.self_list << 46) | ((uint64_t) (R <= whole_k_rows()) << 47) |
+                           ((uint64_t) T << 48) |
+                           // soft_max self rows: the key-split grid has one block per 128 keys of the longest row
+                           ((uint64_t) (sh.self_sm ? std::min(15, (sh.max_keys + 127) / 128 - 1) : 0) << 60);
+    const uint64_t key = (uint64_t) R | ((uint64_t) n_logit_rows << 20) | shape;
+    OWK_HIP_CHECK(hipGraphLaunch(graph_for(key, stream, [&]() { launch_decode(sh); }), stream));
+}
+
+hipGraphExec_t Engine::graph_for(uint64_t key, hipStream_t s, const std::function<void()> & launch) {
+    auto it = graphs_.find(key);
+    if (it != graphs_.end()) return it->second;
+    if (graphs_.size() >= 64) clear_graphs();
+    hipGraph_t g = nullptr;
+    OWK_HIP_CHECK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+    try {
+        launch();
+    } catch (...) {
+        (void) hipStreamEndCapture(s, &g);
+        if (g) (void) hipGraphDestroy(g);
+        throw;
     }
-    OWK_HIP_CHECK(hipGraphLaunch(it->second, stream));
+    OWK_HIP_CHECK(hipStreamEndCapture(s, &g));
+    hipGraphExec_t ex = nullptr;
+    const hipError_t e = hipGraphInstantiate(&ex, g, nullptr, nullptr, 0);
+    (void) hipGraphDestroy(g);
+    OWK_HIP_CHECK(e);
+    graphs_.emplace(key, ex);
+    return ex;
 }
 
 void Engine::launch_decode(const DecShape & sh) {
+    if (sh.R <= 32 && !m->q5) {  // F16 passes of <= 32 rows: the decode-row chain
+        fused_part(sh, 0, sh.R, stream, &gws_);
+        launch_logits(sh);
+        return;
+    }
     const HParams & hp = m->hp;
-    const int R = sh.R, n_logit_rows = sh.n_logit;
+    const int R = sh.R;
     const int d = hp.n_text_state, H = hp.n_text_head, T = n_ctx();
     const int n_ctx_pad = (T + 255) / 256 * 256;
     const int nv = hp.n_vocab;
@@ -734,121 +746,6 @@ void Engine::launch_decode(const DecShape & sh) {
         attn_decoder(stream, qv, d, cross_k_.as<_Float16>() + l * cross_stride, cross_v_.as<_Float16>() + l * cross_stride,
                      64, T * 64, d_rc, R, nullptr, H, kq_scale, T, o16, d, cross_oc, cross_tl, o32, true, q8, q8d);
     };
-    // R <= 32 rows (F16 weights): the per-layer chain of decode-row GEMMs. Each residual matmul site
-    // (attn.out, cross_attn.out, mlp.2) is either
-    //   split: split-K partial tiles + resid_layernorm, which adds bias + residual and writes the next
-    //          LayerNorm's f16 rows for the next matmul (2 launches), or
-    //   whole-K (passes of <= whole_k_rows() rows): one launch (gemm_rows_res) adding the same partial
-    //          sums in the same order, bias and residual; the next matmul runs the LayerNorm in its
-    //          prologue (gemm_rows_lnx) with the statistics in the order of the kernel it replaces --
-    //          bit-identical to the split chain, so a clip's result does not depend on its pass size.
-    // Whole-K saves a launch per site but every block of the consumer recomputes the row statistics
-    // from the f32 rows, and the exact split-order reduction costs more than the launch it saves:
-    // 36.8 vs 32.5 us per layer at 1 row, 48.3 vs 36.3 at 8 (profiles/r04h_chain_ab.txt), so it is off
-    // by default (whole_k_rows() = 0) and kept as a verified alternative. Earlier measured alternatives (profiles/r02e_ab.txt,
-    // the round-3 ticket finish) lost on the launch boundary or the in-launch seam. soft_max rows
-    // (flash_attn = false) and DTW captures run the soft_max attention launches inside the same chain.
-    // Larger passes use the full-epilogue GEMMs and separate LayerNorms.
-    const bool fused = R <= 32 && !q5;
-    const bool whole_k = fused && R <= whole_k_rows() && gemm_rows_exact_applies(R, hp.n_text_state);
-
-    auto fused_rows = [&]() {
-        hipStream_t s = stream;
-        float * x = d_x_.as<float>();
-        _Float16 * xn = d_xn_.as<_Float16>();
-        _Float16 * qb = d_q_.as<_Float16>();
-        _Float16 * aob = d_ao_.as<_Float16>();
-        _Float16 * hr = d_h_.as<_Float16>();
-        const int n = R;
-        // consumer of a LayerNorm (QKV, cross-Q, mlp.0): from the f16 rows the split producer wrote, or
-        // with the LayerNorm in its prologue; algorithmic bytes: weights + activation rows once
-        // order: 1 for layer 0's attn_ln (layernorm_f16's statistics), 0 after a residual site (resid_layernorm's)
-        auto consumer = [&](int mode, int N, const float * lnw, const float * lnb, const _Float16 * Wt,
-                            const EpiParams & ep, int order) {
-            if (whole_k) {
-                ProfScope ps(prof, s, "gemm_dec", 2.0 * n * (double) N * d, 2.0 * (double) N * d + 4.0 * n * d);
-                gemm_rows_lnx(s, mode, order, n, N, d, x, lnw, lnb, hp.eps, Wt, ep);
-            } else {
-                ProfScope ps(prof, s, "gemm_dec", 2.0 * n * (double) N * d, 2.0 * ((double) n * d + (double) N * d));
-                gemm(s, mode, n, N, d, xn, d, nullptr, d, ep, &gws_, Wt);
-            }
-        };
-        // residual matmul; lnw / lnb: the LayerNorm of the next consumer (null after the last layer)
-        auto resid = [&](const _Float16 * A, const _Float16 * Wt, int K, const float * bias, const float * lnw,
-                         const float * lnb) {
-            if (whole_k) {
-                ProfScope ps(prof, s, "gemm_dec", 2.0 * n * (double) d * K, 2.0 * ((double) n * K + (double) d * K));
-                gemm_rows_res(s, n, d, K, A, Wt, bias, x);
-                return;
-            }
-            {
-                ProfScope ps(prof, s, "gemm_dec", 2.0 * n * (double) d * K, 2.0 * ((double) n * K + (double) d * K));
-                gemm(s, EPI_PARTIAL, n, d, K, A, K, nullptr, K, EpiParams(), &gws_, Wt);
-            }
-            ProfScope ps(prof, s, "layernorm");
-            resid_layernorm(s, n, d, gemm_partial_splits(K), gws_.partial, bias, x, lnw, lnb, hp.eps, xn, d);
-        };
-        if (!whole_k) {  // layer 0's attn_ln of the embeddings
-            ProfScope ps(prof, s, "layernorm");
-            layernorm_f16(s, x, n, d, m->dec[0].attn_ln_w, m->dec[0].attn_ln_b, hp.eps, xn, d, nullptr, nullptr,
-                          nullptr, nullptr);
-        }
-        for (int l = 0; l < hp.n_text_layer; ++l) {
-            const DecLayerW & L = m->dec[l];
-            const DecLayerW * nx = l + 1 < hp.n_text_layer ? &m->dec[l + 1] : nullptr;
-            _Float16 * Kl = self_k_.as<_Float16>() + l * self_stride;
-            _Float16 * Vl = self_v_.as<_Float16>() + l * self_stride;
-            {
-                EpiParams ep;
-                ep.bias = L.b_q;
-                ep.bias2 = L.b_v;
-                ep.scale = kq_scale;
-                ep.out16 = qb;
-                ep.ldo = d;
-                ep.out16b = Kl;
-                ep.out16c = Vl;
-                ep.d = d;
-                ep.row_off = d_rowoff;
-                ep.Tpad = kv_cells * 64;
-                consumer(EPI_QKV_DEC, 3 * d, L.attn_ln_w, L.attn_ln_b, L.t_qkv, ep, l == 0 ? 1 : 0);
-            }
-            {
-                ProfScope ps(prof, s, "attn_self");
-                attn_decoder(s, qb, d, Kl, Vl, 64, kv_cells * 64, d_rs, n, d_keys, H, 1.0f, max_keys, aob, d,
-                             self_oc, self_tl, nullptr, sh.self_list, nullptr, nullptr);
-                if (sh.self_sm)  // flash_attn = false rows: masked soft_max (scale 1; Q, K pre-scaled)
-                    attn_decoder_softmax(s, qb, d, Kl, Vl, 64, kv_cells * 64, d_rs, n, d_keys, H, 1.0f, max_keys, aob,
-                                         d, nullptr, nullptr, 0, nullptr, sm_ws(), sm_ws_floats());
-            }
-            resid(aob, L.t_o, d, L.b_o, L.cross_ln_w, L.cross_ln_b);
-            {
-                EpiParams ep;
-                ep.bias = L.cb_q;
-                ep.out16 = qb;
-                ep.ldo = d;
-                consumer(EPI_F16, d, L.cross_ln_w, L.cross_ln_b, L.t_cq, ep, 0);
-            }
-            {
-                ProfScope ps(prof, s, "attn_cross", 4.0 * n * (double) n_ctx_pad * d, 2.0 * 2.0 * n * (double) T * d);
-                cross_attn(l, qb, aob, nullptr, nullptr, nullptr);
-                if (sh.cross_sm)  // soft_max_ext over n_audio_ctx keys, DTW capture of the alignment heads
-                    attn_decoder_softmax(s, qb, d, cross_k_.as<_Float16>() + l * cross_stride,
-                                         cross_v_.as<_Float16>() + l * cross_stride, 64, T * 64, d_rc, n, nullptr, H,
-                                         kq_scale, T, aob, d, sh.capture ? amap_.as<int>() + l * H : nullptr,
-                                         sh.capture ? cap_.as<float>() : nullptr, R, nullptr, sm_ws(), sm_ws_floats());
-            }
-            resid(aob, L.t_co, d, L.cb_o, L.mlp_ln_w, L.mlp_ln_b);
-            {
-                EpiParams ep;
-                ep.bias = L.b_mlp0;
-                ep.gelu_tab = m->gelu_tab;
-                ep.out16 = hr;
-                ep.ldo = 4 * d;
-                consumer(EPI_GELU_F16, 4 * d, L.mlp_ln_w, L.mlp_ln_b, L.t_mlp0, ep, 0);
-            }
-            resid(hr, L.t_mlp1, 4 * d, L.b_mlp1, nx ? nx->attn_ln_w : nullptr, nx ? nx->attn_ln_b : nullptr);
-        }
-    };
     auto resid_full = [&](const _Float16 * A, const float * A32, const _Float16 * W, const _Float16 * Wt,
                           const Q5W & q, int K, const float * bias, bool a_q8 = false) {
         EpiParams ep;
@@ -863,7 +760,6 @@ void Engine::launch_decode(const DecShape & sh) {
         layernorm_f16(stream, d_x_.as<float>(), R, d, w, b, hp.eps, d_xn_.as<_Float16>(), d, nullptr, xn32, q8a(),
                       q8d());
     };
-    if (fused) fused_rows();
     // quantized decode passes of <= 32 rows (the bench's greedy steps): the residual matmuls (attn.out,
     // cross_attn.out, mlp.2) write split-K partial tiles and resid_layernorm adds them to the residual
     // stream with bias and emits the next LayerNorm as f16 AND as Q8_0 rows (the next GEMM's operand):
@@ -931,7 +827,7 @@ void Engine::launch_decode(const DecShape & sh) {
         resid_q5p(d_h_.as<_Float16>(), nullptr, L.q_mlp1, 4 * d, L.b_mlp1, nx ? nx->attn_ln_w : nullptr,
                   nx ? nx->attn_ln_b : nullptr, false);
     }
-    for (int l = 0; l < hp.n_text_layer && !fused && !q5p; ++l) {
+    for (int l = 0; l < hp.n_text_layer && !q5p; ++l) {
         const DecLayerW & L = m->dec[l];
         _Float16 * Kl = self_k_.as<_Float16>() + l * self_stride;
         _Float16 * Vl = self_v_.as<_Float16>() + l * self_stride;
@@ -993,19 +889,167 @@ void Engine::launch_decode(const DecShape & sh) {
         }
         resid_full(d_h_.as<_Float16>(), nullptr, L.w_mlp1, L.t_mlp1, L.q_mlp1, 4 * d, L.b_mlp1);
     }
-    if (n_logit_rows > 0) {
-        {
-            ProfScope ps(prof, stream, "layernorm");
-            layernorm_f16(stream, d_x_.as<float>(), n_logit_rows, d, m->d_ln_w, m->d_ln_b, hp.eps, d_xl_.as<_Float16>(),
-                          d, d_lsel, kq ? d_xl32_.as<float>() : nullptr, q8a(), q8d());
-        }
-        kq_rmul_ = nullptr;  // the token embedding is not repacked (a get_rows tensor): quantize_row_q8_K
-        EpiParams ep;
-        ep.out32 = logits_.as<float>();
-        ep.ldo = nv;
-        linear(n_logit_rows <= 64 ? "gemm_logits" : "gemm_logits_big", EPI_F32, n_logit_rows, nv, d,
-               d_xl_.as<_Float16>(), kq ? d_xl32_.as<float>() : nullptr, d, m->d_te, m->q_te, ep, m->d_te_t, true, q5 && !kq);
+    launch_logits(sh);
+}
+
+// F16 passes of <= 32 rows: the per-layer chain of decode-row GEMMs over rows [r0, r0 + n) of the pass.
+// Each residual matmul site (attn.out, cross_attn.out, mlp.2) is either
+//   split: split-K partial tiles + resid_layernorm, which adds bias + residual and writes the next
+//          LayerNorm's f16 rows for the next matmul (2 launches), or
+//   whole-K (passes of <= whole_k_rows() rows): one launch (gemm_rows_res) adding the same partial
+//          sums in the same order, bias and residual; the next matmul runs the LayerNorm in its
+//          prologue (gemm_rows_lnx) with the statistics in the order of the kernel it replaces --
+//          bit-identical to the split chain, so a clip's result does not depend on its pass size.
+// Whole-K saves a launch per site but every block of the consumer recomputes the row statistics
+// from the f32 rows, and the exact split-order reduction costs more than the launch it saves:
+// 36.8 vs 32.5 us per layer at 1 row, 48.3 vs 36.3 at 8 (profiles/r04h_chain_ab.txt), so it is off
+// by default (whole_k_rows() = 0) and kept as a verified alternative. Earlier measured alternatives
+// (profiles/r02e_ab.txt, the round-3 ticket finish) lost on the launch boundary or the in-launch seam.
+// soft_max rows (flash_attn = false) and DTW captures run the soft_max attention launches inside the
+// same chain. Every kernel here is row-independent: the row activations / GEMM outputs are addressed
+// from row r0, the attention kernels take the pass's AttnRow entries r0.. (absolute q_row) and the
+// key-split soft_max workspace of those rows, so a row group's results equal the whole pass's.
+void Engine::fused_part(const DecShape & sh, int r0, int n, hipStream_t s, const GemmWs * ws) {
+    const HParams & hp = m->hp;
+    const int d = hp.n_text_state, H = hp.n_text_head, T = n_ctx();
+    const int n_ctx_pad = (T + 255) / 256 * 256;
+    char * dv = d_stg_.as<char>();
+    const int * d_tok = (const int *) (dv + st_tok_) + r0;
+    const int * d_pos = (const int *) (dv + st_pos_) + r0;
+    const int64_t * d_rowoff = (const int64_t *) (dv + st_rowoff_) + r0;
+    const AttnRow * d_rs = (const AttnRow *) (dv + st_rs_) + r0;
+    const AttnRow * d_rc = (const AttnRow *) (dv + st_rc_) + r0;
+    const int * d_keys = (const int *) (dv + st_keys_);
+    const int max_keys = sh.max_keys;
+    const bool whole_k = sh.R <= whole_k_rows() && gemm_rows_exact_applies(sh.R, d);
+    const float kq_scale = powf(64.0f, -0.25f);
+    const size_t self_stride = (size_t) cap_slots * kv_cells * d;
+    const size_t cross_stride = (size_t) cap_slots * hp.n_audio_ctx * d;
+    const size_t sm_off = attn_softmax_ws_floats(r0, H);
+    float * smw = sm_ws_.ptr ? sm_ws_.as<float>() + sm_off : nullptr;
+    const size_t smw_floats = sm_ws_.ptr ? sm_ws_.bytes / 4 - sm_off : 0;
+    // row-relative operands of the matmuls / LayerNorms; attention reads q and writes its output at
+    // the absolute rows (AttnRow.q_row) of the pass buffers
+    float * x = d_x_.as<float>() + (size_t) r0 * d;
+    _Float16 * xn = d_xn_.as<_Float16>() + (size_t) r0 * d;
+    _Float16 * qb = d_q_.as<_Float16>() + (size_t) r0 * d;
+    _Float16 * aob = d_ao_.as<_Float16>() + (size_t) r0 * d;
+    _Float16 * hr = d_h_.as<_Float16>() + (size_t) r0 * 4 * d;
+    _Float16 * q_abs = d_q_.as<_Float16>();
+    _Float16 * ao_abs = d_ao_.as<_Float16>();
+    {
+        ProfScope ps(prof, s, "embed");
+        embed_tokens(s, m->d_te, m->d_pe, d_tok, d_pos, n, d, x);
     }
+    // consumer of a LayerNorm (QKV, cross-Q, mlp.0): from the f16 rows the split producer wrote, or
+    // with the LayerNorm in its prologue; algorithmic bytes: weights + activation rows once
+    // order: 1 for layer 0's attn_ln (layernorm_f16's statistics), 0 after a residual site (resid_layernorm's)
+    auto consumer = [&](int mode, int N, const float * lnw, const float * lnb, const _Float16 * Wt,
+                        const EpiParams & ep, int order) {
+        if (whole_k) {
+            ProfScope ps(prof, s, "gemm_dec", 2.0 * n * (double) N * d, 2.0 * (double) N * d + 4.0 * n * d);
+            gemm_rows_lnx(s, mode, order, n, N, d, x, lnw, lnb, hp.eps, Wt, ep);
+        } else {
+            ProfScope ps(prof, s, "gemm_dec", 2.0 * n * (double) N * d, 2.0 * ((double) n * d + (double) N * d));
+            gemm(s, mode, n, N, d, xn, d, nullptr, d, ep, ws, Wt);
+        }
+    };
+    // residual matmul; lnw / lnb: the LayerNorm of the next consumer (null after the last layer)
+    auto resid = [&](const _Float16 * A, const _Float16 * Wt, int K, const float * bias, const float * lnw,
+                     const float * lnb) {
+        if (whole_k) {
+            ProfScope ps(prof, s, "gemm_dec", 2.0 * n * (double) d * K, 2.0 * ((double) n * K + (double) d * K));
+            gemm_rows_res(s, n, d, K, A, Wt, bias, x);
+            return;
+        }
+        {
+            ProfScope ps(prof, s, "gemm_dec", 2.0 * n * (double) d * K, 2.0 * ((double) n * K + (double) d * K));
+            gemm(s, EPI_PARTIAL, n, d, K, A, K, nullptr, K, EpiParams(), ws, Wt);
+        }
+        ProfScope ps(prof, s, "layernorm");
+        resid_layernorm(s, n, d, gemm_partial_splits(K), ws->partial, bias, x, lnw, lnb, hp.eps, xn, d);
+    };
+    if (!whole_k) {  // layer 0's attn_ln of the embeddings
+        ProfScope ps(prof, s, "layernorm");
+        layernorm_f16(s, x, n, d, m->dec[0].attn_ln_w, m->dec[0].attn_ln_b, hp.eps, xn, d, nullptr, nullptr, nullptr,
+                      nullptr);
+    }
+    for (int l = 0; l < hp.n_text_layer; ++l) {
+        const DecLayerW & L = m->dec[l];
+        const DecLayerW * nx = l + 1 < hp.n_text_layer ? &m->dec[l + 1] : nullptr;
+        _Float16 * Kl = self_k_.as<_Float16>() + l * self_stride;
+        _Float16 * Vl = self_v_.as<_Float16>() + l * self_stride;
+        const _Float16 * Kc = cross_k_.as<_Float16>() + l * cross_stride;
+        const _Float16 * Vc = cross_v_.as<_Float16>() + l * cross_stride;
+        {
+            EpiParams ep;
+            ep.bias = L.b_q;
+            ep.bias2 = L.b_v;
+            ep.scale = kq_scale;
+            ep.out16 = qb;
+            ep.ldo = d;
+            ep.out16b = Kl;
+            ep.out16c = Vl;
+            ep.d = d;
+            ep.row_off = d_rowoff;
+            ep.Tpad = kv_cells * 64;
+            consumer(EPI_QKV_DEC, 3 * d, L.attn_ln_w, L.attn_ln_b, L.t_qkv, ep, l == 0 ? 1 : 0);
+        }
+        {
+            ProfScope ps(prof, s, "attn_self");
+            attn_decoder(s, q_abs, d, Kl, Vl, 64, kv_cells * 64, d_rs, n, d_keys, H, 1.0f, max_keys, ao_abs, d,
+                         sh.self_oc, sh.self_tl, nullptr, sh.self_list, nullptr, nullptr);
+            if (sh.self_sm)  // flash_attn = false rows: masked soft_max (scale 1; Q, K pre-scaled)
+                attn_decoder_softmax(s, q_abs, d, Kl, Vl, 64, kv_cells * 64, d_rs, n, d_keys, H, 1.0f, max_keys, ao_abs,
+                                     d, nullptr, nullptr, 0, nullptr, smw, smw_floats);
+        }
+        resid(aob, L.t_o, d, L.b_o, L.cross_ln_w, L.cross_ln_b);
+        {
+            EpiParams ep;
+            ep.bias = L.cb_q;
+            ep.out16 = qb;
+            ep.ldo = d;
+            consumer(EPI_F16, d, L.cross_ln_w, L.cross_ln_b, L.t_cq, ep, 0);
+        }
+        {
+            ProfScope ps(prof, s, "attn_cross", 4.0 * n * (double) n_ctx_pad * d, 2.0 * 2.0 * n * (double) T * d);
+            attn_decoder(s, q_abs, d, Kc, Vc, 64, T * 64, d_rc, n, nullptr, H, kq_scale, T, ao_abs, d, sh.cross_oc,
+                         sh.cross_tl, nullptr, true, nullptr, nullptr);
+            if (sh.cross_sm)  // soft_max_ext over n_audio_ctx keys, DTW capture of the alignment heads
+                attn_decoder_softmax(s, q_abs, d, Kc, Vc, 64, T * 64, d_rc, n, nullptr, H, kq_scale, T, ao_abs, d,
+                                     sh.capture ? amap_.as<int>() + l * H : nullptr,
+                                     sh.capture ? cap_.as<float>() : nullptr, sh.R, nullptr, smw, smw_floats);
+        }
+        resid(aob, L.t_co, d, L.cb_o, L.mlp_ln_w, L.mlp_ln_b);
+        {
+            EpiParams ep;
+            ep.bias = L.b_mlp0;
+            ep.gelu_tab = m->gelu_tab;
+            ep.out16 = hr;
+            ep.ldo = 4 * d;
+            consumer(EPI_GELU_F16, 4 * d, L.mlp_ln_w, L.mlp_ln_b, L.t_mlp0, ep, 0);
+        }
+        resid(hr, L.t_mlp1, 4 * d, L.b_mlp1, nx ? nx->attn_ln_w : nullptr, nx ? nx->attn_ln_b : nullptr);
+    }
+}
+
+void Engine::launch_logits(const DecShape & sh) {
+    const HParams & hp = m->hp;
+    const int n_logit_rows = sh.n_logit, d = hp.n_text_state, nv = hp.n_vocab;
+    if (n_logit_rows <= 0) return;
+    const bool kq = m->kq;
+    const int * d_lsel = (const int *) (d_stg_.as<char>() + st_lsel_);
+    {
+        ProfScope ps(prof, stream, "layernorm");
+        layernorm_f16(stream, d_x_.as<float>(), n_logit_rows, d, m->d_ln_w, m->d_ln_b, hp.eps, d_xl_.as<_Float16>(), d,
+                      d_lsel, kq ? d_xl32_.as<float>() : nullptr, q8a(), q8d());
+    }
+    kq_rmul_ = nullptr;  // the token embedding is not repacked (a get_rows tensor): quantize_row_q8_K
+    EpiParams ep;
+    ep.out32 = logits_.as<float>();
+    ep.ldo = nv;
+    linear(n_logit_rows <= 64 ? "gemm_logits" : "gemm_logits_big", EPI_F32, n_logit_rows, nv, d, d_xl_.as<_Float16>(),
+           kq ? d_xl32_.as<float>() : nullptr, d, m->d_te, m->q_te, ep, m->d_te_t, true, m->q5 && !kq);
 }
 
 void Engine::download_logits(int logit_row, float * host) const {

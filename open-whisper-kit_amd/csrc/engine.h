@@ -2,6 +2,7 @@
 // and batched decoder passes over rows drawn from any number of clips / decoders.
 #pragma once
 
+#include <functional>
 #include <map>
 #include <string>
 #include <vector>
@@ -18,6 +19,7 @@ namespace owk {
 constexpr int kWholeKRowsDefault = 0;
 int whole_k_rows();           // the current limit (kWholeKRowsDefault unless a test hook changed it)
 int set_whole_k_rows(int n);  // test hook (owk_debug_set_whole_k_rows); returns the previous limit
+
 
 // per-kernel-class HIP-event timing + algorithmic work counters
 // eager launches with an event pair around each kernel-class launch on the engine stream; with a
@@ -153,6 +155,10 @@ public:
 
 private:
     void launch_decode(const DecShape & sh);
+    // the F16 <= 32-row chain (embedding, every layer) of rows [r0, r0 + n) on stream s with GEMM
+    // workspace ws; attention kernels address rows by their absolute index (AttnRow.q_row)
+    void fused_part(const DecShape & sh, int r0, int n, hipStream_t s, const GemmWs * ws);
+    void launch_logits(const DecShape & sh);  // final LayerNorm of the logit rows + logits GEMM
     void stage_layout(int C, int KC);
     void clear_graphs();
     uint64_t buffers_signature() const;
@@ -185,6 +191,7 @@ private:
     size_t st_rmul_ = 0;  // K-quants (repacked formats): per-row Q8_K rounding path (quantize_q8k_f16)
     std::map<uint64_t, hipGraphExec_t> graphs_;
     uint64_t graphs_sig_ = 0;
+    hipGraphExec_t graph_for(uint64_t key, hipStream_t s, const std::function<void()> & launch);
 
     // Q5_0 models: f32 activations feeding the quantized GEMMs and their Q8_0 copy
     void linear(const char * cls, int mode, int M, int N, int K, const _Float16 * A16, const float * A32, int lda,

@@ -267,3 +267,4 @@ def test_whole_k_chain_bit_identical(model, model_path, clips):
     assert seg_split == seg_whole, f"{model}: whisper_full results differ between the chains"
     print(f"{model}: {len(lg_split)} decode calls and {sum(len(s['tokens']) for s in seg_split)} whisper_full tokens "
           f"bit-identical")
+
