@@ -500,6 +500,9 @@ void Engine::stage_layout(int C, int KC) {
 }
 
 void Engine::clear_graphs() {
+    if (graphs_.empty()) return;
+    // a replay may still be running on the stream: destroy the executables only once it has drained
+    (void) hipStreamSynchronize(stream);
     for (auto & kv : graphs_) (void) hipGraphExecDestroy(kv.second);
     graphs_.clear();
 }

@@ -255,31 +255,48 @@ std::vector<int32_t> dtw_time_indices(const float * cap, int n_ah, int n_audio_c
             for (int u = 0; u < n_tok; ++u) y[u] *= sc;
         }
     // median filter (width medfilt, reflect padding) along audio, mean over heads, * -1;
-    // the sot sequence and eot columns are dropped
+    // the sot sequence and eot columns are dropped. The median is a selection (exact whatever the
+    // method): for each (head, audio position) the filter's rows are contiguous over the tokens, so
+    // the width-7 filter is a 16-comparator sorting network over whole token rows (vectorised over
+    // tokens); the head sum is accumulated in double in head order, as ggml_mean's ggml_vec_sum_f32
     const int N = n_tok - sot_len - 1, M = n_audio;
     std::vector<float> xm((size_t) N * M);  // [audio j][token i]
-    std::vector<float> filt;
-    std::vector<float> med((size_t) n_ah);
-    for (int i = 0; i < N; ++i) {
-        const int t = i + sot_len;
+    std::vector<double> hsum((size_t) N * M, 0.0);
+    const int fw = 2 * (medfilt / 2) + 1;  // the reference's window: offsets -medfilt/2 .. medfilt/2
+    std::vector<float> med((size_t) N), filt((size_t) fw);
+    auto reflect = [&](int idx) { return idx < 0 ? -idx : idx >= M ? 2 * (M - 1) - idx : idx; };
+    for (int k = 0; k < n_ah; ++k)
         for (int j = 0; j < M; ++j) {
-            for (int k = 0; k < n_ah; ++k) {
-                filt.clear();
-                for (int off = -medfilt / 2; off <= medfilt / 2; ++off) {
-                    int idx = j + off;
-                    if (idx < 0) idx = -idx;
-                    else if (idx >= M) idx = 2 * (M - 1) - idx;
-                    filt.push_back(w[((size_t) k * n_audio + idx) * n_tok + t]);
+            if (fw == 7) {
+                const float * r[7];
+                for (int off = -3; off <= 3; ++off) r[off + 3] = &w[((size_t) k * n_audio + reflect(j + off)) * n_tok + sot_len];
+                for (int i = 0; i < N; ++i) {
+                    float a[7];
+                    for (int e = 0; e < 7; ++e) a[e] = r[e][i];
+                    auto ce = [&](int p, int q) {
+                        const float lo = a[q] < a[p] ? a[q] : a[p], hi = a[q] < a[p] ? a[p] : a[q];
+                        a[p] = lo;
+                        a[q] = hi;
+                    };
+                    ce(0, 6); ce(2, 3); ce(4, 5); ce(0, 2); ce(1, 4); ce(3, 6); ce(0, 1); ce(2, 5);
+                    ce(3, 4); ce(1, 2); ce(4, 6); ce(2, 3); ce(4, 5); ce(1, 2); ce(3, 4); ce(5, 6);
+                    med[i] = a[3];
                 }
-                std::sort(filt.begin(), filt.end());
-                med[k] = filt[filt.size() / 2];
+            } else {
+                for (int i = 0; i < N; ++i) {
+                    for (int off = -medfilt / 2; off <= medfilt / 2; ++off)
+                        filt[off + medfilt / 2] = w[((size_t) k * n_audio + reflect(j + off)) * n_tok + sot_len + i];
+                    std::nth_element(filt.begin(), filt.begin() + medfilt / 2, filt.end());
+                    med[i] = filt[medfilt / 2];
+                }
             }
-            double s = 0.0;  // ggml_mean: ggml_vec_sum_f32 (double accumulate -> float) / n
-            for (int k = 0; k < n_ah; ++k) s += (double) med[k];
-            float mval = (float) s;
-            mval /= (float) n_ah;
-            xm[(size_t) j * N + i] = mval * -1.0f;
+            double * hs = &hsum[(size_t) j * N];
+            for (int i = 0; i < N; ++i) hs[i] += (double) med[i];
         }
+    for (size_t q = 0; q < xm.size(); ++q) {
+        float mval = (float) hsum[q];
+        mval /= (float) n_ah;
+        xm[q] = mval * -1.0f;
     }
     // DTW cost / trace over (token i, audio j), then backtrace
     std::vector<float> cost((size_t) (N + 1) * (M + 1), INFINITY);
