@@ -24,12 +24,29 @@ static float voice_length(const std::string & text) {
 
 std::vector<float> signal_energy(const float * signal, int n_samples, int hw) {
     std::vector<float> out(n_samples);
-    for (int i = 0; i < n_samples; i++) {
+    // every output's float sum runs over j = -hw .. hw in order, as the reference's; the interior
+    // samples are summed in blocks with j outermost, so the loop over samples vectorises with the
+    // per-sample order unchanged (a 10 min buffer: 9.6 M samples x 65 terms)
+    auto edge = [&](int i) {
         float sum = 0;
         for (int j = -hw; j <= hw; j++)
             if (i + j >= 0 && i + j < n_samples) sum += fabsf(signal[i + j]);
         out[i] = sum / (2 * hw + 1);
+    };
+    const int lo = std::min(hw, n_samples), hi = std::max(lo, n_samples - hw);
+    for (int i = 0; i < lo; ++i) edge(i);
+    constexpr int B = 2048;
+    float acc[B];
+    for (int b = lo; b < hi; b += B) {
+        const int nb = std::min(B, hi - b);
+        for (int i = 0; i < nb; ++i) acc[i] = 0.0f;
+        for (int j = -hw; j <= hw; ++j) {
+            const float * s = signal + b + j;
+            for (int i = 0; i < nb; ++i) acc[i] += fabsf(s[i]);
+        }
+        for (int i = 0; i < nb; ++i) out[b + i] = acc[i] / (2 * hw + 1);
     }
+    for (int i = hi; i < n_samples; ++i) edge(i);
     return out;
 }
 
