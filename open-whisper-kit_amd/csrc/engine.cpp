@@ -636,7 +636,7 @@ void Engine::decode(const std::vector<DecodeRow> & rows, const std::vector<int> 
     if (sh.self_oc && sh.max_keys > attn_max_listed_keys()) throw std::runtime_error("decode: too many self-attention keys");
     if (sh.self_tl && sh.max_keys > attn_max_tiled_keys()) throw std::runtime_error("decode: too many self-attention keys");
 
-    if ((sh.self_sm || sh.cross_sm) && sm_ws_.bytes < attn_softmax_ws_floats(dec_rows_cap_, hp.n_text_head) * 4) {
+    if (sh.cross_sm && sm_ws_.bytes < attn_softmax_ws_floats(dec_rows_cap_, hp.n_text_head) * 4) {
         sync();  // soft_max rows: the key-split attention workspace for the row capacity
         sm_ws_.alloc(attn_softmax_ws_floats(dec_rows_cap_, hp.n_text_head) * 4);
     }
@@ -658,15 +658,12 @@ void Engine::decode(const std::vector<DecodeRow> & rows, const std::vector<int> 
         clear_graphs();
         graphs_sig_ = sig;
     }
-    // bits 0-19 R, 20-39 n_logit_rows, 40-47 flags,
-    // 48-58 T (the cross head stride baked in), 60-63 the soft_max self-attention chunk count
+    // bits 0-19 R, 20-39 n_logit_rows, 40-47 flags, 48-58 T (the cross head stride baked in)
     const uint64_t shape = ((uint64_t) sh.self_oc << 40) | ((uint64_t) sh.self_tl << 41) |
                            ((uint64_t) sh.cross_oc << 42) | ((uint64_t) sh.cross_tl << 43) |
                            ((uint64_t) sh.self_sm << 44) | ((uint64_t) sh.cross_sm << 45) |
                            ((uint64_t) sh.self_list << 46) | ((uint64_t) (R <= whole_k_rows()) << 47) |
-                           ((uint64_t) T << 48) |
-                           // soft_max self rows: the key-split grid has one block per 128 keys of the longest row
-                           ((uint64_t) (sh.self_sm ? std::min(15, (sh.max_keys + 127) / 128 - 1) : 0) << 60);
+                           ((uint64_t) T << 48);
     const uint64_t key = (uint64_t) R | ((uint64_t) n_logit_rows << 20) | shape;
     OWK_HIP_CHECK(hipGraphLaunch(graph_for(key, stream, [&]() { launch_decode(sh); }), stream));
 }
@@ -858,7 +855,7 @@ void Engine::launch_decode(const DecShape & sh) {
             if (sh.self_sm)  // masked soft_max with scale 1 (Q, K pre-scaled; whisper.cpp:2614-2628)
                 attn_decoder_softmax(stream, d_q_.as<_Float16>(), d, Kl, Vl, 64, kv_cells * 64, d_rs, R, d_keys, H, 1.0f,
                                      max_keys,
-                                     d_ao_.as<_Float16>(), d, nullptr, nullptr, 0, ao32, sm_ws(), sm_ws_floats());
+                                     d_ao_.as<_Float16>(), d, nullptr, nullptr, 0, ao32);
         }
         resid_full(d_ao_.as<_Float16>(), ao32, L.w_o, L.t_o, L.q_o, d, L.b_o, fq_self);
         ln(L.cross_ln_w, L.cross_ln_b);
@@ -1002,9 +999,12 @@ void Engine::fused_part(const DecShape & sh, int r0, int n, hipStream_t s, const
             ProfScope ps(prof, s, "attn_self");
             attn_decoder(s, q_abs, d, Kl, Vl, 64, kv_cells * 64, d_rs, n, d_keys, H, 1.0f, max_keys, ao_abs, d,
                          sh.self_oc, sh.self_tl, nullptr, sh.self_list, nullptr, nullptr);
-            if (sh.self_sm)  // flash_attn = false rows: masked soft_max (scale 1; Q, K pre-scaled)
+            // flash_attn = false rows: masked soft_max (scale 1; Q, K pre-scaled), one block per (row, head):
+            // at most n_text_ctx keys, so one launch beats the key-split form's three at configs[4]'s one-row
+            // steps (the cross rows below, 1500 keys, take the key-split form)
+            if (sh.self_sm)
                 attn_decoder_softmax(s, q_abs, d, Kl, Vl, 64, kv_cells * 64, d_rs, n, d_keys, H, 1.0f, max_keys, ao_abs,
-                                     d, nullptr, nullptr, 0, nullptr, smw, smw_floats);
+                                     d, nullptr, nullptr, 0, nullptr);
         }
         resid(aob, L.t_o, d, L.b_o, L.cross_ln_w, L.cross_ln_b);
         {
@@ -1018,7 +1018,7 @@ void Engine::fused_part(const DecShape & sh, int r0, int n, hipStream_t s, const
             ProfScope ps(prof, s, "attn_cross", 4.0 * n * (double) n_ctx_pad * d, 2.0 * 2.0 * n * (double) T * d);
             attn_decoder(s, q_abs, d, Kc, Vc, 64, T * 64, d_rc, n, nullptr, H, kq_scale, T, ao_abs, d, sh.cross_oc,
                          sh.cross_tl, nullptr, true, nullptr, nullptr);
-            if (sh.cross_sm)  // soft_max_ext over n_audio_ctx keys, DTW capture of the alignment heads
+            if (sh.cross_sm)  // soft_max_ext over n_audio_ctx keys (key-split), DTW capture of the alignment heads
                 attn_decoder_softmax(s, q_abs, d, Kc, Vc, 64, T * 64, d_rc, n, nullptr, H, kq_scale, T, ao_abs, d,
                                      sh.capture ? amap_.as<int>() + l * H : nullptr,
                                      sh.capture ? cap_.as<float>() : nullptr, sh.R, nullptr, smw, smw_floats);
