@@ -133,6 +133,11 @@ WHISPER_API int owk_debug_gemm_rows_ln(int device, int M, int N, int K, const fl
 /* test hook: decode passes of at most n rows run the whole-K decoder chain (0 = never; bit-identical to the
  * split-K chain by construction); returns the previous limit */
 WHISPER_API int owk_debug_set_whole_k_rows(int n);
+/* soft_max decoder attention on random data: key-split form (split != 0) or single-block kernel; R rows x H
+ * (>= 4) heads x T keys, heads 0..3 captured as alignment heads; out [R][H*64] f16, cap [4][T][R] f32
+ * (either may be null); returns us per call over iters timed calls (-1: error) */
+WHISPER_API double owk_debug_attn_softmax(int device, int split, int R, int H, int T, uint16_t * out, float * cap,
+                                          int iters);
 /* library identity: 1 when the gfx950 HIP code object is present and a device is usable */
 WHISPER_API int owk_device_ok(int device);
 WHISPER_API const char * owk_build_info(void);

@@ -639,6 +639,7 @@ void Engine::decode(const std::vector<DecodeRow> & rows, const std::vector<int> 
     if (sh.cross_sm && sm_ws_.bytes < attn_softmax_ws_floats(dec_rows_cap_, hp.n_text_head) * 4) {
         sync();  // soft_max rows: the key-split attention workspace for the row capacity
         sm_ws_.alloc(attn_softmax_ws_floats(dec_rows_cap_, hp.n_text_head) * 4);
+        OWK_HIP_CHECK(hipMemsetAsync(sm_ws_.ptr, 0, sm_ws_.bytes, stream));  // arrival tickets start at 0
     }
     if (capture) {
         if (!n_ah_ || !amap_.ptr) throw std::runtime_error("decode: capture without alignment heads");

@@ -19,6 +19,14 @@ namespace owk {
 
 typedef __attribute__((address_space(3))) void * lds_ptr_t;
 
+// soft_max probability -> f16 after its f32 rounding (ggml_soft_max writes f32, mul_mat converts
+// that to f16): the empty asm keeps hipcc from folding the multiply into v_fma_mixlo_f16, one
+// rounding of the exact product, which differs on f16 ties (as f16_rn in k_gemm.hip)
+__device__ __forceinline__ _Float16 p_f16(float p) {
+    asm volatile("" : "+v"(p));
+    return (_Float16) p;
+}
+
 // ----------------------------------------------------------------------------------
 // Encoder flash attention.
 // Block = 4 waves = 64 queries of one (clip, head); KV tiles of 64 keys staged in LDS:
@@ -310,7 +318,7 @@ __global__ __launch_bounds__(256, 2) void k_attn_encoder_sm(const _Float16 * __r
 #pragma unroll
         for (int t = 0; t < 4; ++t)
 #pragma unroll
-            for (int e = 0; e < 4; ++e) pb[t >> 1][(t & 1) * 4 + e] = (_Float16) (expf(sc[t][e] - m) * inv);
+            for (int e = 0; e < 4; ++e) pb[t >> 1][(t & 1) * 4 + e] = p_f16(expf(sc[t][e] - m) * inv);
 #pragma unroll
         for (int dt = 0; dt < 4; ++dt) {
             const int row = dt * 16 + l16;
@@ -772,6 +780,19 @@ __global__ __launch_bounds__(NT) void k_attn_softmax(const _Float16 * __restrict
     const _Float16 * kh = kb + job.kv_base + (size_t) h * hs;
     const _Float16 * vh = vb + job.kv_base + (size_t) h * hs;
     const _Float16 * qr = q + (size_t) job.q_row * ldq + h * 64;
+    // P . V thread groups (below): tg (8 threads, head dims 8 seg .. +8) owns the key residues
+    // g = tg + TG j (mod SM_PV_GROUPS). The V rows of the first P . V iteration do not depend on the
+    // scores: their loads go out now, with the K rows, so the row pays one HBM round trip, not two
+    const int tg = tid >> 3, seg = tid & 7;
+    half8 vv0[GPT][U];
+#pragma unroll
+    for (int j = 0; j < GPT; ++j)
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int i = max(0, min(tg + TG * j + SM_PV_GROUPS * u, n - 1));
+            const int cell = list ? list[i] : i;
+            vv0[j][u] = *(const half8 *) (vh + (size_t) cell * ld_kv + seg * 8);
+        }
 
     // scores (lane = key; iterations unrolled so several keys' loads are in flight)
     float mx = -INFINITY;
@@ -816,13 +837,12 @@ __global__ __launch_bounds__(NT) void k_attn_softmax(const _Float16 * __restrict
     const int a = amap ? amap[h] : -1;
     for (int i = tid; i < n; i += NT) {
         const float p = sp[i] * inv;
-        p16[i] = (_Float16) p;
+        p16[i] = p_f16(p);
         if (a >= 0) cap[((size_t) a * n + i) * cap_rows + job.q_row] = p;
     }
     __syncthreads();
     // P . V: thread group tg (8 threads, head dims 8 seg .. +8: one 16-byte load per key) owns the
     // key residues g = tg + TG j (mod SM_PV_GROUPS), each accumulated in key order
-    const int tg = tid >> 3, seg = tid & 7;
     float acc[GPT][8];
 #pragma unroll
     for (int j = 0; j < GPT; ++j)
@@ -837,8 +857,12 @@ __global__ __launch_bounds__(NT) void k_attn_softmax(const _Float16 * __restrict
             for (int u = 0; u < U; ++u) {
                 const int ii = i0 + tg + TG * j + SM_PV_GROUPS * u;
                 const int i = min(ii, n - 1);
-                const int cell = list ? list[i] : i;
-                vv[j][u] = *(const half8 *) (vh + (size_t) cell * ld_kv + seg * 8);
+                if (i0 == 0) {
+                    vv[j][u] = vv0[j][u];
+                } else {
+                    const int cell = list ? list[i] : i;
+                    vv[j][u] = *(const half8 *) (vh + (size_t) cell * ld_kv + seg * 8);
+                }
                 pp[j][u] = ii < n ? (float) p16[i] : 0.0f;
             }
 #pragma unroll
@@ -863,17 +887,29 @@ __global__ __launch_bounds__(NT) void k_attn_softmax(const _Float16 * __restrict
     }
 }
 
-// The same soft_max attention with every (row, head) spread over ceil(n / SMS_CK) blocks: a block per 128
-// keys computes their scores (A), every chunk block then recomputes the row's exact max and double sum
-// from the stored scores -- the same per-thread residues (mod 256) and wave trees as k_attn_softmax, so
-// probabilities (and DTW captures) are bit-identical to it -- and the P.V partial of its keys (B); a
-// third launch adds the chunk partials in chunk order (C). One (row, head) in one block reads 384 KB
-// of K / V through one CU (configs[4]'s one-row steps: 20 blocks on 256 CUs, ~25 us per cross pass);
-// spread over 12 blocks per head it streams at the chip's rate. Workspace per (row, head): scores
-// [SM_MAX_KEYS] f32, chunk maxima [SMS_MAXC], partials [SMS_MAXC][64] (attn_softmax_ws_floats).
+// The same soft_max attention with every (row, head) spread over several blocks, bit-identical to
+// k_attn_softmax (probabilities, DTW captures and outputs):
+//   (A) k_sm_split_scores: a block per 128 consecutive keys computes their scores and the chunk maximum;
+//   (B) k_sm_split_pv: SMS_GB blocks per (row, head), block b owning the P.V key residues (mod 128)
+//       g = 16 b .. 16 b + 15 -- k_attn_softmax's P.V groups. Every block recomputes the row's exact max
+//       and double sum from the stored scores with k_attn_softmax's per-thread residues (mod 256) and
+//       wave trees, forms the probabilities of its keys, and runs each group's fma chain over its keys
+//       in key order; the (row, head)'s last-arriving block adds the 128 group partials in group order
+//       (an arrival ticket per (row, head) in the workspace, zero between launches: the workspace is
+//       zeroed when allocated and the last arriver resets its ticket).
+// One (row, head) in one block reads 384 KB of K / V through one CU (configs[4]'s one-row steps: 20
+// blocks on 256 CUs, ~25 us per cross pass); spread over 12 + 8 blocks per head it streams at the chip's
+// rate. Workspace per (row, head): scores [SM_MAX_KEYS] f32, chunk maxima [SMS_MAXC], group partials
+// [128][64], ticket (attn_softmax_ws_floats).
 constexpr int SMS_CK = 128;
 constexpr int SMS_MAXC = SM_MAX_KEYS / SMS_CK;
-constexpr int SMS_PER_RH = SM_MAX_KEYS + SMS_MAXC + SMS_MAXC * 64;
+constexpr int SMS_GB = 8;                              // P.V blocks per (row, head)
+constexpr int SMS_GPB = SM_PV_GROUPS / SMS_GB;         // residue groups per P.V block (16)
+constexpr int SMS_UMAX = SM_MAX_KEYS / SM_PV_GROUPS;   // keys per residue group (16)
+constexpr int SMS_PART = SM_MAX_KEYS + SMS_MAXC;       // group partials [SM_PV_GROUPS][64]
+constexpr int SMS_TICKET = SMS_PART + SM_PV_GROUPS * 64;  // the (row, head)'s arrival ticket (int)
+constexpr int SMS_PER_RH = SMS_TICKET + 16;
+static_assert(SMS_GPB * 8 == 128 && SMS_GPB * SMS_UMAX == 256, "P.V block thread layout");
 
 __global__ __launch_bounds__(SMS_CK) void k_sm_split_scores(const _Float16 * __restrict__ q, int ldq,
                                                             const _Float16 * __restrict__ kb, int ld_kv, int hs,
@@ -920,18 +956,32 @@ __global__ __launch_bounds__(SMS_CK) void k_sm_split_scores(const _Float16 * __r
 __global__ __launch_bounds__(256) void k_sm_split_pv(const _Float16 * __restrict__ vb, int ld_kv, int hs,
                                                      const AttnRow * __restrict__ rows, const int * __restrict__ key_idx,
                                                      int H, const int * __restrict__ amap, float * __restrict__ cap,
-                                                     int cap_rows, float * __restrict__ ws) {
-    __shared__ _Float16 p16[SMS_CK];
+                                                     int cap_rows, float * ws, _Float16 * __restrict__ out, int ldo,
+                                                     float * __restrict__ out32) {
+    __shared__ _Float16 p16[SMS_GPB][SMS_UMAX];
     __shared__ double redd[4];
-    __shared__ float red[32][64];
+    __shared__ int s_last;
     const AttnRow job = rows[blockIdx.y];
     if (job.mode != 2) return;
-    const int h = blockIdx.x % H, c = blockIdx.x / H;
+    const int h = blockIdx.x % H, b = blockIdx.x / H;
     const int n = job.n_keys;
-    if (c * SMS_CK >= n) return;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     float * w = ws + ((size_t) blockIdx.y * H + h) * SMS_PER_RH;
-    const int nc = (n + SMS_CK - 1) / SMS_CK;
+    const int nc = (n + SMS_CK - 1) / SMS_CK;  // score chunks = keys per residue group, rounded up
+    const int * list = job.key_list >= 0 ? key_idx + job.key_list : nullptr;
+    const _Float16 * vh = vb + job.kv_base + (size_t) h * hs;
+    // P.V thread (tid < 128): residue group g of this block, head dims 8 seg .. +8, keys g + 128 u. Its V
+    // rows go out first (they do not depend on the softmax): the HBM round trip overlaps the sum below
+    const int gl = (tid >> 3) & (SMS_GPB - 1), seg = tid & 7, g = b * SMS_GPB + gl;
+    half8 vv[SMS_UMAX];
+#pragma unroll
+    for (int u = 0; u < SMS_UMAX; ++u) {
+        if (u < nc && tid < 128) {
+            const int k = max(0, min(g + SM_PV_GROUPS * u, n - 1));
+            const int cell = list ? list[k] : k;
+            vv[u] = *(const half8 *) (vh + (size_t) cell * ld_kv + seg * 8);
+        }
+    }
     float mx = w[SM_MAX_KEYS];
     for (int k = 1; k < nc; ++k) mx = fmaxf(mx, w[SM_MAX_KEYS + k]);
     // k_attn_softmax's sum: thread t < 256 over keys t + 256 j, each exp as its (float) sp, then the trees
@@ -942,57 +992,56 @@ __global__ __launch_bounds__(256) void k_sm_split_pv(const _Float16 * __restrict
     if (lane == 0) redd[wave] = sum;
     __syncthreads();
     const float inv = (float) (1.0 / ((redd[0] + redd[1]) + (redd[2] + redd[3])));
-    const int i0 = c * SMS_CK, nk = min(SMS_CK, n - i0);
-    const int a = amap ? amap[h] : -1;
-    if (tid < nk) {
-        const float p = expf(w[i0 + tid] - mx) * inv;
-        p16[tid] = (_Float16) p;
-        if (a >= 0) cap[((size_t) a * n + i0 + tid) * cap_rows + job.q_row] = p;
+    {  // the probabilities of this block's keys: thread (group tid & 15, key tid >> 4 of the group)
+        const int a = amap ? amap[h] : -1;
+        const int i = b * SMS_GPB + (tid & (SMS_GPB - 1)) + SM_PV_GROUPS * (tid >> 4);
+        float p = 0.0f;
+        if (i < n) {
+            p = expf(w[i] - mx) * inv;
+            if (a >= 0) cap[((size_t) a * n + i) * cap_rows + job.q_row] = p;
+        }
+        p16[tid & (SMS_GPB - 1)][tid >> 4] = p_f16(p);
     }
     __syncthreads();
-    // P . V over this chunk: 32 groups of 8 threads (16 bytes of a V row each), keys g + 32 u in order
-    const int * list = job.key_list >= 0 ? key_idx + job.key_list : nullptr;
-    const _Float16 * vh = vb + job.kv_base + (size_t) h * hs;
-    const int g = tid >> 3, seg = tid & 7;
-    half8 vv[SMS_CK / 32];
+    float * part = w + SMS_PART;
+    if (tid < 128) {
+        // k_attn_softmax's chain for group g: fma over its keys in key order (keys past n: p = 0, exact)
+        float acc[8];
 #pragma unroll
-    for (int u = 0; u < SMS_CK / 32; ++u) {
-        const int k = min(g + 32 * u, nk - 1);
-        const int cell = list ? list[i0 + k] : i0 + k;
-        vv[u] = *(const half8 *) (vh + (size_t) cell * ld_kv + seg * 8);
+        for (int e = 0; e < 8; ++e) acc[e] = 0.0f;
+#pragma unroll
+        for (int u = 0; u < SMS_UMAX; ++u) {
+            if (u < nc) {
+                const float pp = g + SM_PV_GROUPS * u < n ? (float) p16[gl][u] : 0.0f;
+#pragma unroll
+                for (int e = 0; e < 8; ++e) acc[e] = fmaf(pp, (float) vv[u][e], acc[e]);
+            }
+        }
+        // hand-off inside the launch (cdna_hip_programming.md Guideline 16, R1): partials stored
+        // write-through (agent-scope atomic stores) and drained before the arrival ticket
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+            __hip_atomic_store(part + g * 64 + seg * 8 + e, acc[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
-    float acc[8];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) acc[e] = 0.0f;
-#pragma unroll
-    for (int u = 0; u < SMS_CK / 32; ++u) {
-        const int k = g + 32 * u;
-        const float pp = k < nk ? (float) p16[k] : 0.0f;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) acc[e] = fmaf(pp, (float) vv[u][e], acc[e]);
-    }
-#pragma unroll
-    for (int e = 0; e < 8; ++e) red[g][seg * 8 + e] = acc[e];
     __syncthreads();
-    if (tid < 64) {
-        float r = 0.0f;
-        for (int gg = 0; gg < 32; ++gg) r += red[gg][tid];
-        w[SM_MAX_KEYS + SMS_MAXC + c * 64 + tid] = r;
-    }
-}
-
-__global__ __launch_bounds__(64) void k_sm_split_combine(const AttnRow * __restrict__ rows, int H,
-                                                         const float * __restrict__ ws, _Float16 * __restrict__ out,
-                                                         int ldo, float * __restrict__ out32) {
-    const AttnRow job = rows[blockIdx.y];
-    if (job.mode != 2) return;
-    const int h = blockIdx.x, d = threadIdx.x;
-    const float * w = ws + ((size_t) blockIdx.y * H + h) * SMS_PER_RH + SM_MAX_KEYS + SMS_MAXC;
-    const int nc = (job.n_keys + SMS_CK - 1) / SMS_CK;
+    int * ticket = (int *) (w + SMS_TICKET);
+    if (tid == 0) s_last = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == SMS_GB - 1;
+    __syncthreads();
+    if (!s_last || tid >= 64) return;
+    // the last arriver: the 128 group partials in group order (agent-scope, L1-bypassing loads), as
+    // k_attn_softmax's wave 0 adds them; then the ticket is reset for the next launch
     float r = 0.0f;
-    for (int c = 0; c < nc; ++c) r += w[c * 64 + d];
-    if (out32) out32[(size_t) job.q_row * ldo + h * 64 + d] = r;
-    else out[(size_t) job.q_row * ldo + h * 64 + d] = (_Float16) r;
+    for (int g0 = 0; g0 < SM_PV_GROUPS; g0 += 16) {
+        float v[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) v[j] = __hip_atomic_load(part + (g0 + j) * 64 + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+        for (int j = 0; j < 16; ++j) r += v[j];
+    }
+    if (out32) out32[(size_t) job.q_row * ldo + h * 64 + tid] = r;
+    else out[(size_t) job.q_row * ldo + h * 64 + tid] = (_Float16) r;
+    if (tid == 0) __hip_atomic_store(ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 size_t attn_softmax_ws_floats(int n_rows, int H) { return (size_t) n_rows * H * SMS_PER_RH; }
@@ -1003,14 +1052,17 @@ void attn_decoder_softmax(hipStream_t s, const _Float16 * q, int ldq, const _Flo
                           float * out32, float * ws, size_t ws_floats) {
     if (n_rows <= 0) return;
     if (max_keys > SM_MAX_KEYS) throw std::runtime_error("attn_decoder_softmax: too many keys");
-    if (ws) {  // key-split form (every pass that has the workspace: a row's bits do not depend on its pass)
+    // key-split form (bit-identical to the single-block kernel below) for passes of few (row, head)
+    // blocks, where one block per head leaves the chip idle: 12.3 vs 17.3 us at 1 row x 1500 keys;
+    // at 32 rows its per-block recomputation of the row's softmax costs more (102 vs 45 us;
+    // tests/test_gpu_kernels.py::test_softmax_attention_split_bit_identical)
+    if (ws && n_rows * H <= 128) {
         if (ws_floats < attn_softmax_ws_floats(n_rows, H)) throw std::runtime_error("attn_decoder_softmax: workspace");
         const int nc = (max_keys + SMS_CK - 1) / SMS_CK;
         OWK_LAUNCH(k_sm_split_scores, dim3(H * nc, n_rows), dim3(SMS_CK), 0, s, q, ldq, kbase, ld_kv, hs, rows_dev,
                    key_idx, scale, H, ws);
-        OWK_LAUNCH(k_sm_split_pv, dim3(H * nc, n_rows), dim3(256), 0, s, vbase, ld_kv, hs, rows_dev, key_idx, H, amap,
-                   cap, cap_rows, ws);
-        OWK_LAUNCH(k_sm_split_combine, dim3(H, n_rows), dim3(64), 0, s, rows_dev, H, ws, out, ldo, out32);
+        OWK_LAUNCH(k_sm_split_pv, dim3(H * SMS_GB, n_rows), dim3(256), 0, s, vbase, ld_kv, hs, rows_dev, key_idx, H,
+                   amap, cap, cap_rows, ws, out, ldo, out32);
         return;
     }
     // outputs do not depend on the width (k_attn_softmax): 1024 threads when the pass has few

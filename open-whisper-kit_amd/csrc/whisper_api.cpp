@@ -1617,6 +1617,71 @@ double owk_debug_attn_cross(int device, int which, int R, int H, int T, int n_ze
     }
 }
 
+// soft_max decoder attention (flash_attn = false rows) on random q / K / V: the key-split form (split
+// != 0, attn_decoder_softmax with its workspace) or the single-block kernel; R rows x H heads x T keys
+// (cross layout), heads 0 .. 3 captured as DTW alignment heads. Writes out [R][H*64] f16 and cap
+// [4][T][R] f32 (either may be null); returns us per call over `iters` timed calls, or -1 on error.
+double owk_debug_attn_softmax(int device, int split, int R, int H, int T, uint16_t * out, float * cap_out, int iters) {
+    try {
+        if (R <= 0 || H < 4 || T <= 0 || iters < 0) throw std::runtime_error("bad arguments");
+        OWK_HIP_CHECK(hipSetDevice(device));
+        hipStream_t s;
+        OWK_HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+        const size_t nq = (size_t) R * H * 64, nkv = (size_t) R * H * T * 64;
+        DevBuf dq, dk, dv, dout, drows, damap, dcap, dws;
+        dq.alloc(nq * 2);
+        dk.alloc(nkv * 2);
+        dv.alloc(nkv * 2);
+        dout.alloc(nq * 2);
+        hipLaunchKernelGGL(k_fill_rand_f16, dim3(1024), dim3(256), 0, s, dq.as<_Float16>(), nq, 3u);
+        hipLaunchKernelGGL(k_fill_rand_f16, dim3(4096), dim3(256), 0, s, dk.as<_Float16>(), nkv, 5u);
+        hipLaunchKernelGGL(k_fill_rand_f16, dim3(4096), dim3(256), 0, s, dv.as<_Float16>(), nkv, 9u);
+        std::vector<AttnRow> rows(R);
+        for (int r = 0; r < R; ++r) rows[r] = AttnRow{r, r * H * T * 64, T, -1, 0, 2};
+        drows.alloc(R * sizeof(AttnRow));
+        OWK_HIP_CHECK(hipMemcpy(drows.ptr, rows.data(), R * sizeof(AttnRow), hipMemcpyHostToDevice));
+        std::vector<int> amap(H, -1);
+        for (int h = 0; h < 4; ++h) amap[h] = h;
+        damap.alloc(H * sizeof(int));
+        OWK_HIP_CHECK(hipMemcpy(damap.ptr, amap.data(), H * sizeof(int), hipMemcpyHostToDevice));
+        dcap.alloc((size_t) 4 * T * R * 4);
+        if (split) {
+            dws.alloc(attn_softmax_ws_floats(R, H) * 4);
+            OWK_HIP_CHECK(hipMemsetAsync(dws.ptr, 0, dws.bytes, s));
+        }
+        auto run = [&] {
+            attn_decoder_softmax(s, dq.as<_Float16>(), H * 64, dk.as<_Float16>(), dv.as<_Float16>(), 64, T * 64,
+                                 (const AttnRow *) drows.ptr, R, nullptr, H, 0.125f, T, dout.as<_Float16>(), H * 64,
+                                 damap.as<int>(), dcap.as<float>(), R, nullptr, split ? dws.as<float>() : nullptr,
+                                 split ? dws.bytes / 4 : 0);
+        };
+        run();
+        double us = 0.0;
+        if (iters > 0) {
+            hipEvent_t e0, e1;
+            OWK_HIP_CHECK(hipEventCreate(&e0));
+            OWK_HIP_CHECK(hipEventCreate(&e1));
+            OWK_HIP_CHECK(hipEventRecord(e0, s));
+            for (int i = 0; i < iters; ++i) run();
+            OWK_HIP_CHECK(hipEventRecord(e1, s));
+            OWK_HIP_CHECK(hipEventSynchronize(e1));
+            float ms = 0;
+            OWK_HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
+            (void) hipEventDestroy(e0);
+            (void) hipEventDestroy(e1);
+            us = 1e3 * ms / iters;
+        }
+        OWK_HIP_CHECK(hipStreamSynchronize(s));
+        if (out) OWK_HIP_CHECK(hipMemcpy(out, dout.ptr, nq * 2, hipMemcpyDeviceToHost));
+        if (cap_out) OWK_HIP_CHECK(hipMemcpy(cap_out, dcap.ptr, (size_t) 4 * T * R * 4, hipMemcpyDeviceToHost));
+        OWK_HIP_CHECK(hipStreamDestroy(s));
+        return us;
+    } catch (const std::exception & ex) {
+        log_msg(GGML_LOG_LEVEL_ERROR, "owk_debug_attn_softmax: %s\n", ex.what());
+        return -1;
+    }
+}
+
 // one large-tile GEMM epilogue mode through the 128x128 kernel (per-element epilogue) and the
 // 256x256 ring kernel (C^T tiles, 16-byte vector epilogue) on the same random operands, bias,
 // residual, positional rows and the real GELU table; returns the max |difference| over every
