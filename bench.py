@@ -114,6 +114,29 @@ def pmc_traffic(cls, path):
     return round(tot / n * 1024 * 2) if n else None
 
 
+def rocprof_class_us(cls, path):
+    """Total device time (us) of the class's kernels in the committed rocprofv3 stats summary, or None."""
+    import re
+
+    pat = CLASS_KERNELS.get(cls)
+    if not pat or not path:
+        return None
+    tot = [float(p[1]) for p in (line.split(None, 6) for line in open(path))
+           if len(p) == 7 and p[0].isdigit() and re.search(pat, p[6])]
+    return sum(tot) if tot else None
+
+
+def dominant_class(classes, model):
+    """The class with the largest device time by the committed rocprofv3 stats of this command (kernel
+    timestamps, no per-launch event overhead), else by the HIP-event table."""
+    stats_path, _ = profile_files(model)
+    tot = {c: rocprof_class_us(c, stats_path) for c in classes} if stats_path else {}
+    tot = {c: v for c, v in tot.items() if v}
+    if tot:
+        return max(tot, key=tot.get)
+    return max(classes, key=lambda c: classes[c]["ms"]) if classes else None
+
+
 def rocprof_avg_ms(cls, path):
     """Average launch duration (ms) of the class's kernels in the committed rocprofv3 stats summary
     (calls-weighted over the matching kernels), or None."""
@@ -317,11 +340,12 @@ class GpuRunner:
 
 
 def roofline(classes, ms_per_step, alone=None, model="large-v3"):
-    """`roofline` of the class with the largest device time; `alone` = {class: record} of the top
-    classes each timed in a step where only its launches carry events (preferred when given)."""
+    """`roofline` of the class with the largest device time (dominant_class: by the committed rocprof
+    stats when present); `alone` = {class: record} of the classes each timed in a step where only its
+    launches carry events (preferred when it holds the dominant class)."""
     stats_path, pmc_path = profile_files(model)
-    src = alone or classes
-    dom = max(src, key=lambda c: src[c]["ms"])
+    dom = dominant_class(classes, model)
+    src = alone if alone and dom in alone else classes
     d = src[dom]
     avg_ms = d["ms"] / max(1, d["launches"])
     if dom in MFMA_CLASSES:
@@ -397,6 +421,9 @@ def main(argv=None, runner=None):
     classes = run.profile() if not args.no_prof else {}
     if classes:
         top = sorted(classes, key=lambda c: -classes[c]["ms"])[:TOP_CLASSES]
+        dom = dominant_class(classes, args.model)
+        if dom and dom not in top:
+            top.append(dom)
         alone = {}
         for c in top:
             got = run.profile([c])
