@@ -255,12 +255,6 @@ void Engine::linear(const char * cls, int mode, int M, int N, int K, const _Floa
         gemm_q16(stream, mode, M, N, K, q16a_.as<_Float16>(), q16d_.as<float>(), mpad, q, ep);
         return;
     }
-    if (!a_q8 && !A32 && A16 && lda == K && gemm_q5_a16_applies(M, N, K, q)) {
-        // exact f16 rows (the GELU output): rounded to Q8_0 in the GEMM's prologue, no quantize launch
-        ProfScope ps(prof, stream, cls, gemm_flops(M, N, K), (double) N * K * qf_block_bytes(q.fmt) / 32.0 + 2.0 * M * K);
-        gemm_q5_a16(stream, mode, M, N, K, A16, q, ep);
-        return;
-    }
     if (!a_q8) {
         ProfScope ps(prof, stream, "quantize_q8");
         quantize_q8(stream, A32, A16, lda, M, K, q8a_.as<int8_t>(), q8d_.as<float>());

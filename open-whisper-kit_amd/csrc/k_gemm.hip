@@ -2104,14 +2104,9 @@ constexpr int GQ_MAX_SCALES = 32 * 160;  // M x K/32 activation scales in LDS
 // activation scales per thread: M * nb <= 32 * nb over blockDim = 64 * ceil(nb / J) threads
 // -> at most 32 * J / 64 + 1
 
-// A16: the activation is given as exact f16 rows a16 [M][K] (the GELU output feeding mlp.2) and each
-// wave rounds its own K blocks to Q8_0 in registers -- k_quantize_q8's arithmetic (block amax over 32,
-// d = amax / 127, q = rint(x * 127 / amax)), so the operands are identical -- instead of a separate
-// quantize launch; the block scales go to LDS as the loaded ones do
-template <int MODE, int MT, int FMT, int GQ_J, bool A16 = false>  // FMT: QFmt; GQ_J K blocks per wave
+template <int MODE, int MT, int FMT, int GQ_J>  // FMT: QFmt; GQ_J K blocks per wave
 __global__ __launch_bounds__(GQ_MAXW * 64) void k_gemm_q5_rows(int M, int N, int K, const int8_t * __restrict__ qa,
-                                                               const float * __restrict__ da, Q5W w, EpiParams ep,
-                                                               const _Float16 * __restrict__ a16 = nullptr) {
+                                                               const float * __restrict__ da, Q5W w, EpiParams ep) {
     constexpr int GQ_DA_PER_THREAD = 32 * GQ_J / 64 + 1;
     constexpr bool HAS_M = qf_has_m(FMT), HAS_QH = qf_has_qh(FMT);
     constexpr int TB = qf_tile_bytes(FMT), QSB = qf_qs_bytes(FMT);
@@ -2132,7 +2127,6 @@ __global__ __launch_bounds__(GQ_MAXW * 64) void k_gemm_q5_rows(int M, int N, int
     uint32_t qh[GQ_J];
     _Float16 dw[GQ_J], mw[GQ_J];
     long a[MT][GQ_J];
-    half8 ah[A16 ? MT : 1][A16 ? GQ_J : 1];
     // the tile's blocks are contiguous records (qf_tile_bytes): coalesced loads. Blocks past this
     // wave's range load a valid record and a zero activation (adds exact zeros). Record format at
     // compile time: the load phase stays branch-free.
@@ -2148,41 +2142,13 @@ __global__ __launch_bounds__(GQ_MAXW * 64) void k_gemm_q5_rows(int M, int N, int
 #pragma unroll
         for (int i = 0; i < MT; ++i) {
             const int ra = min(i * 16 + c16, M - 1);
-            if constexpr (A16) {
-                ah[i][j] = *(const half8 *) (a16 + (size_t) ra * K + kb * 32 + 8 * g);
-            } else {
-                const long t = *(const long *) (qa + (size_t) ra * K + kb * 32 + 8 * g);
-                a[i][j] = j < nj ? t : 0L;
-            }
+            const long t = *(const long *) (qa + (size_t) ra * K + kb * 32 + 8 * g);
+            a[i][j] = j < nj ? t : 0L;
         }
     }
     // activation scales of this block's K range (raw f32 d; at most GQ_DA_PER_THREAD per thread:
     // M <= 32, nbl <= nw * J) to LDS as [row][kb - kblo]; every load of the launch is issued before
     // the first wait (one round trip)
-    if constexpr (A16) {
-        // Q8_0 of this wave's K blocks: the 32 values of (row i * 16 + c16, block kb0 + j) are the half8s
-        // of lanes c16, c16 + 16, c16 + 32, c16 + 48 (g = 0..3)
-#pragma unroll
-        for (int j = 0; j < GQ_J; ++j)
-#pragma unroll
-            for (int i = 0; i < MT; ++i) {
-                float x[8], am = 0.0f;
-#pragma unroll
-                for (int e = 0; e < 8; ++e) {
-                    x[e] = (float) ah[i][j][e];
-                    am = fmaxf(am, fabsf(x[e]));
-                }
-                am = fmaxf(am, __shfl_xor(am, 16, 64));
-                am = fmaxf(am, __shfl_xor(am, 32, 64));
-                const float id = am != 0.0f ? 127.f / am : 0.0f;
-                uint64_t q = 0;
-#pragma unroll
-                for (int e = 0; e < 8; ++e) q |= (uint64_t) (uint8_t) (int8_t) rintf(x[e] * id) << (8 * e);
-                a[i][j] = j < nj ? (long) q : 0L;
-                const int ra = i * 16 + c16;
-                if (g == 0 && j < nj && ra < M) sda[ra * nbl + (kb0 + j - kblo)] = am / 127.f;
-            }
-    } else {
         float dv[GQ_DA_PER_THREAD];
 #pragma unroll
         for (int u = 0; u < GQ_DA_PER_THREAD; ++u) {
@@ -2196,7 +2162,6 @@ __global__ __launch_bounds__(GQ_MAXW * 64) void k_gemm_q5_rows(int M, int N, int
             const int i = tid + u * blockDim.x;
             if (i < M * nbl) sda[i] = dv[u];
         }
-    }
     __syncthreads();
     floatx4 acc[MT], accm[MT];
 #pragma unroll
@@ -2334,18 +2299,12 @@ __global__ __launch_bounds__(256) void k_gemm_q5_big(int M, int N, int K, const 
 int q5_partial_splits(int K) { return std::min(4, std::max(1, (K / 32 + 19) / 20)); }
 size_t q5_partial_floats(int N, int K) { return (size_t) q5_partial_splits(K) * 32 * N; }
 
-static bool q5_rows_applies(int M, int K, const Q5W & w) {
-    const int nb = K / 32;
-    return M <= 32 && w.tiled && nb <= GQ_MAXW * GQ_JMAX && M * nb <= GQ_MAX_SCALES;
-}
 template <int MODE> struct LaunchQ5 {
-    // a16: exact f16 activation rows quantized to Q8_0 in the decode-row kernel's prologue (null: qa / da)
     static void run(hipStream_t s, int M, int N, int K, const int8_t * qa, const float * da, const Q5W & w,
-                    const EpiParams & ep, const _Float16 * a16 = nullptr) {
+                    const EpiParams & ep) {
         const int nb = K / 32;
         if (MODE == EPI_PARTIAL && !(M <= 32 && w.tiled)) throw std::runtime_error("gemm_q5: EPI_PARTIAL needs the decode-row path");
-        if (a16 && !q5_rows_applies(M, K, w)) throw std::runtime_error("gemm_q5: f16 activations need the decode-row path");
-        if (q5_rows_applies(M, K, w)) {
+        if (M <= 32 && w.tiled && nb <= GQ_MAXW * GQ_JMAX && M * nb <= GQ_MAX_SCALES) {
             // more, shorter waves when K allows: 3 K blocks per wave up to K = 1536; partial launches
             // (EPI_PARTIAL, summed by resid_layernorm) split K over gridDim.y (q5_partial_splits)
             const int KS = MODE == EPI_PARTIAL ? q5_partial_splits(K) : 1;
@@ -2354,11 +2313,7 @@ template <int MODE> struct LaunchQ5 {
             const int nw = (per + J - 1) / J;
             if (nw > GQ_MAXW) throw std::runtime_error("gemm_q5: decode-row plan");
             const dim3 grid((N + 15) / 16, KS), block(nw * 64);
-#define OWK_Q_ROWS(MT_, F_, J_)                                                                                  \
-    do {                                                                                                         \
-        if (a16) OWK_LAUNCH((k_gemm_q5_rows<MODE, MT_, F_, J_, true>), grid, block, 0, s, M, N, K, qa, da, w, ep, a16); \
-        else OWK_LAUNCH((k_gemm_q5_rows<MODE, MT_, F_, J_>), grid, block, 0, s, M, N, K, qa, da, w, ep, nullptr);       \
-    } while (0)
+#define OWK_Q_ROWS(MT_, F_, J_) OWK_LAUNCH((k_gemm_q5_rows<MODE, MT_, F_, J_>), grid, block, 0, s, M, N, K, qa, da, w, ep)
 #define OWK_Q_ROWS_J(MT_, F_) do { if (J == 3) OWK_Q_ROWS(MT_, F_, 3); else OWK_Q_ROWS(MT_, F_, GQ_JMAX); } while (0)
 #define OWK_Q_ROWS_F(MT_)                                                 \
     switch (w.fmt) {                                                      \
@@ -2496,20 +2451,6 @@ void gemm_q5(hipStream_t s, int mode, int M, int N, int K, const int8_t * qa, co
         return;
     }
     dispatch_mode<LaunchQ5>(mode, s, M, N, K, qa, da, w, ep);
-}
-
-bool gemm_q5_a16_applies(int M, int N, int K, const Q5W & w) { return w && K % 32 == 0 && N > 0 && q5_rows_applies(M, K, w); }
-
-void gemm_q5_a16(hipStream_t s, int mode, int M, int N, int K, const _Float16 * a16, const Q5W & w, const EpiParams & ep) {
-    if (!gemm_q5_a16_applies(M, N, K, w) || !a16) throw std::runtime_error("gemm_q5_a16: unsupported shape");
-    if (mode == EPI_PARTIAL) {
-        if (!ep.out32) throw std::runtime_error("gemm_q5_a16: EPI_PARTIAL needs the partial workspace in out32");
-        LaunchQ5<EPI_PARTIAL>::run(s, M, N, K, nullptr, nullptr, w, ep, a16);
-        return;
-    }
-    const int8_t * qa = nullptr;
-    const float * da = nullptr;
-    dispatch_mode<LaunchQ5>(mode, s, M, N, K, qa, da, w, ep, a16);
 }
 
 bool gemm_q16_applies(const Q5W & w, int M, int N, int K) {

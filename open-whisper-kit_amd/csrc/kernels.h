@@ -175,10 +175,6 @@ void quantize_q8(hipStream_t s, const float * A32, const _Float16 * A16, int lda
 // split-K partial tiles [q5_partial_splits(K)][M][N] to ep.out32, finished by resid_layernorm
 void gemm_q5(hipStream_t s, int mode, int M, int N, int K, const int8_t * qa, const float * da, const Q5W & w,
              const EpiParams & ep);
-// the decode-row Q5_0 / Q8_0 / Q4_x GEMM (M <= 32, tiled weights) from exact f16 activation rows: the
-// kernel rounds them to Q8_0 in its prologue (k_quantize_q8's arithmetic) -- no quantize launch
-bool gemm_q5_a16_applies(int M, int N, int K, const Q5W & w);
-void gemm_q5_a16(hipStream_t s, int mode, int M, int N, int K, const _Float16 * a16, const Q5W & w, const EpiParams & ep);
 // the same product through the f16 MFMA ring kernel (M >= 2048 tiles): A = the Q8_0 integers of the
 // activation as exact f16 values [M][K] + scales (quantize_q8_f16), W = Q5W::wi / dwt; every 32-block
 // dot is exact, then acc = fma(dot, d_w * d_a, acc) in f32 (ggml_vec_dot_q5_0_q8_0's per-block term)

@@ -1536,16 +1536,6 @@ int owk_debug_gemm_quant2(int device, int fmt, int M, int N, int K, const float 
             q16d.alloc((size_t) nb * mpad * 4);
             quantize_q8_f16(s, da.as<float>(), nullptr, K, M, K, q16.as<_Float16>(), q16d.as<float>(), mpad);
             gemm_q16(s, EPI_F32, M, N, K, q16.as<_Float16>(), q16d.as<float>(), mpad, w, ep);
-        } else if (use_q16 == 2) {
-            // the decode-row kernel quantizing f16 activation rows in its prologue (gemm_q5_a16); `a` must
-            // hold f16-exact values for its result to equal the f32 path's
-            std::vector<uint16_t> h((size_t) M * K);
-            for (size_t i = 0; i < h.size(); ++i) h[i] = f32_to_f16_host(a[i]);
-            DevBuf a16;
-            a16.alloc(h.size() * 2);
-            OWK_HIP_CHECK(hipMemcpy(a16.ptr, h.data(), h.size() * 2, hipMemcpyHostToDevice));
-            gemm_q5_a16(s, EPI_F32, M, N, K, a16.as<_Float16>(), w, ep);
-            OWK_HIP_CHECK(hipStreamSynchronize(s));
         } else {
             gemm_q5(s, EPI_F32, M, N, K, q8.as<int8_t>(), q8d.as<float>(), w, ep);
         }

@@ -281,30 +281,3 @@ def test_quant_gemm_q16_vs_reference(kind):
     assert err < 2e-6, (kind, err)
 
 
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("kind", list(QFMT))
-@pytest.mark.parametrize("M,N,K", [(1, 1280, 5120), (17, 384, 1536), (32, 1280, 5120), (5, 1280, 1280)])
-def test_quant_gemm_a16_prologue(kind, M, N, K):
-    """The decode-row quantized GEMM that rounds exact f16 activation rows (the GELU output feeding
-    mlp.2) to Q8_0 in its own prologue equals quantize_q8 + the same GEMM bit for bit."""
-    import owk_synth as S
-
-    L = owk.load()
-    fmt, wtype, bb = QFMT[kind]
-    L.owk_debug_gemm_quant2.argtypes = [C.c_int] * 5 + [C.POINTER(C.c_float), C.c_void_p, C.POINTER(C.c_float),
-                                                        C.c_void_p, C.c_void_p, C.c_int]
-    rng = np.random.default_rng(M * 13 + N + K)
-    a = (rng.standard_normal((M, K)) * 0.7).astype(np.float16).astype(np.float32)  # f16-exact
-    a[:, :32] = 0.0  # an all-zero Q8 block (amax 0)
-    wf = (rng.standard_normal((N, K)) / np.sqrt(K) + 0.02).astype(np.float32)
-    blocks = S._QKIND[kind][2](wf)
-    outs = []
-    for mode in (0, 2):
-        out = np.zeros((M, N), np.float32)
-        assert L.owk_debug_gemm_quant2(0, fmt, M, N, K, a.ctypes.data_as(C.POINTER(C.c_float)), blocks,
-                                       out.ctypes.data_as(C.POINTER(C.c_float)), None, None, mode) == 0
-        outs.append(out)
-    assert np.array_equal(outs[0].view(np.uint32), outs[1].view(np.uint32)), \
-        f"{kind} {M}x{N}x{K}: max diff {np.abs(outs[0] - outs[1]).max()}"
