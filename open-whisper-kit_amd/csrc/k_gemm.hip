@@ -678,6 +678,19 @@ __global__ __launch_bounds__(512, 1) void k_gemm_8p(int M, int N, int K, const _
 #undef G8_SYNC_MMA
     if (wr == 0) __builtin_amdgcn_s_barrier();  // every wave ends on the same barrier count
 
+    // GELU epilogues: the 64 K-entry f16 table (128 KB) is staged in the operand LDS once the main loop's
+    // reads are done, so the tile's 65 536 lookups are LDS reads, not scattered 2-byte global loads
+    EpiParams epl = ep;
+    if constexpr (MODE == EPI_GELU_F16 || MODE == EPI_CONV2) {
+        static_assert(2 * G8_BUF >= 65536 * 2, "GELU table in the operand LDS");
+        __syncthreads();
+        uint4 * lt = (uint4 *) smem;
+        const uint4 * gt = (const uint4 *) ep.gelu_tab;
+#pragma unroll 4
+        for (int k = tid; k < 65536 * 2 / 16; k += 512) lt[k] = gt[k];
+        __syncthreads();
+        epl.gelu_tab = (const uint16_t *) smem;
+    }
     if (SWAP) {
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
@@ -689,11 +702,11 @@ __global__ __launch_bounds__(512, 1) void k_gemm_8p(int M, int N, int K, const _
                 const float v[8] = {acc[i][2 * h][0], acc[i][2 * h][1], acc[i][2 * h][2], acc[i][2 * h][3],
                                     acc[i][2 * h + 1][0], acc[i][2 * h + 1][1], acc[i][2 * h + 1][2], acc[i][2 * h + 1][3]};
                 if (c + 8 <= N) {
-                    epi_row8<MODE>(ep, r, c, v, ep.vec != 0);
+                    epi_row8<MODE>(epl, r, c, v, ep.vec != 0);
                 } else {
 #pragma unroll
                     for (int e = 0; e < 8; ++e)
-                        if (c + e < N) epi_store<MODE>(ep, r, c + e, v[e]);
+                        if (c + e < N) epi_store<MODE>(epl, r, c + e, v[e]);
                 }
             }
         }
@@ -722,7 +735,7 @@ __global__ __launch_bounds__(512, 1) void k_gemm_8p(int M, int N, int K, const _
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
                 const int r = r0 + e;
-                if (r < M && cl < N) epi_store<MODE>(ep, r, c, acc[i][j][e]);
+                if (r < M && cl < N) epi_store<MODE>(epl, r, c, acc[i][j][e]);
             }
         }
 }

@@ -1,0 +1,13 @@
+#!/bin/bash
+# GELU table in LDS: epilogue equality tests, encoder parity, turbo and F16 bench timing
+set -o pipefail
+TAG=${1:-gelu}
+mkdir -p gpurun_out/$TAG
+export OWK_MODEL_CACHE=/tmp/owk_models
+timeout -k 10 600 python -u -m pytest tests/test_gpu_kernels.py tests/test_gpu_large.py tests/test_gpu_parity.py -m gpu -q -k "gemm256 or gemm_mid_matches or large or encoder or parity" --timeout 300 --timeout-method thread > gpurun_out/$TAG/k.log 2>&1
+rc=$?; tail -1 gpurun_out/$TAG/k.log
+[ $rc -eq 0 ] || { grep -E "^E |FAILED" gpurun_out/$TAG/k.log | head -10; exit $rc; }
+for m in large-v3-turbo large-v3; do
+  timeout -k 10 300 python bench.py --model $m --steps 3 --warmup 1 --no-cpu-baseline --no-prof > gpurun_out/$TAG/b_$m.json 2> gpurun_out/$TAG/b_$m.err || exit 1
+  python -c "import json; d=json.load(open('gpurun_out/$TAG/b_$m.json')); print('$m RTF', d['value'], 'ms/step', d['ms_per_step'])"
+done
