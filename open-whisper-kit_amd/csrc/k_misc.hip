@@ -18,10 +18,11 @@ namespace owk {
 constexpr int LN_V4 = 8;  // float4 per lane held in registers -> d <= 2048
 
 // LayerNorm of one row held in registers (lane owns float4 groups lane + 64 j)
+// yout (optional): the f32 output row kept in registers (what o32 receives; zeros past the row)
 __device__ __forceinline__ void ln_row_regs(const float4 (&xv)[LN_V4], int lane, int d, const float * __restrict__ w,
                                             const float * __restrict__ b, float eps, _Float16 * __restrict__ o,
                                             float * __restrict__ o32, int8_t * __restrict__ q8 = nullptr,
-                                            float * __restrict__ q8d = nullptr) {
+                                            float * __restrict__ q8d = nullptr, float4 (*yout)[LN_V4] = nullptr) {
     const int n4 = d >> 2;
     double s = 0.0;
 #pragma unroll
@@ -42,6 +43,9 @@ __device__ __forceinline__ void ln_row_regs(const float4 (&xv)[LN_V4], int lane,
     const float scale = 1.0f / sqrtf(var + eps);
     const float4 * w4 = (const float4 *) w;
     const float4 * b4 = (const float4 *) b;
+    if (yout)
+#pragma unroll
+        for (int j = 0; j < LN_V4; ++j) (*yout)[j] = float4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int j = 0; j < LN_V4; ++j) {
         const int i = lane + 64 * j;
@@ -57,6 +61,7 @@ __device__ __forceinline__ void ln_row_regs(const float4 (&xv)[LN_V4], int lane,
             h[0] = (_Float16) y.x; h[1] = (_Float16) y.y; h[2] = (_Float16) y.z; h[3] = (_Float16) y.w;
             *(half4 *) (o + 4 * i) = h;
             if (o32) *(float4 *) (o32 + 4 * i) = y;
+            if (yout) (*yout)[j] = y;
         }
         if (q8) {
             // Q8_0 of the f32 output (x86 quantize_row_q8_0, as k_quantize_q8): a 32-element
@@ -135,6 +140,38 @@ void layernorm_f16(hipStream_t s, const float * x, int rows, int d, const float 
     if (q8 && (d % 32 != 0 || !q8d)) throw std::runtime_error("layernorm_f16: Q8_0 output needs d % 32 == 0");
     OWK_LAUNCH(k_layernorm_f16, dim3((rows + 3) / 4), dim3(256), 0, s, x, rows, d, w, b, eps, out, ldo,
                        row_idx, out32, q8, q8d);
+}
+
+// two LayerNorms in a row (the SortFormer conformer: a layer's final norm, then the next layer's first):
+// y = LN1(x) -> out1 (f16) / out1_32 (f32, the new residual stream), then LN2(y) from the same f32
+// registers -> out2 (f16) / out2_32 -- exactly the two layernorm_f16 launches it replaces
+__global__ __launch_bounds__(256) void k_layernorm2_f16(const float * __restrict__ x, int rows, int d,
+                                                        const float * __restrict__ w1, const float * __restrict__ b1,
+                                                        _Float16 * __restrict__ out1, float * __restrict__ out1_32,
+                                                        const float * __restrict__ w2, const float * __restrict__ b2,
+                                                        _Float16 * __restrict__ out2, float * __restrict__ out2_32,
+                                                        float eps) {
+    const int lane = threadIdx.x & 63;
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= rows) return;
+    const float4 * xr = (const float4 *) (x + (size_t) row * d);
+    const int n4 = d >> 2;
+    float4 xv[LN_V4], yv[LN_V4];
+#pragma unroll
+    for (int j = 0; j < LN_V4; ++j) {
+        const int i = lane + 64 * j;
+        xv[j] = i < n4 ? xr[i] : float4{0.f, 0.f, 0.f, 0.f};
+    }
+    ln_row_regs(xv, lane, d, w1, b1, eps, out1 + (size_t) row * d, out1_32 + (size_t) row * d, nullptr, nullptr, &yv);
+    ln_row_regs(yv, lane, d, w2, b2, eps, out2 + (size_t) row * d, out2_32 ? out2_32 + (size_t) row * d : nullptr);
+}
+
+void layernorm2_f16(hipStream_t s, const float * x, int rows, int d, const float * w1, const float * b1, _Float16 * out1,
+                    float * out1_32, const float * w2, const float * b2, _Float16 * out2, float * out2_32, float eps) {
+    if (rows <= 0) return;
+    if (d % 4 != 0 || d > 4 * 64 * LN_V4 || !out1 || !out1_32 || !out2) throw std::runtime_error("layernorm2_f16: unsupported");
+    OWK_LAUNCH(k_layernorm2_f16, dim3((rows + 3) / 4), dim3(256), 0, s, x, rows, d, w1, b1, out1, out1_32, w2, b2, out2,
+               out2_32, eps);
 }
 
 // token + position embedding (whisper.cpp:2515-2518: get_rows(d_te) + get_rows(d_pe))

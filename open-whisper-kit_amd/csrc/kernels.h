@@ -210,6 +210,10 @@ size_t q5_partial_floats(int N, int K);  // workspace floats of a partial quanti
 void layernorm_f16(hipStream_t s, const float * x, int rows, int d, const float * w, const float * b,
                    float eps, _Float16 * out, int ldo, const int * row_idx = nullptr, float * out32 = nullptr,
                    int8_t * q8 = nullptr, float * q8d = nullptr);
+// y = LayerNorm1(x) -> out1 (f16) + out1_32 (f32), then LayerNorm2(y) -> out2 (f16) + out2_32 (f32, optional):
+// bit-identical to the two layernorm_f16 calls (one launch; rows of width d, ldo = d)
+void layernorm2_f16(hipStream_t s, const float * x, int rows, int d, const float * w1, const float * b1, _Float16 * out1,
+                    float * out1_32, const float * w2, const float * b2, _Float16 * out2, float * out2_32, float eps);
 // decoder input embedding: x[r] = f32(tok_emb[tok[r]]) + pos_emb[pos[r]]
 void embed_tokens(hipStream_t s, const _Float16 * tok_emb, const float * pos_emb, const int * tokens,
                   const int * pos, int rows, int d, float * x);

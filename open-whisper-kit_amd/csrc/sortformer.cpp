@@ -656,16 +656,17 @@ float * run_conformer(sortformer_context * ctx, float * x, const Segs & segs, in
     _Float16 * hbuf = grow<_Float16>(ctx->s_h, (size_t) T * 4 * d);
     float * qkv = grow<float>(ctx->s_qkv, (size_t) T * 3 * d);
     float * P = grow<float>(ctx->s_P, (size_t) (2 * Tmax - 1) * d);
+    const size_t p0 = (size_t) ensure_pos(ctx, Tmax) * d;  // table row of position Tmax-1
     _Float16 * ao = grow<_Float16>(ctx->s_ao, (size_t) T * d);
     float * cv = grow<float>(ctx->s_cv, (size_t) T * 2 * d);
     _Float16 * g = grow<_Float16>(ctx->s_g, (size_t) T * d);
-    const size_t p0 = (size_t) ensure_pos(ctx, Tmax) * d;  // table row of position Tmax-1
     const float eps = 1e-5f;
+    bool ff1_done = false;  // the layer's first LayerNorm already ran with the previous layer's last
     for (int il = 0; il <= last; ++il) {
         const ConfLayer & L = ctx->conf[il];
-        auto ffn = [&](size_t lnw, size_t lnb, const Lin & up, size_t upb, const Lin & dn, size_t dnb) {
+        auto ffn = [&](size_t lnw, size_t lnb, const Lin & up, size_t upb, const Lin & dn, size_t dnb, bool ln_done) {
             float * xn32 = f32_for(ctx, up, ctx->s_xn32, (size_t) T * d);
-            layernorm_f16(s, x, T, d, ctx->f(lnw), ctx->f(lnb), eps, xn, d, nullptr, xn32);
+            if (!ln_done) layernorm_f16(s, x, T, d, ctx->f(lnw), ctx->f(lnb), eps, xn, d, nullptr, xn32);
             float * h32 = f32_for(ctx, dn, ctx->s_h32, (size_t) T * 4 * d);
             EpiParams e1;
             e1.bias = ctx->f(upb); e1.out16 = hbuf; e1.out32 = h32; e1.ldo = 4 * d;
@@ -675,7 +676,7 @@ float * run_conformer(sortformer_context * ctx, float * x, const Segs & segs, in
             sf_lin(ctx, EPI_HALF_RESID, T, d, 4 * d, hbuf, h32, 4 * d, dn, e2);
         };
         // FFN1 (ref:1159-1168)
-        ffn(L.ln_ff1_w, L.ln_ff1_b, L.ff1_up, L.ff1_up_b, L.ff1_dn, L.ff1_dn_b);
+        ffn(L.ln_ff1_w, L.ln_ff1_b, L.ff1_up, L.ff1_up_b, L.ff1_dn, L.ff1_dn_b, ff1_done);
         // relative-position MHSA (ref:1170-1235)
         {
             float * xn32 = f32_for(ctx, L.qkv, ctx->s_xn32, (size_t) T * d);
@@ -714,9 +715,17 @@ float * run_conformer(sortformer_context * ctx, float * x, const Segs & segs, in
             sf_lin(ctx, EPI_RESID_F32, T, d, d, g, nullptr, d, L.pw2, eo);
         }
         // FFN2 (ref:1276-1285)
-        ffn(L.ln_ff2_w, L.ln_ff2_b, L.ff2_up, L.ff2_up_b, L.ff2_dn, L.ff2_dn_b);
-        // final LayerNorm (ref:1288) -> y, then swap
-        layernorm_f16(s, x, T, d, ctx->f(L.ln_out_w), ctx->f(L.ln_out_b), eps, xn, d, nullptr, y);
+        ffn(L.ln_ff2_w, L.ln_ff2_b, L.ff2_up, L.ff2_up_b, L.ff2_dn, L.ff2_dn_b, false);
+        // final LayerNorm (ref:1288) -> y, then swap; below the last layer the next layer's FFN1 LayerNorm
+        // runs in the same launch from the f32 rows in registers (bit-identical to two launches)
+        if (il < last) {
+            const ConfLayer & N = ctx->conf[il + 1];
+            layernorm2_f16(s, x, T, d, ctx->f(L.ln_out_w), ctx->f(L.ln_out_b), xn, y, ctx->f(N.ln_ff1_w),
+                           ctx->f(N.ln_ff1_b), xn, f32_for(ctx, N.ff1_up, ctx->s_xn32, (size_t) T * d), eps);
+            ff1_done = true;
+        } else {
+            layernorm_f16(s, x, T, d, ctx->f(L.ln_out_w), ctx->f(L.ln_out_b), eps, xn, d, nullptr, y);
+        }
         std::swap(x, y);
     }
     // keep the output in s_x so callers find it there
