@@ -243,8 +243,8 @@ constexpr int AKT = 64;  // keys per tile
 template <int DH, bool REL>
 __global__ __launch_bounds__(256) void k_sf_attn(const float * __restrict__ qkv, int ldq, int kcol, int vcol, int T,
                                                  int H, const float * __restrict__ ub, const float * __restrict__ vb,
-                                                 const float * __restrict__ P, float sc, _Float16 * __restrict__ out,
-                                                 float * __restrict__ out32, int Tpad) {
+                                                 const float * __restrict__ P, int ldP, float sc,
+                                                 _Float16 * __restrict__ out, float * __restrict__ out32, int Tpad) {
     extern __shared__ float smem[];
     constexpr int LDK = DH + 4;
     constexpr int TPQ = 256 / AQ;                   // threads per query row
@@ -280,7 +280,7 @@ __global__ __launch_bounds__(256) void k_sf_attn(const float * __restrict__ qkv,
 #pragma unroll
         for (int u = 0; u < PPT; ++u) {
             const int i = tid + 256 * u, r = i / DH, d = i - r * DH, p = pbase + r;
-            preg[u] = (i < PR * DH && p >= 0 && p < 2 * T - 1) ? P[(size_t) p * ldp + h * DH + d] : 0.0f;
+            preg[u] = (i < PR * DH && p >= 0 && p < 2 * T - 1) ? P[(size_t) p * ldP + h * DH + d] : 0.0f;
         }
     };
     auto store_p = [&]() {
@@ -398,24 +398,25 @@ __global__ __launch_bounds__(256) void k_sf_attn(const float * __restrict__ qkv,
 
 template <int DH, bool REL>
 static void launch_attn(hipStream_t s, const float * qkv, int ldq, int kcol, int vcol, int T, int H, const float * u,
-                        const float * v, const float * P, float sc, _Float16 * out, float * out32) {
+                        const float * v, const float * P, int ldP, float sc, _Float16 * out, float * out32) {
     const int Tpad = (T + AKT - 1) / AKT * AKT;
     const size_t lds = ((size_t) AQ * Tpad + (size_t) AKT * (DH + 4) +
                         (REL ? (size_t) (AQ - 1 + AKT) * (DH + 4) + (size_t) AQ * DH : 0)) * sizeof(float);
     if (lds > 160 * 1024) throw std::runtime_error("sf::attention: T too large for the LDS score tile");
     OWK_LAUNCH((k_sf_attn<DH, REL>), dim3(H, (T + AQ - 1) / AQ), dim3(256), lds, s, qkv, ldq, kcol, vcol, T, H,
-                       u, v, P, sc, out, out32, Tpad);
+                       u, v, P, ldP, sc, out, out32, Tpad);
 }
 
 void attention(hipStream_t s, int dh, bool rel, const float * qkv, int ldq, int kcol, int vcol, int T, int H,
-               const float * u, const float * v, const float * P, float sc, _Float16 * out, float * out32) {
+               const float * u, const float * v, const float * P, float sc, _Float16 * out, float * out32, int ldP) {
     if (T <= 0) return;
+    if (ldP <= 0) ldP = H * dh;
     if (dh == 64 && rel)
-        launch_attn<64, true>(s, qkv, ldq, kcol, vcol, T, H, u, v, P, sc, out, out32);
+        launch_attn<64, true>(s, qkv, ldq, kcol, vcol, T, H, u, v, P, ldP, sc, out, out32);
     else if (dh == 24 && !rel)
-        launch_attn<24, false>(s, qkv, ldq, kcol, vcol, T, H, u, v, P, sc, out, out32);
+        launch_attn<24, false>(s, qkv, ldq, kcol, vcol, T, H, u, v, P, ldP, sc, out, out32);
     else if (dh == 64 && !rel)
-        launch_attn<64, false>(s, qkv, ldq, kcol, vcol, T, H, u, v, P, sc, out, out32);
+        launch_attn<64, false>(s, qkv, ldq, kcol, vcol, T, H, u, v, P, ldP, sc, out, out32);
     else
         throw std::runtime_error("sf::attention: unsupported head size");
 }

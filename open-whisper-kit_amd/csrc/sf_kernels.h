@@ -38,9 +38,11 @@ void to_f16(hipStream_t s, const float * x, size_t n, _Float16 * out);
 //   score[i][j] = ((q_i + u) . k_j + [REL] (q_i + v) . P[T-1-i+j]) * sc, softmax over j, out = sum_j p_ij v_j
 // qkv: [T][ldq] f32 with Q at column 0, K at kcol, V at vcol (head h at h*dh); u, v: [H][dh]
 // (REL only, else null); P: [2T-1][H*dh] f32 (REL only). out: [T][H*dh] f16, or f32 into out32 when
-// given (the operand a quantized linear_out / out_projection rounds to Q8 itself)
+// given (the operand a quantized linear_out / out_projection rounds to Q8 itself); ldP: P's row stride
+// (0: H*dh; the conformer passes every layer's P side by side)
 void attention(hipStream_t s, int dh, bool rel, const float * qkv, int ldq, int kcol, int vcol, int T, int H,
-               const float * u, const float * v, const float * P, float sc, _Float16 * out, float * out32 = nullptr);
+               const float * u, const float * v, const float * P, float sc, _Float16 * out, float * out32 = nullptr,
+               int ldP = 0);
 
 // conformer conv module middle: GLU over pw1 output x [T][2C] (a * sigmoid(g)), depthwise conv
 // (k taps, zero padded (k-1)/2, ggml_ssm_conv order) + bias, SiLU -> out16 [T][C]

@@ -252,6 +252,9 @@ struct sortformer_context {
     // position-embedding cache (ref:140-142, 1127-1136): f16 table of the current n_pos
     int pos_T = 0;  // positions pos_T-1 .. -(pos_T-1) in pos16 / pos32
     DevBuf pos16;
+    // every conformer layer's linear_pos weight stacked [n_conf * d][d] (F16 models): one GEMM of the
+    // position table gives all layers' projections (a pass's 17 launches in one)
+    DevBuf pos_all;
 
     // scratch (grown on demand)
     DevBuf s_pcm, s_mel, s_c1, s_c2, s_c3, s_c4, s_flat, s_pre;
@@ -494,6 +497,16 @@ void load_weights(sortformer_context * ctx, const Gguf & g) {
         OWK_HIP_CHECK(hipStreamSynchronize(ctx->stream));
         SF_LOG("sortformer_init: %.1f MB of quantized linears\n", qb.host.size() / 1e6);
     }
+    bool all_f16 = !ctx->conf.empty();
+    for (const auto & L : ctx->conf) all_f16 = all_f16 && !L.pos.quant();
+    if (all_f16) {
+        const size_t dd = (size_t) ctx->d_model * ctx->d_model;
+        ctx->pos_all.alloc(ctx->conf.size() * dd * 2);
+        for (size_t il = 0; il < ctx->conf.size(); ++il)
+            OWK_HIP_CHECK(hipMemcpyAsync(ctx->pos_all.as<_Float16>() + il * dd, ctx->h(ctx->conf[il].pos.off), dd * 2,
+                                         hipMemcpyDeviceToDevice, ctx->stream));
+        OWK_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    }
     SF_LOG("sortformer_init: %.1f MB of weights resident on device %d\n", blob.host.size() / 1e6, ctx->device);
 }
 
@@ -655,8 +668,17 @@ float * run_conformer(sortformer_context * ctx, float * x, const Segs & segs, in
     _Float16 * xn = grow<_Float16>(ctx->s_xn, (size_t) T * d);
     _Float16 * hbuf = grow<_Float16>(ctx->s_h, (size_t) T * 4 * d);
     float * qkv = grow<float>(ctx->s_qkv, (size_t) T * 3 * d);
-    float * P = grow<float>(ctx->s_P, (size_t) (2 * Tmax - 1) * d);
     const size_t p0 = (size_t) ensure_pos(ctx, Tmax) * d;  // table row of position Tmax-1
+    // linear_pos of every layer at once when the weights are stacked: P_all [2 Tmax - 1][n_conf * d]
+    const bool pos_batched = ctx->pos_all.ptr != nullptr;
+    const int ldP = pos_batched ? ctx->n_conf * d : d;
+    float * P = grow<float>(ctx->s_P, (size_t) (2 * Tmax - 1) * ldP);
+    if (pos_batched) {
+        EpiParams ep;
+        ep.out32 = P;
+        ep.ldo = ldP;
+        gemm(s, EPI_F32, 2 * Tmax - 1, ldP, d, ctx->pos16.as<_Float16>() + p0, d, ctx->pos_all.as<_Float16>(), d, ep);
+    }
     _Float16 * ao = grow<_Float16>(ctx->s_ao, (size_t) T * d);
     float * cv = grow<float>(ctx->s_cv, (size_t) T * 2 * d);
     _Float16 * g = grow<_Float16>(ctx->s_g, (size_t) T * d);
@@ -684,17 +706,20 @@ float * run_conformer(sortformer_context * ctx, float * x, const Segs & segs, in
             EpiParams e;
             e.bias = ctx->f(L.qkv_b); e.out32 = qkv; e.ldo = 3 * d;
             sf_lin(ctx, EPI_BIAS_F32, T, 3 * d, d, xn, xn32, d, L.qkv, e);
-            EpiParams ep;
-            ep.out32 = P; ep.ldo = d;
-            sf_lin(ctx, EPI_F32, 2 * Tmax - 1, d, d, ctx->pos16.as<_Float16>() + p0, L.pos.quant() ? ctx->pos32.as<float>() + p0 : nullptr,
-                   d, L.pos, ep);
+            if (!pos_batched) {
+                EpiParams ep;
+                ep.out32 = P; ep.ldo = d;
+                sf_lin(ctx, EPI_F32, 2 * Tmax - 1, d, d, ctx->pos16.as<_Float16>() + p0,
+                       L.pos.quant() ? ctx->pos32.as<float>() + p0 : nullptr, d, L.pos, ep);
+            }
+            const float * Pl = pos_batched ? P + (size_t) il * d : P;
             // positions Tb-1 .. -(Tb-1) of a shorter sequence are rows Tmax-Tb .. of the table
             float * ao32 = f32_for(ctx, L.out, ctx->s_ao32, (size_t) T * d);
             for (const auto & sg : segs)
                 sf::attention(s, CONF_DH, true, qkv + (size_t) sg.first * 3 * d, 3 * d, d, 2 * d, sg.second, CONF_H,
-                              ctx->f(L.pbu), ctx->f(L.pbv), P + (size_t) (Tmax - sg.second) * d,
+                              ctx->f(L.pbu), ctx->f(L.pbv), Pl + (size_t) (Tmax - sg.second) * ldP,
                               1.0f / sqrtf((float) CONF_DH), ao + (size_t) sg.first * d,
-                              ao32 ? ao32 + (size_t) sg.first * d : nullptr);
+                              ao32 ? ao32 + (size_t) sg.first * d : nullptr, ldP);
             EpiParams eo;
             eo.bias = ctx->f(L.out_b); eo.resid = x; eo.out32 = x; eo.ldo = d;
             sf_lin(ctx, EPI_RESID_F32, T, d, d, ao, ao32, d, L.out, eo);
