@@ -1031,13 +1031,15 @@ __global__ __launch_bounds__(256) void k_sm_split_pv(const _Float16 * __restrict
     if (!s_last || tid >= 64) return;
     // the last arriver: the 128 group partials in group order (agent-scope, L1-bypassing loads), as
     // k_attn_softmax's wave 0 adds them; then the ticket is reset for the next launch
+    // two batches of 64 loads in flight (the vmcnt limit), then the adds: two memory round trips
     float r = 0.0f;
-    for (int g0 = 0; g0 < SM_PV_GROUPS; g0 += 16) {
-        float v[16];
 #pragma unroll
-        for (int j = 0; j < 16; ++j) v[j] = __hip_atomic_load(part + (g0 + j) * 64 + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int g0 = 0; g0 < SM_PV_GROUPS; g0 += 64) {
+        float v[64];
 #pragma unroll
-        for (int j = 0; j < 16; ++j) r += v[j];
+        for (int j = 0; j < 64; ++j) v[j] = __hip_atomic_load(part + (g0 + j) * 64 + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+        for (int j = 0; j < 64; ++j) r += v[j];
     }
     if (out32) out32[(size_t) job.q_row * ldo + h * 64 + tid] = r;
     else out[(size_t) job.q_row * ldo + h * 64 + tid] = (_Float16) r;
