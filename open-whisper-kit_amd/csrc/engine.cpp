@@ -216,7 +216,8 @@ void Engine::download_mel(int slot, float * host) const {
 static double gemm_flops(double M, double N, double K) { return 2.0 * M * N * K; }
 
 void Engine::linear(const char * cls, int mode, int M, int N, int K, const _Float16 * A16, const float * A32, int lda,
-                    const _Float16 * W, const Q5W & q, const EpiParams & ep, const _Float16 * Wt, bool dec, bool a_q8) {
+                    const _Float16 * W, const Q5W & q, const EpiParams & ep, const _Float16 * Wt, bool dec, bool a_q8,
+                    const int8_t * qa, const float * qd) {
     if (!q) {
         ProfScope ps(prof, stream, cls, gemm_flops(M, N, K), 2.0 * ((double) M * K + (double) N * K));
         if (dec) gemm(stream, mode, M, N, K, A16, lda, W, K, ep, &gws_, Wt);
@@ -225,7 +226,7 @@ void Engine::linear(const char * cls, int mode, int M, int N, int K, const _Floa
     }
     // the reference rounds each activation row to Q8_0 / Q8_1 (x86 quantize_row_q8_0 / _q8_1) before
     // the block dot; bytes: the weight blocks (18-34 B per 32) + the int8 activations. a_q8: the
-    // producer (LayerNorm, one_chunk attention) already wrote q8a_ / q8d_
+    // producer (LayerNorm, one_chunk attention) already wrote q8a_ / q8d_ (or qa / qd: the MLP0 epilogue's rows)
     if (qf_is_k(q.fmt)) {
         // K-quants: Q8_K rows in the virtual-block layout (kquant.h), then the f16 MFMA ring kernel
         // over the virtual K at every shape
@@ -259,8 +260,9 @@ void Engine::linear(const char * cls, int mode, int M, int N, int K, const _Floa
         ProfScope ps(prof, stream, "quantize_q8");
         quantize_q8(stream, A32, A16, lda, M, K, q8a_.as<int8_t>(), q8d_.as<float>());
     }
+    if (qa && !a_q8) throw std::runtime_error("linear: operand rows without a_q8");
     ProfScope ps(prof, stream, cls, gemm_flops(M, N, K), (double) N * K * qf_block_bytes(q.fmt) / 32.0 + (double) M * K);
-    gemm_q5(stream, mode, M, N, K, q8a_.as<int8_t>(), q8d_.as<float>(), q, ep);
+    gemm_q5(stream, mode, M, N, K, qa ? qa : q8a_.as<int8_t>(), qd ? qd : q8d_.as<float>(), q, ep);
 }
 
 void Engine::encode(const std::vector<int> & slots, const std::vector<int> & offsets) {
@@ -510,7 +512,7 @@ void Engine::clear_graphs() {
 uint64_t Engine::buffers_signature() const {
     uint64_t h = 1469598103934665603ull;
     for (const void * p : {d_x_.ptr, d_xn_.ptr, d_q_.ptr, d_ao_.ptr, d_h_.ptr, d_xl_.ptr, logits_.ptr, d_stg_.ptr,
-                           q8a_.ptr, q8d_.ptr, d_xn32_.ptr, d_ao32_.ptr, d_xl32_.ptr, q16a_.ptr, q16d_.ptr,
+                           q8a_.ptr, q8d_.ptr, q8h_.ptr, q8hd_.ptr, d_xn32_.ptr, d_ao32_.ptr, d_xl32_.ptr, q16a_.ptr, q16d_.ptr,
                            self_k_.ptr, self_v_.ptr, cross_k_.ptr, cross_v_.ptr, gws_part_.ptr, sm_ws_.ptr})
         h = (h ^ (uint64_t) (uintptr_t) p) * 1099511628211ull;
     return h;
@@ -560,6 +562,8 @@ void Engine::decode(const std::vector<DecodeRow> & rows, const std::vector<int> 
                 d_ao32_.alloc((size_t) C * d * 4);
                 q8a_.alloc(std::max(q8a_.bytes, (size_t) C * 4 * d));
                 q8d_.alloc(std::max(q8d_.bytes, (size_t) C * 4 * d / 32 * 4));
+                q8h_.alloc((size_t) C * 4 * d);
+                q8hd_.alloc((size_t) C * 4 * d / 32 * 4);
             }
             if (m->kq) {  // f32 LayerNorm rows (quantized to Q8_K like the reference) + gemm_q16 operands
                 d_xn32_.alloc((size_t) C * d * 4);
@@ -767,11 +771,12 @@ void Engine::launch_decode(const DecShape & sh) {
     // one launch where a full-epilogue GEMM plus a LayerNorm launch were
     const bool q5p = q5 && !kq && R <= 32 && !sh.self_sm && !sh.cross_sm && !sh.capture;
     auto resid_q5p = [&](const _Float16 * A16, const float * A32, const Q5W & q, int K, const float * bias,
-                         const float * lnw, const float * lnb, bool a_q8) {
+                         const float * lnw, const float * lnb, bool a_q8, const int8_t * qa = nullptr,
+                         const float * qd = nullptr) {
         EpiParams ep;
         ep.out32 = gws_.partial;
         if (gws_.partial_floats < q5_partial_floats(d, K)) throw std::runtime_error("decode: partial workspace");
-        linear("gemm_dec", EPI_PARTIAL, R, d, K, A16, A32, K, nullptr, q, ep, nullptr, true, a_q8);
+        linear("gemm_dec", EPI_PARTIAL, R, d, K, A16, A32, K, nullptr, q, ep, nullptr, true, a_q8, qa, qd);
         ProfScope ps(prof, stream, "layernorm");
         resid_layernorm(stream, R, d, q5_partial_splits(K), gws_.partial, bias, d_x_.as<float>(), lnw, lnb, hp.eps,
                         d_xn_.as<_Float16>(), d, lnw ? q8a() : nullptr, lnw ? q8d() : nullptr);
@@ -822,11 +827,14 @@ void Engine::launch_decode(const DecShape & sh) {
             ep.gelu_tab = m->gelu_tab;
             ep.out16 = d_h_.as<_Float16>();
             ep.ldo = 4 * d;
+            // GELU outputs are F16 table values: exact as the f32 tensor the reference quantizes; their
+            // Q8_0 rows (mlp.2's operand) come from the MLP0 epilogue
+            ep.q8 = q8h_.as<int8_t>();
+            ep.q8d = q8hd_.as<float>();
             G("mlp0", EPI_GELU_F16, 4 * d, d, d_xn_.as<_Float16>(), nullptr, L.w_mlp0, L.t_mlp0, L.q_mlp0, ep, R, true);
         }
-        // GELU outputs are F16 table values: exact as the f32 tensor the reference quantizes
         resid_q5p(d_h_.as<_Float16>(), nullptr, L.q_mlp1, 4 * d, L.b_mlp1, nx ? nx->attn_ln_w : nullptr,
-                  nx ? nx->attn_ln_b : nullptr, false);
+                  nx ? nx->attn_ln_b : nullptr, true, q8h_.as<int8_t>(), q8hd_.as<float>());
     }
     for (int l = 0; l < hp.n_text_layer && !q5p; ++l) {
         const DecLayerW & L = m->dec[l];

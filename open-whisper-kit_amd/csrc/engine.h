@@ -197,8 +197,9 @@ private:
     void linear(const char * cls, int mode, int M, int N, int K, const _Float16 * A16, const float * A32, int lda,
                 const _Float16 * W, const Q5W & q, const EpiParams & ep, const _Float16 * Wt = nullptr,
                 bool dec = false,
-                bool a_q8 = false);
+                bool a_q8 = false, const int8_t * qa = nullptr, const float * qd = nullptr);
     DevBuf q8a_, q8d_;
+    DevBuf q8h_, q8hd_;  // Q8_0 rows of the GELU output (MLP0 epilogue -> MLP1 operand; decode passes <= 32 rows)
     DevBuf q16a_, q16d_;  // gemm_q16 operands: Q8_0 integers as f16 [M][K], scales [K/32][mpad]
     // Q5_0 models: the Q8_0 activation buffers producers write for the next linear (else null)
     // Q8_0 / Q8_1 rows written by producers (LayerNorm, attention); K-quant models quantize to Q8_K

@@ -2117,17 +2117,20 @@ constexpr int GQ_MAX_SCALES = 32 * 160;  // M x K/32 activation scales in LDS
 // activation scales per thread: M * nb <= 32 * nb over blockDim = 64 * ceil(nb / J) threads
 // -> at most 32 * J / 64 + 1
 
-template <int MODE, int MT, int FMT, int GQ_J>  // FMT: QFmt; GQ_J K blocks per wave
+// NT column tiles per block (full epilogues, one k split): a wave's activation fragments and scales
+// serve NT weight tiles (the MLP0 / logits launches, whose activation rows every block reads again);
+// per output the same MFMA chain and the same wave order as NT = 1: bit-identical
+template <int MODE, int MT, int FMT, int GQ_J, int NT = 1>  // FMT: QFmt; GQ_J K blocks per wave
 __global__ __launch_bounds__(GQ_MAXW * 64) void k_gemm_q5_rows(int M, int N, int K, const int8_t * __restrict__ qa,
                                                                const float * __restrict__ da, Q5W w, EpiParams ep) {
     constexpr int GQ_DA_PER_THREAD = 32 * GQ_J / 64 + 1;
     constexpr bool HAS_M = qf_has_m(FMT), HAS_QH = qf_has_qh(FMT);
     constexpr int TB = qf_tile_bytes(FMT), QSB = qf_qs_bytes(FMT);
-    __shared__ floatx4 red[GQ_MAXW][MT][64];
+    __shared__ floatx4 red[GQ_MAXW][NT][MT][64];
     __shared__ float sda[GQ_MAX_SCALES];
     const int tid = threadIdx.x, lane = tid & 63, nw = blockDim.x >> 6;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: branch-free k range
-    const int n0 = blockIdx.x * 16;
+    const int ntiles = (N + 15) >> 4, t0 = blockIdx.x * NT;
     const int nb = K >> 5;
     // split-K (gridDim.y > 1, EPI_PARTIAL): block y covers K blocks [kblo, kblo + nbl)
     const int kblo = blockIdx.y * nw * GQ_J;
@@ -2136,22 +2139,29 @@ __global__ __launch_bounds__(GQ_MAXW * 64) void k_gemm_q5_rows(int M, int N, int
     const int nj = max(0, min(GQ_J, nb - kb0));
     const int g = lane >> 4;
     const int c16 = lane & 15;
-    uint64_t raw[GQ_J];
-    uint32_t qh[GQ_J];
-    _Float16 dw[GQ_J], mw[GQ_J];
+    uint64_t raw[NT][GQ_J];
+    uint32_t qh[NT][GQ_J];
+    _Float16 dw[NT][GQ_J], mw[NT][GQ_J];
     long a[MT][GQ_J];
     // the tile's blocks are contiguous records (qf_tile_bytes): coalesced loads. Blocks past this
     // wave's range load a valid record and a zero activation (adds exact zeros). Record format at
     // compile time: the load phase stays branch-free.
-    const uint8_t * tb = w.tiled + (size_t) blockIdx.x * nb * TB;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+        const uint8_t * tb = w.tiled + (size_t) min(t0 + t, ntiles - 1) * nb * TB;
+#pragma unroll
+        for (int j = 0; j < GQ_J; ++j) {
+            const int kb = min(kb0 + j, nb - 1);
+            const uint8_t * rec = tb + (size_t) kb * TB;
+            raw[t][j] = *(const uint64_t *) (rec + c16 * QSB + (QSB == 32 ? g * 8 : (g & 1) * 8));
+            qh[t][j] = HAS_QH ? *(const uint32_t *) (rec + qf_tile_off_qh(FMT) + c16 * 4) : 0u;
+            dw[t][j] = *(const _Float16 *) (rec + qf_tile_off_d(FMT) + c16 * 2);
+            mw[t][j] = HAS_M ? *(const _Float16 *) (rec + qf_tile_off_m(FMT) + c16 * 2) : (_Float16) 0.0f;
+        }
+    }
 #pragma unroll
     for (int j = 0; j < GQ_J; ++j) {
         const int kb = min(kb0 + j, nb - 1);
-        const uint8_t * rec = tb + (size_t) kb * TB;
-        raw[j] = *(const uint64_t *) (rec + c16 * QSB + (QSB == 32 ? g * 8 : (g & 1) * 8));
-        qh[j] = HAS_QH ? *(const uint32_t *) (rec + qf_tile_off_qh(FMT) + c16 * 4) : 0u;
-        dw[j] = *(const _Float16 *) (rec + qf_tile_off_d(FMT) + c16 * 2);
-        mw[j] = HAS_M ? *(const _Float16 *) (rec + qf_tile_off_m(FMT) + c16 * 2) : (_Float16) 0.0f;
 #pragma unroll
         for (int i = 0; i < MT; ++i) {
             const int ra = min(i * 16 + c16, M - 1);
@@ -2162,6 +2172,7 @@ __global__ __launch_bounds__(GQ_MAXW * 64) void k_gemm_q5_rows(int M, int N, int
     // activation scales of this block's K range (raw f32 d; at most GQ_DA_PER_THREAD per thread:
     // M <= 32, nbl <= nw * J) to LDS as [row][kb - kblo]; every load of the launch is issued before
     // the first wait (one round trip)
+    {
         float dv[GQ_DA_PER_THREAD];
 #pragma unroll
         for (int u = 0; u < GQ_DA_PER_THREAD; ++u) {
@@ -2175,47 +2186,82 @@ __global__ __launch_bounds__(GQ_MAXW * 64) void k_gemm_q5_rows(int M, int N, int
             const int i = tid + u * blockDim.x;
             if (i < M * nbl) sda[i] = dv[u];
         }
+    }
     __syncthreads();
-    floatx4 acc[MT], accm[MT];
+    floatx4 acc[NT][MT], accm[NT][MT];
 #pragma unroll
-    for (int i = 0; i < MT; ++i) acc[i] = accm[i] = floatx4{0.f, 0.f, 0.f, 0.f};
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int i = 0; i < MT; ++i) acc[t][i] = accm[t][i] = floatx4{0.f, 0.f, 0.f, 0.f};
     const long ones = 0x0101010101010101L;
 #pragma unroll
     for (int j = 0; j < GQ_J; ++j) {
         const int kb = min(kb0 + j, nb - 1);
-        const uint64_t v = unpack_group<FMT>(raw[j], qh[j], g);
-        const float dwf = (float) dw[j];
 #pragma unroll
         for (int i = 0; i < MT; ++i) {
             const intx4 z = {0, 0, 0, 0};
-            const intx4 iv = __builtin_amdgcn_mfma_i32_16x16x32_i8(a[i][j], (long) v, z, 0, 0, 0);
             intx4 is = z;
             if constexpr (HAS_M) is = __builtin_amdgcn_mfma_i32_16x16x32_i8(a[i][j], ones, z, 0, 0, 0);
+            float dr[4];
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
                 const int r = min(i * 16 + 4 * g + e, M - 1);
-                const float dr = j < nj ? sda[r * nbl + (kb - kblo)] : 0.0f;  // past the wave's range: zeros
-                acc[i][e] += (float) iv[e] * ((float) (_Float16) dr * dwf);
-                if constexpr (HAS_M) accm[i][e] += (float) mw[j] * q8_1_sum(dr, is[e]);
+                dr[e] = j < nj ? sda[r * nbl + (kb - kblo)] : 0.0f;  // past the wave's range: zeros
+            }
+#pragma unroll
+            for (int t = 0; t < NT; ++t) {
+                const uint64_t v = unpack_group<FMT>(raw[t][j], qh[t][j], g);
+                const float dwf = (float) dw[t][j];
+                const intx4 iv = __builtin_amdgcn_mfma_i32_16x16x32_i8(a[i][j], (long) v, z, 0, 0, 0);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    acc[t][i][e] += (float) iv[e] * ((float) (_Float16) dr[e] * dwf);
+                    if constexpr (HAS_M) accm[t][i][e] += (float) mw[t][j] * q8_1_sum(dr[e], is[e]);
+                }
             }
         }
     }
 #pragma unroll
-    for (int i = 0; i < MT; ++i) red[wave][i][lane] = HAS_M ? acc[i] + accm[i] : acc[i];
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int i = 0; i < MT; ++i) red[wave][t][i][lane] = HAS_M ? acc[t][i] + accm[t][i] : acc[t][i];
     __syncthreads();
-    for (int o = tid; o < MT * 256; o += blockDim.x) {
-        const int r = o >> 4, cc = o & 15;
+    for (int o = tid; o < NT * MT * 256; o += blockDim.x) {
+        const int t = o / (MT * 256), q = o - t * (MT * 256);
+        const int r = q >> 4, cc = q & 15;
         const int i = r >> 4, rr = r & 15;
         const int ln = 16 * (rr >> 2) + cc, e = rr & 3;
-        const float * rp = (const float *) &red[0][i][ln] + e;
+        const float * rp = (const float *) &red[0][t][i][ln] + e;
         float sum = rp[0];
-        for (int ww = 1; ww < nw; ++ww) sum += rp[ww * MT * 64 * 4];
-        const int c = n0 + cc;
+        for (int ww = 1; ww < nw; ++ww) sum += rp[ww * NT * MT * 64 * 4];
+        const int c = (t0 + t) * 16 + cc;
         if (r < M && c < N) {
-            if constexpr (MODE == EPI_PARTIAL)
+            if constexpr (MODE == EPI_PARTIAL) {
                 ep.out32[((size_t) blockIdx.y * M + r) * N + c] = sum;  // [ks][M][N] for resid_layernorm
-            else
+            } else if constexpr (MODE == EPI_GELU_F16 && NT == 2) {
+                const _Float16 h = (_Float16) gelu_lookup(ep.gelu_tab, sum + ep.bias[c]);
+                ep.out16[(size_t) r * ep.ldo + c] = h;
+                sda[r * 32 + t * 16 + cc] = (float) h;  // the scales are read: sda is free
+            } else {
                 epi_store<MODE>(ep, r, c, sum);
+            }
+        }
+    }
+    if constexpr (MODE == EPI_GELU_F16 && NT == 2) {
+        // ep.q8: the block's 32 columns are one Q8_0 block of each row -- the next GEMM's operand rounded
+        // here (k_quantize_q8's arithmetic on the same f16 values) instead of in a launch of its own
+        if (ep.q8) {
+            __syncthreads();
+            for (int o = tid; o < M * 32; o += blockDim.x) {  // half-waves stay whole: M * 32, blockDim % 64 == 0
+                const int r = o >> 5, cl = o & 31;
+                const float x = sda[o];
+                float am = fabsf(x);
+#pragma unroll
+                for (int sh = 16; sh > 0; sh >>= 1) am = fmaxf(am, __shfl_xor(am, sh, 32));
+                const float id = am != 0.0f ? 127.f / am : 0.0f;
+                ep.q8[(size_t) r * N + blockIdx.x * 32 + cl] = (int8_t) rintf(x * id);
+                if (cl == 0) ep.q8d[(size_t) r * (N >> 5) + blockIdx.x] = am / 127.f;
+            }
         }
     }
 }
@@ -2325,8 +2371,18 @@ template <int MODE> struct LaunchQ5 {
             const int per = (nb + KS - 1) / KS;
             const int nw = (per + J - 1) / J;
             if (nw > GQ_MAXW) throw std::runtime_error("gemm_q5: decode-row plan");
-            const dim3 grid((N + 15) / 16, KS), block(nw * 64);
-#define OWK_Q_ROWS(MT_, F_, J_) OWK_LAUNCH((k_gemm_q5_rows<MODE, MT_, F_, J_>), grid, block, 0, s, M, N, K, qa, da, w, ep)
+            // full-epilogue launches with many column tiles take 2 per block (as LaunchRows: the activation
+            // rows are read once per 2 tiles): MLP0 and the logits
+            const int tiles = (N + 15) / 16;
+            // ep.q8 (GELU rows): 2 tiles per block are one Q8_0 block per row, quantized in the epilogue
+            const bool fq = MODE == EPI_GELU_F16 && ep.q8 && N % 32 == 0;
+            const bool nt2 = MODE != EPI_PARTIAL && KS == 1 && (fq || (tiles + 1) / 2 >= 128);
+            const dim3 grid(nt2 ? (tiles + 1) / 2 : tiles, KS), block(nw * 64);
+#define OWK_Q_ROWS(MT_, F_, J_)                                                                                 \
+    do {                                                                                                        \
+        if (nt2) OWK_LAUNCH((k_gemm_q5_rows<MODE, MT_, F_, J_, 2>), grid, block, 0, s, M, N, K, qa, da, w, ep); \
+        else OWK_LAUNCH((k_gemm_q5_rows<MODE, MT_, F_, J_, 1>), grid, block, 0, s, M, N, K, qa, da, w, ep);     \
+    } while (0)
 #define OWK_Q_ROWS_J(MT_, F_) do { if (J == 3) OWK_Q_ROWS(MT_, F_, 3); else OWK_Q_ROWS(MT_, F_, GQ_JMAX); } while (0)
 #define OWK_Q_ROWS_F(MT_)                                                 \
     switch (w.fmt) {                                                      \
@@ -2340,11 +2396,16 @@ template <int MODE> struct LaunchQ5 {
 #undef OWK_Q_ROWS_F
 #undef OWK_Q_ROWS_J
 #undef OWK_Q_ROWS
-        } else if (M <= 64)
+            if (ep.q8 && !fq) quantize_q8(s, nullptr, ep.out16, ep.ldo, M, N, ep.q8, ep.q8d);
+            return;
+        }
+        if (M <= 64)
             OWK_LAUNCH(k_gemm_q5_skinny<MODE>, dim3((N + 15) / 16), dim3(512), 0, s, M, N, K, qa, da, w, ep);
         else
             OWK_LAUNCH(k_gemm_q5_big<MODE>, dim3(((M + 63) / 64) * ((N + 63) / 64)), dim3(256), 0, s, M, N, K,
                                qa, da, w, ep);
+        // Q8_0 rows of an f16 output requested by the caller: a launch of their own on these paths
+        if (ep.q8) quantize_q8(s, nullptr, ep.out16, ep.ldo, M, N, ep.q8, ep.q8d);
     }
 };
 

@@ -54,6 +54,10 @@ struct EpiParams {
     const float * qs_dw = nullptr;        // weight d
     int qs_mpad = 0, qs_npad = 0;
     int c_off = 0;                        // large-tile launch over a column range: its first column
+    // gemm_q5 with an f16 output (EPI_GELU_F16 decode rows fuse it): its Q8_0 rows [M][N] and raw f32
+    // block d [M][N/32], the next quantized GEMM's operand (must not alias that GEMM's own operand)
+    int8_t * q8 = nullptr;
+    float * q8d = nullptr;
 };
 
 // large tiles (encoder / conv / cross-KV / long prefill): A [M,lda] f16, W [N,ldw] f16
