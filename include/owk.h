@@ -105,7 +105,9 @@ WHISPER_API int owk_debug_gemm_q5(int device, int M, int N, int K, const float *
  * Q2_K / Q4_K / Q5_K, K for Q3_K, 2K for Q6_K), d_out the Q8_K scale per row and 256-block [M][K/256] */
 WHISPER_API int owk_debug_gemm_quant(int device, int fmt, int M, int N, int K, const float * a, const uint8_t * w_blocks,
                                      float * out, int8_t * q_out, float * d_out);
-// use_q16 = 1: the large-tile encoder path (expanded f16 integers, gemm_q16; M >= 2048, symmetric formats)
+// use_q16 = 1: the large-tile encoder path (expanded f16 integers, gemm_q16; M >= 2048, symmetric formats);
+// use_q16 = 2: the MLP0 decode-row form (M <= 32, N % 32 == 0): EPI_GELU_F16 with an identity GELU table,
+// out = the f16 outputs as f32, q_out [M][N] / d_out [M][N/32] = the Q8_0 rows its epilogue writes
 WHISPER_API int owk_debug_gemm_quant2(int device, int fmt, int M, int N, int K, const float * a, const uint8_t * w_blocks,
                                       float * out, int8_t * q_out, float * d_out, int use_q16);
 /* host-only test hook (no device): N rows of ggml K-quant blocks (fmt 5..9 as above) -> the virtual-block

@@ -1522,7 +1522,7 @@ int owk_debug_gemm_quant2(int device, int fmt, int M, int N, int K, const float 
         ep.out32 = dout.as<float>();
         ep.ldo = N;
         DevBuf wi, dwt, q16, q16d;
-        if (use_q16) {
+        if (use_q16 == 1) {
             // the large-tile path of the encoder: expanded weights, f16 Q8_0 integers, gemm_q16
             w.npad = (N + 255) / 256 * 256;
             wi.alloc((size_t) N * K * 2);
@@ -1536,6 +1536,36 @@ int owk_debug_gemm_quant2(int device, int fmt, int M, int N, int K, const float 
             q16d.alloc((size_t) nb * mpad * 4);
             quantize_q8_f16(s, da.as<float>(), nullptr, K, M, K, q16.as<_Float16>(), q16d.as<float>(), mpad);
             gemm_q16(s, EPI_F32, M, N, K, q16.as<_Float16>(), q16d.as<float>(), mpad, w, ep);
+        } else if (use_q16 == 2) {
+            // the MLP0 form: EPI_GELU_F16 decode rows that also write the next GEMM's Q8_0 rows. The GELU
+            // table is the identity (out16 = f16(row . col)), so out is comparable with the EPI_F32 launch;
+            // q_out [M][N] / d_out [M][N/32] receive the epilogue's Q8_0 rows
+            if (M > 32 || N % 32) throw std::runtime_error("GELU + Q8_0 rows: M <= 32, N % 32 == 0");
+            std::vector<uint16_t> tab(65536), o16((size_t) M * N);
+            for (int i = 0; i < 65536; ++i) tab[i] = (uint16_t) i;
+            DevBuf dtab, do16, dbias, hq, hqd;
+            dtab.alloc(tab.size() * 2);
+            do16.alloc(o16.size() * 2);
+            dbias.alloc((size_t) N * 4);
+            hq.alloc((size_t) M * N);
+            hqd.alloc((size_t) M * (N / 32) * 4);
+            OWK_HIP_CHECK(hipMemcpy(dtab.ptr, tab.data(), tab.size() * 2, hipMemcpyHostToDevice));
+            OWK_HIP_CHECK(hipMemset(dbias.ptr, 0, dbias.bytes));
+            EpiParams eg;
+            eg.bias = dbias.as<float>();
+            eg.gelu_tab = dtab.as<uint16_t>();
+            eg.out16 = do16.as<_Float16>();
+            eg.ldo = N;
+            eg.q8 = hq.as<int8_t>();
+            eg.q8d = hqd.as<float>();
+            gemm_q5(s, EPI_GELU_F16, M, N, K, q8.as<int8_t>(), q8d.as<float>(), w, eg);
+            OWK_HIP_CHECK(hipStreamSynchronize(s));
+            OWK_HIP_CHECK(hipMemcpy(o16.data(), do16.ptr, o16.size() * 2, hipMemcpyDeviceToHost));
+            for (size_t i = 0; i < o16.size(); ++i) out[i] = f16_to_f32_host(o16[i]);
+            if (q_out) OWK_HIP_CHECK(hipMemcpy(q_out, hq.ptr, (size_t) M * N, hipMemcpyDeviceToHost));
+            if (d_out) OWK_HIP_CHECK(hipMemcpy(d_out, hqd.ptr, (size_t) M * (N / 32) * 4, hipMemcpyDeviceToHost));
+            OWK_HIP_CHECK(hipStreamDestroy(s));
+            return 0;
         } else {
             gemm_q5(s, EPI_F32, M, N, K, q8.as<int8_t>(), q8d.as<float>(), w, ep);
         }

@@ -244,6 +244,41 @@ def test_quant_gemm_vs_reference(kind, M, N, K):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["q5_0", "q8_0", "q4_1"])
+@pytest.mark.parametrize("M,N,K", [(1, 2048, 1280), (17, 5120, 1280), (32, 2048, 384)])
+def test_gelu_rows_emit_q8(kind, M, N, K):
+    """The MLP0 decode-row launch (two column tiles per block, its epilogue writing mlp.2's Q8_0 rows):
+    f16 outputs bit-identical to the one-tile EPI_F32 launch rounded to f16 (identity GELU table), and the
+    Q8_0 rows equal to quantize_row_q8_0 of those f16 values (x86 rounding: d = amax / 127,
+    q = rint(x * 127 / amax), in f32)."""
+    import owk_synth as S
+
+    L = owk.load()
+    fmt, _, _ = QFMT[kind]
+    L.owk_debug_gemm_quant2.argtypes = [C.c_int] * 5 + [C.POINTER(C.c_float), C.c_void_p, C.POINTER(C.c_float),
+                                                        C.c_void_p, C.c_void_p, C.c_int]
+    rng = np.random.default_rng(M * 3 + N + K)
+    a = (rng.standard_normal((M, K)) * 0.7).astype(np.float32)
+    wf = (rng.standard_normal((N, K)) / np.sqrt(K) + 0.02).astype(np.float32)
+    blocks = S._QKIND[kind][2](wf)
+    pf = lambda x: x.ctypes.data_as(C.POINTER(C.c_float))
+    out32 = np.zeros((M, N), np.float32)
+    assert L.owk_debug_gemm_quant2(0, fmt, M, N, K, pf(a), blocks, pf(out32), None, None, 0) == 0
+    out16 = np.zeros((M, N), np.float32)
+    q = np.zeros((M, N), np.int8)
+    d = np.zeros((M, N // 32), np.float32)
+    assert L.owk_debug_gemm_quant2(0, fmt, M, N, K, pf(a), blocks, pf(out16), q.ctypes.data, d.ctypes.data, 2) == 0
+    np.testing.assert_array_equal(out16, out32.astype(np.float16).astype(np.float32))
+    x = out16.reshape(M, N // 32, 32)
+    am = np.abs(x).max(axis=2)
+    with np.errstate(divide="ignore"):
+        inv = np.where(am != 0, np.float32(127.0) / am, np.float32(0.0)).astype(np.float32)
+    qr = np.rint(x * inv[:, :, None]).astype(np.int8).reshape(M, N)
+    np.testing.assert_array_equal(q, qr)
+    np.testing.assert_array_equal(d, (am / np.float32(127.0)).astype(np.float32))
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("kind", ["q5_0", "q8_0", "q4_0"])
 def test_quant_gemm_q16_vs_reference(kind):
     """The encoder's large-tile quantized GEMM (gemm_q16: the weight and Q8_0 activation integers as
