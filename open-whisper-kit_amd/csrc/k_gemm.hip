@@ -1007,6 +1007,21 @@ __global__ __launch_bounds__(512) void k_gemm_skinny(int M, int N, int K, const 
 // ---------------------------------------------------------------------------------
 constexpr int GR_MAXW = 16;  // waves per block
 
+// one output's wave partials summed in wave order 0 .. nw-1 (the decode-row GEMMs' fixed order), every
+// LDS read issued before the first add: rp[w * stride] for w < MAXW stays inside the MAXW-row
+// reduction array; rows past nw are read and not used
+template <int MAXW>
+__device__ __forceinline__ float wave_order_sum(const float * rp, int stride, int nw) {
+    float v[MAXW];
+#pragma unroll
+    for (int w = 0; w < MAXW; ++w) v[w] = rp[w * stride];
+    float s = v[0];
+#pragma unroll
+    for (int w = 1; w < MAXW; ++w)
+        if (w < nw) s += v[w];
+    return s;
+}
+
 __global__ void k_tile_weights(const _Float16 * __restrict__ W, int N, int K, _Float16 * __restrict__ out) {
     const int nsteps = K >> 5;
     const size_t total = (size_t) ((N + 15) >> 4) * nsteps * 64;
@@ -1089,9 +1104,7 @@ __global__ __launch_bounds__(GR_MAXW * 64) void k_gemm_rows(int M, int N, int K,
         const int r = o >> 4, cc = o & 15;
         const int i = r >> 4, rr = r & 15;
         const int ln = 16 * (rr >> 2) + cc, e = rr & 3;
-        const float * rp = (const float *) &red[0][i][ln] + e;
-        float sum = rp[0];
-        for (int w = 1; w < nw; ++w) sum += rp[w * MT * 64 * 4];
+        const float sum = wave_order_sum<GR_MAXW>((const float *) &red[0][i][ln] + e, MT * 64 * 4, nw);
         const int c = n0 + cc;
         if (r < M && c < N) {
             if constexpr (MODE == EPI_PARTIAL)
@@ -1156,8 +1169,7 @@ __global__ __launch_bounds__(GR_MAXW * 64) void k_gemm_rows_nt(int M, int N, int
         const int r = q >> 4, cc = q & 15;
         const int i = r >> 4, rr = r & 15;
         const int ln = 16 * (rr >> 2) + cc, e = rr & 3;
-        float sum = ((const float *) &red[0][t][i][ln])[e];
-        for (int w = 1; w < nw; ++w) sum += ((const float *) &red[w][t][i][ln])[e];
+        const float sum = wave_order_sum<GR_MAXW>((const float *) &red[0][t][i][ln] + e, NT * MT * 64 * 4, nw);
         const int c = (t0 + t) * 16 + cc;
         if (r < M && c < N) {
             if constexpr (MODE == EPI_PARTIAL)
@@ -2231,9 +2243,7 @@ __global__ __launch_bounds__(GQ_MAXW * 64) void k_gemm_q5_rows(int M, int N, int
         const int r = q >> 4, cc = q & 15;
         const int i = r >> 4, rr = r & 15;
         const int ln = 16 * (rr >> 2) + cc, e = rr & 3;
-        const float * rp = (const float *) &red[0][t][i][ln] + e;
-        float sum = rp[0];
-        for (int ww = 1; ww < nw; ++ww) sum += rp[ww * NT * MT * 64 * 4];
+        const float sum = wave_order_sum<GQ_MAXW>((const float *) &red[0][t][i][ln] + e, NT * MT * 64 * 4, nw);
         const int c = (t0 + t) * 16 + cc;
         if (r < M && c < N) {
             if constexpr (MODE == EPI_PARTIAL) {
