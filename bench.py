@@ -52,7 +52,8 @@ CLIP_SAMPLES = 480000     # 30 s at 16 kHz
 MFMA_CLASSES = {"gemm_enc", "gemm_cross", "gemm_conv", "gemm_dec_big", "gemm_logits_big", "attn_encoder"}
 MAX_TOKENS = 219          # completion at i >= max_tokens -> 220 tokens per clip
 TOP_CLASSES = 3           # classes re-timed alone for the roofline
-# kernels of each class (mangled-name patterns, for the rocprof / PMC lookups). Decode-row GEMMs:
+# kernels of each class (name patterns for the rocprof / PMC lookups; rocprofv3 prints some template
+# instances demangled -- k_gemm_q5_rows<8, 2, 0, 3, 1>(...) -- and the rest mangled, so both forms). Decode-row GEMMs:
 # epilogue 7 (EPI_F32) is the logits matmul, every other epilogue is gemm_dec; the quantized models'
 # decode-row GEMMs are k_gemm_q5_rows (every block format). Large GEMMs: epilogue 5 (EPI_KV_CROSS) is
 # gemm_cross, 3 (EPI_CONV2) gemm_conv, the encoder's QKV / O / MLP0 / MLP1 epilogues 0, 1, 2, 4
@@ -62,8 +63,9 @@ CLASS_KERNELS = {
     "attn_cross": r"k_attn_stepILb0ELb1E",
     "attn_self": r"k_attn_stepILb[01]ELb0E",
     "attn_encoder": r"k_attn_encoder(?:_sm)?E",
-    "gemm_dec": r"k_gemm_rows(?:_nt|_ln)?ILi(?!7E)\d+E|k_gemm_rows_reduceILi(?!7E)\d+E|k_gemm_q5_rowsILi(?!7E)\d+E",
-    "gemm_logits": r"k_gemm_rows(?:_nt)?ILi7E|k_gemm_q5_rowsILi7E",
+    "gemm_dec": r"k_gemm_rows(?:_nt|_ln)?ILi(?!7E)\d+E|k_gemm_rows_reduceILi(?!7E)\d+E|k_gemm_q5_rowsILi(?!7E)\d+E"
+                r"|k_gemm_q5_rows<(?!7,)\d+,",
+    "gemm_logits": r"k_gemm_rows(?:_nt)?ILi7E|k_gemm_q5_rowsILi7E|k_gemm_q5_rows<7,",
     "layernorm": r"k_layernorm_f16|k_resid_layernorm",
     "gemm_enc": _BIG + r"ILi[0124]E",
     "gemm_cross": _BIG + r"ILi5E",
