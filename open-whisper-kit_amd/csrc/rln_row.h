@@ -9,10 +9,31 @@
 
 namespace owk {
 
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double v) {
+    const uint64_t u = __builtin_bit_cast(uint64_t, v);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int) (uint32_t) u, CTRL, 0xf, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int) (uint32_t) (u >> 32), CTRL, 0xf, 0xf, false);
+    return __builtin_bit_cast(double, ((uint64_t) (uint32_t) hi << 32) | (uint32_t) lo);
+}
+__device__ __forceinline__ double readlane_d(double v, int l) {
+    const uint64_t u = __builtin_bit_cast(uint64_t, v);
+    const uint32_t lo = __builtin_amdgcn_readlane((int) (uint32_t) u, l);
+    const uint32_t hi = __builtin_amdgcn_readlane((int) (uint32_t) (u >> 32), l);
+    return __builtin_bit_cast(double, ((uint64_t) hi << 32) | lo);
+}
+
+// the xor butterfly's sum over the wave (offsets 1, 2, 4, 8, 16, 32; every lane ends with the same
+// bits): offsets 1 and 2 as DPP quad permutes, 4 and 8 as the half-row / row mirrors (after the quad
+// steps every lane of a quad holds the quad's sum, so the mirror partner carries the xor partner's
+// bits), then the four row sums broadcast and added as the butterfly's last two steps add them at
+// lane 0 -- no LDS-crossbar permutes. Bit-identical to the butterfly in every lane.
 __device__ __forceinline__ double wave_sum_d(double v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
+    v += dpp_d<0xB1>(v);   // quad_perm [1,0,3,2]: xor 1
+    v += dpp_d<0x4E>(v);   // quad_perm [2,3,0,1]: xor 2
+    v += dpp_d<0x141>(v);  // row_half_mirror: the other quad of the 8
+    v += dpp_d<0x140>(v);  // row_mirror: the other 8 of the row
+    return (readlane_d(v, 0) + readlane_d(v, 16)) + (readlane_d(v, 32) + readlane_d(v, 48));
 }
 
 constexpr int RL_V4 = 2;     // float4 per thread -> N <= 2048
