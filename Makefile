@@ -82,7 +82,46 @@ $(CALLERS)/test-streaming-api: $(REF)/streaming-sortformer/src/test-streaming-ap
 	@mkdir -p $(CALLERS)
 	g++ $(CALLFLAGS) $< -o $@ -L$(PKG)/lib -lsortformer -Wl,-rpath,'$$ORIGIN/..'
 
-clean:
-	rm -rf $(OBJDIR) $(PKG)/lib
+# Host-side AddressSanitizer + UndefinedBehaviorSanitizer build of both libraries (the reference's
+# WHISPER_SANITIZE_ADDRESS / _UNDEFINED, ref CMakeLists.txt:74-76, 99-101). Only host code is
+# instrumented (each -fsanitize= after -Xarch_host; device code objects are unchanged), so the
+# libraries load and run their host paths on this GPU-less container: tokenizer, model/GGUF header
+# parsing, GBNF grammar, aligner, RTTM, DTW, k-quant expansion, VAD segments, KV-cell allocator.
+#   make sanitize        -> open-whisper-kit_amd/lib/san/{libwhisper,libsortformer}.so
+#   make sanitize-test   -> the CPU tests of those paths against them (tools/sanitize_tests.sh)
+SANDIR   := $(PKG)/build_san
+SANLIB   := $(PKG)/lib/san
+SANFLAGS := -Xarch_host -fsanitize=address -Xarch_host -fsanitize=undefined -Xarch_host -fno-sanitize-recover=undefined \
+            -Xarch_host -fno-omit-frame-pointer -Xarch_host -fno-sanitize=vptr
+SAN_OBJS_ALL := $(patsubst $(SRC)/%.hip,$(SANDIR)/%.hip.o,$(HIP_SRCS)) $(patsubst $(SRC)/%.cpp,$(SANDIR)/%.cpp.o,$(CPP_SRCS))
+SAN_SF_ONLY  := $(SANDIR)/sortformer.cpp.o $(SANDIR)/k_sortformer.hip.o
+SAN_OBJS     := $(filter-out $(SAN_SF_ONLY),$(SAN_OBJS_ALL))
+SAN_SF_OBJS  := $(SAN_SF_ONLY) $(SANDIR)/k_gemm.hip.o $(SANDIR)/k_misc.hip.o $(SANDIR)/kquant.cpp.o
 
-.PHONY: all clean oracle selftest callers
+sanitize: $(SANLIB)/libwhisper.so $(SANLIB)/libsortformer.so
+
+$(SANLIB)/libwhisper.so: $(SAN_OBJS)
+	@mkdir -p $(dir $@)
+	$(HIPCC) -shared --offload-arch=$(ARCH) -shared-libasan -fsanitize=address,undefined -o $@ $(SAN_OBJS) -rdynamic \
+	    -Wl,-soname,libwhisper.so
+
+$(SANLIB)/libsortformer.so: $(SAN_SF_OBJS)
+	@mkdir -p $(dir $@)
+	$(HIPCC) -shared --offload-arch=$(ARCH) -shared-libasan -fsanitize=address,undefined -o $@ $(SAN_SF_OBJS) \
+	    -Wl,-soname,libsortformer.so
+
+$(SANDIR)/%.hip.o: $(SRC)/%.hip $(HDRS)
+	@mkdir -p $(SANDIR)
+	$(HIPCC) $(FLAGS) $(SANFLAGS) -c $< -o $@
+
+$(SANDIR)/%.cpp.o: $(SRC)/%.cpp $(HDRS)
+	@mkdir -p $(SANDIR)
+	$(HIPCC) $(FLAGS) $(SANFLAGS) -x hip -c $< -o $@
+
+sanitize-test: sanitize
+	bash tools/sanitize_tests.sh
+
+clean:
+	rm -rf $(OBJDIR) $(SANDIR) $(PKG)/lib
+
+.PHONY: all clean oracle selftest callers sanitize sanitize-test

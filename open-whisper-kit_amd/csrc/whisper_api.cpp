@@ -24,23 +24,72 @@ const std::vector<uint16_t> & gelu_table_host();
 
 // OWK_BACKTRACE=1: print a native backtrace on SIGSEGV/SIGABRT (host-side debugging on
 // the GPU box, where no debugger may attach to a GPU process)
+// Each frame is printed as library + offset from its load base (resolvable offline with
+// llvm-addr2line / llvm-objdump against the same image's libraries), with the nearest exported
+// symbol, and the /proc/self/maps lines around the faulting address.
 #include <csignal>
+#include <dlfcn.h>
 #include <execinfo.h>
+#include <ucontext.h>
 #include <unistd.h>
-static void owk_crash_handler(int sig) {
+static void owk_crash_print_pc(const void * pc) {
+    Dl_info di{};
+    char line[768];
+    int n;
+    if (dladdr(pc, &di) && di.dli_fname)
+        n = snprintf(line, sizeof(line), "  %p  %s+0x%lx  (%s+0x%lx)\n", pc, di.dli_fname,
+                     (unsigned long) ((const char *) pc - (const char *) di.dli_fbase), di.dli_sname ? di.dli_sname : "?",
+                     di.dli_saddr ? (unsigned long) ((const char *) pc - (const char *) di.dli_saddr) : 0ul);
+    else
+        n = snprintf(line, sizeof(line), "  %p  (no mapping)\n", pc);
+    (void) !write(2, line, (size_t) std::min(n, (int) sizeof(line) - 1));
+}
+static void owk_crash_handler(int sig, siginfo_t * si, void * uc_) {
+    char line[512];
+    const ucontext_t * uc = (const ucontext_t *) uc_;
+    const void * pc = uc ? (const void *) uc->uc_mcontext.gregs[REG_RIP] : nullptr;
+    int n = snprintf(line, sizeof(line), "\n[owk] fatal signal %d, fault address %p, pc:\n", sig, si ? si->si_addr : nullptr);
+    (void) !write(2, line, (size_t) n);
+    owk_crash_print_pc(pc);
     void * frames[64];
-    const int n = backtrace(frames, 64);
-    const char msg[] = "\n[owk] fatal signal, native backtrace:\n";
+    const int nf = backtrace(frames, 64);
+    const char msg[] = "[owk] native backtrace (library+offset, nearest exported symbol):\n";
     (void) !write(2, msg, sizeof(msg) - 1);
-    backtrace_symbols_fd(frames, n, 2);
+    for (int i = 0; i < nf; ++i) owk_crash_print_pc(frames[i]);
+    // the mappings around the fault address: which allocation the access ran off
+    FILE * f = si ? fopen("/proc/self/maps", "r") : nullptr;
+    if (f) {
+        const uintptr_t a = (uintptr_t) si->si_addr;
+        char buf[512], prev[512] = "";
+        const char hdr[] = "[owk] /proc/self/maps around the fault address:\n";
+        (void) !write(2, hdr, sizeof(hdr) - 1);
+        while (fgets(buf, sizeof(buf), f)) {
+            unsigned long lo = 0, hi = 0;
+            if (sscanf(buf, "%lx-%lx", &lo, &hi) != 2) continue;
+            if (hi + (64ul << 20) >= a && lo <= a + (64ul << 20)) {
+                if (prev[0]) (void) !write(2, prev, strlen(prev));
+                prev[0] = 0;
+                (void) !write(2, buf, strlen(buf));
+            } else if (lo > a) {
+                break;
+            } else {
+                snprintf(prev, sizeof(prev), "%s", buf);
+            }
+        }
+        fclose(f);
+    }
     signal(sig, SIG_DFL);
     raise(sig);
 }
 static int owk_install_crash_handler = [] {
     const char * e = getenv("OWK_BACKTRACE");
     if (e && e[0] == '1') {
-        signal(SIGSEGV, owk_crash_handler);
-        signal(SIGABRT, owk_crash_handler);
+        struct sigaction sa{};
+        sa.sa_sigaction = owk_crash_handler;
+        sa.sa_flags = SA_SIGINFO;
+        sigaction(SIGSEGV, &sa, nullptr);
+        sigaction(SIGABRT, &sa, nullptr);
+        sigaction(SIGBUS, &sa, nullptr);
     }
     return 0;
 }();

@@ -36,7 +36,7 @@ _cache: dict[str, C.CDLL] = {}
 
 
 def load(path: str | None = None) -> C.CDLL:
-    path = os.path.abspath(path or LIB)
+    path = os.path.abspath(path or os.environ.get("OWK_SF_LIB", LIB))
     if path in _cache:
         return _cache[path]
     if not os.path.exists(path):

@@ -19,7 +19,11 @@ tests/golden/sf_test60.wav = the first 60 s of the reference's streaming-sortfor
     tokens (Swift WordTiming per token: token text, t0/100, t1/100, p; WhisperContext.swift:126-139)
     and the parsed reference RTTM: words with speakers and utterances.
 
-Usage (container with /root/reference; ~5 min on 8 cores):  python tests/golden/make_golden_c4.py
+Usage (container with /root/reference):
+    python tests/golden/make_golden_c4.py              -> c4_golden.*      (60 s, ~15 min on 8 cores)
+    python tests/golden/make_golden_c4.py --minutes 10 -> c4_10m_golden.*  (round 5: the 10 minutes BASELINE
+        configs[4] states, on tools/pipeline_bench.py's own clip owk_synth.synth_audio(600 s, seed 5); about
+        20 windows with prompt carry and the AOSC speaker cache well past its first minute)
 """
 import ctypes as C
 import json
@@ -96,10 +100,20 @@ def words_of(L, ctx, segs):
     return out
 
 
+def workload(minutes):
+    """(audio, fixture name) of a configs[4] fixture: the 60 s of real speech, or the bench's synthetic clip"""
+    if minutes == 1:
+        return S.read_wav_16k_mono(os.path.join(OUT, "sf_test60.wav")), "c4_golden"
+    return S.synth_audio(int(minutes * 60 * 16000), 5), f"c4_{minutes}m_golden"
+
+
 def main():
+    minutes = int(sys.argv[sys.argv.index("--minutes") + 1]) if "--minutes" in sys.argv else 1
     cache = os.environ.get("OWK_MODEL_CACHE", "/tmp/owk_models")
-    pcm = S.read_wav_16k_mono(os.path.join(OUT, "sf_test60.wav"))
-    meta = {"seed": SEED, "aheads_preset": AHEADS_LARGE_V3, "params": PARAMS, "block": BLOCK, "results": {}}
+    pcm, name = workload(minutes)
+    meta = {"seed": SEED, "aheads_preset": AHEADS_LARGE_V3, "params": PARAMS, "block": BLOCK, "results": {},
+            "minutes": minutes, "audio": "tests/golden/sf_test60.wav" if minutes == 1 else
+            f"owk_synth.synth_audio({minutes * 60 * 16000}, 5)"}
     arrays = {}
 
     # --- transcription + DTW ---
@@ -131,7 +145,7 @@ def main():
     # the next call), decoder-call prefixes traced with the logits untouched (record_topk = 2; the
     # other fixtures assert that tracing changes nothing, make_golden_nofa_windows.py)
     ref.close()
-    stage1 = os.path.join(cache, f"c4_stage1-{meta['model_sha256'][:16]}.json")  # the 15-min run, kept
+    stage1 = os.path.join(cache, f"c4_stage1-{meta['model_sha256'][:16]}" + ("" if minutes == 1 else f"-{minutes}m") + ".json")  # the 15-min run, kept
     if os.path.exists(stage1):
         st1 = json.load(open(stage1))
     else:
@@ -182,10 +196,10 @@ def main():
                                   "text": al["text"]}
     print("aligned", len(words), "words,", len(al["segments"]), "utterances", flush=True)
 
-    np.savez_compressed(os.path.join(OUT, "c4_golden.npz"), **arrays)
-    with open(os.path.join(OUT, "c4_golden.json"), "w") as f:
+    np.savez_compressed(os.path.join(OUT, name + ".npz"), **arrays)
+    with open(os.path.join(OUT, name + ".json"), "w") as f:
         json.dump(meta, f, indent=0)
-    print("wrote c4_golden.json / .npz")
+    print(f"wrote {name}.json / .npz")
 
 
 if __name__ == "__main__":

@@ -8,7 +8,9 @@ under results/"tdtw_floor": the tokens compared (the identical-token prefix of t
 many t_dtw differ and by how much -- tests/test_gpu_c4.py bounds the GPU's differences by it.
 
 Usage (container with /root/reference; ~15 min per seed on 8 cores):
-    python tests/golden/make_golden_c4_floor.py [seed ...]      (default: seed 0)
+    python tests/golden/make_golden_c4_floor.py [--minutes 10] [seed ...]      (default: seed 0)
+(--minutes 10: the 10-minute fixture c4_10m_golden.json of make_golden_c4.py --minutes 10; the perturbed run
+is cached under OWK_MODEL_CACHE, so it may run beside make_golden_c4.py and be compared afterwards)
 Seed 0 writes results/"tdtw_floor"; every seed's summary goes to results/"tdtw_floor_seeds" (the
 union of decisions a 1e-7 perturbation flips).
 """
@@ -25,17 +27,19 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "open-whisper-kit_amd", "python"))
 import owk_synth as S  # noqa: E402
 import ref_oracle as R  # noqa: E402
-from make_golden_c4 import AHEADS_LARGE_V3, NT, OUT, PARAMS  # noqa: E402
+from make_golden_c4 import AHEADS_LARGE_V3, NT, OUT, PARAMS, workload  # noqa: E402
 from make_golden_large import SEED  # noqa: E402
 
+MINUTES = int(sys.argv[sys.argv.index("--minutes") + 1]) if "--minutes" in sys.argv else 1
 
-def run(seed):
-    path_json = os.path.join(OUT, "c4_golden.json")
-    meta = json.load(open(path_json))
+
+def perturbed_run(seed, name):
     cache = os.environ.get("OWK_MODEL_CACHE", "/tmp/owk_models")
     path = S.ensure_model("large-v3", SEED, cache)
-    assert S.file_sha256(path) == meta["model_sha256"]
-    pcm = S.read_wav_16k_mono(os.path.join(OUT, "sf_test60.wav"))
+    keep = os.path.join(cache, f"{name}_floor_seed{seed}-{S.file_sha256(path)[:16]}.json")
+    if os.path.exists(keep):
+        return json.load(open(keep))["segments"]
+    pcm, _ = workload(MINUTES)
     rng = np.random.default_rng(seed)
     pp = (pcm * (1 + 1e-7 * rng.standard_normal(len(pcm)))).astype(np.float32)
     ref = R.Ref(path, flash_attn=False, dtw_preset=AHEADS_LARGE_V3)
@@ -43,6 +47,15 @@ def run(seed):
     ret, segs = ref.full(pp, n_threads=NT, **PARAMS)
     ref.close()
     print("perturbed whisper_full", ret, f"{time.time() - t:.0f} s", flush=True)
+    with open(keep, "w") as f:
+        json.dump({"ret": ret, "segments": segs}, f)
+    return segs
+
+
+def run(seed):
+    _, name = workload(MINUTES)
+    segs = perturbed_run(seed, name)
+    meta = json.load(open(os.path.join(OUT, name + ".json")))
     want = [tk for s in meta["results"]["full"]["segments"] for tk in s["tokens"]]
     got = [tk for s in segs for tk in s["tokens"]]
     n = 0
@@ -58,9 +71,13 @@ def run(seed):
 
 
 def main():
-    seeds = [int(a) for a in sys.argv[1:]] or [0]
+    args = sys.argv[1:]
+    if "--minutes" in args:
+        i = args.index("--minutes")
+        args = args[:i] + args[i + 2:]
+    seeds = [int(a) for a in args] or [0]
     recs = [run(sd) for sd in seeds]
-    path_json = os.path.join(OUT, "c4_golden.json")
+    path_json = os.path.join(OUT, workload(MINUTES)[1] + ".json")
     meta = json.load(open(path_json))  # re-read: several of these may run side by side
     for rec in recs:
         if rec["seed"] == 0:
