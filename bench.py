@@ -128,14 +128,20 @@ def rocprof_class_us(cls, path):
     return sum(tot) if tot else None
 
 
-def dominant_class(classes, model):
-    """The class with the largest device time by the committed rocprofv3 stats of this command (kernel
-    timestamps, no per-launch event overhead), else by the HIP-event table."""
+def rocprof_dominant(classes, model):
+    """The class with the largest device time in the committed rocprofv3 stats of this command (kernel
+    timestamps of an earlier run of the tree), or None: a cross-check only."""
     stats_path, _ = profile_files(model)
     tot = {c: rocprof_class_us(c, stats_path) for c in classes} if stats_path else {}
     tot = {c: v for c, v in tot.items() if v}
-    if tot:
-        return max(tot, key=tot.get)
+    return max(tot, key=tot.get) if tot else None
+
+
+def dominant_class(classes, alone=None):
+    """The class with the largest device time in THIS run: by the per-class steps where only that class's
+    dispatches carry events (`alone`, kernel start/stop timestamps), else by the all-class event table."""
+    if alone:
+        return max(alone, key=lambda c: alone[c]["ms"])
     return max(classes, key=lambda c: classes[c]["ms"]) if classes else None
 
 
@@ -342,11 +348,11 @@ class GpuRunner:
 
 
 def roofline(classes, ms_per_step, alone=None, model="large-v3"):
-    """`roofline` of the class with the largest device time (dominant_class: by the committed rocprof
-    stats when present); `alone` = {class: record} of the classes each timed in a step where only its
-    launches carry events (preferred when it holds the dominant class)."""
+    """`roofline` of the class with the largest device time in this run (dominant_class over `alone` =
+    {class: record} of the classes each timed in a step where only its launches carry events); the
+    committed rocprof stats of this command only cross-check it (rocprof_dominant, events_vs_rocprof)."""
     stats_path, pmc_path = profile_files(model)
-    dom = dominant_class(classes, model)
+    dom = dominant_class(classes, alone)
     src = alone if alone and dom in alone else classes
     d = src[dom]
     avg_ms = d["ms"] / max(1, d["launches"])
@@ -374,6 +380,11 @@ def roofline(classes, ms_per_step, alone=None, model="large-v3"):
     roof["rocprof_avg_launch_ms"] = rp
     roof["rocprof_stats"] = os.path.relpath(stats_path, ROOT) if rp is not None else None
     roof["events_vs_rocprof"] = round(avg_ms / rp, 4) if rp else None
+    rd = rocprof_dominant(classes, model)
+    roof["rocprof_dominant_class"] = rd
+    if rd is not None and rd != dom:
+        log(f"[bench] WARNING: the committed rocprof stats ({roof['rocprof_stats'] or stats_path}) name {rd} dominant, "
+            f"this run {dom}: the profile is stale for this tree")
     roof["phases"] = phase_fractions(classes, ms_per_step)
     return roof
 
@@ -423,9 +434,9 @@ def main(argv=None, runner=None):
     classes = run.profile() if not args.no_prof else {}
     if classes:
         top = sorted(classes, key=lambda c: -classes[c]["ms"])[:TOP_CLASSES]
-        dom = dominant_class(classes, args.model)
-        if dom and dom not in top:
-            top.append(dom)
+        rd = rocprof_dominant(classes, args.model)  # also time the committed profile's dominant class
+        if rd and rd not in top:
+            top.append(rd)
         alone = {}
         for c in top:
             got = run.profile([c])

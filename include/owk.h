@@ -71,6 +71,14 @@ WHISPER_API const uint16_t * owk_debug_gelu_table(void);
  * its header, mel filters and vocabulary are read). Returns the token count (written to out when
  * it fits cap), -count when it does not, INT32_MIN when the file cannot be parsed. */
 WHISPER_API int owk_debug_tokenize(const char * path_model, const char * text, int * out, int cap);
+/* test hook (host only): the self-attention KV-cell allocator (csrc/kv_cells.h, the reference's
+ * whisper_kv_cache_find_slot / _seq_rm / _seq_cp / _cell_max, ref whisper.cpp:1019-1137) driven by a
+ * script of n_ops records of 5 ints (op, a, b, c, d) on n_ctx cells:
+ *   0 find_slot of a tokens at positions c .. c + a - 1 of sequence b (result: first cell or -1)
+ *   1 seq_rm(seq a, p0 b, p1 c)   2 seq_cp(src a, dst b, p0 c, p1 d)   3 cell_max (result)   4 clear
+ * out: the n_ops results, the head, then (pos, sequence bitmask) per cell. Returns the ints written
+ * (n_ops + 1 + 2 n_ctx), -1 if cap is too small, -2 on an invalid record. */
+WHISPER_API int owk_debug_kv_cells(int n_ctx, const int * ops, int n_ops, int * out, int cap);
 /* out[M][N] = A[M][K] . W[N][K]^T (f16 bits in, f32 out) through the engine's GEMM dispatch */
 WHISPER_API int owk_debug_gemm(int device, int M, int N, int K, const uint16_t * a, const uint16_t * w, float * out);
 // one large-tile epilogue mode through the 128x128 and 256x256 kernels on the same random operands: max |diff|

@@ -624,6 +624,13 @@ void Engine::decode(const std::vector<DecodeRow> & rows, const std::vector<int> 
         (x.mode_cross == 2 ? sh.cross_sm : x.mode_cross ? sh.cross_tl : sh.cross_oc) = true;
         if (x.logit_row >= 0) lsel[x.logit_row] = r;
     }
+    {
+        std::vector<int> slots;
+        slots.reserve(R);
+        for (const auto & x : rows) slots.push_back(x.slot);
+        std::sort(slots.begin(), slots.end());
+        sh.n_clips = (int) (std::unique(slots.begin(), slots.end()) - slots.begin());
+    }
     if (m->kq && qf_k_repacked(m->qfmt)) {
         // each clip's rows of this pass are one reference decode batch (its decoders' tokens, or a
         // prompt): the rows of its complete groups of 4 take the repack quantizer
@@ -640,9 +647,12 @@ void Engine::decode(const std::vector<DecodeRow> & rows, const std::vector<int> 
     if (sh.self_oc && sh.max_keys > attn_max_listed_keys()) throw std::runtime_error("decode: too many self-attention keys");
     if (sh.self_tl && sh.max_keys > attn_max_tiled_keys()) throw std::runtime_error("decode: too many self-attention keys");
 
-    if (sh.cross_sm && sm_ws_.bytes < attn_softmax_ws_floats(dec_rows_cap_, hp.n_text_head) * 4) {
-        sync();  // soft_max rows: the key-split attention workspace for the row capacity
-        sm_ws_.alloc(attn_softmax_ws_floats(dec_rows_cap_, hp.n_text_head) * 4);
+    // soft_max cross rows take the key-split attention only in passes of <= 128 (row, head) blocks
+    // (attn_decoder_softmax): its workspace (~0.8 MB per large-v3 row) is sized for those passes only
+    const int sm_rows = std::max(1, 128 / hp.n_text_head);
+    if (sh.cross_sm && R * hp.n_text_head <= 128 && sm_ws_.bytes < attn_softmax_ws_floats(sm_rows, hp.n_text_head) * 4) {
+        sync();
+        sm_ws_.alloc(attn_softmax_ws_floats(sm_rows, hp.n_text_head) * 4);
         OWK_HIP_CHECK(hipMemsetAsync(sm_ws_.ptr, 0, sm_ws_.bytes, stream));  // arrival tickets start at 0
     }
     if (capture) {
@@ -816,7 +826,7 @@ void Engine::launch_decode(const DecShape & sh) {
             G("cq", EPI_F16, d, d, d_xn_.as<_Float16>(), nullptr, L.cw_q, L.t_cq, L.q_cq, ep, R, true);
         }
         {
-            ProfScope ps(prof, stream, "attn_cross", 4.0 * R * (double) n_ctx_pad * d, 2.0 * 2.0 * R * (double) T * d);
+            ProfScope ps(prof, stream, "attn_cross", 4.0 * R * (double) n_ctx_pad * d, 2.0 * 2.0 * sh.n_clips * (double) T * d);
             cross_attn(l, d_q_.as<_Float16>(), d_ao_.as<_Float16>(), fq_cross ? nullptr : ao32, fq_cross ? q8a() : nullptr,
                        fq_cross ? q8d() : nullptr);
         }
@@ -877,7 +887,7 @@ void Engine::launch_decode(const DecShape & sh) {
         }
         {
             // bytes: cross K and V of each row's clip (the HBM-bound part of a decode step)
-            ProfScope ps(prof, stream, "attn_cross", 4.0 * R * (double) n_ctx_pad * d, 2.0 * 2.0 * R * (double) T * d);
+            ProfScope ps(prof, stream, "attn_cross", 4.0 * R * (double) n_ctx_pad * d, 2.0 * 2.0 * sh.n_clips * (double) T * d);
             cross_attn(l, d_q_.as<_Float16>(), d_ao_.as<_Float16>(), fq_cross ? nullptr : ao32, fq_cross ? q8a() : nullptr,
                        fq_cross ? q8d() : nullptr);
             if (sh.cross_sm)  // soft_max_ext(KQ, nullptr, KQscale) over n_audio_ctx keys (whisper.cpp:2697-2738)
@@ -935,8 +945,9 @@ void Engine::fused_part(const DecShape & sh, int r0, int n, hipStream_t s, const
     const size_t self_stride = (size_t) cap_slots * kv_cells * d;
     const size_t cross_stride = (size_t) cap_slots * hp.n_audio_ctx * d;
     const size_t sm_off = attn_softmax_ws_floats(r0, H);
-    float * smw = sm_ws_.ptr ? sm_ws_.as<float>() + sm_off : nullptr;
-    const size_t smw_floats = sm_ws_.ptr ? sm_ws_.bytes / 4 - sm_off : 0;
+    const bool smw_ok = sm_ws_.ptr && sm_off < sm_ws_.bytes / 4;
+    float * smw = smw_ok ? sm_ws_.as<float>() + sm_off : nullptr;
+    const size_t smw_floats = smw_ok ? sm_ws_.bytes / 4 - sm_off : 0;
     // row-relative operands of the matmuls / LayerNorms; attention reads q and writes its output at
     // the absolute rows (AttnRow.q_row) of the pass buffers
     float * x = d_x_.as<float>() + (size_t) r0 * d;
@@ -1024,7 +1035,7 @@ void Engine::fused_part(const DecShape & sh, int r0, int n, hipStream_t s, const
             consumer(EPI_F16, d, L.cross_ln_w, L.cross_ln_b, L.t_cq, ep, 0);
         }
         {
-            ProfScope ps(prof, s, "attn_cross", 4.0 * n * (double) n_ctx_pad * d, 2.0 * 2.0 * n * (double) T * d);
+            ProfScope ps(prof, s, "attn_cross", 4.0 * n * (double) n_ctx_pad * d, 2.0 * 2.0 * sh.n_clips * (double) T * d);
             attn_decoder(s, q_abs, d, Kc, Vc, 64, T * 64, d_rc, n, nullptr, H, kq_scale, T, ao_abs, d, sh.cross_oc,
                          sh.cross_tl, nullptr, true, nullptr, nullptr);
             if (sh.cross_sm)  // soft_max_ext over n_audio_ctx keys (key-split), DTW capture of the alignment heads

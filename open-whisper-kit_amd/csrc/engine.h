@@ -79,6 +79,8 @@ struct DecShape {
     bool self_sm = false, cross_sm = false;     // soft_max rows (flash_attn = false contexts)
     bool capture = false;                       // DTW: capture alignment-head cross-attention
     bool self_list = false;                     // a one_chunk self row whose cells are not one run
+    int n_clips = 0;                            // distinct clips (cross K/V slots) among the rows: the
+                                                // cross K/V a pass must read is per clip, not per row
 };
 
 // per-step bookkeeping of the emulated reference state->logits buffer (no-speech prob)

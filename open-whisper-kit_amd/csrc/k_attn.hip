@@ -785,19 +785,51 @@ __global__ __launch_bounds__(NT) void k_attn_softmax(const _Float16 * __restrict
     // scores: their loads go out now, with the K rows, so the row pays one HBM round trip, not two
     const int tg = tid >> 3, seg = tid & 7;
     half8 vv0[GPT][U];
+    half8 k0[8];
+    {
+        // every cell index first (one round trip when the row has a cell list), then this thread's
+        // first K row and every V row: a list load between them made hipcc wait for all earlier
+        // loads before each one, and a K load issued behind the V rows waited for them
+        int kcell = max(0, min(tid, n - 1));
+        int cell[GPT][U];
 #pragma unroll
-    for (int j = 0; j < GPT; ++j)
+        for (int j = 0; j < GPT; ++j)
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int i = max(0, min(tg + TG * j + SM_PV_GROUPS * u, n - 1));
-            const int cell = list ? list[i] : i;
-            vv0[j][u] = *(const half8 *) (vh + (size_t) cell * ld_kv + seg * 8);
+            for (int u = 0; u < U; ++u) cell[j][u] = max(0, min(tg + TG * j + SM_PV_GROUPS * u, n - 1));
+        if (list) {
+            kcell = list[kcell];
+#pragma unroll
+            for (int j = 0; j < GPT; ++j)
+#pragma unroll
+                for (int u = 0; u < U; ++u) cell[j][u] = list[cell[j][u]];
         }
+#pragma unroll
+        for (int c = 0; c < 8; ++c) k0[c] = ((const half8 *) (kh + (size_t) kcell * ld_kv))[c];
+#pragma unroll
+        for (int j = 0; j < GPT; ++j)
+#pragma unroll
+            for (int u = 0; u < U; ++u) vv0[j][u] = *(const half8 *) (vh + (size_t) cell[j][u] * ld_kv + seg * 8);
+    }
 
-    // scores (lane = key; iterations unrolled so several keys' loads are in flight)
+    // scores (lane = key; the first key's K row is already loaded, later iterations unrolled so
+    // several keys' loads are in flight)
     float mx = -INFINITY;
+    if (tid < n) {
+        float part[8];
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+            const half8 qv = ((const half8 *) qr)[c];
+            float a = 0.0f;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) a = fmaf((float) k0[c][e], (float) qv[e], a);
+            part[c] = a;
+        }
+        const float s = (((part[0] + part[1]) + (part[2] + part[3])) + ((part[4] + part[5]) + (part[6] + part[7]))) * scale;
+        sp[tid] = s;
+        mx = s;
+    }
 #pragma unroll 3
-    for (int i = tid; i < n; i += NT) {
+    for (int i = tid + NT; i < n; i += NT) {
         const int cell = list ? list[i] : i;
         const half8 * kr = (const half8 *) (kh + (size_t) cell * ld_kv);
         float part[8];
@@ -851,19 +883,34 @@ __global__ __launch_bounds__(NT) void k_attn_softmax(const _Float16 * __restrict
     for (int i0 = 0; i0 < n; i0 += SM_PV_GROUPS * U) {
         half8 vv[GPT][U];
         float pp[GPT][U];
+        if (i0 == 0) {
+#pragma unroll
+            for (int j = 0; j < GPT; ++j)
+#pragma unroll
+                for (int u = 0; u < U; ++u) vv[j][u] = vv0[j][u];
+        } else {  // cell indices first, then the V rows (as the first iteration's prefetch)
+            int cell[GPT][U];
+#pragma unroll
+            for (int j = 0; j < GPT; ++j)
+#pragma unroll
+                for (int u = 0; u < U; ++u) cell[j][u] = min(i0 + tg + TG * j + SM_PV_GROUPS * u, n - 1);
+            if (list) {
+#pragma unroll
+                for (int j = 0; j < GPT; ++j)
+#pragma unroll
+                    for (int u = 0; u < U; ++u) cell[j][u] = list[cell[j][u]];
+            }
+#pragma unroll
+            for (int j = 0; j < GPT; ++j)
+#pragma unroll
+                for (int u = 0; u < U; ++u) vv[j][u] = *(const half8 *) (vh + (size_t) cell[j][u] * ld_kv + seg * 8);
+        }
 #pragma unroll
         for (int j = 0; j < GPT; ++j)
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 const int ii = i0 + tg + TG * j + SM_PV_GROUPS * u;
-                const int i = min(ii, n - 1);
-                if (i0 == 0) {
-                    vv[j][u] = vv0[j][u];
-                } else {
-                    const int cell = list ? list[i] : i;
-                    vv[j][u] = *(const half8 *) (vh + (size_t) cell * ld_kv + seg * 8);
-                }
-                pp[j][u] = ii < n ? (float) p16[i] : 0.0f;
+                pp[j][u] = ii < n ? (float) p16[min(ii, n - 1)] : 0.0f;
             }
 #pragma unroll
         for (int u = 0; u < U; ++u)
@@ -910,6 +957,7 @@ constexpr int SMS_PART = SM_MAX_KEYS + SMS_MAXC;       // group partials [SM_PV_
 constexpr int SMS_TICKET = SMS_PART + SM_PV_GROUPS * 64;  // the (row, head)'s arrival ticket (int)
 constexpr int SMS_PER_RH = SMS_TICKET + 16;
 static_assert(SMS_GPB * 8 == 128 && SMS_GPB * SMS_UMAX == 256, "P.V block thread layout");
+static_assert(SMS_MAXC <= 64, "one chunk maximum per lane");
 
 __global__ __launch_bounds__(SMS_CK) void k_sm_split_scores(const _Float16 * __restrict__ q, int ldq,
                                                             const _Float16 * __restrict__ kb, int ld_kv, int hs,
@@ -973,20 +1021,40 @@ __global__ __launch_bounds__(256) void k_sm_split_pv(const _Float16 * __restrict
     // P.V thread (tid < 128): residue group g of this block, head dims 8 seg .. +8, keys g + 128 u. Its V
     // rows go out first (they do not depend on the softmax): the HBM round trip overlaps the sum below
     const int gl = (tid >> 3) & (SMS_GPB - 1), seg = tid & 7, g = b * SMS_GPB + gl;
+    // cell indices first, then every V row with no branch between the loads: a list load or a guard
+    // between them made hipcc wait for every earlier load before each one (12 serial round trips at
+    // 1500 keys). Rows past the last chunk repeat the last key and threads 128.. repeat 0..127's rows
+    // (cache hits, never used).
     half8 vv[SMS_UMAX];
+    {
+        int cell[SMS_UMAX];
 #pragma unroll
-    for (int u = 0; u < SMS_UMAX; ++u) {
-        if (u < nc && tid < 128) {
-            const int k = max(0, min(g + SM_PV_GROUPS * u, n - 1));
-            const int cell = list ? list[k] : k;
-            vv[u] = *(const half8 *) (vh + (size_t) cell * ld_kv + seg * 8);
+        for (int u = 0; u < SMS_UMAX; ++u) cell[u] = max(0, min(g + SM_PV_GROUPS * u, n - 1));
+        if (list) {
+#pragma unroll
+            for (int u = 0; u < SMS_UMAX; ++u) cell[u] = list[cell[u]];
         }
+#pragma unroll
+        for (int u = 0; u < SMS_UMAX; ++u) vv[u] = *(const half8 *) (vh + (size_t) cell[u] * ld_kv + seg * 8);
     }
-    float mx = w[SM_MAX_KEYS];
-    for (int k = 1; k < nc; ++k) mx = fmaxf(mx, w[SM_MAX_KEYS + k]);
-    // k_attn_softmax's sum: thread t < 256 over keys t + 256 j, each exp as its (float) sp, then the trees
+    // this thread's stored scores, all loads in flight at once: the sum's keys tid + 256 j and the key
+    // whose probability it forms below
+    constexpr int SJ = SM_MAX_KEYS / 256;
+    float sv[SJ];
+#pragma unroll
+    for (int j = 0; j < SJ; ++j) sv[j] = tid + 256 * j < n ? w[tid + 256 * j] : 0.0f;
+    const int ip = b * SMS_GPB + (tid & (SMS_GPB - 1)) + SM_PV_GROUPS * (tid >> 4);
+    const float wp = ip < n ? w[ip] : 0.0f;
+    // the row maximum over the chunk maxima: one load per lane, then the (exact, order-free) max tree
+    float mx = lane < nc ? w[SM_MAX_KEYS + lane] : -INFINITY;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+    // k_attn_softmax's sum: thread t < 256 over keys t + 256 j in j order, each exp as its (float) sp,
+    // then the trees
     double sum = 0.0;
-    for (int i = tid; i < n; i += 256) sum += (double) expf(w[i] - mx);
+#pragma unroll
+    for (int j = 0; j < SJ; ++j)
+        if (tid + 256 * j < n) sum += (double) expf(sv[j] - mx);
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o, 64);
     if (lane == 0) redd[wave] = sum;
@@ -994,10 +1062,10 @@ __global__ __launch_bounds__(256) void k_sm_split_pv(const _Float16 * __restrict
     const float inv = (float) (1.0 / ((redd[0] + redd[1]) + (redd[2] + redd[3])));
     {  // the probabilities of this block's keys: thread (group tid & 15, key tid >> 4 of the group)
         const int a = amap ? amap[h] : -1;
-        const int i = b * SMS_GPB + (tid & (SMS_GPB - 1)) + SM_PV_GROUPS * (tid >> 4);
+        const int i = ip;
         float p = 0.0f;
         if (i < n) {
-            p = expf(w[i] - mx) * inv;
+            p = expf(wp - mx) * inv;
             if (a >= 0) cap[((size_t) a * n + i) * cap_rows + job.q_row] = p;
         }
         p16[tid & (SMS_GPB - 1)][tid >> 4] = p_f16(p);

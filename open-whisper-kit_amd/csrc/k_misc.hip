@@ -18,6 +18,7 @@ namespace owk {
 constexpr int LN_V4 = 8;  // float4 per lane held in registers -> d <= 2048
 
 // LayerNorm of one row held in registers (lane owns float4 groups lane + 64 j)
+// o (optional, null: no f16 row), o32 (optional): the f16 / f32 output rows
 // yout (optional): the f32 output row kept in registers (what o32 receives; zeros past the row)
 __device__ __forceinline__ void ln_row_regs(const float4 (&xv)[LN_V4], int lane, int d, const float * __restrict__ w,
                                             const float * __restrict__ b, float eps, _Float16 * __restrict__ o,
@@ -59,7 +60,7 @@ __device__ __forceinline__ void ln_row_regs(const float4 (&xv)[LN_V4], int lane,
             y.w = (xv[j].w - mean) * scale * ww.w + bb.w;
             half4 h;
             h[0] = (_Float16) y.x; h[1] = (_Float16) y.y; h[2] = (_Float16) y.z; h[3] = (_Float16) y.w;
-            *(half4 *) (o + 4 * i) = h;
+            if (o) *(half4 *) (o + 4 * i) = h;
             if (o32) *(float4 *) (o32 + 4 * i) = y;
             if (yout) (*yout)[j] = y;
         }
@@ -143,8 +144,9 @@ void layernorm_f16(hipStream_t s, const float * x, int rows, int d, const float 
 }
 
 // two LayerNorms in a row (the SortFormer conformer: a layer's final norm, then the next layer's first):
-// y = LN1(x) -> out1 (f16) / out1_32 (f32, the new residual stream), then LN2(y) from the same f32
-// registers -> out2 (f16) / out2_32 -- exactly the two layernorm_f16 launches it replaces
+// y = LN1(x) -> out1 (f16, optional: null when nothing reads it) / out1_32 (f32, the new residual
+// stream), then LN2(y) from the same f32 registers -> out2 (f16) / out2_32 -- exactly the two
+// layernorm_f16 launches it replaces. out1 and out2 must not overlap (both __restrict__).
 __global__ __launch_bounds__(256) void k_layernorm2_f16(const float * __restrict__ x, int rows, int d,
                                                         const float * __restrict__ w1, const float * __restrict__ b1,
                                                         _Float16 * __restrict__ out1, float * __restrict__ out1_32,
@@ -162,14 +164,17 @@ __global__ __launch_bounds__(256) void k_layernorm2_f16(const float * __restrict
         const int i = lane + 64 * j;
         xv[j] = i < n4 ? xr[i] : float4{0.f, 0.f, 0.f, 0.f};
     }
-    ln_row_regs(xv, lane, d, w1, b1, eps, out1 + (size_t) row * d, out1_32 + (size_t) row * d, nullptr, nullptr, &yv);
+    ln_row_regs(xv, lane, d, w1, b1, eps, out1 ? out1 + (size_t) row * d : nullptr, out1_32 + (size_t) row * d, nullptr,
+                nullptr, &yv);
     ln_row_regs(yv, lane, d, w2, b2, eps, out2 + (size_t) row * d, out2_32 ? out2_32 + (size_t) row * d : nullptr);
 }
 
 void layernorm2_f16(hipStream_t s, const float * x, int rows, int d, const float * w1, const float * b1, _Float16 * out1,
                     float * out1_32, const float * w2, const float * b2, _Float16 * out2, float * out2_32, float eps) {
     if (rows <= 0) return;
-    if (d % 4 != 0 || d > 4 * 64 * LN_V4 || !out1 || !out1_32 || !out2) throw std::runtime_error("layernorm2_f16: unsupported");
+    if (d % 4 != 0 || d > 4 * 64 * LN_V4 || !out1_32 || !out2) throw std::runtime_error("layernorm2_f16: unsupported");
+    if (out1 && out1 < out2 + (size_t) rows * d && out2 < out1 + (size_t) rows * d)
+        throw std::runtime_error("layernorm2_f16: out1 and out2 overlap");
     OWK_LAUNCH(k_layernorm2_f16, dim3((rows + 3) / 4), dim3(256), 0, s, x, rows, d, w1, b1, out1, out1_32, w2, b2, out2,
                out2_32, eps);
 }

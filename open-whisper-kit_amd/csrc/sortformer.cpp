@@ -745,7 +745,8 @@ float * run_conformer(sortformer_context * ctx, float * x, const Segs & segs, in
         // runs in the same launch from the f32 rows in registers (bit-identical to two launches)
         if (il < last) {
             const ConfLayer & N = ctx->conf[il + 1];
-            layernorm2_f16(s, x, T, d, ctx->f(L.ln_out_w), ctx->f(L.ln_out_b), xn, y, ctx->f(N.ln_ff1_w),
+            // LN1's f16 row is read by nothing (the next layer takes the f32 y): not written
+            layernorm2_f16(s, x, T, d, ctx->f(L.ln_out_w), ctx->f(L.ln_out_b), nullptr, y, ctx->f(N.ln_ff1_w),
                            ctx->f(N.ln_ff1_b), xn, f32_for(ctx, N.ff1_up, ctx->s_xn32, (size_t) T * d), eps);
             ff1_done = true;
         } else {
@@ -857,7 +858,8 @@ void update_silence_profile(StreamState & st, const StreamConfig & cfg, const fl
             st.n_sil_frames++;
             const float w_old = (float) (st.n_sil_frames - 1) / (float) st.n_sil_frames;
             const float w_new = 1.0f / (float) st.n_sil_frames;
-            for (int k = 0; k < d; ++k) st.mean_sil_emb[k] = w_old * st.mean_sil_emb[k] + w_new * pop_embs[t * d + k];
+            // the reference as built (gcc contracts w_old * m + w_new * e into one fma on x86-64-v3/v4)
+            for (int k = 0; k < d; ++k) st.mean_sil_emb[k] = fmaf(w_old, st.mean_sil_emb[k], w_new * pop_embs[t * d + k]);
         }
     }
 }
@@ -1529,6 +1531,34 @@ int sortformer_stream_feed(struct sortformer_stream_state * sst, const float * a
         fprintf(stderr, "sortformer_stream_feed: %s\n", e.what());
         return -1;
     }
+}
+
+// host-only AOSC bookkeeping test hook (include/owk_sortformer.h): the silence-profile update of
+// popped FIFO frames, then the speaker-cache compression, exactly as the streaming feed runs them
+int owk_sortformer_debug_aosc(int d, int n_frames, const float * embs, const float * preds, const float * mean_sil,
+                              int n_sil, int n_pop, const float * pop_embs, const float * pop_preds, int spkcache_len,
+                              int sil_frames_per_spk, float * out_embs, float * out_preds, float * out_mean_sil) {
+    StreamConfig cfg;
+    cfg.spkcache_len = spkcache_len;
+    cfg.spkcache_sil_frames_per_spk = sil_frames_per_spk;
+    if (d <= 0 || n_frames < 0 || n_pop < 0 || n_sil < 0 || !mean_sil || !out_mean_sil || validate(cfg) != 0 ||
+        (n_frames > 0 && (!embs || !preds)) || (n_pop > 0 && (!pop_embs || !pop_preds)) ||
+        (n_frames > spkcache_len && (!out_embs || !out_preds)))
+        return -2;
+    StreamState st(d);
+    st.spkcache.assign(embs, embs + (size_t) n_frames * d);
+    st.spkcache_preds.assign(preds, preds + (size_t) n_frames * N_SPK);
+    st.spkcache_len = n_frames;
+    st.spkcache_preds_valid = true;
+    st.mean_sil_emb.assign(mean_sil, mean_sil + d);
+    st.n_sil_frames = n_sil;
+    if (n_pop > 0) update_silence_profile(st, cfg, pop_embs, pop_preds, n_pop, d);
+    std::copy(st.mean_sil_emb.begin(), st.mean_sil_emb.end(), out_mean_sil);
+    if (n_frames <= spkcache_len) return -1;
+    compress_spkcache(st, cfg, d);
+    std::copy(st.spkcache.begin(), st.spkcache.end(), out_embs);
+    std::copy(st.spkcache_preds.begin(), st.spkcache_preds.end(), out_preds);
+    return st.spkcache_len;
 }
 
 // Many live streams of one context fed together (owk.h): their chunks are processed in

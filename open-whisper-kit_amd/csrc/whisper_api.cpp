@@ -13,6 +13,7 @@
 #include <thread>
 
 #include "state.h"
+#include "kv_cells.h"
 #include "kquant.h"
 
 using namespace owk;
@@ -1133,6 +1134,47 @@ int owk_debug_cross(struct whisper_context * ctx, struct whisper_state * st, int
     const int n = st->eng->n_ctx() * ctx->model->hp.n_text_state;
     if (k && v) st->eng->download_cross(slot, layer, k, v);
     return n;
+}
+
+// host-only: the KV-cell allocator (kv_cells.h) driven by a script of find_slot / seq_rm / seq_cp /
+// cell_max / clear records (include/owk.h)
+int owk_debug_kv_cells(int n_ctx, const int * ops, int n_ops, int * out, int cap) {
+    if (n_ctx <= 0 || n_ops < 0 || (n_ops > 0 && !ops) || !out) return -2;
+    if (cap < n_ops + 1 + 2 * n_ctx) return -1;
+    KvCells kv;
+    kv.init((uint32_t) n_ctx);
+    std::vector<int32_t> tpos, tseq;
+    for (int i = 0; i < n_ops; ++i) {
+        const int * o = ops + 5 * i;
+        int r = 0;
+        switch (o[0]) {
+            case 0:
+                if (o[1] < 0 || o[2] < 0 || o[2] > 31) return -2;
+                tpos.resize(o[1]);
+                tseq.assign(o[1], o[2]);
+                for (int t = 0; t < o[1]; ++t) tpos[t] = o[3] + t;
+                r = kv.find_slot(o[1], tpos.data(), tseq.data());
+                break;
+            case 1:
+                if (o[1] > 31) return -2;
+                kv.seq_rm(o[1], o[2], o[3]);
+                break;
+            case 2:
+                if (o[1] < 0 || o[1] > 31 || o[2] < 0 || o[2] > 31) return -2;
+                kv.seq_cp(o[1], o[2], o[3], o[4]);
+                break;
+            case 3: r = kv.cell_max(); break;
+            case 4: kv.clear(); break;
+            default: return -2;
+        }
+        out[i] = r;
+    }
+    out[n_ops] = (int) kv.head;
+    for (int c = 0; c < n_ctx; ++c) {
+        out[n_ops + 1 + 2 * c] = kv.pos[c];
+        out[n_ops + 2 + 2 * c] = (int) kv.seq[c];
+    }
+    return n_ops + 1 + 2 * n_ctx;
 }
 
 // host-only: whisper_tokenize over the vocabulary of a model file (header, mel filters and vocab

@@ -296,6 +296,105 @@ int ref_tokenize(void * vctx, const char * text, int * out, int cap) {
 
 static int ref_full_impl(void * vctx, const float * pcm, int n, const ref_full_cfg * cfg, const ref_full_ext * ext);
 
+// ---------------------------------------------------------------------------------
+// Teacher forcing with the reference's OWN greedy pick recorded at every step (round 5).
+// ref_tf_set(tokens, off, n_windows, force): the per-window decoded token lists the next
+// ref_full / ref_full_ex follows (force = 0: record only, nothing forced). At each
+// logits_filter_callback (whisper.cpp:6254, inside whisper_process_logits) the callback
+//   1. applies the run's own filter callback (fixed-work EOT suppression, tdrz boost);
+//   2. runs the REST of the reference's whisper_process_logits and its greedy
+//      whisper_sample_token (whisper.cpp:6177-6445, 6460-6592) on a copy of the decoder --
+//      no restatement: the reference's own code decides what it would pick here;
+//   3. records (window, step, pick, logprob of the pick, logprob of the teacher token);
+//   4. forces the teacher token (its logit 40 above the finite maximum; <|endoftext|> after
+//      a window's last listed token), as tests/parity_util.Forcer does on the GPU.
+// Greedy at temperature 0 only (one decoder, no fallback; the callback has no temperature).
+static std::vector<int> g_tf_tok, g_tf_off, g_tf_rec;
+static std::vector<float> g_tf_lp;
+static int g_tf_window = -1;
+static bool g_tf_active = false, g_tf_force = true;
+static whisper_full_params g_tf_params;
+static whisper_logits_filter_callback g_tf_base = nullptr;
+
+void ref_tf_set(const int * tokens, const int * off, int n_windows, int force) {
+    g_tf_active = n_windows >= 0;
+    g_tf_force = force != 0;
+    g_tf_off.assign(off, off + std::max(n_windows, 0) + 1);
+    g_tf_tok.assign(tokens, tokens + (n_windows > 0 ? off[n_windows] : 0));
+}
+
+// recorded steps: returns their count; with non-null outputs rec[TF_NI n] = (window, step, pick,
+// teacher token or -1, decoder index, TF_NC candidate ids) and lp[TF_NF n] = (logprob of pick, logprob
+// of teacher, TF_NC candidate logits, timestamp log-mass, best text logit). The candidates are the
+// TF_NC largest text / <|endoftext|> logits at the callback point (before forcing); the timestamp
+// log-mass is the logsumexp of the timestamp logits the rest of whisper_process_logits leaves finite
+// and the best text logit the largest text logit the timestamp pairing rule leaves (whisper.cpp:
+// 6289-6357): the two sides of the timestamp rule, in logit units (same normaliser).
+static constexpr int TF_NC = 16, TF_NI = 5 + TF_NC, TF_NF = 4 + TF_NC;
+int ref_tf_get(int * rec, float * lp) {
+    const int n = (int) g_tf_rec.size() / TF_NI;
+    if (rec) std::copy(g_tf_rec.begin(), g_tf_rec.end(), rec);
+    if (lp) std::copy(g_tf_lp.begin(), g_tf_lp.end(), lp);
+    return n;
+}
+
+static void ref_tf_cb(struct whisper_context * ctx, struct whisper_state * state, const whisper_token_data * tokens,
+                      int n_tokens, float * logits, void * ud) {
+    if (g_tf_base) g_tf_base(ctx, state, tokens, n_tokens, logits, ud);
+    if (n_tokens == 0) ++g_tf_window;
+    const int w = g_tf_window;
+    const int n_win = (int) g_tf_off.size() - 1;
+    int teacher = -1;
+    if (w >= 0 && w < n_win) {
+        const int len = g_tf_off[w + 1] - g_tf_off[w];
+        teacher = n_tokens < len ? g_tf_tok[g_tf_off[w] + n_tokens] : (n_tokens == len ? whisper_token_eot(ctx) : -1);
+    }
+    int j = -1;
+    for (int i = 0; i < WHISPER_MAX_DECODERS; ++i)
+        if (state->decoders[i].logits.data() == logits) j = i;
+    const int n_vocab = whisper_n_vocab(ctx), eot = whisper_token_eot(ctx), beg = whisper_token_beg(ctx);
+    int pick = -1;
+    float lp_pick = -INFINITY, lp_teacher = -INFINITY, ts_lse = -INFINITY, text_max = -INFINITY;
+    if (j >= 0) {
+        whisper_decoder dec = state->decoders[j];
+        whisper_full_params p2 = g_tf_params;
+        p2.logits_filter_callback = g_tf_base;
+        whisper_process_logits(*ctx, *state, dec, p2, 0.0f);
+        const whisper_token_data td = whisper_sample_token(*ctx, dec, true);
+        pick = td.id;
+        lp_pick = dec.logprobs[pick];
+        if (teacher >= 0) lp_teacher = dec.logprobs[teacher];
+        // the timestamp rule's two sides in logits: timestamps the filters left finite
+        double mx = -INFINITY, acc = 0.0;
+        for (int i = beg; i < n_vocab; ++i) if (dec.logits[i] > -INFINITY) mx = std::max(mx, (double) logits[i]);
+        if (mx > -INFINITY) {
+            for (int i = beg; i < n_vocab; ++i) if (dec.logits[i] > -INFINITY) acc += exp((double) logits[i] - mx);
+            ts_lse = (float) (log(acc) + mx);
+        }
+        const bool last_ts = n_tokens > 0 && tokens[n_tokens - 1].id >= beg;
+        const bool pen_ts = n_tokens < 2 || tokens[n_tokens - 2].id >= beg;
+        if (!(last_ts && !pen_ts))
+            for (int i = 0; i < beg; ++i) text_max = std::max(text_max, logits[i]);
+    }
+    std::vector<int> cand;
+    for (int i = 0; i < beg; ++i) if (logits[i] > -INFINITY) cand.push_back(i);
+    const int nc = std::min<int>(TF_NC, (int) cand.size());
+    std::partial_sort(cand.begin(), cand.begin() + nc, cand.end(),
+                      [&](int a, int b) { return logits[a] > logits[b] || (logits[a] == logits[b] && a < b); });
+    g_tf_rec.insert(g_tf_rec.end(), {w, n_tokens, pick, teacher, j});
+    g_tf_lp.insert(g_tf_lp.end(), {lp_pick, lp_teacher});
+    for (int c = 0; c < TF_NC; ++c) {
+        g_tf_rec.push_back(c < nc ? cand[c] : -1);
+        g_tf_lp.push_back(c < nc ? logits[cand[c]] : -INFINITY);
+    }
+    g_tf_lp.insert(g_tf_lp.end(), {ts_lse, text_max});
+    (void) eot;
+    if (!g_tf_force || teacher < 0) return;
+    float mx = -INFINITY;
+    for (int i = 0; i < n_vocab; ++i) mx = std::max(mx, logits[i] > -INFINITY && logits[i] < INFINITY ? logits[i] : mx);
+    logits[teacher] = (mx > -INFINITY ? mx : 0.0f) + 40.0f;
+}
+
 int ref_full(void * vctx, const float * pcm, int n, const ref_full_cfg * cfg) {
     return ref_full_impl(vctx, pcm, n, cfg, nullptr);
 }
@@ -365,6 +464,13 @@ static int ref_full_impl(void * vctx, const float * pcm, int n, const ref_full_c
             p.abort_callback = ref_cb_abort;
             p.new_segment_callback = ref_cb_new_segment;
         }
+    }
+    g_tf_rec.clear(); g_tf_lp.clear();
+    g_tf_window = -1;
+    if (g_tf_active) {  // teacher forcing (ref_tf_set): chain the run's own filter callback
+        g_tf_base = p.logits_filter_callback;
+        p.logits_filter_callback = ref_tf_cb;
+        g_tf_params = p;
     }
     if (cfg->n_processors > 1) return whisper_full_parallel(ctx, p, pcm, n, cfg->n_processors);
     return whisper_full(ctx, p, pcm, n);
@@ -516,3 +622,61 @@ int ref_grammar_rejects(void * vctx, const char * gbnf, const char * root, const
 }
 
 } // extern "C"
+
+extern "C" {
+
+// ---------------------------------------------------------------------------------
+// The reference's self-attention KV-cell allocator driven by a script (round 5; pins
+// csrc/kv_cells.h, tests/test_sanitize_host.py): whisper_kv_cache_find_slot / _seq_rm /
+// _seq_cp / _cell_max (whisper.cpp:1019-1137) on a cache of n_ctx cells (no tensors).
+// ops: n_ops records of 5 ints (op, a, b, c, d):
+//   0 find_slot: a tokens at positions c .. c + a - 1, all of sequence b  -> result head or -1
+//   1 seq_rm(a, b, c)   2 seq_cp(a, b, c, d)   3 cell_max -> result   4 clear
+// out: n_ops results, then head, then per cell (pos, sequence bitmask of ids 0..31).
+int ref_kv_script(int n_ctx, const int * ops, int n_ops, int * out, int cap) {
+    if (cap < n_ops + 1 + 2 * n_ctx) return -1;
+    whisper_kv_cache cache;
+    cache.head = 0;
+    cache.size = n_ctx;
+    cache.cells.assign(n_ctx, whisper_kv_cell{});
+    for (int i = 0; i < n_ops; ++i) {
+        const int * o = ops + 5 * i;
+        int r = 0;
+        if (o[0] == 0) {
+            whisper_batch b = whisper_batch_init(o[1], 1);
+            b.n_tokens = o[1];
+            for (int t = 0; t < o[1]; ++t) {
+                b.pos[t] = o[3] + t;
+                b.n_seq_id[t] = 1;
+                b.seq_id[t][0] = o[2];
+            }
+            r = whisper_kv_cache_find_slot(cache, b) ? (int) cache.head : -1;
+            whisper_batch_free(b);
+        } else if (o[0] == 1) {
+            whisper_kv_cache_seq_rm(cache, o[1], o[2], o[3]);
+        } else if (o[0] == 2) {
+            whisper_kv_cache_seq_cp(cache, o[1], o[2], o[3], o[4]);
+        } else if (o[0] == 3) {
+            r = whisper_kv_cache_cell_max(cache);
+        } else if (o[0] == 4) {  // whisper_kv_cache_clear's cell reset (its ggml buffer clear: no tensors here)
+            for (int32_t c = 0; c < (int32_t) cache.size; ++c) {
+                cache.cells[c].pos = -1;
+                cache.cells[c].seq_id.clear();
+            }
+            cache.head = 0;
+        } else {
+            return -2;
+        }
+        out[i] = r;
+    }
+    out[n_ops] = (int) cache.head;
+    for (int c = 0; c < n_ctx; ++c) {
+        unsigned m = 0;
+        for (int s : cache.cells[c].seq_id) m |= 1u << s;
+        out[n_ops + 1 + 2 * c] = cache.cells[c].pos;
+        out[n_ops + 2 + 2 * c] = (int) m;
+    }
+    return n_ops + 1 + 2 * n_ctx;
+}
+
+}  // extern "C"

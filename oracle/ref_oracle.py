@@ -65,15 +65,19 @@ def available() -> bool:
     return os.path.exists(REF_LIB)
 
 
-_lib = None
+_libs = {}
+# the reference's other x86 SIMD builds (oracle/ref/Makefile `variants`): the same ggml CPU path on a host
+# without AVX-512 (x86-64-v3: AVX2 + F16C + FMA) or with SSE only (x86-64: the scalar / SSE kernels)
+VARIANTS = {"v4": REF_LIB, "v3": os.path.join(HERE, "_ref", "v3", "libwhisper_ref.so"),
+            "v1": os.path.join(HERE, "_ref", "v1", "libwhisper_ref.so")}
 
 
-def lib():
-    global _lib
-    if _lib is None:
-        if not available():
-            raise FileNotFoundError(f"reference oracle not built: {REF_LIB} (make -C oracle/ref)")
-        L = C.CDLL(REF_LIB)
+def lib(path=None):
+    path = path or REF_LIB
+    if path not in _libs:
+        if not os.path.exists(path):
+            raise FileNotFoundError(f"reference oracle not built: {path} (make -C oracle/ref)")
+        L = C.CDLL(path)
         vp, ip, fp = C.c_void_p, C.c_int, C.POINTER(C.c_float)
         L.ref_init.restype = vp
         L.ref_init.argtypes = [C.c_char_p, ip, ip]
@@ -101,6 +105,8 @@ def lib():
         L.whisper_full_get_segment_speaker_turn_next.argtypes = [vp, ip]
         L.ref_record_get.argtypes = [C.POINTER(ip), C.POINTER(ip), C.POINTER(ip), fp, C.POINTER(ip)]
         L.ref_timings.argtypes = [vp] + [C.POINTER(C.c_double)] * 6 + [C.POINTER(ip)]
+        L.ref_tf_set.argtypes = [C.POINTER(ip), C.POINTER(ip), ip, ip]
+        L.ref_tf_get.argtypes = [C.POINTER(ip), fp]
         L.whisper_full_n_segments.argtypes = [vp]
         L.whisper_full_get_segment_t0.restype = C.c_int64
         L.whisper_full_get_segment_t0.argtypes = [vp, ip]
@@ -116,8 +122,8 @@ def lib():
         L.whisper_n_vocab.argtypes = [vp]
         L.whisper_token_sot.argtypes = [vp]
         L.whisper_lang_auto_detect.argtypes = [vp, ip, ip, fp]
-        _lib = L
-    return _lib
+        _libs[path] = L
+    return _libs[path]
 
 
 def fptr(a):
@@ -125,8 +131,9 @@ def fptr(a):
 
 
 class Ref:
-    def __init__(self, model_path: str, flash_attn: bool = True, dtw_preset: int = 0, dtw_n_top: int = -1):
-        self.L = lib()
+    def __init__(self, model_path: str, flash_attn: bool = True, dtw_preset: int = 0, dtw_n_top: int = -1,
+                 lib_path: str | None = None):
+        self.L = lib(lib_path)
         self.ctx = self.L.ref_init_ex(model_path.encode(), 1 if flash_attn else 0, dtw_preset, dtw_n_top)
         if not self.ctx:
             raise RuntimeError("reference init failed")
@@ -209,6 +216,38 @@ class Ref:
         for i, s in enumerate(segs):
             s["speaker_turn_next"] = bool(self.L.whisper_full_get_segment_speaker_turn_next(self.ctx, i))
         return ret, segs, self.cb_log()
+
+    def tf_set(self, windows=None, force=True):
+        """Teacher forcing for the following full() / full_ex() calls (ref_probe.cpp ref_tf_set): the
+        per-window decoded token lists to force (None: off; [] with force=False: record only). Every
+        greedy step records the reference's own pick on the forced prefix (its whisper_process_logits +
+        whisper_sample_token on a copy of the decoder)."""
+        if windows is None:
+            self.L.ref_tf_set((C.c_int * 1)(0), (C.c_int * 1)(0), -1, 0)
+            return
+        flat = [t for w in windows for t in w]
+        off = np.cumsum([0] + [len(w) for w in windows]).astype(np.int32)
+        tok = np.asarray(flat + [0], np.int32)
+        P = lambda a: a.ctypes.data_as(C.POINTER(C.c_int))
+        self.L.ref_tf_set(P(tok), P(off), len(windows), int(force))
+
+    TF_NC = 16
+
+    def tf_steps(self):
+        """Steps of the last run (ref_probe.cpp ref_tf_get): dict of arrays -- window, step, pick, teacher
+        (-1: none), lp_pick, lp_teacher (the reference's final logprobs), cand [n][16] / cand_logit [n][16]
+        (the largest text / EOT logits at the callback point), ts_lse / text_max (the timestamp rule's two
+        sides in logits)."""
+        nc = self.TF_NC
+        n = self.L.ref_tf_get(None, None)
+        rec = np.zeros(max((5 + nc) * n, 1), np.int32)
+        lp = np.zeros(max((4 + nc) * n, 1), np.float32)
+        self.L.ref_tf_get(rec.ctypes.data_as(C.POINTER(C.c_int)), fptr(lp))
+        rec = rec[:(5 + nc) * n].reshape(n, 5 + nc)
+        lp = lp[:(4 + nc) * n].reshape(n, 4 + nc)
+        return {"window": rec[:, 0], "step": rec[:, 1], "pick": rec[:, 2], "teacher": rec[:, 3],
+                "lp_pick": lp[:, 0], "lp_teacher": lp[:, 1], "cand": rec[:, 5:], "cand_logit": lp[:, 2:2 + nc],
+                "ts_lse": lp[:, 2 + nc], "text_max": lp[:, 3 + nc]}
 
     def cb_log(self):
         n = self.L.ref_cb_log(None, 0)

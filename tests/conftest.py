@@ -56,3 +56,15 @@ def clips():
     import owk_synth as S
 
     return {"jfk": S.read_wav_16k_mono(os.path.join(GOLDEN, "jfk.wav")), "synth30": S.synth_audio(480000, 7)}
+
+
+@pytest.fixture(scope="session")
+def tf_golden():
+    """Teacher-forced reference decisions and per-step floors (tests/golden/make_golden_tf.py); None
+    before they are generated"""
+    path = os.path.join(GOLDEN, "tf_golden.json")
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        meta = json.load(f)
+    return meta, np.load(os.path.join(GOLDEN, "tf_golden.npz"))

@@ -165,6 +165,121 @@ class Forcer:
         lg[t] = (float(lg[fin].max()) if fin.any() else 0.0) + 40.0
 
 
+class StepForcer:
+    """logits_filter_callback of the decision check: teacher-forces the reference's decoded tokens
+    (tf_golden.json `windows`) at every global step <= `upto` and leaves every later step to the
+    decoder, recording the prefix each call sees -- so the decoder's own greedy pick at each step after
+    `upto` is read back from the next call (tokens[n_tokens - 1]) or from where its window ended.
+    Global step index: windows in order, a window contributing len(tokens) steps plus its
+    <|endoftext|> step (none for an open window, which ended at the step limit or on a timestamp
+    reaching the end of the audio). `watch`: the one state of a batch to force (None: every call)."""
+
+    def __init__(self, tf, eot, n_vocab, token_data_type, upto, watch=None):
+        self.windows, self.open_end = tf["windows"], tf["open_end"]
+        self.eot, self.n_vocab, self.upto, self.watch = eot, n_vocab, upto, watch
+        self.n_steps = [len(w) + (0 if o else 1) for w, o in zip(self.windows, self.open_end)]
+        self.start = np.concatenate([[0], np.cumsum(self.n_steps)]).astype(int).tolist()
+        self.seen = []  # per window: the decoder's picks at steps 0 .. calls - 2
+        self.window = -1
+        TD = C.POINTER(token_data_type)
+        proto = C.CFUNCTYPE(None, C.c_void_p, C.c_void_p, TD, C.c_int, C.POINTER(C.c_float), C.c_void_p)
+        self.cfunc = proto(self._cb)
+
+    def _cb(self, ctx, state, tokens, n_tokens, logits, user):
+        if self.watch is not None and state != self.watch:
+            return
+        if n_tokens == 0:
+            self.window += 1
+            self.seen.append([])
+        w = self.window
+        if n_tokens > 0:
+            self.seen[w].append(int(tokens[n_tokens - 1].id))
+        if w >= len(self.windows) or self.start[w] + n_tokens > self.upto:
+            return
+        win = self.windows[w]
+        if n_tokens > len(win) or (n_tokens == len(win) and self.open_end[w]):
+            return
+        t = win[n_tokens] if n_tokens < len(win) else self.eot
+        lg = np.ctypeslib.as_array(logits, shape=(self.n_vocab,))
+        fin = np.isfinite(lg)
+        lg[t] = (float(lg[fin].max()) if fin.any() else 0.0) + 40.0
+
+    def first_disagreement(self):
+        """(global step, decoder pick (-1: ended the window there), reference token) of the first step
+        after `upto` where the decoder's own pick is not the reference's; None if every step agrees"""
+        for w, picks in enumerate(self.seen):
+            if w >= len(self.windows):
+                return self.start[-1], -2, -1  # a window the reference never decoded
+            win = self.windows[w]
+            for k, p in enumerate(picks):
+                g = self.start[w] + k
+                t = win[k] if k < len(win) else self.eot
+                if g > self.upto and p != t:
+                    return g, p, t
+            if len(picks) + 1 < self.n_steps[w]:  # the window ended at step len(picks); the reference went on
+                g = self.start[w] + len(picks)
+                if g > self.upto:
+                    return g, -1, win[len(picks)]
+        if len(self.seen) < len(self.windows):
+            return self.start[len(self.seen)], -2, -1
+        return None
+
+
+def decision_check(run, tf, arr, key, eot, beg, n_vocab, token_data_type, want_segments, watch=None, max_iter=16,
+                   log=print):
+    """Every decode step of a greedy run compared with the reference's decision on the same prefix.
+
+    `run(cfunc)` runs the case's whisper_full with `cfunc` as logits_filter_callback and returns its
+    segments. Iteratively: force the reference's tokens up to the last disagreement found, leave the
+    rest to the decoder, find the next step whose greedy pick differs (StepForcer). Each disagreement
+    must be a step the reference does not decide itself (tests/golden/make_golden_tf.py): one of its own
+    realisations (its x86-64-v3 / baseline x86-64 builds, 1e-7 input perturbations) flips it, or its
+    own gap between the two choices is within 2x the largest movement of those logits across its
+    realisations at that step (the timestamp rule's margin when a timestamp is involved). The final run
+    (forced through the last disagreement, free after it) must give the reference's tokens. Returns
+    (steps compared, [(step, pick, reference, reason)])."""
+    upto, found = -1, []
+    for _ in range(max_iter):
+        f = StepForcer(tf, eot, n_vocab, token_data_type, upto, watch)
+        segs = run(f.cfunc)
+        d = f.first_disagreement()
+        if d is None:
+            break
+        assert d[1] != -2, f"{key}: the decoder's windows differ from the reference's at step {d[0]}"
+        found.append(d)
+        upto = d[0]
+    else:
+        raise AssertionError(f"{key}: more than {max_iter} disagreeing steps: {found}")
+    assert [t[0] for s in segs for t in s["tokens"]] == [t[0] for s in want_segments for t in s["tokens"]], \
+        f"{key}: the run forced through step {upto} does not end on the reference's tokens"
+    flips = {}
+    for name, r in tf["realisations"].items():
+        for g, _, _ in r["flips"]:
+            flips.setdefault(g, []).append(name)
+    cand, cval = arr[key + "/cand"], arr[key + "/cand_logit"]
+    floor, floor_ts, ts_margin = arr[key + "/floor"], arr[key + "/floor_ts"], arr[key + "/ts_margin"]
+    out = []
+    for g, p, t in found:
+        if g in flips:
+            out.append((g, p, t, f"reference self-flip ({', '.join(flips[g])})"))
+            continue
+        pp = eot if p == -1 else p
+        if pp >= beg or t >= beg:  # a timestamp on either side: the timestamp rule decided the step
+            gap, bound, what = abs(float(ts_margin[g])), 2.0 * float(floor_ts[g]), "timestamp-rule margin"
+        else:
+            ids = cand[g].tolist()
+            assert pp in ids and t in ids, f"{key} step {g}: pick {pp} / reference {t} not among the reference's candidates"
+            gap = float(cval[g][ids.index(t)] - cval[g][ids.index(pp)])
+            bound, what = 2.0 * float(floor[g]), "logit gap"
+        assert gap <= bound, (f"{key} step {g}: decoder picks {p}, reference {t}: the reference's {what} {gap:.3e} is "
+                              f"above 2x its own per-step floor {bound / 2:.3e} and no realisation of it flips the step")
+        out.append((g, p, t, f"{what} {gap:.2e} <= 2 x reference floor {bound / 2:.2e}"))
+    n = sum(StepForcer(tf, eot, n_vocab, token_data_type, -1).n_steps)
+    log(f"[decisions] {key}: {n}/{n} steps compared on the reference's prefixes, {len(out)} disagreement(s)"
+        + "".join(f"; step {g}: {p} vs {t} ({why})" for g, p, t, why in out))
+    return n, out
+
+
 def check_cross_rows(w, st, arr, key, layer, name, n_rows=16):
     """The engine's cross-attention K/V cache rows 0..n_rows-1 of `layer` (slot 0, [t][d] f16 via
     owk_debug_cross) against the reference's kv_cross rows (whisper_build_graph_cross,
@@ -213,3 +328,23 @@ def rttm_activity_diff(got_rttm, ref_rttm, ref_probs, floor_max, threshold=0.5, 
     for s in range(-(median // 2), median // 2 + 1):
         near_w |= np.roll(near, s, axis=0)
     return int((got_m != ref_m).sum()), (got_m != ref_m) & ~near_w
+
+
+def compare_all_steps(w, tf_golden, key, run, want_segments, n_cmp, watch=None, log=print):
+    """After a free-run comparison (compare_segments) that parted from the reference at a near-tie
+    (n_cmp < the reference's token count), compare every remaining step with decision_check on the
+    reference's prefixes; a parting without a teacher-forced fixture fails (its tail would be
+    unverified). Returns the steps compared (None when the free run already matched completely)."""
+    import owk
+
+    n_ref = sum(len(s["tokens"]) for s in want_segments)
+    if n_cmp >= n_ref:
+        return None
+    assert tf_golden is not None and key in tf_golden[0]["cases"], \
+        f"{key}: the free run parted at token {n_cmp} and no teacher-forced fixture covers the rest (make_golden_tf.py)"
+    meta, arr = tf_golden
+    L = w.L
+    L.whisper_token_beg.argtypes = [C.c_void_p]
+    n, _ = decision_check(run, meta["cases"][key], arr, key, L.whisper_token_eot(w.ctx), L.whisper_token_beg(w.ctx),
+                          w.n_vocab, owk.TokenData, want_segments, watch=watch, log=log)
+    return n

@@ -20,7 +20,7 @@ import numpy as np
 import pytest
 
 import owk
-from parity_util import LOGIT_RTOL, Forcer, LogitError, check_cross_rows, compare_segments
+from parity_util import LOGIT_RTOL, Forcer, LogitError, check_cross_rows, compare_all_steps, compare_segments
 
 pytestmark = pytest.mark.gpu
 
@@ -136,7 +136,7 @@ def _batch_clips(clips):
 
 @pytest.mark.parametrize("model", MODELS)
 @pytest.mark.parametrize("cfg", ["greedy", "fixed_work"])
-def test_large_batch32(large, clips, model, cfg):
+def test_large_batch32(large, tf_golden, clips, model, cfg):
     meta, arr = large
     owk.quiet()
     w = whisper(meta, model)
@@ -169,7 +169,15 @@ def test_large_batch32(large, clips, model, cfg):
                 compare_segments(got, want["segments"], f"{key}/{cfg}/slot{slot}", tie=fl, p_atol=fl, min_compared=0)
         else:
             tie = LogitError.tie(w, meta, arr, key, clips[clip])
-            compare_segments(got, want["segments"], f"{key}/{cfg}/slot{slot}", tie=tie)
+            n_cmp = compare_segments(got, want["segments"], f"{key}/{cfg}/slot{slot}", tie=tie)
+
+            def run(cfunc):  # the same 32-clip batch; the forcer acts on this slot's state only
+                p.logits_filter_callback = C.cast(cfunc, C.c_void_p)
+                r = w.full_batch(states, _batch_clips(clips), p, suppress_eot=cfg == "fixed_work")
+                p.logits_filter_callback = None
+                assert r == 0
+                return w.segments(states[slot])
+            compare_all_steps(w, tf_golden, f"large/{key}/full/{cfg}", run, want["segments"], n_cmp, watch=states[slot])
     for s in states:
         w.L.whisper_free_state(s)
     w._states = [s for s in w._states if s not in states]
@@ -177,7 +185,7 @@ def test_large_batch32(large, clips, model, cfg):
 
 @pytest.mark.parametrize("model", ["large-v3", "large-v3-turbo"])
 @pytest.mark.parametrize("clip", ["jfk", "synth30"])
-def test_large_dtw(large, clips, model, clip):
+def test_large_dtw(large, tf_golden, clips, model, clip):
     meta, arr = large
     owk.quiet()
     w = whisper(meta, model, nofa=True)
@@ -191,6 +199,14 @@ def test_large_dtw(large, clips, model, clip):
     r_ids = [t[0] for s in want["segments"] for t in s["tokens"]]
     n_same = next((i for i, (a, b) in enumerate(zip(g_ids, r_ids)) if a != b), min(len(g_ids), len(r_ids)))
     print(f"[large-dtw] {key}: free run {n_same}/{len(r_ids)} tokens identical")
+    if n_same < len(r_ids) and tf_golden is not None and f"large/{key}/full/greedy_dtw" in tf_golden[0]["cases"]:
+        def run(cfunc):  # every decode step on the reference's prefixes (parity_util.decision_check)
+            s2 = w.new_state()
+            p2 = w.params(0, language="en", temperature_inc=0.0, no_timestamps=want["no_timestamps"])
+            p2.logits_filter_callback = C.cast(cfunc, C.c_void_p)
+            assert w.full(s2, clips[clip], p2) == want["ret"]
+            return w.segments(s2)
+        compare_all_steps(w, tf_golden, f"large/{key}/full/greedy_dtw", run, want["segments"], n_same)
     windows = meta["results"].get(key + "/dtw_windows")
     if windows is not None:  # teacher-force the reference's per-window tokens, then compare t_dtw
         force = Forcer(windows, w.L.whisper_token_eot(w.ctx), w.n_vocab, owk.TokenData)

@@ -24,7 +24,7 @@ import numpy as np
 import pytest
 
 import owk
-from parity_util import LOGIT_RTOL, Forcer, LogitError
+from parity_util import compare_all_steps, LOGIT_RTOL, Forcer, LogitError
 from test_gpu_parity import _compare
 
 pytestmark = pytest.mark.gpu
@@ -87,7 +87,7 @@ def test_nofa_encoder_and_logits(nofa, model_path, clips, model, clip):
 
 @pytest.mark.parametrize("model", ["tiny.en", "tiny", "l3-mini"])
 @pytest.mark.parametrize("clip", ["jfk", "synth30"])
-def test_dtw_timestamps(nofa, model_path, clips, model, clip):
+def test_dtw_timestamps(nofa, tf_golden, model_path, clips, model, clip):
     meta, _ = nofa
     owk.quiet()
     w = whisper_nofa(model_path, meta, model)
@@ -96,7 +96,15 @@ def test_dtw_timestamps(nofa, model_path, clips, model, clip):
     p = w.params(0, language="en", temperature_inc=0.0, no_timestamps=want["no_timestamps"])
     assert w.full(st, clips[clip], p) == want["ret"]
     tie = LogitError.tie(w, meta, nofa[1], f"{model}/{clip}", clips[clip])
-    _compare(w.segments(st), want["segments"], f"{model}/{clip}/dtw", tie=tie)
+    n_cmp = _compare(w.segments(st), want["segments"], f"{model}/{clip}/dtw", tie=tie)
+
+    def run(cfunc):  # every step on the reference's prefixes (tests/parity_util.decision_check)
+        s2 = w.new_state()
+        p2 = w.params(0, language="en", temperature_inc=0.0, no_timestamps=want["no_timestamps"])
+        p2.logits_filter_callback = C.cast(cfunc, C.c_void_p)
+        assert w.full(s2, clips[clip], p2) == want["ret"]
+        return w.segments(s2)
+    compare_all_steps(w, tf_golden, f"nofa/{model}/{clip}/full/greedy_dtw", run, want["segments"], n_cmp)
     got = w.segments(st)
     g_ids = [t[0] for s in got for t in s["tokens"]]
     r_ids = [t[0] for s in want["segments"] for t in s["tokens"]]

@@ -18,7 +18,7 @@ import numpy as np
 import pytest
 
 import owk
-from parity_util import LOGIT_RTOL, MIN_COMPARED, LogitError, check_cross_rows, compare_segments
+from parity_util import LOGIT_RTOL, MIN_COMPARED, LogitError, check_cross_rows, compare_all_steps, compare_segments
 from recording import Injector
 
 pytestmark = pytest.mark.gpu
@@ -135,10 +135,14 @@ CONFIGS = {
     "fixed_work": dict(no_timestamps=True, max_tokens=40, suppress_eot=True, temperature_inc=0.0),
     "token_ts": dict(temperature_inc=0.0, token_timestamps=True),
     "sampled": dict(temperature=0.4, temperature_inc=0.0, best_of=5),
+    # whisper-cli's literal defaults (ref examples/cli/cli.cpp:44-54, 79, 1168-1212): beam search 5, best_of 5,
+    # the 0.2 temperature-fallback ladder; the golden windows fall back from beam to sampled best-of
+    # (tests/golden/make_golden_cli_default.py records the attempts)
+    "cli_default": dict(strategy=1, best_of=5, temperature=0.0, temperature_inc=0.2),
 }
 
 
-STOCHASTIC = ("greedy_fallback", "beam5", "sampled")  # see tests/golden/recording.py
+STOCHASTIC = ("greedy_fallback", "beam5", "sampled", "cli_default")  # see tests/golden/recording.py
 
 
 def _compare(got, want, key, exact=False, p_atol=None, tie=None, min_compared=MIN_COMPARED):
@@ -157,7 +161,7 @@ def _tie(w, golden, model, clip, clips):
 @pytest.mark.parametrize("model", MODELS)
 @pytest.mark.parametrize("clip", ["jfk", "synth30"])
 @pytest.mark.parametrize("cfg", list(CONFIGS))
-def test_whisper_full(lib, golden, model_path, clips, model, clip, cfg):
+def test_whisper_full(lib, golden, tf_golden, model_path, clips, model, clip, cfg):
     meta, arr = golden
     key = f"{model}/{clip}/full/{cfg}"
     if key not in meta["results"]:
@@ -183,7 +187,16 @@ def test_whisper_full(lib, golden, model_path, clips, model, clip, cfg):
         assert inj.calls > 0 and inj.misses == 0, (inj.calls, inj.misses)
         _compare(w.segments(st), want["segments"], key, exact=True, p_atol=1e-5)
     else:
-        _compare(w.segments(st), want["segments"], key, tie=_tie(w, golden, model, clip, clips))
+        n_cmp = _compare(w.segments(st), want["segments"], key, tie=_tie(w, golden, model, clip, clips))
+
+        def run(cfunc):  # the same call with a logits_filter_callback (tests/parity_util.StepForcer)
+            s2 = w.new_state()
+            p2, _ = _cfg_params(w, CONFIGS[cfg])
+            p2.logits_filter_callback = C.cast(cfunc, C.c_void_p)
+            r = w.full_batch([s2], [clips[clip]], p2, suppress_eot=True) if suppress_eot else w.full(s2, clips[clip], p2)
+            assert r == want["ret"]
+            return w.segments(s2)
+        compare_all_steps(w, tf_golden, key, run, want["segments"], n_cmp)
 
 
 def test_greedy_then_beam_on_one_state(lib, golden, model_path, clips):
@@ -224,7 +237,7 @@ def test_batch_matches_single(lib, golden, model_path, clips):
                  tie=_tie(w, golden, model, n, clips))
 
 
-def test_auto_language(lib, golden, model_path, clips):
+def test_auto_language(lib, golden, tf_golden, model_path, clips):
     meta, _ = golden
     for model in ("tiny", "l3-mini"):
         w = whisper(model_path, model)
@@ -232,8 +245,16 @@ def test_auto_language(lib, golden, model_path, clips):
         p = w.params(0, language="auto", temperature_inc=0.0)
         assert w.full(st, clips["jfk"], p) == 0
         assert lib.whisper_full_lang_id_from_state(st) == meta["results"][f"{model}/jfk/lang_detect"][0]
-        _compare(w.segments(st), meta["results"][f"{model}/jfk/full/auto_lang"]["segments"], f"{model}/auto",
-                 tie=_tie(w, golden, model, "jfk", clips))
+        want = meta["results"][f"{model}/jfk/full/auto_lang"]["segments"]
+        n_cmp = _compare(w.segments(st), want, f"{model}/auto", tie=_tie(w, golden, model, "jfk", clips))
+
+        def run(cfunc):
+            s2 = w.new_state()
+            p2 = w.params(0, language="auto", temperature_inc=0.0)
+            p2.logits_filter_callback = C.cast(cfunc, C.c_void_p)
+            assert w.full(s2, clips["jfk"], p2) == 0
+            return w.segments(s2)
+        compare_all_steps(w, tf_golden, f"{model}/jfk/full/auto_lang", run, want, n_cmp)
 
 
 def test_concurrent_states(lib, golden, model_path, clips):

@@ -18,4 +18,4 @@ export UBSAN_OPTIONS=halt_on_error=1:print_stacktrace=1
 cd "$ROOT"
 LD_PRELOAD=$RT python -m pytest -x -q -p no:cacheprovider -m "not gpu" "$@" \
     tests/test_tokenize.py tests/test_grammar.py tests/test_diarize_align.py tests/test_dtw_cpu.py \
-    tests/test_abi.py tests/test_kquant.py tests/test_vad.py tests/test_sortformer.py
+    tests/test_abi.py tests/test_kquant.py tests/test_vad.py tests/test_sortformer.py tests/test_sanitize_host.py
