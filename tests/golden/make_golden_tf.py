@@ -205,7 +205,7 @@ def main():
     audio = clips()
     only = sys.argv[2:] if len(sys.argv) > 2 else None
     for c in cases(which):
-        if c[0] in meta["cases"] or (only and not any(o in c[0] for o in only)):
+        if c[0] in meta["cases"] or (only and not any(c[0] == o or c[0].endswith("/" + o) for o in only)):
             continue
         rec, arr = run_case(*c, which, audio, cache, fixtures)
         meta["cases"][c[0]] = rec
