@@ -2206,9 +2206,23 @@ __global__ __launch_bounds__(GQ_MAXW * 64) void k_gemm_q5_rows(int M, int N, int
 #pragma unroll
         for (int i = 0; i < MT; ++i) acc[t][i] = accm[t][i] = floatx4{0.f, 0.f, 0.f, 0.f};
     const long ones = 0x0101010101010101L;
+    // every activation scale of this wave first: unconditional LDS reads (in-array indices; a value past
+    // the wave's K range is replaced by zero afterwards), so they go out together -- a guarded read per
+    // scale made hipcc branch and wait on each one
+    float drs[GQ_J][MT][4];
 #pragma unroll
     for (int j = 0; j < GQ_J; ++j) {
         const int kb = min(kb0 + j, nb - 1);
+#pragma unroll
+        for (int i = 0; i < MT; ++i)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int r = min(i * 16 + 4 * g + e, M - 1);
+                drs[j][i][e] = sda[min(r * nbl + (kb - kblo), GQ_MAX_SCALES - 1)];
+            }
+    }
+#pragma unroll
+    for (int j = 0; j < GQ_J; ++j) {
 #pragma unroll
         for (int i = 0; i < MT; ++i) {
             const intx4 z = {0, 0, 0, 0};
@@ -2216,10 +2230,7 @@ __global__ __launch_bounds__(GQ_MAXW * 64) void k_gemm_q5_rows(int M, int N, int
             if constexpr (HAS_M) is = __builtin_amdgcn_mfma_i32_16x16x32_i8(a[i][j], ones, z, 0, 0, 0);
             float dr[4];
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const int r = min(i * 16 + 4 * g + e, M - 1);
-                dr[e] = j < nj ? sda[r * nbl + (kb - kblo)] : 0.0f;  // past the wave's range: zeros
-            }
+            for (int e = 0; e < 4; ++e) dr[e] = j < nj ? drs[j][i][e] : 0.0f;  // past the wave's range: zeros
 #pragma unroll
             for (int t = 0; t < NT; ++t) {
                 const uint64_t v = unpack_group<FMT>(raw[t][j], qh[t][j], g);

@@ -28,6 +28,8 @@ Per case (oracle/ref/ref_probe.cpp ref_tf_set / ref_tf_get; oracle/ref_oracle.py
 Usage (container with /root/reference, after make -C oracle/ref all variants):
     python tests/golden/make_golden_tf.py            small models (golden.json + nofa_golden.json cases)
     python tests/golden/make_golden_tf.py large      large-v3 / large-v3-turbo (large_golden.json cases)
+    python tests/golden/make_golden_tf.py params     the SDK / CLI parameter cases (params_golden.json; whisper_full
+                                                      through ref_full_ext with the case's own parameters)
 Cases already in tf_golden.json are kept (delete an entry to regenerate it).
 """
 import ctypes as C
@@ -60,7 +62,13 @@ LARGE_CFG = {"greedy": dict(temperature_inc=0.0),
 
 
 def clips():
-    return {"jfk": S.read_wav_16k_mono(os.path.join(OUT, "jfk.wav")), "synth30": S.synth_audio(480000, 7)}
+    return {"jfk": S.read_wav_16k_mono(os.path.join(OUT, "jfk.wav")), "synth30": S.synth_audio(480000, 7),
+            "test60": S.read_wav_16k_mono(os.path.join(OUT, "sf_test60.wav"))}
+
+
+def params_ext(c):
+    """ref_full_ext fields of a params_golden.json case (bytes fields stored as hex)"""
+    return {k: (bytes.fromhex(v) if k in c["bytes_fields"] else v) for k, v in c["ext"].items()}
 
 
 def cases(which):
@@ -81,6 +89,10 @@ def cases(which):
                 out.append(("nofa/" + k, model, clip, dict(flash_attn=False, dtw_preset=preset, dtw_n_top=n_top),
                             dict(language="en", temperature_inc=0.0, no_timestamps=clip == "synth30"),
                             ("nofa_golden.json", k)))
+    elif which == "params":
+        pg = json.load(open(os.path.join(OUT, "params_golden.json")))
+        for name, c in sorted(pg["cases"].items()):
+            out.append(("params/" + name, c["model"], c["clip"], {}, dict(c["params"]), ("params_golden.json", name)))
     else:
         for model in ("large-v3", "large-v3-turbo"):
             for clip in ("jfk", "synth30"):
@@ -96,7 +108,7 @@ def cases(which):
 def realisations(which):
     """(name, library variant, perturbation seed or None)"""
     r = [("v4/p0", "v4", 0), ("v4/p1", "v4", 1), ("v3", "v3", None), ("v3/p0", "v3", 0)]
-    if which == "small":
+    if which in ("small", "params"):
         r.append(("v1", "v1", None))
     return r
 
@@ -139,7 +151,8 @@ def floors(base, steps):
 
 def run_case(key, model, clip, init_kw, full_kw, fixture, which, audio, cache, fixtures):
     meta = fixtures[fixture[0]]
-    want = meta["results"][fixture[1]]
+    want = meta["results"][fixture[1]] if fixture[0] != "params_golden.json" else meta["cases"][fixture[1]]
+    ext = params_ext(want) if fixture[0] == "params_golden.json" else None
     if full_kw is None:  # large DTW fixture: its own no_timestamps flag
         full_kw = dict(language="en", temperature_inc=0.0, no_timestamps=want["no_timestamps"])
     if model in MODELS:
@@ -150,18 +163,24 @@ def run_case(key, model, clip, init_kw, full_kw, fixture, which, audio, cache, f
         path = S.ensure_model(model, SEED, cache)
     pcm = audio[clip]
     kw = dict(n_threads=NT, **full_kw)
+
+    def full(r, x):
+        return r.full(x, **kw) if ext is None else r.full_ex(x, ext, **kw)[:2]
     t0 = time.time()
     ref = R.Ref(path, **init_kw)
     ref.L.whisper_token_eot.argtypes = [C.c_void_p]
     eot = ref.L.whisper_token_eot(ref.ctx)
     ref.tf_set([], force=False)
-    ret, segs = ref.full(pcm, **kw)
+    ret, segs = full(ref, pcm)
     assert ret == want["ret"]
     flat = [t[0] for s in segs for t in s["tokens"]]
     assert flat == [t[0] for s in want["segments"] for t in s["tokens"]], f"{key}: the recorded run is not the fixture's"
     windows, open_end = windows_of(ref.tf_steps(), eot)
+    ref.tf_set(None)
+    ref.close()  # a fresh context: no_context = false carries a state's prompt history into its next call
+    ref = R.Ref(path, **init_kw)
     ref.tf_set(windows, force=True)
-    ret, segs = ref.full(pcm, **kw)
+    ret, segs = full(ref, pcm)
     base = ref.tf_steps()
     assert [t[0] for s in segs for t in s["tokens"]] == flat, f"{key}: teacher-forced run left the tokens"
     assert (base["pick"] == base["teacher"]).all(), f"{key}: the reference's own pick differs from its forced token"
@@ -177,7 +196,7 @@ def run_case(key, model, clip, init_kw, full_kw, fixture, which, audio, cache, f
         x = pcm if seed is None else (pcm * (1 + 1e-7 * np.random.default_rng(seed).standard_normal(len(pcm)))).astype(np.float32)
         r = R.Ref(path, lib_path=R.VARIANTS[var], **init_kw)
         r.tf_set(windows, force=True)
-        r.full(x, **kw)
+        full(r, x)
         st = r.tf_steps()
         r.tf_set(None)
         r.close()
@@ -196,12 +215,13 @@ def run_case(key, model, clip, init_kw, full_kw, fixture, which, audio, cache, f
 
 
 def main():
-    which = "large" if len(sys.argv) > 1 and sys.argv[1] == "large" else "small"
+    which = sys.argv[1] if len(sys.argv) > 1 and sys.argv[1] in ("large", "params") else "small"
     cache = os.environ.get("OWK_MODEL_CACHE", "/tmp/owk_models")
     path_json, path_npz = os.path.join(OUT, "tf_golden.json"), os.path.join(OUT, "tf_golden.npz")
     meta = json.load(open(path_json)) if os.path.exists(path_json) else {"seed": SEED, "cases": {}}
     arrays = dict(np.load(path_npz)) if os.path.exists(path_npz) else {}
-    fixtures = {f: json.load(open(os.path.join(OUT, f))) for f in ("golden.json", "nofa_golden.json", "large_golden.json")}
+    fixtures = {f: json.load(open(os.path.join(OUT, f)))
+                for f in ("golden.json", "nofa_golden.json", "large_golden.json", "params_golden.json")}
     audio = clips()
     only = sys.argv[2:] if len(sys.argv) > 2 else None
     for c in cases(which):

@@ -22,7 +22,7 @@ import numpy as np
 import pytest
 
 import owk
-from parity_util import LogitError, compare_segments
+from parity_util import compare_all_steps, LogitError, compare_segments
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
@@ -127,7 +127,7 @@ EXT_KEYS = {"initial_prompt", "carry_initial_prompt", "translate", "max_len", "s
             "suppress_blank", "detect_language"}
 
 
-def run_case(w, c, pcm):
+def run_case(w, c, pcm, force=None):
     kw = dict(c["params"])
     assert set(kw) <= FULL_KEYS, set(kw) - FULL_KEYS
     ext = dict(c["ext"])
@@ -156,6 +156,8 @@ def run_case(w, c, pcm):
     if ext.get("tdrz_boost"):
         boost = TdrzBoost(w)
         p.logits_filter_callback = C.cast(boost.cfunc, C.c_void_p)
+    if force is not None:  # parity_util.StepForcer (it applies the boost itself, first)
+        p.logits_filter_callback = C.cast(force, C.c_void_p)
     st = w.new_state()
     ret = w.full(st, pcm, p)
     segs = w.segments(st)
@@ -170,7 +172,7 @@ CASES = sorted(json.load(open(os.path.join(GOLDEN, "params_golden.json")))["case
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("case", CASES)
-def test_params_case(pg, pg_arrays, model_path, audio, case):
+def test_params_case(pg, pg_arrays, tf_golden, model_path, audio, case):
     c = pg["cases"][case]
     owk.quiet()
     w = whisper(model_path, c["model"])
@@ -185,11 +187,24 @@ def test_params_case(pg, pg_arrays, model_path, audio, case):
         assert rec.events == c["callbacks"]["events"], f"{case}: callback sequence differs"
         assert rec.texts == c["callbacks"]["texts"], f"{case}: new_segment texts differ"
     else:
-        # parted at a near-tie: callbacks up to the first new_segment after the parting agree
+        # parted at a near-tie: callbacks up to the first new_segment after the parting agree, and every
+        # later decode step is compared on the reference's prefixes (parity_util.decision_check); the run
+        # forced through the last disagreement reproduces the reference's callback log exactly
         print(f"[params] {case}: near-tie parting, callback log compared up to the first segment")
         ev = c["callbacks"]["events"]
         k = next((i for i, e in enumerate(ev) if e[0] == 4), len(ev))
         assert rec.events[:k] == ev[:k]
+        last = {}
+
+        def run(cfunc):
+            r, segs, rr = run_case(w, c, audio[c["clip"]], force=cfunc)
+            assert r == c["ret"]
+            last["rec"] = rr
+            return segs
+        pre = TdrzBoost(w)._cb if c["ext"].get("tdrz_boost") else None
+        compare_all_steps(w, tf_golden, "params/" + case, run, want, n_cmp, pre=pre)
+        assert last["rec"].events == c["callbacks"]["events"], f"{case}: callback sequence differs on the forced run"
+        assert last["rec"].texts == c["callbacks"]["texts"], f"{case}: new_segment texts differ on the forced run"
     if "tdrz" in case and "boost" in case and "off" not in case:
         assert any(s["speaker_turn_next"] for s in want), "fixture must contain speaker turns"
 
