@@ -40,13 +40,30 @@ __device__ __forceinline__ _Float16 p_f16(float p) {
 constexpr int FA_KT = 64;                     // keys per tile
 constexpr int FA_TILE_BYTES = FA_KT * 64 * 2; // 8 KB (K tile or Vt tile)
 
+// XCD-aware block order of the encoder attention (1-D grid): the 8 XCDs, each with a private L2, take
+// blocks round-robin by linear id, so a (clip, head)'s query tiles laid out consecutively landed on 8
+// XCDs and each XCD fetched that pair's K / V tiles again (FETCH_SIZE 5.8x the Q/K/V bytes). Here the
+// s-th block of XCD x (linear id 8 s + x) takes (clip, head) pair x + 8 (s / nt), query tile s % nt: all
+// tiles of a pair on one XCD. The grid is padded to whole groups of 8 pairs; padding blocks exit.
+__device__ __forceinline__ bool enc_attn_block(int nt, int H, int n_clips, int & qt, int & h, int & clip) {
+    const int L = blockIdx.x, x = L & 7, sl = L >> 3;
+    const int p = x + 8 * (sl / nt);
+    if (p >= H * n_clips) return false;
+    qt = sl % nt;
+    h = p % H;
+    clip = p / H;
+    return true;
+}
+inline dim3 enc_attn_grid(int nt, int H, int n_clips) { return dim3(8 * nt * ((H * n_clips + 7) / 8)); }
+
 __global__ __launch_bounds__(256, 2) void k_attn_encoder(const _Float16 * __restrict__ q, const _Float16 * __restrict__ k,
                                                          const _Float16 * __restrict__ vt, int T, int Tpad, int H,
                                                          float scale, int n_zero_pad, _Float16 * __restrict__ out,
-                                                         float * __restrict__ out32) {
+                                                         float * __restrict__ out32, int n_clips) {
     __shared__ __attribute__((aligned(1024))) char smem[4 * FA_TILE_BYTES];  // 2 stages x (K, Vt)
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int qt = blockIdx.x, h = blockIdx.y, clip = blockIdx.z;
+    int qt, h, clip;
+    if (!enc_attn_block((T + 63) / 64, H, n_clips, qt, h, clip)) return;
     const int d = H * 64;
     const int g = lane >> 4, l16 = lane & 15;
 
@@ -214,10 +231,11 @@ __global__ __launch_bounds__(256, 2) void k_attn_encoder_sm(const _Float16 * __r
                                                             const _Float16 * __restrict__ k,
                                                             const _Float16 * __restrict__ vt, int T, int Tpad, int H,
                                                             float scale, _Float16 * __restrict__ out,
-                                                            float * __restrict__ out32) {
+                                                            float * __restrict__ out32, int n_clips) {
     __shared__ __attribute__((aligned(1024))) char smem[4 * FA_TILE_BYTES];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int qt = blockIdx.x, h = blockIdx.y, clip = blockIdx.z;
+    int qt, h, clip;
+    if (!enc_attn_block((T + 63) / 64, H, n_clips, qt, h, clip)) return;
     const int d = H * 64;
     const int g = lane >> 4, l16 = lane & 15;
     const int qi = qt * 64 + wave * 16 + l16;
@@ -357,15 +375,15 @@ __global__ __launch_bounds__(256, 2) void k_attn_encoder_sm(const _Float16 * __r
 void attn_encoder_softmax(hipStream_t s, const _Float16 * q, const _Float16 * k, const _Float16 * vt, int n_clips, int T,
                           int Tpad, int H, float scale, _Float16 * out, float * out32) {
     if (Tpad < ((T + FA_KT - 1) / FA_KT) * FA_KT) throw std::runtime_error("attn_encoder_softmax: Tpad too small");
-    OWK_LAUNCH(k_attn_encoder_sm, dim3((T + 63) / 64, H, n_clips), dim3(256), 0, s, q, k, vt, T, Tpad, H, scale,
-                       out, out32);
+    OWK_LAUNCH(k_attn_encoder_sm, enc_attn_grid((T + 63) / 64, H, n_clips), dim3(256), 0, s, q, k, vt, T, Tpad, H,
+               scale, out, out32, n_clips);
 }
 
 void attn_encoder(hipStream_t s, const _Float16 * q, const _Float16 * k, const _Float16 * vt, int n_clips, int T,
                   int Tpad, int H, float scale, int n_zero_pad, _Float16 * out, float * out32) {
     if (Tpad < ((T + FA_KT - 1) / FA_KT) * FA_KT) throw std::runtime_error("attn_encoder: Tpad too small");
-    OWK_LAUNCH(k_attn_encoder, dim3((T + 63) / 64, H, n_clips), dim3(256), 0, s, q, k, vt, T, Tpad, H, scale,
-                       n_zero_pad, out, out32);
+    OWK_LAUNCH(k_attn_encoder, enc_attn_grid((T + 63) / 64, H, n_clips), dim3(256), 0, s, q, k, vt, T, Tpad, H,
+               scale, n_zero_pad, out, out32, n_clips);
 }
 
 // ----------------------------------------------------------------------------------
@@ -1115,6 +1133,7 @@ __global__ __launch_bounds__(256) void k_sm_split_pv(const _Float16 * __restrict
 }
 
 size_t attn_softmax_ws_floats(int n_rows, int H) { return (size_t) n_rows * H * SMS_PER_RH; }
+int attn_softmax_force_nt = 0;
 
 void attn_decoder_softmax(hipStream_t s, const _Float16 * q, int ldq, const _Float16 * kbase, const _Float16 * vbase,
                           int ld_kv, int hs, const AttnRow * rows_dev, int n_rows, const int * key_idx, int H, float scale,
@@ -1136,12 +1155,12 @@ void attn_decoder_softmax(hipStream_t s, const _Float16 * q, int ldq, const _Flo
         return;
     }
     // outputs do not depend on the width (k_attn_softmax): 1024 threads when the pass has few
-    // (row, head) blocks (configs[4]'s one-row steps), 256 otherwise
-    if (n_rows * H <= 128)
-        OWK_LAUNCH(k_attn_softmax<1024>, dim3(H, n_rows), dim3(1024), 0, s, q, ldq, kbase, vbase, ld_kv, hs, rows_dev,
+    // (row, head) blocks (configs[4]'s one-row steps), 256 otherwise (attn_softmax_force_nt: a test hook's A/B)
+    if (attn_softmax_force_nt == 256 || (attn_softmax_force_nt != 1024 && n_rows * H > 128))
+        OWK_LAUNCH(k_attn_softmax<256>, dim3(H, n_rows), dim3(256), 0, s, q, ldq, kbase, vbase, ld_kv, hs, rows_dev,
                            key_idx, scale, out, ldo, amap, cap, cap_rows, out32);
     else
-        OWK_LAUNCH(k_attn_softmax<256>, dim3(H, n_rows), dim3(256), 0, s, q, ldq, kbase, vbase, ld_kv, hs, rows_dev,
+        OWK_LAUNCH(k_attn_softmax<1024>, dim3(H, n_rows), dim3(1024), 0, s, q, ldq, kbase, vbase, ld_kv, hs, rows_dev,
                            key_idx, scale, out, ldo, amap, cap, cap_rows, out32);
 }
 

@@ -297,6 +297,8 @@ void attn_decoder_softmax(hipStream_t s, const _Float16 * q, int ldq, const _Flo
 // workspace of the key-split soft_max form (ws non-null above): every (row, head) over ceil(keys / 128)
 // blocks, probabilities bit-identical to the one-block kernel, P.V partials added in chunk order
 size_t attn_softmax_ws_floats(int n_rows, int H);
+// test hook: 256 / 1024 forces the single-block soft_max attention's width (0: by the pass size)
+extern int attn_softmax_force_nt;
 // test/bench hook: the one_chunk cross-attention kernels on contiguous head-major keys (ld 64):
 // which = 1 the one-wave k_attn_step
 void attn_cross_kernel(hipStream_t s, int which, const _Float16 * q, int ldq, const _Float16 * kbase,

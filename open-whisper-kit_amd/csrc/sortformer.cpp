@@ -674,10 +674,16 @@ float * run_conformer(sortformer_context * ctx, float * x, const Segs & segs, in
     const int ldP = pos_batched ? ctx->n_conf * d : d;
     float * P = grow<float>(ctx->s_P, (size_t) (2 * Tmax - 1) * ldP);
     if (pos_batched) {
+        // only the layers this call runs (0 .. last): the stacked weights are layer-major. Each P value is
+        // the same MFMA chain over K = d whichever tile kernel the N of the call selects: the 64x64 ring
+        // (a per-layer N = d at these M) and the 128x128 tile are bit-identical (test_gpu_kernels.py
+        // test_gemm_mid_matches_128, f32 epilogue at K = 512), and M >= 2048 takes the 8-phase kernel for
+        // both, whose outputs do not depend on N
         EpiParams ep;
         ep.out32 = P;
         ep.ldo = ldP;
-        gemm(s, EPI_F32, 2 * Tmax - 1, ldP, d, ctx->pos16.as<_Float16>() + p0, d, ctx->pos_all.as<_Float16>(), d, ep);
+        gemm(s, EPI_F32, 2 * Tmax - 1, (last + 1) * d, d, ctx->pos16.as<_Float16>() + p0, d, ctx->pos_all.as<_Float16>(),
+             d, ep);
     }
     _Float16 * ao = grow<_Float16>(ctx->s_ao, (size_t) T * d);
     float * cv = grow<float>(ctx->s_cv, (size_t) T * 2 * d);

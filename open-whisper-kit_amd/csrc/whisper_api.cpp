@@ -1766,15 +1766,19 @@ double owk_debug_attn_softmax(int device, int split, int R, int H, int T, uint16
         damap.alloc(H * sizeof(int));
         OWK_HIP_CHECK(hipMemcpy(damap.ptr, amap.data(), H * sizeof(int), hipMemcpyHostToDevice));
         dcap.alloc((size_t) 4 * T * R * 4);
-        if (split) {
+        if (split == 1) {
             dws.alloc(attn_softmax_ws_floats(R, H) * 4);
             OWK_HIP_CHECK(hipMemsetAsync(dws.ptr, 0, dws.bytes, s));
         }
+        // split: 0 single-block kernel at the engine's width, 1 key-split form, 256 / 1024 single-block at
+        // that width
         auto run = [&] {
+            attn_softmax_force_nt = split >= 256 ? split : 0;
             attn_decoder_softmax(s, dq.as<_Float16>(), H * 64, dk.as<_Float16>(), dv.as<_Float16>(), 64, T * 64,
                                  (const AttnRow *) drows.ptr, R, nullptr, H, 0.125f, T, dout.as<_Float16>(), H * 64,
-                                 damap.as<int>(), dcap.as<float>(), R, nullptr, split ? dws.as<float>() : nullptr,
-                                 split ? dws.bytes / 4 : 0);
+                                 damap.as<int>(), dcap.as<float>(), R, nullptr, split == 1 ? dws.as<float>() : nullptr,
+                                 split == 1 ? dws.bytes / 4 : 0);
+            attn_softmax_force_nt = 0;
         };
         run();
         double us = 0.0;

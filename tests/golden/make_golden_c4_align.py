@@ -11,7 +11,7 @@ keep the speaker turns:
   * fill:     sentenceSmoothing = false, fillNearest = true (nil words take the nearest segment);
   * smooth5:  sentenceSmoothing = true, maxWordsInSentence = 5 (majority over short windows).
 
-Usage:  python tests/golden/make_golden_c4_align.py   (after make_golden_c4.py)
+Usage:  python tests/golden/make_golden_c4_align.py [c4_10m_golden]  (after make_golden_c4.py [--minutes 10])
 """
 import collections
 import json
@@ -31,7 +31,7 @@ VARIANTS = {
 
 
 def main():
-    path = os.path.join(OUT, "c4_golden.json")
+    path = os.path.join(OUT, (sys.argv[1] if len(sys.argv) > 1 else "c4_golden") + ".json")
     meta = json.load(open(path))
     words = [tuple(w) for w in meta["results"]["words"]]
     dsegs = DA.rttm_parse(meta["results"]["rttm"])

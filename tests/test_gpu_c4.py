@@ -33,19 +33,28 @@ pytestmark = pytest.mark.gpu
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
 
-@pytest.fixture(scope="module")
-def c4():
-    path = os.path.join(GOLDEN, "c4_golden.json")
+# the 60 s fixture (real speech, tests/golden/sf_test60.wav) and the 10 minutes BASELINE configs[4] states
+# (tools/pipeline_bench.py's clip, owk_synth.synth_audio(600 s, seed 5)): make_golden_c4.py [--minutes 10]
+FIXTURES = ["c4_golden", "c4_10m_golden"]
+
+
+@pytest.fixture(scope="module", params=FIXTURES)
+def c4(request):
+    path = os.path.join(GOLDEN, request.param + ".json")
     if not os.path.exists(path):
-        pytest.skip("c4_golden.json not generated")
-    return json.load(open(path)), np.load(os.path.join(GOLDEN, "c4_golden.npz"))
+        pytest.skip(f"{request.param}.json not generated")
+    return json.load(open(path)), np.load(os.path.join(GOLDEN, request.param + ".npz"))
 
 
 @pytest.fixture(scope="module")
-def test60():
+def test60(c4):
+    """the fixture's audio (named for the 60 s clip it first was)"""
     import owk_synth as S
 
-    return S.read_wav_16k_mono(os.path.join(GOLDEN, "sf_test60.wav"))
+    meta, _ = c4
+    if meta.get("minutes", 1) == 1:
+        return S.read_wav_16k_mono(os.path.join(GOLDEN, "sf_test60.wav"))
+    return S.synth_audio(int(meta["minutes"] * 60 * 16000), 5)
 
 
 @pytest.fixture(scope="module")
@@ -82,7 +91,7 @@ def _logit_error(w, meta, arr, pcm):
     return max(e1, e2)
 
 
-_free_run = {}  # test_configs4_transcription's result, aligned by test_configs4_stream_and_align
+_free_run = {}  # test_configs4_transcription's result per fixture, aligned by test_configs4_stream_and_align
 
 
 def _runs(diffs):
@@ -141,7 +150,7 @@ def test_configs4_transcription(c4, w4, test60):
                                                                 [t for x in want["segments"] for t in x["tokens"]])) if a[8] != b[8]]
         print(f"[c4] free run: {len(g_ids)} tokens identical")
         _check_tdtw(meta, diff, "free run")
-    _free_run["segments"] = got
+    _free_run[meta.get("minutes", 1)] = got
 
 
 def _forced_run(w, meta, pcm):
@@ -213,7 +222,7 @@ def test_configs4_stream_and_align(c4, w4, test60):
     assert not bad.any(), np.argwhere(bad)[:10]
 
     # aligner over the free run's tokens (Swift WordTiming per token: text, t0, t1, p) and the RTTMs
-    got = _free_run.get("segments")
+    got = _free_run.get(meta.get("minutes", 1))
     if got is None:
         st = w4.new_state()
         assert w4.full(st, test60, _params(w4, meta)) == meta["results"]["full"]["ret"]

@@ -270,7 +270,8 @@ def test_whole_k_chain_bit_identical(model, model_path, clips):
 
 
 
-@pytest.mark.parametrize("R,T", [(1, 1500), (3, 1500), (2, 100), (1, 128), (1, 129), (5, 384), (32, 1500), (7, 2048)])
+@pytest.mark.parametrize("R,T", [(1, 1500), (3, 1500), (2, 100), (1, 128), (1, 129), (5, 384), (32, 1500), (7, 2048),
+                                 (1, 60), (1, 200)])
 def test_softmax_attention_split_bit_identical(R, T):
     """The key-split soft_max attention (k_sm_split_scores + k_sm_split_pv: scores per 128-key chunk,
     P.V per block of 16 residue groups, in-launch combine by the last-arriving block) reproduces the
@@ -282,18 +283,21 @@ def test_softmax_attention_split_bit_identical(R, T):
     f.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_uint16), C.POINTER(C.c_float), C.c_int]
     H = 20
     outs, caps = [], []
-    for split in (0, 1, 1):  # the split form twice: its arrival tickets must be reset between launches
+    # the split form twice (its arrival tickets must be reset between launches), then the single-block
+    # kernel at both widths (outputs do not depend on the width)
+    for split in (0, 1, 1, 256, 1024):
         o = np.zeros(R * H * 64, np.uint16)
         cp = np.zeros(4 * T * R, np.float32)
         assert f(0, split, R, H, T, o.ctypes.data_as(C.POINTER(C.c_uint16)), cp.ctypes.data_as(C.POINTER(C.c_float)), 3) >= 0
         outs.append(o)
         caps.append(cp)
     assert np.abs(outs[0].view(np.float16).astype(np.float32)).max() > 0
-    for i in (1, 2):
+    for i in (1, 2, 3, 4):
         bad = np.nonzero(outs[0] != outs[i])[0]
         a16, b16 = outs[0].view(np.float16), outs[i].view(np.float16)
         assert bad.size == 0, (f"R={R} T={T}: split outputs differ ({bad.size} values): " +
                                ", ".join(f"[r{k // (H * 64)} h{k // 64 % H} d{k % 64}] {a16[k]} vs {b16[k]}" for k in bad[:8]))
         assert np.array_equal(caps[0].view(np.uint32), caps[i].view(np.uint32)), f"R={R} T={T}: captures differ"
-    us = [f(0, s, R, H, T, None, None, 20) for s in (0, 1)]
-    print(f"R={R} T={T}: bit-identical; single-block {us[0]:.1f} us, key-split {us[1]:.1f} us")
+    us = [f(0, s, R, H, T, None, None, 20) for s in (0, 1, 256, 1024)]
+    print(f"R={R} T={T}: bit-identical; single-block {us[0]:.1f} us (256 threads {us[2]:.1f}, 1024 threads {us[3]:.1f}), "
+          f"key-split {us[1]:.1f} us")
