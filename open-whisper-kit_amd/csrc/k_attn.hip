@@ -1154,9 +1154,11 @@ void attn_decoder_softmax(hipStream_t s, const _Float16 * q, int ldq, const _Flo
                    amap, cap, cap_rows, ws, out, ldo, out32);
         return;
     }
-    // outputs do not depend on the width (k_attn_softmax): 1024 threads when the pass has few
-    // (row, head) blocks (configs[4]'s one-row steps), 256 otherwise (attn_softmax_force_nt: a test hook's A/B)
-    if (attn_softmax_force_nt == 256 || (attn_softmax_force_nt != 1024 && n_rows * H > 128))
+    // outputs do not depend on the width (k_attn_softmax): 1024 threads when the pass has few (row, head)
+    // blocks AND long rows, 256 otherwise -- measured (test_softmax_attention_split_bit_identical, r05q): one
+    // row of <= 200 keys (configs[4]'s self attention) 5.0-5.5 us at 256 threads vs 5.9-6.4 at 1024; 32 rows
+    // x 1500 keys 42 vs 60 us; 5 rows x 384 keys 7.7 vs 7.4 us (attn_softmax_force_nt: the test hook's A/B)
+    if (attn_softmax_force_nt == 256 || (attn_softmax_force_nt != 1024 && (n_rows * H > 128 || max_keys <= 256)))
         OWK_LAUNCH(k_attn_softmax<256>, dim3(H, n_rows), dim3(256), 0, s, q, ldq, kbase, vbase, ld_kv, hs, rows_dev,
                            key_idx, scale, out, ldo, amap, cap, cap_rows, out32);
     else

@@ -209,8 +209,9 @@ def run_case(key, model, clip, init_kw, full_kw, fixture, which, audio, cache, f
     arrays[key + "/floor"] = fl
     arrays[key + "/floor_ts"] = fl_ts
     print(f"{key}: {rec['n_steps']} steps in {len(windows)} windows; flips "
-          f"{ {n: len(v['flips']) for n, v in rec['realisations'].items()} }; floor median {np.median(fl):.2e} "
-          f"max {fl.max():.2e} ({time.time() - t0:.0f} s)", flush=True)
+          f"{ {n: len(v['flips']) for n, v in rec['realisations'].items()} }; floor median "
+          f"{np.median(fl) if len(fl) else 0:.2e} max {fl.max() if len(fl) else 0:.2e} ({time.time() - t0:.0f} s)",
+          flush=True)
     return rec, arrays
 
 
