@@ -1,20 +1,19 @@
 #!/bin/bash
-# Round-5 closing measurements on one box: rocprofv3 --kernel-trace --stats and the PMC FETCH_SIZE pass of
-# each bench model (copied into profiles/r05_* so the bench lines cross-check against this tree), the three
-# bench lines WITH the reference CPU leg and the clip-0 token check, configs[4] (10 min, both modes) and its
-# sequential kernel trace with graphs on (packet capture off: profiles/r05_rocprof_graph_segv.txt).
-#   tools/gpu_r05_final.sh TAG
+# Round-5 closing measurements on the final tree, in two calls:
+#   tools/gpu_r05_final.sh TAG prof   rocprofv3 --kernel-trace --stats + the PMC FETCH_SIZE pass of each bench model
+#                                     (gpurun_out/TAG/<model>/; copied to profiles/r05_* for bench.py PROFILES)
+#   tools/gpu_r05_final.sh TAG bench  the three bench lines WITH the reference CPU leg and the clip-0 token check,
+#                                     configs[4] at 10 min (both modes)
 set -o pipefail
-TAG=${1:-r05f}
+TAG=${1:-r05z}
+PART=${2:-prof}
 mkdir -p gpurun_out/$TAG
 export OWK_MODEL_CACHE=/tmp/owk_models
-bash tools/gpu_profiles.sh $TAG large-v3 large-v3-turbo large-v3-q5_0 || exit 1
-cp gpurun_out/$TAG/large-v3/kernel_stats.txt profiles/r05_bench_kernel_stats.txt
-cp gpurun_out/$TAG/large-v3/fetch_summary.txt profiles/r05_pmc_fetch_summary.txt
-cp gpurun_out/$TAG/large-v3-turbo/kernel_stats.txt profiles/r05_turbo_kernel_stats.txt
-cp gpurun_out/$TAG/large-v3-turbo/fetch_summary.txt profiles/r05_turbo_pmc_fetch_summary.txt
-cp gpurun_out/$TAG/large-v3-q5_0/kernel_stats.txt profiles/r05_q5_kernel_stats.txt
-cp gpurun_out/$TAG/large-v3-q5_0/fetch_summary.txt profiles/r05_q5_pmc_fetch_summary.txt
+if [ "$PART" = prof ]; then
+  bash tools/gpu_profiles.sh $TAG large-v3 large-v3-turbo large-v3-q5_0
+  exit $?
+fi
+[ "$PART" = bench ] || exit 2
 for m in large-v3 large-v3-turbo large-v3-q5_0; do
   timeout -k 10 900 python bench.py --model $m > gpurun_out/$TAG/bench_$m.json 2> gpurun_out/$TAG/bench_$m.err \
       || { echo "$m bench failed"; tail -5 gpurun_out/$TAG/bench_$m.err; exit 1; }
@@ -29,9 +28,3 @@ timeout -k 10 600 python -u tools/pipeline_bench.py --minutes 10 --no-cpu > gpur
 python -c "
 import json; d=json.load(open('gpurun_out/$TAG/pipeline.json'))
 print('configs[4] chunked', d['chunked']['value'], 'sequential', d['sequential']['value'], 'asr_wall', d['sequential']['asr_wall_s'])"
-export DEBUG_CLR_GRAPH_PACKET_CAPTURE=0
-cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/seqtr -o run -- \
-    python $GRAFT_REPO_ROOT/tools/pipeline_bench.py --minutes 2 --no-cpu --mode sequential --serial \
-    > $GRAFT_REPO_ROOT/gpurun_out/$TAG/seq.json 2> $GRAFT_REPO_ROOT/gpurun_out/$TAG/seq.err || { echo "trace failed"; exit 1; }
-cd $GRAFT_REPO_ROOT
-python tools/prof_summary.py /tmp/seqtr > gpurun_out/$TAG/c4seq_kernel_stats.txt && head -14 gpurun_out/$TAG/c4seq_kernel_stats.txt
