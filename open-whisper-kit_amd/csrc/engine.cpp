@@ -978,9 +978,9 @@ void Engine::launch_decode(const DecShape & sh) {
 //          bit-identical to the split chain, so a clip's result does not depend on its pass size.
 // Whole-K saves a launch per site but every block of the consumer recomputes the row statistics
 // from the f32 rows, and the exact split-order reduction costs more than the launch it saves:
-// 36.8 vs 32.5 us per layer at 1 row, 48.3 vs 36.3 at 8 (profiles/r04h_chain_ab.txt), so it is off
+// 36.8 vs 32.5 us per layer at 1 row, 48.3 vs 36.3 at 8 (profiles/archive/r04h_chain_ab.txt), so it is off
 // by default (whole_k_rows() = 0) and kept as a verified alternative. Earlier measured alternatives
-// (profiles/r02e_ab.txt, the round-3 ticket finish) lost on the launch boundary or the in-launch seam.
+// (profiles/archive/r02e_ab.txt, the round-3 ticket finish) lost on the launch boundary or the in-launch seam.
 // soft_max rows (flash_attn = false) and DTW captures run the soft_max attention launches inside the
 // same chain. Every kernel here is row-independent: the row activations / GEMM outputs are addressed
 // from row r0, the attention kernels take the pass's AttnRow entries r0.. (absolute q_row) and the

@@ -15,7 +15,7 @@ namespace owk {
 // decode passes of at most whole_k_rows() rows run the whole-K residual + LayerNorm-prologue chain
 // (engine.cpp launch_decode; bit-identical to the split chain), larger passes the split-K +
 // resid_layernorm chain. Default 0: the whole-K chain measured slower at every row count
-// (tools/chain_ab.py, profiles/r04h_chain_ab.txt); the test hook keeps it verified bit-identical.
+// (tools/chain_ab.py, profiles/archive/r04h_chain_ab.txt); the test hook keeps it verified bit-identical.
 constexpr int kWholeKRowsDefault = 0;
 int whole_k_rows();           // the current limit (kWholeKRowsDefault unless a test hook changed it)
 int set_whole_k_rows(int n);  // test hook (owk_debug_set_whole_k_rows); returns the previous limit

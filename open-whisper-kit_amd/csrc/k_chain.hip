@@ -9,7 +9,7 @@
 //      -> residual + the next layer's attn_ln -> its fused Q/K/V (K/V into the self-attention cells)
 // Each chain is ONE launch of one 16-wave block per item (a 16-column tile group and k split of a stage):
 //   * a block streams its item's weight tiles into LDS (global_load_lds, non-temporal) BEFORE it waits for
-//     the previous stage: the one thing a kernel boundary cannot do (profiles/r03s_lab_prefetch.txt);
+//     the previous stage: the one thing a kernel boundary cannot do (profiles/archive/r03s_lab_prefetch.txt);
 //   * stage hand-off (cdna_hip_programming.md Guideline 16, R1; MI355X_MICROARCH.md visibility table,
 //     first row): every handed-off value is stored write-through (agent-scope atomic stores) and drained
 //     (vmcnt(0)) before one lane adds the block's arrival to its XCD shard of the stage's count; a consumer

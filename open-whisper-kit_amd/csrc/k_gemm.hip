@@ -383,7 +383,7 @@ constexpr int G2_M = 256, G2_N = 256, G2_K = 32;
 // by column, so the ~32 tiles an XCD runs at once cover 8 row panels x 4 column panels -- A and W
 // panels both re-used from that XCD's L2 (row-major order ran 1.6 row panels x all 20 column
 // panels of MLP0 at once: every W panel re-fetched per row panel, 2 GB of FETCH_SIZE per launch,
-// profiles/r02n_pmc_fetch_summary.txt)
+// profiles/archive/r02n_pmc_fetch_summary.txt)
 constexpr int TO_GM = 8;
 __device__ __forceinline__ void tile_order(int t, int ntiles, int nbn, int & bm, int & bn) {
     static const bool grouped = true;
@@ -1625,7 +1625,7 @@ template <int MODE> struct LaunchRows {
         const bool one = M <= 16;
         // full-epilogue launches with many column tiles take 2 per block (a wave's activation
         // fragments serve both): the logits GEMM 47.7 -> 37.0 us for 32 x 51866 x 1280
-        // (profiles/r03n_logits_gemm_nt.txt), MLP0 9.7 -> 8.0 us; where halving the grid would leave
+        // (profiles/archive/r03n_logits_gemm_nt.txt), MLP0 9.7 -> 8.0 us; where halving the grid would leave
         // fewer than 128 blocks (cross-Q, attn.out: N = 1280 -> 40 blocks) one tile per block is faster
         // (r04: cross-Q 7.1 us with 2, 5.7 with 1); split-K partial launches measured slower with 2
         // (r04b A/B, large-v3 RTF 1017 vs 1026)
@@ -1717,7 +1717,7 @@ __global__ __launch_bounds__(256) void k_quantize_q8_f16(const TA * __restrict__
 
 // the same with 8 consecutive elements per lane (one 16/32-byte load, one 16-byte store; four lanes
 // per block, amax over the quad): the per-element version moved 2.3 TB/s (f32 rows, 163 us for the
-// 48000 x 1280 encoder operand, profiles/r03g_q5_kernel_stats.txt)
+// 48000 x 1280 encoder operand, profiles/archive/r03g_q5_kernel_stats.txt)
 template <typename TA>
 __global__ __launch_bounds__(256) void k_quantize_q8_f16_v8(const TA * __restrict__ A, int lda, int M, int K,
                                                             _Float16 * __restrict__ q, float * __restrict__ dat, int mpad) {
@@ -2419,7 +2419,7 @@ static bool use_mid(int M, int N) {
 }
 // tile edge of the ring kernel: 32 where the 64x64 grid would still leave CUs idle (SortFormer chunk
 // shapes at M = 413, tests/test_gpu_kernels.py::test_gemm_mid_speed: 32x32 4.6-15.7 us against 64x64
-// 6.2-21.7 us, N = 2048 included, whose 64x64 grid is 224 blocks; profiles/r03h_gemm_mid_speed.txt)
+// 6.2-21.7 us, N = 2048 included, whose 64x64 grid is 224 blocks; profiles/archive/r03h_gemm_mid_speed.txt)
 static int mid_tile(int M, int N) {
     const int m = gemm256_mode();
     if (m == GEMM_MID_FORCED || m == GEMM_MID32_FORCED) return m == GEMM_MID32_FORCED ? 32 : 64;

@@ -543,7 +543,7 @@ void process_logits(hipStream_t s, float * logits, int n_vocab, const LogitJob *
                     void * ws, size_t ws_bytes) {
     if (n_jobs <= 0) return;
     // (turbo bench, interleaved on one box: 3819-3844 one block per row, 3897-3916 split;
-    // profiles/r03l_ab_logits_split_turbo.txt)
+    // profiles/archive/r03l_ab_logits_split_turbo.txt)
     if (any_nosp || !ws || ws_bytes < process_logits_ws_bytes(n_jobs)) {
         OWK_LAUNCH(k_process_logits, dim3(n_jobs), dim3(LG_THREADS), 0, s, logits, n_vocab, jobs_dev, vi, out_dev,
                    logprobs_out, probs_out);

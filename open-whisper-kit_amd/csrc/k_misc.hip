@@ -129,7 +129,7 @@ void resid_layernorm(hipStream_t s, int M, int N, int ks, const float * part, co
         throw std::runtime_error("resid_layernorm: unsupported shape");
     if (q8 && (N % 32 != 0 || !q8d)) throw std::runtime_error("resid_layernorm: Q8_0 output needs N % 32 == 0");
     // (a one-wave-per-row variant measured slower: 159 -> 249 ms per step, the row's split partials
-    // are too many serial loads for one wave, profiles/r02e_ab.txt)
+    // are too many serial loads for one wave, profiles/archive/r02e_ab.txt)
     OWK_LAUNCH(k_resid_layernorm, dim3(M), dim3(256), 0, s, M, N, ks, part, bias, x, lnw, lnb, eps, xn, ldo,
                        q8, q8d);
 }

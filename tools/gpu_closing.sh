@@ -1,8 +1,8 @@
 #!/bin/bash
-# Round-5 closing measurements on the final tree, in two calls:
-#   tools/gpu_r05_final.sh TAG prof   rocprofv3 --kernel-trace --stats + the PMC FETCH_SIZE pass of each bench model
-#                                     (gpurun_out/TAG/<model>/; copied to profiles/r05_* for bench.py PROFILES)
-#   tools/gpu_r05_final.sh TAG bench  the three bench lines WITH the reference CPU leg and the clip-0 token check,
+# Closing measurements of a round on the final tree, in two calls:
+#   tools/gpu_closing.sh TAG prof   rocprofv3 --kernel-trace --stats + the PMC FETCH_SIZE pass of each bench model
+#                                     (gpurun_out/TAG/<model>/; copied to profiles/r<NN>_* for bench.py PROFILES)
+#   tools/gpu_closing.sh TAG bench  the three bench lines WITH the reference CPU leg and the clip-0 token check,
 #                                     configs[4] at 10 min (both modes)
 set -o pipefail
 TAG=${1:-r05z}

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Profiles bench.py's roofline cross-checks read (bench.py PROFILES), for each bench model on this tree:
-#   rocprofv3 --kernel-trace --stats of one bench step  -> profiles/r04_<m>_kernel_stats.txt
-#   rocprofv3 --pmc FETCH_SIZE of one bench step        -> profiles/r04_<m>_pmc_fetch_summary.txt
+#   rocprofv3 --kernel-trace --stats of one bench step  -> profiles/r05_<m>_kernel_stats.txt (copied by hand)
+#   rocprofv3 --pmc FETCH_SIZE of one bench step        -> profiles/r05_<m>_pmc_fetch_summary.txt
 # (counters in a run of their own, MI355X_MICROARCH.md). Outputs under gpurun_out/$TAG/<model>.
 #   tools/gpu_profiles.sh TAG [models...]
 set -o pipefail

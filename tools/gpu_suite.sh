@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round 5: the GPU suite on the current tree in two parts (A: everything but the full-depth large / configs[4]
+# The GPU suite on the current tree in two parts (A: everything but the full-depth large / configs[4]
 # files, B: those), logs under gpurun_out/TAG
 set -o pipefail
 TAG=${1:-r05f}

@@ -2,7 +2,7 @@
 """Per-kernel summary (calls, total/avg/min/max us, %) of a rocprofv3 --kernel-trace run.
 
 Reads the rocpd SQLite output (<dir>/*_results.db) or kernel_stats.csv, prints a table.
-    python tools/prof_summary.py gpurun_out/r1a/prof > profiles/r01_bench_kernel_stats.txt
+    python tools/prof_summary.py gpurun_out/r1a/prof > profiles/archive/r01_bench_kernel_stats.txt
 """
 import csv
 import glob
