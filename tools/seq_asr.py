@@ -2,7 +2,7 @@
 windows, prompt carry, greedy, token timestamps), large-v3 F16, flash_attn = false + DTW (LARGE_V3
 heads) unless --fa / --no-dtw. Prints wall time, tokens and ms per token (for profiling under rocprofv3).
 
-    python tools/seq_asr.py [--minutes 2] [--fa] [--no-dtw]
+    python tools/seq_asr.py [--minutes 2] [--fa] [--no-dtw] [--model large-v3-turbo]
 """
 import argparse
 import json
@@ -23,8 +23,9 @@ def main():
     ap.add_argument("--minutes", type=float, default=2.0)
     ap.add_argument("--fa", action="store_true", help="flash_attn = true")
     ap.add_argument("--no-dtw", action="store_true")
+    ap.add_argument("--model", default="large-v3", help="a bench model (large-v3-turbo: 4 decoder layers)")
     a = ap.parse_args()
-    model = S.ensure_model("large-v3", cache_dir=os.environ.get("OWK_MODEL_CACHE", "/tmp/owk_models"))
+    model = S.ensure_model(a.model, cache_dir=os.environ.get("OWK_MODEL_CACHE", "/tmp/owk_models"))
     n = int(a.minutes * 60 * 16000)
     pcm = S.synth_audio(n, 5)
     owk.quiet()
@@ -39,7 +40,7 @@ def main():
     dt = time.perf_counter() - t0
     toks = sum(len(s["tokens"]) for s in w.segments(st))
     print(json.dumps({"ret": ret, "audio_s": n / 16000, "wall_s": round(dt, 3), "rtf": round(n / 16000 / dt, 2),
-                      "tokens": toks, "ms_per_token": round(1e3 * dt / max(toks, 1), 3), "fa": a.fa, "dtw": not a.no_dtw}))
+                      "tokens": toks, "ms_per_token": round(1e3 * dt / max(toks, 1), 3), "fa": a.fa, "dtw": not a.no_dtw, "model": a.model}))
 
 
 if __name__ == "__main__":
