@@ -249,8 +249,18 @@ __global__ __launch_bounds__(LG_THREADS) void k_rowmax_update(const float * __re
         return;
     }
     const float * L = logits + (size_t) e.z * n_vocab;
+    // 8 loads in flight per thread (a max is exact in any order): a loop of single loads waited on
+    // each one in turn (51 round trips per thread over a 51866-entry row)
     float mx = -INFINITY;
-    for (int i = threadIdx.x; i < n_vocab; i += LG_THREADS) mx = fmaxf(mx, L[i]);
+    int i = threadIdx.x;
+    for (; i + 7 * LG_THREADS < n_vocab; i += 8 * LG_THREADS) {
+        float v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = L[i + u * LG_THREADS];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) mx = fmaxf(mx, v[u]);
+    }
+    for (; i < n_vocab; i += LG_THREADS) mx = fmaxf(mx, L[i]);
     mx = block_max(mx, redf);
     if (threadIdx.x == 0) *dst = mx;
 }

@@ -316,11 +316,21 @@ static bool g_tf_active = false, g_tf_force = true;
 static whisper_full_params g_tf_params;
 static whisper_logits_filter_callback g_tf_base = nullptr;
 
+static std::vector<int> g_tf_open;  // per window: 1 = its end is open (no <|endoftext|> forced after it)
+
 void ref_tf_set(const int * tokens, const int * off, int n_windows, int force) {
     g_tf_active = n_windows >= 0;
     g_tf_force = force != 0;
     g_tf_off.assign(off, off + std::max(n_windows, 0) + 1);
     g_tf_tok.assign(tokens, tokens + (n_windows > 0 ? off[n_windows] : 0));
+    g_tf_open.assign(std::max(n_windows, 0), 0);
+}
+
+// windows whose end is open (the step limit, or a timestamp reaching the end of the audio): the step after
+// the last listed token is left to the reference, as on the GPU (tests/parity_util.Forcer). Call after ref_tf_set.
+void ref_tf_set_open(const int * open, int n_windows) {
+    g_tf_open.assign(open, open + std::min<int>(n_windows, (int) g_tf_open.size()));
+    g_tf_open.resize(g_tf_off.size() - 1, 0);
 }
 
 // recorded steps: returns their count; with non-null outputs rec[TF_NI n] = (window, step, pick,
@@ -347,7 +357,8 @@ static void ref_tf_cb(struct whisper_context * ctx, struct whisper_state * state
     int teacher = -1;
     if (w >= 0 && w < n_win) {
         const int len = g_tf_off[w + 1] - g_tf_off[w];
-        teacher = n_tokens < len ? g_tf_tok[g_tf_off[w] + n_tokens] : (n_tokens == len ? whisper_token_eot(ctx) : -1);
+        teacher = n_tokens < len ? g_tf_tok[g_tf_off[w] + n_tokens]
+                                 : (n_tokens == len && !g_tf_open[w] ? whisper_token_eot(ctx) : -1);
     }
     int j = -1;
     for (int i = 0; i < WHISPER_MAX_DECODERS; ++i)

@@ -106,6 +106,7 @@ def lib(path=None):
         L.ref_record_get.argtypes = [C.POINTER(ip), C.POINTER(ip), C.POINTER(ip), fp, C.POINTER(ip)]
         L.ref_timings.argtypes = [vp] + [C.POINTER(C.c_double)] * 6 + [C.POINTER(ip)]
         L.ref_tf_set.argtypes = [C.POINTER(ip), C.POINTER(ip), ip, ip]
+        L.ref_tf_set_open.argtypes = [C.POINTER(ip), ip]
         L.ref_tf_get.argtypes = [C.POINTER(ip), fp]
         L.whisper_full_n_segments.argtypes = [vp]
         L.whisper_full_get_segment_t0.restype = C.c_int64
@@ -217,7 +218,7 @@ class Ref:
             s["speaker_turn_next"] = bool(self.L.whisper_full_get_segment_speaker_turn_next(self.ctx, i))
         return ret, segs, self.cb_log()
 
-    def tf_set(self, windows=None, force=True):
+    def tf_set(self, windows=None, force=True, open_end=None):
         """Teacher forcing for the following full() / full_ex() calls (ref_probe.cpp ref_tf_set): the
         per-window decoded token lists to force (None: off; [] with force=False: record only). Every
         greedy step records the reference's own pick on the forced prefix (its whisper_process_logits +
@@ -230,6 +231,9 @@ class Ref:
         tok = np.asarray(flat + [0], np.int32)
         P = lambda a: a.ctypes.data_as(C.POINTER(C.c_int))
         self.L.ref_tf_set(P(tok), P(off), len(windows), int(force))
+        if open_end is not None:  # open windows: nothing forced after the last listed token
+            o = np.asarray([1 if x else 0 for x in open_end], np.int32)
+            self.L.ref_tf_set_open(P(o), len(o))
 
     TF_NC = 16
 

@@ -83,9 +83,11 @@ def traced_windows(ref, flat):
             longest[-1] = p
     open_end = [len(w) + 1 >= 220 for w in longest]
     # the last window may also end on a kept token that follows no call: a timestamp reaching the
-    # end of the audio (ref 7359-7441) -- the last result token, forced like the rest
+    # end of the audio (ref 7359-7441) -- the last result token, appended; that window's end is open too
+    # (no <|endoftext|> step: its last token is the decoder's, read back from the result)
     if flat and not open_end[-1] and (not longest[-1] or longest[-1][-1] != flat[-1]):
         longest[-1].append(flat[-1])
+        open_end[-1] = True
     return longest, open_end
 
 

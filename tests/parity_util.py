@@ -198,6 +198,10 @@ class StepForcer:
         if n_tokens > 0:
             self.seen[w].append(int(tokens[n_tokens - 1].id))
         if w >= len(self.windows) or self.start[w] + n_tokens > self.upto:
+            if getattr(self, "kept", None) is not None and w < len(self.windows) and n_tokens <= len(self.windows[w]):
+                win = self.windows[w]
+                self._keep(self.start[w] + n_tokens, win[n_tokens] if n_tokens < len(win) else self.eot,
+                           np.ctypeslib.as_array(logits, shape=(self.n_vocab,)), [int(tokens[i].id) for i in range(n_tokens)])
             return
         win = self.windows[w]
         if n_tokens > len(win) or (n_tokens == len(win) and self.open_end[w]):
@@ -206,6 +210,42 @@ class StepForcer:
         lg = np.ctypeslib.as_array(logits, shape=(self.n_vocab,))
         fin = np.isfinite(lg)
         lg[t] = (float(lg[fin].max()) if fin.any() else 0.0) + 40.0
+
+    def keep_logits(self, beg, space=-1, tid_initial=-1):
+        """record, at every step the decoder decides itself (global step > upto), what a decision between two
+        tokens needs from the logits this call sees (the callback point, ref whisper.cpp:6254), after the
+        filters the reference applies between that point and its timestamp rule (6258-6329: blank suppression
+        at the first step, timestamps in pairs, the initial-timestamp limit `tid_initial` (round(max_initial_ts
+        / 0.02)), timestamps increasing): the top 8 ids' logits, the reference token's logit and the rule's
+        margin |logsumexp(timestamp logits) - max(text logits)| (decision_ties)"""
+        self.beg, self.space, self.tid_initial, self.kept = beg, space, tid_initial, {}
+        return self
+
+    def _keep(self, g, t, lg, prefix):
+        lg = np.where(np.isfinite(lg), lg, -np.inf).astype(np.float64)
+        beg = self.beg
+        if not prefix:
+            if self.space >= 0:
+                lg[self.space] = -np.inf
+            lg[self.eot] = -np.inf
+            if self.tid_initial >= 0:
+                lg[beg + self.tid_initial + 1:] = -np.inf
+        else:
+            last_ts = prefix[-1] >= beg
+            penult_ts = len(prefix) < 2 or prefix[-2] >= beg
+            if last_ts:
+                if penult_ts:
+                    lg[beg:] = -np.inf
+                else:
+                    lg[:self.eot] = -np.inf
+        ts_seen = [x for x in prefix if x >= beg]
+        if ts_seen:
+            lg[beg:ts_seen[-1]] = -np.inf  # decoder.seek_delta / 2 = the last timestamp's index
+        ts = lg[beg:]
+        m = float(ts.max())
+        lse = m + float(np.log(np.exp(ts - m).sum())) if np.isfinite(m) else -np.inf
+        top = np.argpartition(-lg, 8)[:8]
+        self.kept[g] = ({int(i): float(lg[i]) for i in top}, float(lg[t]), abs(lse - float(lg[:beg].max())))
 
     def first_disagreement(self):
         """(global step, decoder pick (-1: ended the window there), reference token) of the first step
@@ -281,6 +321,51 @@ def decision_check(run, tf, arr, key, eot, beg, n_vocab, token_data_type, want_s
     log(f"[decisions] {key}: {n}/{n} steps compared on the reference's prefixes, {len(out)} disagreement(s)"
         + "".join(f"; step {g}: {p} vs {t} ({why})" for g, p, t, why in out))
     return n, out
+
+
+def decision_ties(run, windows, open_end, eot, beg, n_vocab, token_data_type, tie, key, max_iter, log=print, space=-1,
+                  tid_initial=-1, want_tokens=None):
+    """The every-step check for a run no teacher-forced reference fixture covers (configs[4] at 10 minutes,
+    14 312 steps): as decision_check -- force the reference's tokens up to the last disagreement, leave the
+    rest to the decoder, find the next step whose greedy pick differs -- but each disagreement is judged on
+    the GPU's own logits at that step: the two choices (or the timestamp rule's two sides, when a timestamp
+    is involved) must lie within `tie`, the near-tie bound the free-run comparison uses (TIE_FACTOR x the
+    measured logit error). A pick no later call sees (an open window's last step) is read from the result:
+    the run forced through the last disagreement must end on `want_tokens`, the reference's result tokens.
+    At most `max_iter` runs; returns (steps compared on the reference's prefixes, total steps,
+    [(step, pick, reference, gap)])."""
+    tf = {"windows": windows, "open_end": open_end}
+    total = sum(StepForcer(tf, eot, n_vocab, token_data_type, -1).n_steps)
+    upto, out = -1, []
+    for _ in range(max_iter):
+        f = StepForcer(tf, eot, n_vocab, token_data_type, upto).keep_logits(beg, space, tid_initial)
+        segs = run(f.cfunc)
+        d = f.first_disagreement()
+        if d is None:
+            upto = total
+            if want_tokens is not None:
+                assert [t[0] for s in segs for t in s["tokens"]] == list(want_tokens), \
+                    f"{key}: the run forced through step {max([-1] + [o[0] for o in out])} does not end on the reference's tokens"
+            break
+        g, p, t = d
+        assert p != -2, f"{key}: the decoder's windows differ from the reference's at step {g}"
+        top, lt, ts_margin = f.kept[g]
+        pp = eot if p == -1 else p  # -1: the decoder ended the window at this step (its pick: <|endoftext|>)
+        if pp >= beg or t >= beg:  # a timestamp on either side: the timestamp rule decided the step
+            gap, what = ts_margin, "timestamp-rule margin"
+        else:
+            assert pp in top, f"{key} step {g}: the decoder's pick {pp} is not among its own top logits"
+            gap, what = top[pp] - lt, "logit gap"
+        assert gap <= tie, f"{key} step {g}: decoder picks {p}, reference {t}: {what} {gap:.3e} above the tie bound {tie:.3e}"
+        out.append((g, p, t, f"{what} {gap:.2e}"))
+        log(f"[decisions] {key}: run {len(out)}: step {g}: decoder {p}, reference {t} ({what} {gap:.2e})")
+        upto = g
+    n = min(upto, total)
+    log(f"[decisions] {key}: {n}/{total} steps compared on the reference's prefixes, {len(out)} disagreement(s), "
+        f"each within the tie bound {tie:.2e} of the GPU's own logits"
+        + "".join(f"; step {g}: {p} vs {t} ({why})" for g, p, t, why in out)
+        + ("" if n >= total else f"; steps after {n} not compared ({max_iter} runs)"))
+    return n, total, out
 
 
 def check_cross_rows(w, st, arr, key, layer, name, n_rows=16):

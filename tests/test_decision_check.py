@@ -15,7 +15,7 @@ import numpy as np
 import pytest
 
 import owk
-from parity_util import StepForcer, decision_check
+from parity_util import StepForcer, decision_check, decision_ties
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 EOT, BEG, NV = 50, 60, 80
@@ -105,6 +105,36 @@ def test_open_window_has_no_eot_step():
     n, found = decision_check(fake_run(windows, open_end, {}, limit=4), tf, arr, "k", EOT, BEG, NV, owk.TokenData,
                               want_of(windows))
     assert n == 4 and found == []
+
+
+def flat_of(windows):
+    return [t for w in windows for t in w]
+
+
+def test_decision_ties_judged_on_own_logits():
+    """decision_ties (configs[4] at 10 minutes): each disagreement judged by the decoder's own logit gap
+    (1.0 in the scripted decoder) against the tie bound"""
+    windows, open_end = [[1, 2, 3, 4], [5, 6]], [False, False]
+    plant = {1: 9, 6: -1}  # a different token; window 2 ended early (<|endoftext|> at its step 1)
+    n, total, out = decision_ties(fake_run(windows, open_end, plant, limit=6), windows, open_end, EOT, BEG, NV,
+                                  owk.TokenData, 1.5, "k", 8, log=lambda s: None, want_tokens=flat_of(windows))
+    assert n == total == 8 and [(g, p, t) for g, p, t, _ in out] == [(1, 9, 2), (6, -1, 6)]
+    with pytest.raises(AssertionError, match="above the tie bound"):
+        decision_ties(fake_run(windows, open_end, plant, limit=6), windows, open_end, EOT, BEG, NV, owk.TokenData,
+                      0.5, "k", 8, log=lambda s: None)
+
+
+def test_decision_ties_reads_open_window_end_from_result():
+    """the last step of an open window (a timestamp reaching the end of the audio) follows no call: the
+    decoder's pick there is checked through the final run's result tokens"""
+    windows, open_end = [[1, 2, 3]], [True]
+    run = fake_run(windows, open_end, {2: 9}, limit=3)
+    with pytest.raises(AssertionError, match="does not end on the reference's tokens"):
+        decision_ties(run, windows, open_end, EOT, BEG, NV, owk.TokenData, 1.5, "k", 8, log=lambda s: None,
+                      want_tokens=flat_of(windows))
+    n, total, out = decision_ties(fake_run(windows, open_end, {}, limit=3), windows, open_end, EOT, BEG, NV,
+                                  owk.TokenData, 1.5, "k", 8, log=lambda s: None, want_tokens=flat_of(windows))
+    assert n == total == 3 and out == []
 
 
 def test_tf_golden_fixture_consistent():
