@@ -434,9 +434,15 @@ __device__ __forceinline__ void wait_vmcnt() {
 constexpr int AS_MAX_LIST = 2048;  // listed keys (self-attention cells) per row
 
 // CROSS: the head-major cross K/V (non-temporal loads; also names the instantiation so cross
-// and self attention are apart in profiles)
-template <bool LIST, bool CROSS>
-__global__ __launch_bounds__(64) void k_attn_step(const _Float16 * __restrict__ q, int ldq,
+// and self attention are apart in profiles).
+// NW = 2 (cross attention): a loader wave and a math wave per (row, head). Under the full decode step's
+// HBM load a wave's LDS-DMA issue stalls while the memory pipeline is backed up, and with one wave those
+// stalls stopped its math too (SQ_WAIT_INST_ANY 27 % of the wave's cycles at 32 rows x 20 heads x 1500
+// keys, profiles/r05n_attn_cross_ab.txt); the loader wave takes the stalls, the math wave runs on.
+// Hand-off per chunk by two workgroup barriers: B1 (loader: chunk c landed, vmcnt) and B2 (math wave:
+// chunk c is in its registers, so the loader may refill that buffer with chunk c + AS_NBUF).
+template <bool LIST, bool CROSS, int NW = 1>
+__global__ __launch_bounds__(64 * NW) void k_attn_step(const _Float16 * __restrict__ q, int ldq,
                                                   const _Float16 * __restrict__ kb, const _Float16 * __restrict__ vb,
                                                   int ld_kv, int hs, const AttnRow * __restrict__ rows,
                                                   const int * __restrict__ key_idx, float scale,
@@ -447,7 +453,9 @@ __global__ __launch_bounds__(64) void k_attn_step(const _Float16 * __restrict__ 
     // chunk; the host therefore launches LIST = true only for passes with a listed row
     __shared__ __attribute__((aligned(1024))) char smem[AS_NBUF * 2 * AS_TILE];
     __shared__ int s_list[LIST ? AS_MAX_LIST : 1];
-    const int lane = threadIdx.x;
+    static_assert(NW == 1 || (NW == 2 && !LIST), "the two-wave form streams contiguous keys only");
+    const int lane = threadIdx.x & 63;
+    const bool loader = NW == 2 && threadIdx.x < 64;  // wave 0 of a two-wave block
     const AttnRow job = rows[blockIdx.y];
     if (job.mode != 0) return;  // tiled (F32) rows: k_attn_decoder
     const int h = blockIdx.x;
@@ -468,7 +476,7 @@ __global__ __launch_bounds__(64) void k_attn_step(const _Float16 * __restrict__ 
         }
     };
     if (n <= 0) {
-        emit(0.0f);
+        if (!loader) emit(0.0f);
         return;
     }
     // a listed row whose cells are not one contiguous run (the host passes contiguous runs
@@ -492,50 +500,100 @@ __global__ __launch_bounds__(64) void k_attn_step(const _Float16 * __restrict__ 
     for (int c = 0; c < 8; ++c) qv[c] = qp[c];
 
     const int nchunks = (n + AS_KC - 1) / AS_KC;
+    // LDS images of a chunk, 8 keys x 128 B per KB: K rows with their 16-B segments XOR-swizzled
+    // (segment s of key row kk at s ^ (kk & 7): conflict-free lane-per-key ds_read_b128 rows), V rows
+    // plain. The load of row kk = 8i + (lane >> 3) by lane: the XOR term depends on the lane only.
+    const int kseg = (lane & 7) ^ (lane >> 3);
+    const int vseg = lane & 7;
+    // contiguous keys (no cell list): buffer loads off one per-lane offset and a scalar chunk offset (no
+    // per-load 64-bit address math); the resource's range ends at the last key's row, so the rows past n of
+    // a partial last chunk read as nothing from memory (they are never used)
+    const int row_b = ld_kv * 2;
+    const uint32_t range = (uint32_t) (((size_t) (n - 1) * ld_kv + 64) * 2);
+    const __amdgpu_buffer_rsrc_t rk = __builtin_amdgcn_make_buffer_rsrc((void *) kh, (short) 0, range, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc((void *) vh, (short) 0, range, 0x00020000);
+    const int ko = (lane >> 3) * row_b + kseg * 16, vo = (lane >> 3) * row_b + vseg * 16;
     // stage chunk c into buffer b: 8 + 8 loads of 1 KB (8 keys x 128 B each)
     auto stage = [&](int b, int c) {
         char * sK = smem + b * 2 * AS_TILE;
         char * sV = sK + AS_TILE;
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
-            const int kk = i * 8 + (lane >> 3);
-            const int key = min(c * AS_KC + kk, n - 1);
-            const int cell = listed ? s_list[key] : key;
-            const int seg = (lane & 7) ^ (kk & 7);  // K rows XOR-swizzled for the lane-per-key reads
             // cross K/V are read once per decode step (larger than the MALL): non-temporal
-            __builtin_amdgcn_global_load_lds((const void *) (kh + (size_t) cell * ld_kv + seg * 8),
-                                             (lds_ptr_t) (sK + i * 1024), 16, 0, CROSS ? 2 : 0);
-            __builtin_amdgcn_global_load_lds((const void *) (vh + (size_t) cell * ld_kv + (lane & 7) * 8),
-                                             (lds_ptr_t) (sV + i * 1024), 16, 0, CROSS ? 2 : 0);
+            if (listed) {
+                const int kk = i * 8 + (lane >> 3);
+                const int cell = s_list[min(c * AS_KC + kk, n - 1)];
+                __builtin_amdgcn_global_load_lds((const void *) (kh + (size_t) cell * ld_kv + kseg * 8),
+                                                 (lds_ptr_t) (sK + i * 1024), 16, 0, CROSS ? 2 : 0);
+                __builtin_amdgcn_global_load_lds((const void *) (vh + (size_t) cell * ld_kv + vseg * 8),
+                                                 (lds_ptr_t) (sV + i * 1024), 16, 0, CROSS ? 2 : 0);
+            } else {
+                const int so = (c * AS_KC + i * 8) * row_b;
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(rk, (lds_ptr_t) (sK + i * 1024), 16, ko, so, 0, CROSS ? 2 : 0);
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(rv, (lds_ptr_t) (sV + i * 1024), 16, vo, so, 0, CROSS ? 2 : 0);
+            }
         }
     };
 
-    float M = -INFINITY, S = 0.0f;
-    _Float16 acc = (_Float16) 0.0f;  // the reference's F16 VKQ accumulator (VKQ16)
-#pragma unroll
-    for (int c = 0; c < AS_NBUF; ++c)
-        if (c < nchunks) stage(c, c);
-
-    for (int c = 0; c < nchunks; ++c) {
-        // chunk c has landed once at most the chunks staged after it are outstanding
+    // chunk c has landed once at most the chunks staged after it are outstanding
+    auto wait_chunk = [&](int c) {
         const int ahead = min(AS_NBUF - 1, nchunks - 1 - c);
         static_assert(AS_NBUF == 3, "vmcnt ladder below assumes 3 buffers");
         if (ahead == 2) wait_vmcnt<32>();
         else if (ahead == 1) wait_vmcnt<16>();
         else wait_vmcnt<0>();
+    };
+    if (NW == 1 || loader) {
+#pragma unroll
+        for (int c = 0; c < AS_NBUF; ++c)
+            if (c < nchunks) stage(c, c);
+    }
+    if (loader) {
+        for (int c = 0; c < nchunks; ++c) {
+            wait_chunk(c);
+            __builtin_amdgcn_s_barrier();  // B1
+            __builtin_amdgcn_s_barrier();  // B2
+            if (c + AS_NBUF < nchunks) stage(c % AS_NBUF, c + AS_NBUF);
+        }
+        return;
+    }
+
+    float M = -INFINITY, S = 0.0f;
+    _Float16 acc = (_Float16) 0.0f;  // the reference's F16 VKQ accumulator (VKQ16)
+    for (int c = 0; c < nchunks; ++c) {
+        if (NW == 1) wait_chunk(c);
+        else __builtin_amdgcn_s_barrier();  // B1
         const char * sK = smem + (c % AS_NBUF) * 2 * AS_TILE;
         const char * sV = sK + AS_TILE;
         const int base = c * AS_KC;
         const int nk = min(AS_KC, n - base);
 
+        // the chunk's K row (lane = key) and V column (lane = head dim) go to registers first and the
+        // buffer is refilled (chunk c + AS_NBUF) before any math: AS_NBUF chunks stay in flight across
+        // the scores and the sequential part (rows nk.. of a partial chunk are read but not used)
+        half8 krow[8];
+        {
+            const char * kr = sK + lane * 128;
+#pragma unroll
+            for (int cc = 0; cc < 8; ++cc) krow[cc] = *(const half8 *) (kr + ((cc ^ (lane & 7)) << 4));
+        }
+        const _Float16 * vcol = (const _Float16 *) sV + lane;
+        const bool full = nk == AS_KC;
+        _Float16 vv[AS_KC];
+#pragma unroll
+        for (int kk = 0; kk < AS_KC; ++kk) vv[kk] = vcol[kk * 64];
+        if (NW == 2) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // K and V reads of this buffer done
+            __builtin_amdgcn_s_barrier();                       // B2
+        } else if (c + AS_NBUF < nchunks) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // K and V reads of this buffer done
+            stage(c % AS_NBUF, c + AS_NBUF);
+        }
+
         // 2. scores, lane = key: f32 dot2 of f16 pairs, 8 independent partial sums
         float s;
         {
-            const char * kr = sK + lane * 128;
             float part[8];
-            half8 krow[8];  // the whole key row first: one LDS round trip, not four
-#pragma unroll
-            for (int cc = 0; cc < 8; ++cc) krow[cc] = *(const half8 *) (kr + ((cc ^ (lane & 7)) << 4));
 #pragma unroll
             for (int cc = 0; cc < 8; ++cc) {
                 const half8 kv = krow[cc];
@@ -559,19 +617,7 @@ __global__ __launch_bounds__(64) void k_attn_step(const _Float16 * __restrict__ 
         const float vs = nm ? 1.0f : e;
         M = fmaxf(M, __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, pm), 63)));
 
-        // 3. recurrence, lane = head dim. The chunk's V column goes to registers first, so
-        // the chunk's buffer is refilled (chunk c + AS_NBUF) before the sequential part runs:
-        // AS_NBUF chunks stay in flight across it (rows nk.. of a partial chunk hold the
-        // clamped key n-1 and are read but not used)
-        const _Float16 * vcol = (const _Float16 *) sV + lane;
-        const bool full = nk == AS_KC;
-        _Float16 vv[AS_KC];
-#pragma unroll
-        for (int kk = 0; kk < AS_KC; ++kk) vv[kk] = vcol[kk * 64];
-        if (c + AS_NBUF < nchunks) {
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // K and V reads of this buffer done
-            stage(c % AS_NBUF, c + AS_NBUF);
-        }
+        // 3. recurrence, lane = head dim
         if (full && __builtin_amdgcn_ballot_w64(nm) == 0) {
             // no new maximum in the chunk (the common case once the first keys are seen):
             // every ms is 1, so acc*ms and S*ms are exact and each key costs one mixed FMA on
@@ -1173,9 +1219,14 @@ void attn_cross_kernel(hipStream_t s, int which, const _Float16 * q, int ldq, co
                        const _Float16 * vbase, int hs, const AttnRow * rows_dev, int n_rows, int H, float scale,
                        _Float16 * out, int ldo) {
     if (n_rows <= 0) return;
-    if (which != 1) throw std::runtime_error("attn_cross_kernel: only the one-wave kernel (1)");
-    OWK_LAUNCH((k_attn_step<false, true>), dim3(H, n_rows), dim3(64), 0, s, q, ldq, kbase, vbase, 64, hs, rows_dev,
-                       nullptr, scale, out, ldo, nullptr, nullptr, nullptr);
+    if (which == 1)
+        OWK_LAUNCH((k_attn_step<false, true>), dim3(H, n_rows), dim3(64), 0, s, q, ldq, kbase, vbase, 64, hs, rows_dev,
+                           nullptr, scale, out, ldo, nullptr, nullptr, nullptr);
+    else if (which == 2)
+        OWK_LAUNCH((k_attn_step<false, true, 2>), dim3(H, n_rows), dim3(128), 0, s, q, ldq, kbase, vbase, 64, hs,
+                           rows_dev, nullptr, scale, out, ldo, nullptr, nullptr, nullptr);
+    else
+        throw std::runtime_error("attn_cross_kernel: which is 1 (one wave) or 2 (loader + math waves)");
 }
 
 void attn_decoder(hipStream_t s, const _Float16 * q, int ldq, const _Float16 * kbase, const _Float16 * vbase, int ld_kv,
@@ -1190,8 +1241,10 @@ void attn_decoder(hipStream_t s, const _Float16 * q, int ldq, const _Float16 * k
                                rows_dev, key_idx, scale, out, ldo, out32, q8, q8d);
         } else {
             // cross attention (no cell lists): the once-per-step K/V stream, one wave per (row, head)
+            // (the loader + math wave form: RTF 1073 / 1070 vs 1064 with one wave, attn_cross 47.8 vs 48.5 us in
+            // the F16 bench step, bit-identical; profiles/r05n_attn_cross_ab.txt)
             if (!key_idx)
-                OWK_LAUNCH((k_attn_step<false, true>), dim3(H, n_rows), dim3(64), 0, s, q, ldq, kbase, vbase, ld_kv,
+                OWK_LAUNCH((k_attn_step<false, true, 2>), dim3(H, n_rows), dim3(128), 0, s, q, ldq, kbase, vbase, ld_kv,
                                    hs, rows_dev, key_idx, scale, out, ldo, out32, q8, q8d);
             else
                 OWK_LAUNCH((k_attn_step<false, false>), dim3(H, n_rows), dim3(64), 0, s, q, ldq, kbase, vbase, ld_kv,

@@ -1678,22 +1678,25 @@ int owk_debug_gemm_q5(int device, int M, int N, int K, const float * a, const ui
 }
 
 // one_chunk cross attention of R rows (row r over its own clip r: k, v [R][H][T][64] f16 head-major,
-// q [R][H*64]) with the one-wave k_attn_step (which = 1); out [R][H*64] f16.
+// q [R][H*64]) with k_attn_step, one wave (which = 1) or a loader and a math wave (2); out [R][H*64] f16.
 // iters > 0: also returns the mean device time per launch in microseconds (random q/k/v if the host
 // pointers are null); iters == 0 returns 0; -1 on error
 double owk_debug_attn_cross(int device, int which, int R, int H, int T, int n_zero_pad, float scale, const uint16_t * q,
                             const uint16_t * k, const uint16_t * v, uint16_t * out, int iters) {
     try {
-        if (R <= 0 || H <= 0 || T < 0 || n_zero_pad < 0 || which != 1 || iters < 0)
+        if (R <= 0 || H <= 0 || T < 0 || n_zero_pad < 0 || (which != 1 && which != 2) || iters < 0)
             throw std::runtime_error("bad arguments");
         OWK_HIP_CHECK(hipSetDevice(device));
         hipStream_t s;
         OWK_HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
         const size_t nq = (size_t) R * H * 64, nkv = std::max<size_t>((size_t) R * H * T * 64, 64);
+        // random inputs: timed launches rotate over 8 K/V copies, so no launch finds its K/V in the
+        // 256 MB MALL from the one before (as in a decode step, where each layer's cross K/V is cold)
+        const int copies = (q && k && v) ? 1 : 8;
         DevBuf dq, dk, dv, dout, drows;
         dq.alloc(nq * 2);
-        dk.alloc(nkv * 2);
-        dv.alloc(nkv * 2);
+        dk.alloc(nkv * 2 * copies);
+        dv.alloc(nkv * 2 * copies);
         dout.alloc(nq * 2);
         if (q && k && v) {
             OWK_HIP_CHECK(hipMemcpy(dq.ptr, q, nq * 2, hipMemcpyHostToDevice));
@@ -1701,15 +1704,17 @@ double owk_debug_attn_cross(int device, int which, int R, int H, int T, int n_ze
             OWK_HIP_CHECK(hipMemcpy(dv.ptr, v, (size_t) R * H * T * 64 * 2, hipMemcpyHostToDevice));
         } else {
             hipLaunchKernelGGL(k_fill_rand_f16, dim3(1024), dim3(256), 0, s, dq.as<_Float16>(), nq, 3u);
-            hipLaunchKernelGGL(k_fill_rand_f16, dim3(4096), dim3(256), 0, s, dk.as<_Float16>(), nkv, 5u);
-            hipLaunchKernelGGL(k_fill_rand_f16, dim3(4096), dim3(256), 0, s, dv.as<_Float16>(), nkv, 9u);
+            hipLaunchKernelGGL(k_fill_rand_f16, dim3(4096), dim3(256), 0, s, dk.as<_Float16>(), nkv * copies, 5u);
+            hipLaunchKernelGGL(k_fill_rand_f16, dim3(4096), dim3(256), 0, s, dv.as<_Float16>(), nkv * copies, 9u);
         }
         std::vector<AttnRow> rows(R);
         for (int r = 0; r < R; ++r) rows[r] = AttnRow{r, r * H * T * 64, T, -1, n_zero_pad, 0};
         drows.alloc(R * sizeof(AttnRow));
         OWK_HIP_CHECK(hipMemcpy(drows.ptr, rows.data(), R * sizeof(AttnRow), hipMemcpyHostToDevice));
+        int it = 0;
         auto run = [&] {
-            attn_cross_kernel(s, which, dq.as<_Float16>(), H * 64, dk.as<_Float16>(), dv.as<_Float16>(), T * 64,
+            const size_t c = (size_t) (it++ % copies) * nkv;
+            attn_cross_kernel(s, which, dq.as<_Float16>(), H * 64, dk.as<_Float16>() + c, dv.as<_Float16>() + c, T * 64,
                               (const AttnRow *) drows.ptr, R, H, scale, dout.as<_Float16>(), H * 64);
         };
         run();

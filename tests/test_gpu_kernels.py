@@ -84,10 +84,12 @@ def _cross_outputs(R, H, T, pad, which):
 
 @pytest.mark.parametrize("R,H,T,pad", XSHAPES)
 def test_attn_cross_one_wave(R, H, T, pad):
-    """k_attn_step (the production cross-attention kernel, one wave per row and head) against the
-    numpy restatement of the reference's one_chunk recurrence."""
-    q, k, v, scale, outs = _cross_outputs(R, H, T, pad, (1,))
+    """k_attn_step (the cross-attention kernel: one wave per row and head, and the production form with a
+    loader wave beside the math wave) against the numpy restatement of the reference's one_chunk
+    recurrence; the two forms bit-identical"""
+    q, k, v, scale, outs = _cross_outputs(R, H, T, pad, (1, 2))
     assert np.isfinite(outs[1]).all()
+    assert np.array_equal(outs[1].view(np.uint32), outs[2].view(np.uint32))
     for r in range(min(R, 2)):
         for h in range(min(H, 2)):
             ref = _one_chunk_np(q[r, h * 64:(h + 1) * 64], k[r, h], v[r, h], scale, pad)
@@ -101,7 +103,7 @@ def test_attn_cross_speed():
     L.owk_debug_attn_cross.restype = C.c_double
     u16 = C.POINTER(C.c_uint16)
     L.owk_debug_attn_cross.argtypes = [C.c_int] * 6 + [C.c_float, u16, u16, u16, u16, C.c_int]
-    for w, name in ((1, "k_attn_step"),):
+    for w, name in ((1, "k_attn_step one wave"), (2, "k_attn_step loader + math waves")):
         for R in (32, 1):
             t = min(L.owk_debug_attn_cross(0, w, R, 20, 1500, 0, 0.35, None, None, None, None, 30) for _ in range(3))
             print(f"attn_cross {name} R={R}: {t:.1f} us ({R * 20 * 1500 * 64 * 2 * 2 / t / 1e3:.0f} GB/s)")
