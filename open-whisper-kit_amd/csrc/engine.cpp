@@ -490,6 +490,8 @@ void Engine::encode(const std::vector<int> & slots, const std::vector<int> & off
     // cross-attention K/V for every decoder layer (whisper_build_graph_cross, ref 2272-2346)
     const float k_scale = powf(64.0f, -0.25f);
     const size_t layer_stride = (size_t) cap_slots * hp.n_audio_ctx * d;  // capacity; slots of n_ctx() rows inside
+    if ((uint64_t) cap_slots * T * d >= (uint64_t) 1 << 32)  // the KV_CROSS epilogue's 32-bit offsets
+        throw std::runtime_error("encode: cross K/V offsets exceed 32 bits");
     for (int l = 0; l < hp.n_text_layer; ++l) {
         const DecLayerW & L = m->dec[l];
         EpiParams ep;

@@ -90,19 +90,27 @@ __device__ __forceinline__ void epi_row8(const EpiParams & p, int r, int c, cons
             for (int e = 0; e < 8; ++e) epi_store<MODE>(p, r, c + e, acc[e]);
         }
     } else if constexpr (MODE == EPI_KV_CROSS) {
-        const int d = p.d;
-        const int clip = r / p.T, t = r - clip * p.T;
-        const size_t base = (size_t) (p.slot_map ? p.slot_map[clip] : clip) * p.T * d + (size_t) t * 64;
+        // 32-bit offsets (the host checks slots x T x d < 2^32) and the clip by a float reciprocal with an
+        // exact integer fix-up instead of 64-bit products and an integer division: 574 -> 563-567 us per
+        // launch at 32 clips x 1500 rows; the plain F16 epilogue of the same shape runs 346-358 us, so the
+        // rest is the head-major stores (profiles/r05o_gemm_enc_modes.txt)
+        const int d = p.d, T = p.T;
+        int clip = (int) ((float) r * __builtin_amdgcn_rcpf((float) T));
+        clip -= clip * T > r;
+        clip += (clip + 1) * T <= r;
+        const uint32_t t = (uint32_t) (r - clip * T);
+        const uint32_t slot = (uint32_t) (p.slot_map ? p.slot_map[clip] : clip);
+        const uint32_t base = slot * (uint32_t) T * (uint32_t) d + t * 64u;
         if (c < d) {
 #pragma unroll
             for (int e = 0; e < 8; ++e) v[e] = acc[e] * p.scale;
-            *(half8 *) (p.out16b + base + (size_t) (c >> 6) * p.T * 64 + (c & 63)) = to_half8(v);
+            *(half8 *) (p.out16b + (base + (uint32_t) (c >> 6) * (uint32_t) T * 64u + (uint32_t) (c & 63))) = to_half8(v);
         } else {
             const int cv = c - d;
             load8(p.bias2 + cv, bb);
 #pragma unroll
             for (int e = 0; e < 8; ++e) v[e] = acc[e] + bb[e];
-            *(half8 *) (p.out16c + base + (size_t) (cv >> 6) * p.T * 64 + (cv & 63)) = to_half8(v);
+            *(half8 *) (p.out16c + (base + (uint32_t) (cv >> 6) * (uint32_t) T * 64u + (uint32_t) (cv & 63))) = to_half8(v);
         }
     } else if constexpr (MODE == EPI_F32) {
 #pragma unroll

@@ -1327,6 +1327,18 @@ double owk_debug_gemm_bench(int device, int mode, int M, int N, int K, int iters
         ep.out16 = d16.as<_Float16>();
         ep.ldo = N;
         ep.gelu_tab = gtab.as<uint16_t>();
+        if (mode == EPI_QKV_ENC || mode == EPI_KV_CROSS) {  // the encoder's head-major outputs, 1500-row clips
+            ep.d = mode == EPI_QKV_ENC ? N / 3 : N / 2;
+            ep.T = 1500;
+            ep.Tpad = 1536;
+            ep.scale = 1.0f;
+            ep.bias2 = bias.as<float>();
+            ep.out16b = d16.as<_Float16>();
+            ep.out16c = d16.as<_Float16>() + (size_t) M * ep.d;
+            const size_t v_elems = mode == EPI_QKV_ENC ? (size_t) (M / 1500) * ep.d * 1536 : (size_t) M * ep.d;
+            if (M % 1500 != 0 || v_elems > (size_t) M * N - (size_t) M * ep.d)
+                throw std::runtime_error("gemm bench: head-major outputs need M = clips x 1500 and room for V");
+        }
         hipEvent_t e0, e1;
         OWK_HIP_CHECK(hipEventCreate(&e0));
         OWK_HIP_CHECK(hipEventCreate(&e1));
