@@ -116,7 +116,9 @@ def _check_tdtw(meta, diffs, tag):
     attention some path decisions are ties far below any parity bar, and the reference itself flips
     them under that noise (27 / 100 / 75 tokens by seed, in 2-7 runs). Every GPU difference must be
     one of those decisions: a run of tokens shifted alike that overlaps (within 2 tokens) a run some
-    perturbed reference shifts the same way, by no more than the reference's own largest shift."""
+    perturbed reference shifts the same way, by no more than the reference's own largest shift. At 10
+    minutes (teacher-forced floor seeds, make_golden_c4_floor.py --forced) the bar is the reference's own
+    sampling coverage (below)."""
     seeds = meta["results"].get("tdtw_floor_seeds", []) + meta["results"].get("tdtw_floor_tf_seeds", [])
     # a free perturbed run compares t_dtw only over the tokens it shares with the unperturbed one (at 10 minutes
     # the first 1783 of 14 312); the teacher-forced ones (make_golden_c4_floor.py --forced) over the whole clip
@@ -136,10 +138,37 @@ def _check_tdtw(meta, diffs, tag):
           f"{[sd['seed'] for sd in seeds]}): {[sd['n_diff'] for sd in seeds]} tokens, runs "
           f"{sorted({(r[0][0], len(r), r[0][1] - r[0][2]) for r in floor_runs})}")
     for r in got_runs:
-        lo, hi, sh = r[0][0], r[-1][0], r[0][1] - r[0][2]
-        assert abs(sh) <= max_shift, f"{tag}: t_dtw shift {sh} cs beyond the reference's {max_shift}"
-        assert any(f[0][0] - 2 <= hi and lo <= f[-1][0] + 2 and (f[0][1] - f[0][2]) * sh > 0 for f in floor_runs), \
-            f"{tag}: t_dtw run at tokens {lo}..{hi} (shift {sh}) is not a decision the reference flips itself"
+        assert abs(r[0][1] - r[0][2]) <= max_shift, f"{tag}: t_dtw shift {r[0][1] - r[0][2]} cs beyond the reference's {max_shift}"
+    cov = [_flipped(r, floor_runs) for r in got_runs]
+    tf = meta["results"].get("tdtw_floor_tf_seeds", [])
+    if len(tf) < 2:  # every GPU run one of the sampled self-flips (the 60 s fixture: three seeds cover them all)
+        for r, ok in zip(got_runs, cov):
+            assert ok, (f"{tag}: t_dtw run at tokens {r[0][0]}..{r[-1][0]} (shift {r[0][1] - r[0][2]}) is not a "
+                        f"decision the reference flips itself")
+        return
+    # the whole 10-minute clip, teacher-forced: each 1e-7 seed of the reference flips a few hundred tokens, and
+    # no finite set of seeds samples every flippable decision -- the seeds do not even cover each other. The GPU
+    # is held to the reference's own sampling: its runs covered by the seeds' flips at least as well as one seed's
+    # runs are covered by the other seeds', no more tokens moved than a seed moves, no larger shift
+    cross = []
+    for sd in tf:
+        others = [r for o in seeds if o is not sd for r in _runs([tuple(d) for d in o["diffs"]])]
+        own = _runs([tuple(d) for d in sd["diffs"]])
+        cross.append(sum(_flipped(r, others) for r in own) / max(len(own), 1))
+    frac = sum(cov) / max(len(cov), 1)
+    n_max = max(sd["n_diff"] for sd in tf)
+    print(f"[c4] {tag}: {sum(cov)}/{len(cov)} GPU runs are decisions a seed flips ({frac:.2f}); a seed's runs covered by "
+          f"the other seeds: {[round(x, 2) for x in cross]}; tokens moved {len(diffs)} vs the seeds' {[sd['n_diff'] for sd in tf]}")
+    assert len(diffs) <= n_max, f"{tag}: {len(diffs)} t_dtw values moved, more than a perturbed reference moves ({n_max})"
+    assert frac >= min(cross), (f"{tag}: {frac:.2f} of the GPU's t_dtw runs are sampled self-flips, below the "
+                                f"reference's own cross-seed coverage {min(cross):.2f}")
+
+
+def _flipped(r, floor_runs):
+    """a run of tokens shifted alike that overlaps (within 2 tokens) a run some perturbed reference shifts the
+    same way"""
+    lo, hi, sh = r[0][0], r[-1][0], r[0][1] - r[0][2]
+    return any(f[0][0] - 2 <= hi and lo <= f[-1][0] + 2 and (f[0][1] - f[0][2]) * sh > 0 for f in floor_runs)
 
 
 def _params(w, meta):
