@@ -1204,8 +1204,15 @@ void attn_decoder_softmax(hipStream_t s, const _Float16 * q, int ldq, const _Flo
     // blocks AND long rows, 256 otherwise -- measured (test_softmax_attention_split_bit_identical, r05q): one
     // row of <= 200 keys (configs[4]'s self attention) 5.0-5.5 us at 256 threads vs 5.9-6.4 at 1024; 32 rows
     // x 1500 keys 42 vs 60 us; 5 rows x 384 keys 7.7 vs 7.4 us (attn_softmax_force_nt: the test hook's A/B)
-    if (attn_softmax_force_nt == 256 || (attn_softmax_force_nt != 1024 && (n_rows * H > 128 || max_keys <= 256)))
+    // 512 threads for few (row, head) blocks of 257-512 keys (configs[4]'s self attention once the prompt carry
+    // passes 256 keys): one row x 320-448 keys 6.3-6.8 us against 7.2-7.7 at 256 and 6.9-7.3 at 1024 threads
+    // (profiles/r05p_sm_width_sweep.txt)
+    const int f = attn_softmax_force_nt;
+    if (f == 256 || (f == 0 && (n_rows * H > 128 || max_keys <= 256)))
         OWK_LAUNCH(k_attn_softmax<256>, dim3(H, n_rows), dim3(256), 0, s, q, ldq, kbase, vbase, ld_kv, hs, rows_dev,
+                           key_idx, scale, out, ldo, amap, cap, cap_rows, out32);
+    else if (f == 512 || (f == 0 && max_keys <= 512))
+        OWK_LAUNCH(k_attn_softmax<512>, dim3(H, n_rows), dim3(512), 0, s, q, ldq, kbase, vbase, ld_kv, hs, rows_dev,
                            key_idx, scale, out, ldo, amap, cap, cap_rows, out32);
     else
         OWK_LAUNCH(k_attn_softmax<1024>, dim3(H, n_rows), dim3(1024), 0, s, q, ldq, kbase, vbase, ld_kv, hs, rows_dev,

@@ -287,14 +287,14 @@ def test_softmax_attention_split_bit_identical(R, T):
     outs, caps = [], []
     # the split form twice (its arrival tickets must be reset between launches), then the single-block
     # kernel at both widths (outputs do not depend on the width)
-    for split in (0, 1, 1, 256, 1024):
+    for split in (0, 1, 1, 256, 512, 1024):
         o = np.zeros(R * H * 64, np.uint16)
         cp = np.zeros(4 * T * R, np.float32)
         assert f(0, split, R, H, T, o.ctypes.data_as(C.POINTER(C.c_uint16)), cp.ctypes.data_as(C.POINTER(C.c_float)), 3) >= 0
         outs.append(o)
         caps.append(cp)
     assert np.abs(outs[0].view(np.float16).astype(np.float32)).max() > 0
-    for i in (1, 2, 3, 4):
+    for i in (1, 2, 3, 4, 5):
         bad = np.nonzero(outs[0] != outs[i])[0]
         a16, b16 = outs[0].view(np.float16), outs[i].view(np.float16)
         assert bad.size == 0, (f"R={R} T={T}: split outputs differ ({bad.size} values): " +
