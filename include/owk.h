@@ -143,14 +143,6 @@ WHISPER_API int owk_debug_gemm_rows_ln(int device, int M, int N, int K, const fl
 /* test hook: decode passes of at most n rows run the whole-K decoder chain (0 = never; bit-identical to the
  * split-K chain by construction); returns the previous limit */
 WHISPER_API int owk_debug_set_whole_k_rows(int n);
-/* the persistent decode chain (k_chain.hip) of F16 passes of <= 8 rows inside whisper_full: 1 = where it
- * applies, 0 = never (the launch chain; the default: the chain measured slower); returns the previous mode */
-WHISPER_API int owk_debug_set_dec_chain(int mode);
-/* debug: realtime stamps (100 MHz) of decoder layer `layer`'s two chain launches in every later pass (-1: off;
- * eager launches while on); returns the previous layer. owk_debug_dec_chain_stamps copies the state's last
- * stamps [chain 2][block 256][stage 4][6] and returns the words copied */
-WHISPER_API int owk_debug_dec_chain_trace(int layer);
-WHISPER_API int owk_debug_dec_chain_stamps(struct whisper_state * state, unsigned long long * out, int n);
 /* soft_max decoder attention on random data: key-split form (split != 0) or single-block kernel; R rows x H
  * (>= 4) heads x T keys, heads 0..3 captured as alignment heads; out [R][H*64] f16, cap [4][T][R] f32
  * (either may be null); returns us per call over iters timed calls (-1: error) */

@@ -129,58 +129,7 @@ static std::atomic<int> g_whole_k_rows{kWholeKRowsDefault};
 int whole_k_rows() { return g_whole_k_rows.load(std::memory_order_relaxed); }
 int set_whole_k_rows(int n) { return g_whole_k_rows.exchange(n); }
 
-static std::atomic<int> g_dec_chain_mode{0};  // off by default: measured slower (k_chain.hip header)
-int dec_chain_mode() { return g_dec_chain_mode.load(std::memory_order_relaxed); }
-int set_dec_chain_mode(int mode) { return g_dec_chain_mode.exchange(mode); }
-static std::atomic<int> g_dec_chain_trace{-1};
-int set_dec_chain_trace(int layer) { return g_dec_chain_trace.exchange(layer); }
-static size_t chain_trace_words() { return (size_t) 2 * 256 * CH_MAXST * CH_TS; }
-
-size_t Engine::chain_trace(unsigned long long * out, size_t n) {
-    if (!ch_ts_.ptr) return 0;
-    sync();
-    n = std::min(n, chain_trace_words());
-    OWK_HIP_CHECK(hipMemcpy(out, ch_ts_.ptr, n * 8, hipMemcpyDeviceToHost));
-    return n;
-}
-
-void Engine::sync() {
-    OWK_HIP_CHECK(hipStreamSynchronize(stream));
-    if (ch_err_.ptr && *(volatile unsigned *) ch_err_.ptr) {
-        *(volatile unsigned *) ch_err_.ptr = 0;
-        throw std::runtime_error("decode chain: a stage hand-off wait gave up (blocks not co-resident)");
-    }
-}
-
-bool Engine::chain_usable(int rows) {
-    const HParams & hp = m->hp;
-    const int d = hp.n_text_state;
-    if (!chain_allowed || dec_chain_mode() == 0 || m->q5 || rows < 1 || rows > CH_MAXR || d > CH_MAXD || d % 32 ||
-        (rows <= whole_k_rows() && gemm_rows_exact_applies(rows, d)))
-        return false;
-    if (ch_fit_ < 0) {
-        // every stage the chain runs (attn.out / cross_attn.out / mlp.2 partials, cross-Q, mlp.0, Q/K/V)
-        const int grid = dec_chain_grid();
-        ChainStage t[6];
-        t[0].N = d, t[0].K = d, t[0].mode = EPI_PARTIAL;
-        t[1].N = d, t[1].K = 4 * d, t[1].mode = EPI_PARTIAL;
-        t[2].N = d, t[2].K = d, t[2].mode = EPI_F16;
-        t[3].N = 4 * d, t[3].K = d, t[3].mode = EPI_GELU_F16;
-        t[4].N = 3 * d, t[4].K = d, t[4].mode = EPI_QKV_DEC;
-        bool ok = grid > 0 && gemm_partial_splits(d) <= 4 && gemm_partial_splits(4 * d) <= 4;
-        for (int i = 0; i < 5 && ok; ++i) ok = dec_chain_plan(t[i], CH_MAXR, grid);
-        ch_fit_ = ok ? 1 : 0;
-        if (ok) {
-            ch_sync_.alloc(dec_chain_sync_words() * 4);
-            OWK_HIP_CHECK(hipMemsetAsync(ch_sync_.ptr, 0, ch_sync_.bytes, stream));
-            ch_part_.alloc((size_t) (gemm_partial_splits(d) + gemm_partial_splits(4 * d)) * CH_MAXR * d * 4);
-            d_xs_.alloc((size_t) CH_MAXR * d * 4);
-            ch_err_.alloc(64);
-            *(volatile unsigned *) ch_err_.ptr = 0;
-        }
-    }
-    return ch_fit_ == 1;
-}
+void Engine::sync() { OWK_HIP_CHECK(hipStreamSynchronize(stream)); }
 
 void Engine::reserve(int slots, int cells) {
     const HParams & hp = m->hp;
@@ -715,14 +664,9 @@ void Engine::decode(const std::vector<DecodeRow> & rows, const std::vector<int> 
         cap_rows_ = R;
         sh.capture = true;
     }
-    sh.chain = chain_usable(R);
     static const bool no_graph = getenv("OWK_NO_GRAPH") && atoi(getenv("OWK_NO_GRAPH")) != 0;
-    if (sh.chain && g_dec_chain_trace.load() >= 0 && !ch_ts_.ptr) {
-        ch_ts_.alloc(chain_trace_words() * 8);
-        OWK_HIP_CHECK(hipMemsetAsync(ch_ts_.ptr, 0, ch_ts_.bytes, stream));
-    }
-    if ((prof && prof->on) || no_graph || capture || (sh.chain && g_dec_chain_trace.load() >= 0)) {
-        // per-kernel events, debugging, DTW, chain stamps: eager launches
+    if ((prof && prof->on) || no_graph || capture) {
+        // per-kernel events, debugging, DTW: eager launches
         launch_decode(sh);
         return;
     }
@@ -732,8 +676,8 @@ void Engine::decode(const std::vector<DecodeRow> & rows, const std::vector<int> 
         clear_graphs();
         graphs_sig_ = sig;
     }
-    // bits 0-19 R, 20-39 n_logit_rows, 40-47 flags, 48-58 T (the cross head stride baked in), 59 chain
-    const uint64_t shape = ((uint64_t) sh.chain << 59) | ((uint64_t) sh.self_oc << 40) | ((uint64_t) sh.self_tl << 41) |
+    // bits 0-19 R, 20-39 n_logit_rows, 40-47 flags, 48-58 T (the cross head stride baked in)
+    const uint64_t shape = ((uint64_t) sh.self_oc << 40) | ((uint64_t) sh.self_tl << 41) |
                            ((uint64_t) sh.cross_oc << 42) | ((uint64_t) sh.cross_tl << 43) |
                            ((uint64_t) sh.self_sm << 44) | ((uint64_t) sh.cross_sm << 45) |
                            ((uint64_t) sh.self_list << 46) | ((uint64_t) (R <= whole_k_rows()) << 47) |
@@ -1053,18 +997,6 @@ void Engine::fused_part(const DecShape & sh, int r0, int n, hipStream_t s, const
         layernorm_f16(s, x, n, d, m->dec[0].attn_ln_w, m->dec[0].attn_ln_b, hp.eps, xn, d, nullptr, nullptr, nullptr,
                       nullptr);
     }
-    // the persistent chain (k_chain.hip): two launches per layer between the attention launches; the
-    // residual rows alternate between x and the scratch rows xs (a stage's LayerNorm prologue reads the
-    // residual every block of the launch reads while block 0 writes the updated one)
-    const bool chain = sh.chain && !whole_k && n <= CH_MAXR;
-    float * xcur = x;
-    float * xoth = d_xs_.as<float>();
-    float * cp0 = ch_part_.as<float>();
-    float * cp1 = chain ? cp0 + (size_t) gemm_partial_splits(d) * n * d : nullptr;
-    const int grid = chain ? dec_chain_grid() : 0;
-    auto plan = [&](ChainStage & st) {
-        if (!dec_chain_plan(st, n, grid)) throw std::runtime_error("decode chain: stage does not fit");
-    };
     for (int l = 0; l < hp.n_text_layer; ++l) {
         const DecLayerW & L = m->dec[l];
         const DecLayerW * nx = l + 1 < hp.n_text_layer ? &m->dec[l + 1] : nullptr;
@@ -1072,9 +1004,7 @@ void Engine::fused_part(const DecShape & sh, int r0, int n, hipStream_t s, const
         _Float16 * Vl = self_v_.as<_Float16>() + l * self_stride;
         const _Float16 * Kc = cross_k_.as<_Float16>() + l * cross_stride;
         const _Float16 * Vc = cross_v_.as<_Float16>() + l * cross_stride;
-        if (chain && l > 0) {
-            // Q/K/V of this layer ran as the last stage of the previous layer's chain B
-        } else {
+        {
             EpiParams ep;
             ep.bias = L.b_q;
             ep.bias2 = L.b_v;
@@ -1099,25 +1029,8 @@ void Engine::fused_part(const DecShape & sh, int r0, int n, hipStream_t s, const
                 attn_decoder_softmax(s, q_abs, d, Kl, Vl, 64, kv_cells * 64, d_rs, n, d_keys, H, 1.0f, max_keys, ao_abs,
                                      d, nullptr, nullptr, 0, nullptr);
         }
-        if (chain) {
-            // A: attn.out partials -> residual + cross_attn_ln -> cross_attn.query
-            ChainArgs a;
-            a.M = n, a.d = d, a.n_stages = 2, a.eps = hp.eps;
-            a.sync = ch_sync_.as<unsigned>(), a.err = ch_err_.as<unsigned>();
-            if (l == g_dec_chain_trace.load() && ch_ts_.ptr) a.ts = ch_ts_.as<unsigned long long>();
-            ChainStage & s0 = a.st[0];
-            s0.N = d, s0.K = d, s0.mode = EPI_PARTIAL, s0.Wt = L.t_o, s0.A = aob, s0.part = cp0;
-            plan(s0);
-            ChainStage & s1 = a.st[1];
-            s1.N = d, s1.K = d, s1.mode = EPI_F16, s1.Wt = L.t_cq;
-            s1.ln_part = cp0, s1.ln_ks = s0.KS, s1.ln_bias = L.b_o, s1.x_in = xcur, s1.x_out = xoth;
-            s1.lnw = L.cross_ln_w, s1.lnb = L.cross_ln_b;
-            s1.ep.bias = L.cb_q, s1.ep.out16 = qb, s1.ep.ldo = d;
-            plan(s1);
-            ProfScope ps(prof, s, "dec_chain", 2.0 * n * 2.0 * d * d, 2.0 * 2.0 * d * d);
-            dec_chain(s, a);
-        } else {
-            resid(aob, L.t_o, d, L.b_o, L.cross_ln_w, L.cross_ln_b);
+        resid(aob, L.t_o, d, L.b_o, L.cross_ln_w, L.cross_ln_b);
+        {
             EpiParams ep;
             ep.bias = L.cb_q;
             ep.out16 = qb;
@@ -1133,61 +1046,16 @@ void Engine::fused_part(const DecShape & sh, int r0, int n, hipStream_t s, const
                                      sh.capture ? amap_.as<int>() + l * H : nullptr,
                                      sh.capture ? cap_.as<float>() : nullptr, sh.R, nullptr, smw, smw_floats);
         }
-        if (chain) {
-            // B: cross_attn.out partials -> residual + mlp_ln -> mlp.0 + GELU -> mlp.2 partials -> residual +
-            // the next layer's attn_ln -> its Q/K/V (the last layer: the residual update alone, into x)
-            ChainArgs a;
-            a.M = n, a.d = d, a.n_stages = 4, a.eps = hp.eps;
-            a.sync = ch_sync_.as<unsigned>(), a.err = ch_err_.as<unsigned>();
-            if (l == g_dec_chain_trace.load() && ch_ts_.ptr) a.ts = ch_ts_.as<unsigned long long>() + 256 * CH_MAXST * CH_TS;
-            ChainStage & s0 = a.st[0];
-            s0.N = d, s0.K = d, s0.mode = EPI_PARTIAL, s0.Wt = L.t_co, s0.A = aob, s0.part = cp0;
-            plan(s0);
-            ChainStage & s1 = a.st[1];
-            s1.N = 4 * d, s1.K = d, s1.mode = EPI_GELU_F16, s1.Wt = L.t_mlp0;
-            s1.ln_part = cp0, s1.ln_ks = s0.KS, s1.ln_bias = L.cb_o, s1.x_in = xoth, s1.x_out = xcur;
-            s1.lnw = L.mlp_ln_w, s1.lnb = L.mlp_ln_b;
-            s1.ep.bias = L.b_mlp0, s1.ep.gelu_tab = m->gelu_tab, s1.ep.out16 = hr, s1.ep.ldo = 4 * d;
-            plan(s1);
-            ChainStage & s2 = a.st[2];
-            s2.N = d, s2.K = 4 * d, s2.mode = EPI_PARTIAL, s2.Wt = L.t_mlp1, s2.A = hr, s2.a_handoff = 1, s2.part = cp1;
-            plan(s2);
-            ChainStage & s3 = a.st[3];
-            s3.ln_part = cp1, s3.ln_ks = s2.KS, s3.ln_bias = L.b_mlp1, s3.x_in = xcur;
-            if (nx) {
-                s3.N = 3 * d, s3.K = d, s3.mode = EPI_QKV_DEC, s3.Wt = nx->t_qkv;
-                s3.x_out = xoth, s3.lnw = nx->attn_ln_w, s3.lnb = nx->attn_ln_b;
-                EpiParams & ep = s3.ep;
-                ep.bias = nx->b_q;
-                ep.bias2 = nx->b_v;
-                ep.scale = kq_scale;
-                ep.out16 = qb;
-                ep.ldo = d;
-                ep.out16b = self_k_.as<_Float16>() + (l + 1) * self_stride;
-                ep.out16c = self_v_.as<_Float16>() + (l + 1) * self_stride;
-                ep.d = d;
-                ep.row_off = d_rowoff;
-                ep.Tpad = kv_cells * 64;
-                plan(s3);
-            } else {
-                s3.x_out = x;  // in place when xcur == x: only block 0 runs a residual-only stage
-            }
-            ProfScope ps(prof, s, "dec_chain", 2.0 * n * (8.0 * d * d + (nx ? 3.0 * d * d : 0.0)),
-                         2.0 * (9.0 * d * d + (nx ? 3.0 * d * d : 0.0)));
-            dec_chain(s, a);
-            std::swap(xcur, xoth);
-        } else {
-            resid(aob, L.t_co, d, L.cb_o, L.mlp_ln_w, L.mlp_ln_b);
-            {
-                EpiParams ep;
-                ep.bias = L.b_mlp0;
-                ep.gelu_tab = m->gelu_tab;
-                ep.out16 = hr;
-                ep.ldo = 4 * d;
-                consumer(EPI_GELU_F16, 4 * d, L.mlp_ln_w, L.mlp_ln_b, L.t_mlp0, ep, 0);
-            }
-            resid(hr, L.t_mlp1, 4 * d, L.b_mlp1, nx ? nx->attn_ln_w : nullptr, nx ? nx->attn_ln_b : nullptr);
+        resid(aob, L.t_co, d, L.cb_o, L.mlp_ln_w, L.mlp_ln_b);
+        {
+            EpiParams ep;
+            ep.bias = L.b_mlp0;
+            ep.gelu_tab = m->gelu_tab;
+            ep.out16 = hr;
+            ep.ldo = 4 * d;
+            consumer(EPI_GELU_F16, 4 * d, L.mlp_ln_w, L.mlp_ln_b, L.t_mlp0, ep, 0);
         }
+        resid(hr, L.t_mlp1, 4 * d, L.b_mlp1, nx ? nx->attn_ln_w : nullptr, nx ? nx->attn_ln_b : nullptr);
     }
 }
 

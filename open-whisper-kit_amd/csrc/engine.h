@@ -81,17 +81,7 @@ struct DecShape {
     bool self_list = false;                     // a one_chunk self row whose cells are not one run
     int n_clips = 0;                            // distinct clips (cross K/V slots) among the rows: the
                                                 // cross K/V a pass must read is per clip, not per row
-    bool chain = false;                         // the persistent decode chain (k_chain.hip) runs the layers
 };
-
-// the persistent decode chain (k_chain.hip) for F16 passes of <= CH_MAXR rows: 1 = used where it applies,
-// 0 = never (the default: it measured slower than the launch chain, k_chain.hip header); the test hook
-// owk_debug_set_dec_chain switches it (tests/test_gpu_chain.py compares the two bit for bit)
-int dec_chain_mode();
-int set_dec_chain_mode(int mode);
-// debug: stamp the two chain launches of decoder layer `layer` (-1: off) of every later pass, with eager
-// launches; Engine::chain_trace returns the last pass's stamps [chain][block][stage][CH_TS]
-int set_dec_chain_trace(int layer);
 
 // per-step bookkeeping of the emulated reference state->logits buffer (no-speech prob)
 struct StepPost {
@@ -163,19 +153,9 @@ public:
     void load_logits_state(int slot, const std::vector<float> & rowmax, const std::vector<float> & row0);
     static constexpr int RMX = 512;  // rows of the emulated buffer tracked per slot (>= n_text_ctx)
 
-    void sync();  // also raises a persistent-chain hand-off timeout of the work it waited for
-
-    // set by full_batch while it holds the device's chain lock (at most one chain launch in flight per
-    // device: its blocks wait on each other, so they must all be resident)
-    bool chain_allowed = false;
-    size_t chain_trace(unsigned long long * out, size_t n);  // debug stamps (set_dec_chain_trace)
+    void sync();
 
 private:
-    bool chain_usable(int rows);  // this pass may run the persistent chain (allocates its buffers)
-    DevBuf ch_sync_, ch_part_, d_xs_;  // arrival counts, split-K partials of two stages, residual ping-pong rows
-    PinnedBuf ch_err_;                 // host-mapped hand-off timeout word
-    DevBuf ch_ts_;                     // debug stamps of the traced layer's two launches
-    int ch_fit_ = -1;                  // the model's stage plans fit the chain (-1: not yet checked)
 
     void launch_decode(const DecShape & sh);
     // the F16 <= 32-row chain (embedding, every layer) of rows [r0, r0 + n) on stream s with GEMM

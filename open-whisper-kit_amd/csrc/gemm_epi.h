@@ -1,4 +1,4 @@
-// Device helpers of the f16 GEMMs shared by k_gemm.hip and k_chain.hip: the fused epilogue values
+// Device helpers of the f16 GEMMs (k_gemm.hip): the fused epilogue values
 // (gelu_lookup, f16_rn, epi_store) and the fixed wave order of the decode-row reductions.
 #pragma once
 

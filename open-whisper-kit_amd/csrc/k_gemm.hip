@@ -13,7 +13,7 @@
 
 namespace owk {
 
-// the GEMM epilogues and the decode-row reduction order live in gemm_epi.h (shared with k_chain.hip)
+// the GEMM epilogues and the decode-row reduction order live in gemm_epi.h
 
 // Eight consecutive outputs (row r, columns c .. c+7; c % 8 == 0) of one lane: the same values as
 // eight epi_store calls, written with 16-byte vector accesses where the mode's layout allows (the
@@ -1510,25 +1510,6 @@ static RowsPlan rows_plan(int K, bool partial) {
     const int per = (nsteps + p.KS - 1) / p.KS;
     p.nw = (per + p.J - 1) / p.J;
     return p;
-}
-
-// a persistent-chain stage (k_chain.hip) runs the decode-row launch's plan: the same k-steps per wave,
-// waves and k splits, so every output is the same MFMA chain summed in the same wave order
-bool dec_chain_plan(ChainStage & st, int M, int grid) {
-    if (st.N <= 0) return true;
-    if (M < 1 || M > CH_MAXR || st.N % 16 || st.K % 32) return false;
-    const RowsPlan p = rows_plan(st.K, st.mode == EPI_PARTIAL);
-    if (p.J > CH_J || p.nw > GR_MAXW || (st.mode != EPI_PARTIAL && p.KS != 1)) return false;
-    st.J = p.J;
-    st.nw = p.nw;
-    st.KS = p.KS;
-    const int tiles = st.N / 16;
-    for (int tpi = 1; tpi <= CH_TPI; ++tpi)
-        if (((tiles + tpi - 1) / tpi) * p.KS <= grid) {
-            st.tpi = tpi;
-            return true;
-        }
-    return false;
 }
 
 template <template <int> class L, typename... Args> static void dispatch_mode(int mode, Args &&... args) {

@@ -102,52 +102,6 @@ void gemm_rows_res(hipStream_t s, int M, int N, int K, const _Float16 * A, const
                    float * x);
 void gemm_rows_lnx(hipStream_t s, int mode, int order, int M, int N, int K, const float * x, const float * lnw,
                    const float * lnb, float eps, const _Float16 * Wt, const EpiParams & ep);
-// ---------------------------------------------------------------------------------
-// Persistent decode chain (k_chain.hip): the decode-row GEMMs and residual + LayerNorm launches between
-// two attention launches of a pass of <= CH_MAXR rows as ONE launch of one block per item. Stage s + 1
-// starts when every item of stage s has published its outputs (write-through stores, an arrival count);
-// each block requests its next stage's weight tiles before it waits, and a stage with a LayerNorm
-// prologue recomputes the residual row and its LayerNorm in every block from the previous stage's
-// split-K partials -- the arithmetic of k_gemm_rows + k_resid_layernorm, output for output.
-// ---------------------------------------------------------------------------------
-constexpr int CH_MAXST = 4;    // stages per launch
-constexpr int CH_MAXR = 8;     // rows per pass
-constexpr int CH_MAXD = 2048;  // LayerNorm width (the GEMM K of a prologue stage)
-constexpr int CH_J = 4;        // k-steps per wave (rows_plan: J <= 4 for K <= 5120)
-constexpr int CH_TPI = 2;      // 16-column tiles per item
-constexpr int CH_TS = 6;       // debug stamps per stage: entry, weights issued, hand-off seen, LayerNorm, MFMA, published
-struct ChainStage {
-    int N = 0, K = 0;           // GEMM shape; N = 0: residual update only (no GEMM, one item)
-    int J = 0, nw = 0, KS = 1;  // rows_plan(K, mode == EPI_PARTIAL)
-    int tpi = 1;                // column tiles per item
-    int mode = EPI_PARTIAL;     // EPI_PARTIAL, EPI_F16, EPI_GELU_F16 (hand-off output) or EPI_QKV_DEC
-    const _Float16 * Wt = nullptr;  // tiled weights (tile_weights)
-    const _Float16 * A = nullptr;   // input rows [M][K] f16 when there is no LayerNorm prologue
-    int a_handoff = 0;              // A is written by an earlier stage of the launch
-    float * part = nullptr;         // EPI_PARTIAL: [KS][M][N]
-    // LayerNorm prologue (ln_part != null): x_out = x_in + (sum of ln_ks splits of ln_part + ln_bias)
-    // (block 0 stores x_out), A = f16(LayerNorm(x_out) * lnw + lnb) in LDS (no lnw: residual only)
-    const float * ln_part = nullptr;
-    int ln_ks = 0;
-    const float * ln_bias = nullptr;
-    const float * x_in = nullptr;
-    float * x_out = nullptr;
-    const float * lnw = nullptr, * lnb = nullptr;
-    EpiParams ep;
-};
-struct ChainArgs {
-    int M = 0, d = 0, n_stages = 0;
-    float eps = 0.0f;
-    unsigned * sync = nullptr;  // dec_chain_sync_words() zeroed words (arrival counts; left zero by each launch)
-    unsigned * err = nullptr;   // host-mapped word: set to 1 when a hand-off wait gave up
-    unsigned long long * ts = nullptr;  // debug: per block and stage CH_TS realtime stamps (null: none)
-    ChainStage st[CH_MAXST];
-};
-// fills st.J / nw / KS / tpi for an (N, K) stage; false if the stage does not fit the chain (grid blocks)
-bool dec_chain_plan(ChainStage & st, int M, int grid);
-int dec_chain_grid();          // blocks per launch
-size_t dec_chain_sync_words();
-void dec_chain(hipStream_t s, const ChainArgs & a);
 bool gemm_rows_ln_applies(int M, int N, int K);
 void gemm_rows_ln(hipStream_t s, int mode, int M, int N, int K, const float * x, const float * lnw, const float * lnb,
                   float eps, const _Float16 * Wt, const EpiParams & ep, bool debug_no_stats = false);

@@ -2033,16 +2033,5 @@ int owk_debug_gemm_rows_ln(int device, int M, int N, int K, const float * x, con
 // test hook: decode passes of at most n rows take the whole-K chain (engine.cpp; 0 = never); returns
 // the previous limit. Both chains must give the same bits (tests/test_gpu_kernels.py).
 int owk_debug_set_whole_k_rows(int n) { return set_whole_k_rows(n); }
-int owk_debug_set_dec_chain(int mode) { return set_dec_chain_mode(mode); }
-int owk_debug_dec_chain_trace(int layer) { return set_dec_chain_trace(layer); }
-int owk_debug_dec_chain_stamps(struct whisper_state * state, unsigned long long * out, int n) {
-    if (!state || !state->eng || !out || n <= 0) return 0;
-    try {
-        return (int) state->eng->chain_trace(out, (size_t) n);
-    } catch (const std::exception & e) {
-        log_msg(GGML_LOG_LEVEL_ERROR, "owk_debug_dec_chain_stamps: %s\n", e.what());
-        return -1;
-    }
-}
 
 }  // extern "C"

@@ -13,7 +13,6 @@
 #include <cmath>
 #include <cstring>
 #include <map>
-#include <mutex>
 #include <regex>
 #include <set>
 
@@ -829,26 +828,6 @@ int prepare_decode_call(whisper_state * st, int slot, const std::vector<CallToke
     return cell0;
 }
 
-// the persistent decode chain (k_chain.hip) waits across the blocks of a launch, so they must all be
-// resident: at most one engine per device may have chain launches in flight. A call that gets the
-// device's lock lets its engine use the chain for the whole call (whose work is synchronised before it
-// returns); a concurrent call on another state runs the launch chain instead (same results).
-static std::mutex g_chain_mu[16];
-struct ChainLock {
-    Engine & e;
-    std::unique_lock<std::mutex> lk;
-    ChainLock(Engine & e_, int dev) : e(e_), lk(g_chain_mu[dev & 15], std::try_to_lock) { e.chain_allowed = lk.owns_lock(); }
-    ~ChainLock() {
-        if (lk.owns_lock()) {
-            try {
-                e.sync();
-            } catch (...) {
-            }
-        }
-        e.chain_allowed = false;
-    }
-};
-
 int full_batch(whisper_context * ctx, whisper_state ** states, const whisper_full_params * params_v,
                const owk_full_ext * ext, const float * const * samples, const int * n_samples, int n_clips) {
     if (n_clips <= 0) return 0;
@@ -861,7 +840,6 @@ int full_batch(whisper_context * ctx, whisper_state ** states, const whisper_ful
     if (!st0->eng) st0->eng.reset(new Engine(&M, &ctx->prof));
     configure_engine(ctx, st0);
     Engine & eng = *st0->eng;
-    ChainLock chain_lock(eng, M.device);
 
     // capacity: one slot per clip; self-KV cells for the largest decoder count
     int n_dec_max = params.strategy == WHISPER_SAMPLING_GREEDY ? params.greedy.best_of

@@ -170,8 +170,6 @@ def main():
                     help="sequential mode: diarize after the transcription instead of beside it")
     ap.add_argument("--whole-k-rows", type=int, default=None,
                     help="A/B: decode passes of at most this many rows take the whole-K chain (engine default if unset)")
-    ap.add_argument("--dec-chain", type=int, default=None,
-                    help="A/B: 0 = the launch chain for every pass, 1 = the persistent chain where it applies (default)")
     args = ap.parse_args()
     cache = os.environ.get("OWK_MODEL_CACHE", "/tmp/owk_models")
     model = S.ensure_model("large-v3", cache_dir=cache)
@@ -187,10 +185,6 @@ def main():
         import ctypes as C
         owk.load().owk_debug_set_whole_k_rows.argtypes = [C.c_int]
         owk.load().owk_debug_set_whole_k_rows(args.whole_k_rows)
-    if args.dec_chain is not None:
-        import ctypes as C
-        owk.load().owk_debug_set_dec_chain.argtypes = [C.c_int]
-        owk.load().owk_debug_set_dec_chain(args.dec_chain)
     w = owk.Whisper(model, flash_attn=False, dtw_preset=AHEADS_LARGE_V3)
     sf = SF.Sortformer(sf_path)
     import ctypes as C
