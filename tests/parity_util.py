@@ -197,12 +197,13 @@ class StepForcer:
         w = self.window
         if n_tokens > 0:
             self.seen[w].append(int(tokens[n_tokens - 1].id))
+        keep = getattr(self, "kept", None) is not None and w < len(self.windows) and n_tokens <= len(self.windows[w])
         if w >= len(self.windows) or self.start[w] + n_tokens > self.upto:
-            if getattr(self, "kept", None) is not None and w < len(self.windows) and n_tokens <= len(self.windows[w]):
-                win = self.windows[w]
-                self._keep(self.start[w] + n_tokens, win[n_tokens] if n_tokens < len(win) else self.eot,
-                           np.ctypeslib.as_array(logits, shape=(self.n_vocab,)), [int(tokens[i].id) for i in range(n_tokens)])
+            if keep:
+                self._keep_step(w, n_tokens, tokens, logits)
             return
+        if keep and self.every:  # decision_forced: the decoder's view of this step before it is forced
+            self._keep_step(w, n_tokens, tokens, logits)
         win = self.windows[w]
         if n_tokens > len(win) or (n_tokens == len(win) and self.open_end[w]):
             return
@@ -211,14 +212,22 @@ class StepForcer:
         fin = np.isfinite(lg)
         lg[t] = (float(lg[fin].max()) if fin.any() else 0.0) + 40.0
 
-    def keep_logits(self, beg, space=-1, tid_initial=-1):
+    def _keep_step(self, w, n_tokens, tokens, logits):
+        win = self.windows[w]
+        self._keep(self.start[w] + n_tokens, win[n_tokens] if n_tokens < len(win) else self.eot,
+                   np.ctypeslib.as_array(logits, shape=(self.n_vocab,)), [int(tokens[i].id) for i in range(n_tokens)])
+
+    def keep_logits(self, beg, space=-1, tid_initial=-1, every=False):
         """record, at every step the decoder decides itself (global step > upto), what a decision between two
         tokens needs from the logits this call sees (the callback point, ref whisper.cpp:6254), after the
         filters the reference applies between that point and its timestamp rule (6258-6329: blank suppression
         at the first step, timestamps in pairs, the initial-timestamp limit `tid_initial` (round(max_initial_ts
         / 0.02)), timestamps increasing): the top 8 ids' logits, the reference token's logit and the rule's
-        margin |logsumexp(timestamp logits) - max(text logits)| (decision_ties)"""
-        self.beg, self.space, self.tid_initial, self.kept = beg, space, tid_initial, {}
+        margin |logsumexp(timestamp logits) - max(text logits)| (decision_ties) and the decoder's own pick from
+        those logits: the timestamp rule (ref 6331-6357: every text logit dropped when the timestamp log-mass
+        exceeds the best text logit), then the greedy argmax of whisper_sample_token. every: record the steps
+        that are forced too (decision_forced), from the logits the decoder computed before the forcing"""
+        self.beg, self.space, self.tid_initial, self.kept, self.every = beg, space, tid_initial, {}, every
         return self
 
     def _keep(self, g, t, lg, prefix):
@@ -245,7 +254,9 @@ class StepForcer:
         m = float(ts.max())
         lse = m + float(np.log(np.exp(ts - m).sum())) if np.isfinite(m) else -np.inf
         top = np.argpartition(-lg, 8)[:8]
-        self.kept[g] = ({int(i): float(lg[i]) for i in top}, float(lg[t]), abs(lse - float(lg[:beg].max())))
+        text_max = float(lg[:beg].max())
+        pick = beg + int(np.argmax(ts)) if lse > text_max else int(np.argmax(lg))
+        self.kept[g] = ({int(i): float(lg[i]) for i in top}, float(lg[t]), abs(lse - text_max), pick)
 
     def first_disagreement(self):
         """(global step, decoder pick (-1: ended the window there), reference token) of the first step
@@ -295,6 +306,17 @@ def decision_check(run, tf, arr, key, eot, beg, n_vocab, token_data_type, want_s
         raise AssertionError(f"{key}: more than {max_iter} disagreeing steps: {found}")
     assert [t[0] for s in segs for t in s["tokens"]] == [t[0] for s in want_segments for t in s["tokens"]], \
         f"{key}: the run forced through step {upto} does not end on the reference's tokens"
+    out = judge_disagreements(found, tf, arr, key, eot, beg)
+    n = sum(StepForcer(tf, eot, n_vocab, token_data_type, -1).n_steps)
+    log(f"[decisions] {key}: {n}/{n} steps compared on the reference's prefixes, {len(out)} disagreement(s)"
+        + "".join(f"; step {g}: {p} vs {t} ({why})" for g, p, t, why in out))
+    return n, out
+
+
+def judge_disagreements(found, tf, arr, key, eot, beg):
+    """[(global step, decoder pick (-1: ended the window), reference token)] -> the reason each is a step the
+    reference does not decide itself (tf_golden format: `realisations` flips, per-step `floor` / `floor_ts`,
+    the base run's candidates and timestamp margin); an AssertionError for any other"""
     flips = {}
     for name, r in tf["realisations"].items():
         for g, _, _ in r["flips"]:
@@ -317,10 +339,37 @@ def decision_check(run, tf, arr, key, eot, beg, n_vocab, token_data_type, want_s
         assert gap <= bound, (f"{key} step {g}: decoder picks {p}, reference {t}: the reference's {what} {gap:.3e} is "
                               f"above 2x its own per-step floor {bound / 2:.3e} and no realisation of it flips the step")
         out.append((g, p, t, f"{what} {gap:.2e} <= 2 x reference floor {bound / 2:.2e}"))
-    n = sum(StepForcer(tf, eot, n_vocab, token_data_type, -1).n_steps)
-    log(f"[decisions] {key}: {n}/{n} steps compared on the reference's prefixes, {len(out)} disagreement(s)"
-        + "".join(f"; step {g}: {p} vs {t} ({why})" for g, p, t, why in out))
-    return n, out
+    return out
+
+
+def decision_forced(run, tf, arr, key, eot, beg, n_vocab, token_data_type, want_tokens, space=-1, tid_initial=-1,
+                    watch=None, log=print, pre=None):
+    """Every decode step compared with the reference's decision on the same prefix, in ONE run: the run is
+    teacher-forced onto the reference's tokens at every step, and at each step the decoder's own greedy pick
+    is derived from the logits it computed on that prefix, through the reference's filters between the
+    callback point and its pick (StepForcer.keep_logits: blank suppression at a window's first step
+    (`space`), timestamp pairs, the initial-timestamp limit `tid_initial`, increasing timestamps, the
+    timestamp rule, argmax). Each step whose pick differs from the reference's token is judged as
+    decision_check judges it (judge_disagreements: a reference self-flip or within 2x its per-step floor).
+    The run must end on `want_tokens` (an open window's last pick, which no later callback sees, included).
+    Returns (steps compared, [(step, pick, reference, reason)])."""
+    total = sum(StepForcer(tf, eot, n_vocab, token_data_type, -1).n_steps)
+    f = StepForcer(tf, eot, n_vocab, token_data_type, total, watch, pre).keep_logits(beg, space, tid_initial, every=True)
+    segs = run(f.cfunc)
+    assert [t[0] for s in segs for t in s["tokens"]] == list(want_tokens), f"{key}: the forced run left the reference's tokens"
+    assert len(f.kept) == total, f"{key}: {len(f.kept)} of {total} steps seen"
+    found = []
+    for w, win in enumerate(tf["windows"]):
+        for k in range(f.n_steps[w]):
+            g = f.start[w] + k
+            t = win[k] if k < len(win) else eot
+            p = f.kept[g][3]
+            if p != t:
+                found.append((g, -1 if p == eot else p, t))
+    out = judge_disagreements(found, tf, arr, key, eot, beg)
+    log(f"[decisions] {key}: {total}/{total} steps compared on the reference's prefixes (one forced run), "
+        f"{len(out)} disagreement(s)" + "".join(f"; step {g}: {p} vs {t} ({why})" for g, p, t, why in out))
+    return total, out
 
 
 def decision_ties(run, windows, open_end, eot, beg, n_vocab, token_data_type, tie, key, max_iter, log=print, space=-1,
@@ -349,7 +398,7 @@ def decision_ties(run, windows, open_end, eot, beg, n_vocab, token_data_type, ti
             break
         g, p, t = d
         assert p != -2, f"{key}: the decoder's windows differ from the reference's at step {g}"
-        top, lt, ts_margin = f.kept[g]
+        top, lt, ts_margin, _ = f.kept[g]
         pp = eot if p == -1 else p  # -1: the decoder ended the window at this step (its pick: <|endoftext|>)
         if pp >= beg or t >= beg:  # a timestamp on either side: the timestamp rule decided the step
             gap, what = ts_margin, "timestamp-rule margin"

@@ -18,7 +18,8 @@ import numpy as np
 import pytest
 
 import owk
-from parity_util import LOGIT_RTOL, MIN_COMPARED, LogitError, check_cross_rows, compare_all_steps, compare_segments
+from parity_util import (LOGIT_RTOL, MIN_COMPARED, LogitError, check_cross_rows, compare_all_steps, compare_segments,
+                         decision_check, decision_forced)
 from recording import Injector
 
 pytestmark = pytest.mark.gpu
@@ -197,6 +198,41 @@ def test_whisper_full(lib, golden, tf_golden, model_path, clips, model, clip, cf
             assert r == want["ret"]
             return w.segments(s2)
         compare_all_steps(w, tf_golden, key, run, want["segments"], n_cmp)
+
+
+@pytest.mark.parametrize("model", ["tiny", "l3-mini", "tiny.en"])
+def test_forced_decisions_match_iterative(lib, golden, tf_golden, model_path, clips, model):
+    """decision_forced (ONE run forced at every step; each step's greedy pick derived from the logits the decoder
+    computed on the reference's prefix, through the reference's filters after the callback point) finds exactly
+    the disagreements decision_check finds, whose picks are the decoder's own (free after each forced prefix).
+    This pins the derivation the configs[4] 10-minute every-step check (tests/test_gpu_c4.py) rests on."""
+    meta, _ = golden
+    key = f"{model}/synth30/full/greedy"
+    if tf_golden is None or key not in tf_golden[0]["cases"]:
+        pytest.skip("no teacher-forced fixture")
+    tmeta, tarr = tf_golden
+    w = whisper(model_path, model)
+    L = w.L
+    L.whisper_token_beg.argtypes = [C.c_void_p]
+    eot, beg = L.whisper_token_eot(w.ctx), L.whisper_token_beg(w.ctx)
+    L.whisper_tokenize.argtypes = [C.c_void_p, C.c_char_p, C.POINTER(C.c_int32), C.c_int]
+    buf = (C.c_int32 * 4)()
+    assert L.whisper_tokenize(w.ctx, b" ", buf, 4) == 1
+    want = meta["results"][key]
+
+    def run(cfunc):
+        s2 = w.new_state()
+        p2, _ = _cfg_params(w, CONFIGS["greedy"])
+        assert p2.suppress_blank and abs(p2.max_initial_ts - 1.0) < 1e-6
+        p2.logits_filter_callback = C.cast(cfunc, C.c_void_p)
+        assert w.full(s2, clips["synth30"], p2) == want["ret"]
+        return w.segments(s2)
+    tf = tmeta["cases"][key]
+    n1, it = decision_check(run, tf, tarr, key, eot, beg, w.n_vocab, owk.TokenData, want["segments"])
+    n2, fo = decision_forced(run, tf, tarr, key, eot, beg, w.n_vocab, owk.TokenData,
+                             [t[0] for s in want["segments"] for t in s["tokens"]], space=int(buf[0]), tid_initial=50)
+    assert n1 == n2
+    assert [x[:3] for x in fo] == [x[:3] for x in it], (fo, it)
 
 
 def test_greedy_then_beam_on_one_state(lib, golden, model_path, clips):
