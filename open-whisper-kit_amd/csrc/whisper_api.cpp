@@ -23,61 +23,131 @@ void set_log_callback(ggml_log_callback cb, void * ud);
 const std::vector<uint16_t> & gelu_table_host();
 }
 
-// OWK_BACKTRACE=1: print a native backtrace on SIGSEGV/SIGABRT (host-side debugging on
-// the GPU box, where no debugger may attach to a GPU process)
-// Each frame is printed as library + offset from its load base (resolvable offline with
-// llvm-addr2line / llvm-objdump against the same image's libraries), with the nearest exported
-// symbol, and the /proc/self/maps lines around the faulting address.
+// OWK_BACKTRACE=1: print a native backtrace on SIGSEGV/SIGABRT/SIGBUS (host-side debugging on
+// the GPU box, where no debugger may attach to a GPU process). Each frame is printed as the file of
+// its mapping + the file offset (resolvable offline with llvm-addr2line / llvm-objdump against the
+// same image's libraries), then the /proc/self/maps lines around the faulting address. The handler
+// only uses async-signal-safe calls (open / read / write / close, hand-written formatting): an abort
+// raised inside malloc holds the heap lock, where stdio or dladdr could deadlock. backtrace() is
+// called once at install time so its unwinder library is loaded before any signal.
 #include <csignal>
-#include <dlfcn.h>
 #include <execinfo.h>
+#include <fcntl.h>
 #include <ucontext.h>
 #include <unistd.h>
+static char g_crash_maps[1 << 18];  // /proc/self/maps, read by the handler
+static size_t g_crash_maps_n = 0;
+static void crash_put(const char * s) {
+    size_t n = 0;
+    while (s[n]) ++n;
+    (void) !write(2, s, n);
+}
+static void crash_put_n(const char * s, size_t n) { (void) !write(2, s, n); }
+static void crash_put_hex(uintptr_t v) {
+    char b[19];
+    int i = 18;
+    b[i] = 0;
+    do {
+        b[--i] = "0123456789abcdef"[v & 15];
+        v >>= 4;
+    } while (v && i > 2);
+    b[--i] = 'x';
+    b[--i] = '0';
+    crash_put(b + i);
+}
+static uintptr_t crash_parse_hex(const char *& p, const char * end) {
+    uintptr_t v = 0;
+    for (; p < end; ++p) {
+        const char c = *p;
+        const int d = c >= '0' && c <= '9' ? c - '0' : c >= 'a' && c <= 'f' ? c - 'a' + 10 : -1;
+        if (d < 0) break;
+        v = v * 16 + (uintptr_t) d;
+    }
+    return v;
+}
+static void crash_read_maps() {
+    g_crash_maps_n = 0;
+    const int fd = open("/proc/self/maps", O_RDONLY);
+    if (fd < 0) return;
+    for (;;) {
+        const ssize_t r = read(fd, g_crash_maps + g_crash_maps_n, sizeof(g_crash_maps) - 1 - g_crash_maps_n);
+        if (r <= 0) break;
+        g_crash_maps_n += (size_t) r;
+        if (g_crash_maps_n >= sizeof(g_crash_maps) - 1) break;
+    }
+    close(fd);
+    g_crash_maps[g_crash_maps_n] = '\n';  // a last line printed with its terminator
+}
+// visits the maps lines: f(line start, line end, lo, hi, file offset, path start)
+template <typename F> static void crash_maps_each(F && f) {
+    const char * p = g_crash_maps, * end = g_crash_maps + g_crash_maps_n;
+    while (p < end) {
+        const char * e = p;
+        while (e < end && *e != '\n') ++e;
+        const char * q = p;
+        const uintptr_t lo = crash_parse_hex(q, e);
+        ++q;
+        const uintptr_t hi = crash_parse_hex(q, e);
+        while (q < e && *q != ' ') ++q;  // " perms offset"
+        ++q;
+        while (q < e && *q != ' ') ++q;
+        ++q;
+        const uintptr_t off = crash_parse_hex(q, e);
+        const char * path = e;
+        for (const char * c = q; c < e; ++c)
+            if (*c == '/' || *c == '[') {
+                path = c;
+                break;
+            }
+        if (!f(p, e, lo, hi, off, path)) return;
+        p = e + 1;
+    }
+}
 static void owk_crash_print_pc(const void * pc) {
-    Dl_info di{};
-    char line[768];
-    int n;
-    if (dladdr(pc, &di) && di.dli_fname)
-        n = snprintf(line, sizeof(line), "  %p  %s+0x%lx  (%s+0x%lx)\n", pc, di.dli_fname,
-                     (unsigned long) ((const char *) pc - (const char *) di.dli_fbase), di.dli_sname ? di.dli_sname : "?",
-                     di.dli_saddr ? (unsigned long) ((const char *) pc - (const char *) di.dli_saddr) : 0ul);
-    else
-        n = snprintf(line, sizeof(line), "  %p  (no mapping)\n", pc);
-    (void) !write(2, line, (size_t) std::min(n, (int) sizeof(line) - 1));
+    const uintptr_t a = (uintptr_t) pc;
+    bool found = false;
+    crash_put("  ");
+    crash_put_hex(a);
+    crash_maps_each([&](const char *, const char * e, uintptr_t lo, uintptr_t hi, uintptr_t off, const char * path) {
+        if (a < lo || a >= hi) return true;
+        crash_put("  ");
+        crash_put_n(path, (size_t) (e - path));
+        crash_put("+");
+        crash_put_hex(a - lo + off);
+        found = true;
+        return false;
+    });
+    crash_put(found ? "\n" : "  (no mapping)\n");
 }
 static void owk_crash_handler(int sig, siginfo_t * si, void * uc_) {
-    char line[512];
     const ucontext_t * uc = (const ucontext_t *) uc_;
     const void * pc = uc ? (const void *) uc->uc_mcontext.gregs[REG_RIP] : nullptr;
-    int n = snprintf(line, sizeof(line), "\n[owk] fatal signal %d, fault address %p, pc:\n", sig, si ? si->si_addr : nullptr);
-    (void) !write(2, line, (size_t) n);
+    crash_read_maps();
+    crash_put("\n[owk] fatal signal ");
+    crash_put_hex((uintptr_t) sig);
+    crash_put(", fault address ");
+    crash_put_hex(si ? (uintptr_t) si->si_addr : 0);
+    crash_put(", pc:\n");
     owk_crash_print_pc(pc);
     void * frames[64];
     const int nf = backtrace(frames, 64);
-    const char msg[] = "[owk] native backtrace (library+offset, nearest exported symbol):\n";
-    (void) !write(2, msg, sizeof(msg) - 1);
+    crash_put("[owk] native backtrace (mapped file + file offset):\n");
     for (int i = 0; i < nf; ++i) owk_crash_print_pc(frames[i]);
-    // the mappings around the fault address: which allocation the access ran off
-    FILE * f = si ? fopen("/proc/self/maps", "r") : nullptr;
-    if (f) {
+    if (si && sig != SIGABRT) {  // the mappings around the fault address: which allocation the access ran off
         const uintptr_t a = (uintptr_t) si->si_addr;
-        char buf[512], prev[512] = "";
-        const char hdr[] = "[owk] /proc/self/maps around the fault address:\n";
-        (void) !write(2, hdr, sizeof(hdr) - 1);
-        while (fgets(buf, sizeof(buf), f)) {
-            unsigned long lo = 0, hi = 0;
-            if (sscanf(buf, "%lx-%lx", &lo, &hi) != 2) continue;
+        crash_put("[owk] /proc/self/maps around the fault address:\n");
+        const char * prev = nullptr, * prev_e = nullptr;
+        crash_maps_each([&](const char * p, const char * e, uintptr_t lo, uintptr_t hi, uintptr_t, const char *) {
             if (hi + (64ul << 20) >= a && lo <= a + (64ul << 20)) {
-                if (prev[0]) (void) !write(2, prev, strlen(prev));
-                prev[0] = 0;
-                (void) !write(2, buf, strlen(buf));
-            } else if (lo > a) {
-                break;
-            } else {
-                snprintf(prev, sizeof(prev), "%s", buf);
+                if (prev) crash_put_n(prev, (size_t) (prev_e - prev) + 1);
+                prev = nullptr;
+                crash_put_n(p, (size_t) (e - p) + 1);
+                return true;
             }
-        }
-        fclose(f);
+            if (lo > a) return false;
+            prev = p, prev_e = e;
+            return true;
+        });
     }
     signal(sig, SIG_DFL);
     raise(sig);
@@ -85,6 +155,8 @@ static void owk_crash_handler(int sig, siginfo_t * si, void * uc_) {
 static int owk_install_crash_handler = [] {
     const char * e = getenv("OWK_BACKTRACE");
     if (e && e[0] == '1') {
+        void * warm[2];
+        (void) backtrace(warm, 2);  // loads the unwinder now, not inside the handler
         struct sigaction sa{};
         sa.sa_sigaction = owk_crash_handler;
         sa.sa_flags = SA_SIGINFO;

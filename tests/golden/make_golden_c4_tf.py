@@ -72,6 +72,8 @@ def main():
     names = ["v4/p0", "v3"]
     if "--realisations" in sys.argv:
         names = sys.argv[sys.argv.index("--realisations") + 1].split(",")
+    for nm in names:  # every library variant must load (a stale build fails hours later otherwise)
+        R.lib(R.VARIANTS[REALISATIONS[nm][0]])
     cache = os.environ.get("OWK_MODEL_CACHE", "/tmp/owk_models")
     pcm, name = workload(10)
     meta = json.load(open(os.path.join(OUT, name + ".json")))

@@ -225,6 +225,8 @@ def main():
                 for f in ("golden.json", "nofa_golden.json", "large_golden.json", "params_golden.json")}
     audio = clips()
     only = sys.argv[2:] if len(sys.argv) > 2 else None
+    for _, var, _ in realisations(which):  # every library variant must load (a stale build fails late otherwise)
+        R.lib(R.VARIANTS[var])
     for c in cases(which):
         if c[0] in meta["cases"] or (only and not any(c[0] == o or c[0].endswith("/" + o) for o in only)):
             continue

@@ -235,6 +235,26 @@ def test_forced_decisions_match_iterative(lib, golden, tf_golden, model_path, cl
     assert [x[:3] for x in fo] == [x[:3] for x in it], (fo, it)
 
 
+@pytest.mark.parametrize("model", ["tiny.en", "l3-mini"])
+def test_encoder_deterministic(lib, model_path, clips, model):
+    """The encoder (GEMMs, flash attention, LayerNorms) gives the same bits on every run: states of one
+    context encoding the same audio, one after another and on fresh states."""
+    w = whisper(model_path, model)
+    pcm = clips["synth30"]
+    outs = []
+    for _ in range(3):
+        st = w.new_state()
+        assert lib.whisper_pcm_to_mel_with_state(w.ctx, st, owk.fptr(pcm), len(pcm), 1) == 0
+        for _ in range(2):
+            assert lib.whisper_encode_with_state(w.ctx, st, 0, 1) == 0
+            n = lib.owk_debug_enc(w.ctx, st, 0, None, 0)
+            enc = np.zeros(n, np.float32)
+            lib.owk_debug_enc(w.ctx, st, 0, owk.fptr(enc), n)
+            outs.append(enc)
+    for i, e in enumerate(outs[1:], 1):
+        assert np.array_equal(e.view(np.uint32), outs[0].view(np.uint32)), (i, float(np.abs(e - outs[0]).max()))
+
+
 def test_greedy_then_beam_on_one_state(lib, golden, model_path, clips):
     """One state decodes greedy, then beam search (its KV cache grows to n_decoders + 2 sets of
     cells, ref whisper.cpp:7157-7175), then greedy again: captured decode graphs must be rebuilt
