@@ -1149,7 +1149,13 @@ __global__ __launch_bounds__(256) void k_sm_split_pv(const _Float16 * __restrict
             }
         }
         // hand-off inside the launch (cdna_hip_programming.md Guideline 16, R1): partials stored
-        // write-through (agent-scope atomic stores) and drained before the arrival ticket
+        // write-through (agent-scope atomic stores: sc1, past the XCD's non-coherent L2) and drained
+        // (vmcnt(0): every store acknowledged at the coherence point) before the barrier that precedes
+        // the arrival ticket; the last arriver reads them with agent-scope atomic loads. Only the
+        // hand-off's own locations are involved, all accessed as agent-scope atomics, so no cache-wide
+        // release / acquire is needed: the formal fences (buffer_wbl2 of the whole L2 before the ticket,
+        // buffer_inv after it) measured +3.9 us per launch at one row x 448 keys and +2 us at 1500
+        // (13.78 / 14.34 us against 9.88 / 12.3, profiles/r06h_ab.txt), 20-30 % of configs[4]'s step
 #pragma unroll
         for (int e = 0; e < 8; ++e)
             __hip_atomic_store(part + g * 64 + seg * 8 + e, acc[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

@@ -128,8 +128,9 @@ void resid_layernorm(hipStream_t s, int M, int N, int ks, const float * part, co
     if (M > 32 || N % 16 != 0 || N > 4 * 256 * RL_V4 || ks < 1 || ks > RL_KSMAX)
         throw std::runtime_error("resid_layernorm: unsupported shape");
     if (q8 && (N % 32 != 0 || !q8d)) throw std::runtime_error("resid_layernorm: Q8_0 output needs N % 32 == 0");
-    // (a one-wave-per-row variant measured slower: 159 -> 249 ms per step, the row's split partials
-    // are too many serial loads for one wave, profiles/archive/r02e_ab.txt)
+    // (one wave per row measured slower twice: round 2 with its split partials loaded one after another,
+    // 159 -> 249 ms per step, profiles/archive/r02e_ab.txt; round 6 with every load issued first and no
+    // barrier, 5.30 -> 5.39 us per launch alone, F16 RTF 1066 / 1076 -> 1056 / 1060, profiles/r06h_ab.txt)
     OWK_LAUNCH(k_resid_layernorm, dim3(M), dim3(256), 0, s, M, N, ks, part, bias, x, lnw, lnb, eps, xn, ldo,
                        q8, q8d);
 }
