@@ -68,6 +68,12 @@ def forced_steps(name, var, seed, pcm, res, path, cache):
     return st
 
 
+def forced(st):
+    """the steps of a recorded run that were teacher-forced (teacher >= 0), in order"""
+    keep = st["teacher"] >= 0
+    return {k: v[keep] for k, v in st.items()}
+
+
 def main():
     names = ["v4/p0", "v3"]
     if "--realisations" in sys.argv:
@@ -80,7 +86,10 @@ def main():
     res = meta["results"]
     path = S.ensure_model("large-v3", SEED, cache)
     assert S.file_sha256(path) == meta["model_sha256"]
-    base = forced_steps("base", "v4", None, pcm, res, path, cache)
+    # every window of the fixture is open (windows_open): its last step -- the one that ends the window --
+    # is the decoder's own, unforced (teacher -1), and no later callback sees it; the GPU check compares the
+    # forced steps (tests/parity_util.py StepForcer: len(window) per open window) and the run's final tokens
+    base = forced(forced_steps("base", "v4", None, pcm, res, path, cache))
     assert (base["pick"] == base["teacher"]).all(), "the reference's own pick differs from its forced token"
     n = len(base["pick"])
     assert n == sum(len(w) for w in res["windows"]), (n, sum(len(w) for w in res["windows"]))
@@ -92,7 +101,7 @@ def main():
     fl_ts = np.zeros(n, np.float32)
     for nm in names:
         var, seed = REALISATIONS[nm]
-        st = forced_steps(nm, var, seed, pcm, res, path, cache)
+        st = forced(forced_steps(nm, var, seed, pcm, res, path, cache))
         assert len(st["pick"]) == n, f"{nm}: {len(st['pick'])} steps vs {n}"
         flips = [[int(i), int(st["pick"][i]), int(st["teacher"][i])] for i in np.nonzero(st["pick"] != st["teacher"])[0]]
         d, dts = floors(base, st)
