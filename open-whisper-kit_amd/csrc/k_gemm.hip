@@ -2014,14 +2014,18 @@ __global__ __launch_bounds__(512) void k_gemm_q5_skinny(int M, int N, int K, con
 
 // decode rows (M <= 32): one 16-column tile per block, wave w takes J consecutive K blocks
 // and issues ALL its weight (packed Q5_0) and activation (int8) loads before the first
-// MFMA -- like k_gemm_rows, a launch is one memory round trip. Each lane loads the activation
-// scales of its own outputs' rows and K blocks with them (round 6; rounds 1-5 staged the whole
-// M x K/32 scale array in LDS behind a workgroup barrier); every K block's exact integer dot
+// MFMA -- like k_gemm_rows, a launch is one memory round trip. The activation scales of the
+// whole A (M x K/32 floats) are staged in LDS (round 6 measured the alternative -- each lane loading its
+// own scales directly, no LDS stage or barrier: this kernel 7.64 -> 7.45 us and cross-Q 7.86 -> 6.76 us,
+// but the cross attention launched after the cross-Q GEMM 48.0 -> 56.4 us in every layer on the same
+// box and GFX clock, Q5_0 RTF 844 -> 824; reverted, profiles/r06i_q5_direct_scales_ab.txt); every K block's exact integer dot
 // (v_mfma_i32_16x16x32_i8) is scaled by d_a * d_w into the f32 accumulator; wave partial
 // tiles are summed in fixed wave order. K up to GQ_MAXW * J * 32 (5120 at J = 10).
 constexpr int GQ_MAXW = 16;
 constexpr int GQ_JMAX = 10;  // K up to GQ_MAXW * GQ_JMAX * 32; short K uses 3 blocks per wave
-constexpr int GQ_MAX_SCALES = 32 * 160;  // M x K/32 activation scales (launch bound)
+constexpr int GQ_MAX_SCALES = 32 * 160;  // M x K/32 activation scales in LDS
+// activation scales per thread: M * nb <= 32 * nb over blockDim = 64 * ceil(nb / J) threads
+// -> at most 32 * J / 64 + 1
 
 // NT column tiles per block (full epilogues, one k split): a wave's activation fragments and scales
 // serve NT weight tiles (the MLP0 / logits launches, whose activation rows every block reads again);
@@ -2029,16 +2033,18 @@ constexpr int GQ_MAX_SCALES = 32 * 160;  // M x K/32 activation scales (launch b
 template <int MODE, int MT, int FMT, int GQ_J, int NT = 1>  // FMT: QFmt; GQ_J K blocks per wave
 __global__ __launch_bounds__(GQ_MAXW * 64) void k_gemm_q5_rows(int M, int N, int K, const int8_t * __restrict__ qa,
                                                                const float * __restrict__ da, Q5W w, EpiParams ep) {
+    constexpr int GQ_DA_PER_THREAD = 32 * GQ_J / 64 + 1;
     constexpr bool HAS_M = qf_has_m(FMT), HAS_QH = qf_has_qh(FMT);
     constexpr int TB = qf_tile_bytes(FMT), QSB = qf_qs_bytes(FMT);
     __shared__ floatx4 red[GQ_MAXW][NT][MT][64];
-    __shared__ float sda[32 * 32];  // the GELU epilogue's f16 outputs (M <= 32 rows x the block's 32 columns)
+    __shared__ float sda[GQ_MAX_SCALES];
     const int tid = threadIdx.x, lane = tid & 63, nw = blockDim.x >> 6;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: branch-free k range
     const int ntiles = (N + 15) >> 4, t0 = blockIdx.x * NT;
     const int nb = K >> 5;
     // split-K (gridDim.y > 1, EPI_PARTIAL): block y covers K blocks [kblo, kblo + nbl)
     const int kblo = blockIdx.y * nw * GQ_J;
+    const int nbl = min(nw * GQ_J, nb - kblo);
     const int kb0 = kblo + wave * GQ_J;
     const int nj = max(0, min(GQ_J, nb - kb0));
     const int g = lane >> 4;
@@ -2073,16 +2079,34 @@ __global__ __launch_bounds__(GQ_MAXW * 64) void k_gemm_q5_rows(int M, int N, int
             a[i][j] = j < nj ? t : 0L;
         }
     }
-    // the activation scales this lane's outputs need (raw f32 d of rows i * 16 + 4 g + e at this wave's K
-    // blocks), loaded straight into registers with the operands above -- one memory round trip and no
-    // LDS staging / workgroup barrier before the first MFMA; indices clamped into the array, values past
-    // the wave's K range replaced by zero below
+    // activation scales of this block's K range (raw f32 d; at most GQ_DA_PER_THREAD per thread:
+    // M <= 32, nbl <= nw * J) to LDS as [row][kb - kblo]; every load of the launch is issued before
+    // the first wait (one round trip)
+    {
+        float dv[GQ_DA_PER_THREAD];
+#pragma unroll
+        for (int u = 0; u < GQ_DA_PER_THREAD; ++u) {
+            const int i = tid + u * blockDim.x;
+            const int r = i / nbl;
+            dv[u] = i < M * nbl ? da[(size_t) r * nb + kblo + (i - r * nbl)] : 0.0f;
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int u = 0; u < GQ_DA_PER_THREAD; ++u) {
+            const int i = tid + u * blockDim.x;
+            if (i < M * nbl) sda[i] = dv[u];
+        }
+    }
+    __syncthreads();
     floatx4 acc[NT][MT], accm[NT][MT];
 #pragma unroll
     for (int t = 0; t < NT; ++t)
 #pragma unroll
         for (int i = 0; i < MT; ++i) acc[t][i] = accm[t][i] = floatx4{0.f, 0.f, 0.f, 0.f};
     const long ones = 0x0101010101010101L;
+    // every activation scale of this wave first: unconditional LDS reads (in-array indices; a value past
+    // the wave's K range is replaced by zero afterwards), so they go out together -- a guarded read per
+    // scale made hipcc branch and wait on each one
     float drs[GQ_J][MT][4];
 #pragma unroll
     for (int j = 0; j < GQ_J; ++j) {
@@ -2092,7 +2116,7 @@ __global__ __launch_bounds__(GQ_MAXW * 64) void k_gemm_q5_rows(int M, int N, int
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
                 const int r = min(i * 16 + 4 * g + e, M - 1);
-                drs[j][i][e] = da[(size_t) r * nb + kb];
+                drs[j][i][e] = sda[min(r * nbl + (kb - kblo), GQ_MAX_SCALES - 1)];
             }
     }
 #pragma unroll
@@ -2136,7 +2160,7 @@ __global__ __launch_bounds__(GQ_MAXW * 64) void k_gemm_q5_rows(int M, int N, int
             } else if constexpr (MODE == EPI_GELU_F16 && NT == 2) {
                 const _Float16 h = (_Float16) gelu_lookup(ep.gelu_tab, sum + ep.bias[c]);
                 ep.out16[(size_t) r * ep.ldo + c] = h;
-                sda[r * 32 + t * 16 + cc] = (float) h;
+                sda[r * 32 + t * 16 + cc] = (float) h;  // the scales are read: sda is free
             } else {
                 epi_store<MODE>(ep, r, c, sum);
             }
