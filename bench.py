@@ -75,9 +75,9 @@ CLASS_KERNELS = {
 # rocprofv3 --kernel-trace --stats summary (tools/prof_summary.py) and the PMC FETCH_SIZE pass
 # (tools/pmc_summary.py). A model without its own files reports null cross-checks.
 PROFILES = {
-    "large-v3": ("profiles/r05_bench_kernel_stats.txt", "profiles/r05_pmc_fetch_summary.txt"),
-    "large-v3-turbo": ("profiles/r05_turbo_kernel_stats.txt", "profiles/r05_turbo_pmc_fetch_summary.txt"),
-    "large-v3-q5_0": ("profiles/r05_q5_kernel_stats.txt", "profiles/r05_q5_pmc_fetch_summary.txt"),
+    "large-v3": ("profiles/r06_bench_kernel_stats.txt", "profiles/r06_bench_pmc_fetch_summary.txt"),
+    "large-v3-turbo": ("profiles/r06_turbo_kernel_stats.txt", "profiles/r06_turbo_pmc_fetch_summary.txt"),
+    "large-v3-q5_0": ("profiles/r06_q5_kernel_stats.txt", "profiles/r06_q5_pmc_fetch_summary.txt"),
 }
 # human-readable kernel of each class (the mangled names CLASS_KERNELS matches)
 CLASS_KERNEL_NAME = {"attn_cross": "owk::k_attn_step<false, true> (one_chunk cross attention, k_attn.hip)",
