@@ -344,7 +344,50 @@ class GpuRunner:
                          None if len(gpu_ids) == len(ref_ids) else min(len(gpu_ids), len(ref_ids)))
             parity = {"tokens_equal": gpu_ids == ref_ids, "clip": 0, "n_tokens": len(ref_ids), "first_diff": first,
                       "against": "cpu_baseline run: the reference ggml CPU path on the same clip, model and parameters"}
+            if gpu_ids != ref_ids:
+                parity["teacher_forced"] = self.forced_decisions(ref_ids)
         return base, parity
+
+    def forced_decisions(self, ref_ids):
+        """Clip 0 decoded again alone, teacher-forced onto the reference's 220 tokens at EVERY step: the
+        GPU's own greedy pick at each step is read from the logits its decoder computed on the reference's
+        prefix (fixed work: no timestamps, EOT suppressed, so the pick is the argmax). Reports the steps where
+        it differs and the GPU's log-probability margin there (a near-tie: both choices within that margin);
+        the test suite judges such steps against the reference's own per-step floor (tests/parity_util.py)."""
+        import ctypes as C
+
+        import numpy as np
+        import owk
+
+        w = self.w
+        nv = w.n_vocab
+        eot = w.L.whisper_token_eot(w.ctx)
+        picks = []
+
+        def cb(ctx, state, tokens, n_tokens, logits, user):
+            lg = np.ctypeslib.as_array(logits, shape=(nv,))
+            x = np.where(np.isfinite(lg), lg, -np.inf).astype(np.float64)
+            x[eot] = -np.inf
+            m = x.max()
+            lp = x - (m + np.log(np.exp(x - m).sum()))
+            k = n_tokens
+            if k < len(ref_ids):
+                g = int(np.argmax(lp))
+                picks.append((k, g, float(lp[g] - lp[ref_ids[k]])))
+                lg[ref_ids[k]] = (float(lg[np.isfinite(lg)].max())) + 40.0  # force the reference's token
+        TD = C.POINTER(owk.TokenData)
+        cfunc = C.CFUNCTYPE(None, C.c_void_p, C.c_void_p, TD, C.c_int, C.POINTER(C.c_float), C.c_void_p)(cb)
+        st = w.new_state()
+        p = w.params(0, language="en", temperature_inc=0.0, no_timestamps=True, max_tokens=MAX_TOKENS)
+        p.logits_filter_callback = C.cast(cfunc, C.c_void_p)
+        ret = w.full_batch([st], [self.host[0]], p, suppress_eot=True)
+        got = [t[0] for s in w.segments(st) for t in s["tokens"]]
+        w.L.whisper_free_state(st)
+        w._states = [x for x in w._states if x is not st]
+        dis = [(k, g, round(mg, 6)) for k, g, mg in picks if g != ref_ids[k]]
+        return {"ret": ret, "steps": len(picks), "forced_tokens_equal": got == list(ref_ids),
+                "disagreements": [{"step": k, "gpu": g, "ref": int(ref_ids[k]), "logprob_margin": mg} for k, g, mg in dis],
+                "max_margin": max((mg for _, _, mg in dis), default=0.0)}
 
 
 def roofline(classes, ms_per_step, alone=None, model="large-v3"):
