@@ -349,7 +349,7 @@ class GpuRunner:
         return base, parity
 
     def forced_decisions(self, ref_ids):
-        """Clip 0 decoded again alone, teacher-forced onto the reference's 220 tokens at EVERY step: the
+        """The 32-clip step run again with clip 0 teacher-forced onto the reference's 220 tokens at EVERY step: the
         GPU's own greedy pick at each step is read from the logits its decoder computed on the reference's
         prefix (fixed work: no timestamps, EOT suppressed, so the pick is the argmax). Reports the steps where
         it differs and the GPU's log-probability margin there (a near-tie: both choices within that margin);
@@ -364,7 +364,12 @@ class GpuRunner:
         eot = w.L.whisper_token_eot(w.ctx)
         picks = []
 
+        sts = [w.new_state() for _ in self.host]
+        watch = sts[0]
+
         def cb(ctx, state, tokens, n_tokens, logits, user):
+            if state != watch:
+                return
             lg = np.ctypeslib.as_array(logits, shape=(nv,))
             x = np.where(np.isfinite(lg), lg, -np.inf).astype(np.float64)
             x[eot] = -np.inf
@@ -377,13 +382,13 @@ class GpuRunner:
                 lg[ref_ids[k]] = (float(lg[np.isfinite(lg)].max())) + 40.0  # force the reference's token
         TD = C.POINTER(owk.TokenData)
         cfunc = C.CFUNCTYPE(None, C.c_void_p, C.c_void_p, TD, C.c_int, C.POINTER(C.c_float), C.c_void_p)(cb)
-        st = w.new_state()
         p = w.params(0, language="en", temperature_inc=0.0, no_timestamps=True, max_tokens=MAX_TOKENS)
         p.logits_filter_callback = C.cast(cfunc, C.c_void_p)
-        ret = w.full_batch([st], [self.host[0]], p, suppress_eot=True)
-        got = [t[0] for s in w.segments(st) for t in s["tokens"]]
-        w.L.whisper_free_state(st)
-        w._states = [x for x in w._states if x is not st]
+        ret = w.full_batch(sts, list(self.host), p, suppress_eot=True)
+        got = [t[0] for s in w.segments(watch) for t in s["tokens"]]
+        for st in sts:
+            w.L.whisper_free_state(st)
+        w._states = [x for x in w._states if x not in sts]
         dis = [(k, g, round(mg, 6)) for k, g, mg in picks if g != ref_ids[k]]
         return {"ret": ret, "steps": len(picks), "forced_tokens_equal": got == list(ref_ids),
                 "disagreements": [{"step": k, "gpu": g, "ref": int(ref_ids[k]), "logprob_margin": mg} for k, g, mg in dis],
