@@ -13,7 +13,7 @@ else
   [ "$PART" = B ] || exit 2
 fi
 if [ "$PART" = A ]; then TARGET=tests; else TARGET=""; fi
-timeout -k 10 1100 python -u -m pytest $TARGET $SEL -m gpu -q --timeout 300 --timeout-method thread -p no:cacheprovider \
+timeout -k 10 1100 python -u -m pytest $TARGET $SEL -m gpu -q -rP --timeout 300 --timeout-method thread -p no:cacheprovider \
     > gpurun_out/$TAG/gpu_tests_$PART.txt 2>&1
 rc=$?
 tail -5 gpurun_out/$TAG/gpu_tests_$PART.txt
