@@ -52,7 +52,7 @@ __device__ __forceinline__ void epi_store(const EpiParams & p, int r, int c, flo
             const int clip = r / p.T, t = r % p.T;
             const int h = cc >> 6, dim = cc & 63;
             const int H = d >> 6;
-            p.out16c[(((size_t) clip * H + h) * 64 + dim) * p.Tpad + vt_pos(t)] = (_Float16) (acc + p.bias2[cc]);
+            p.out16c[(((size_t) clip * H + h) * 64 + dim) * p.Tpad + t] = (_Float16) (acc + p.bias2[cc]);
         }
     } else if constexpr (MODE == EPI_KV_CROSS) {
         const int d = p.d;

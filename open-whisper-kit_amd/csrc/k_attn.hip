@@ -126,55 +126,50 @@ __global__ __launch_bounds__(256, 2) void k_attn_encoder(const _Float16 * __rest
             z = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1, qf1, z, 0, 0, 0);
             sc[t] = z;
         }
-        // scores to base-2 units (packed multiplies; their results are canonical, so the max chain below is
-        // v_max3 with no operand canonicalisation)
-        const floatx4 s2v = floatx4{scale2, scale2, scale2, scale2};
         float tmax = -INFINITY;
         if ((kt + 1) * FA_KT <= T) {  // a full tile (every one but the last): no key mask
 #pragma unroll
-            for (int t = 0; t < 4; ++t) sc[t] = sc[t] * s2v;
-#pragma unroll
             for (int t = 0; t < 4; ++t)
 #pragma unroll
-                for (int e = 0; e < 4; ++e) tmax = fmaxf(tmax, sc[t][e]);
+                for (int e = 0; e < 4; ++e) {
+                    const float v = sc[t][e] * scale2;
+                    sc[t][e] = v;
+                    tmax = fmaxf(tmax, v);
+                }
         } else {
 #pragma unroll
             for (int t = 0; t < 4; ++t)
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
                     const int key = kt * FA_KT + t * 16 + 4 * g + e;
-                    const float v = sc[t][e] * scale2;
-                    sc[t][e] = key < T ? v : -INFINITY;
-                    tmax = fmaxf(tmax, sc[t][e]);
+                    float v = sc[t][e] * scale2;
+                    if (key >= T) v = -INFINITY;
+                    sc[t][e] = v;
+                    tmax = fmaxf(tmax, v);
                 }
         }
-        // the 4 lanes of a query (l16 + 16 g)
         tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
         tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
         const float mnew = fmaxf(m, tmax);
-        // the accumulator rescale only when some query's max moved (most tiles after the first few)
-        if (__builtin_amdgcn_ballot_w64(mnew != m)) {
-            const float alpha = __builtin_amdgcn_exp2f(m - mnew);  // m = -inf on the first tile -> 0
-            lsum *= alpha;
-#pragma unroll
-            for (int i = 0; i < 4; ++i) o[i] *= alpha;
-        }
+        const float alpha = __builtin_amdgcn_exp2f(m - mnew);  // m = -inf on the first tile -> 0
+        const bool moved = __builtin_amdgcn_ballot_w64(mnew != m) != 0;  // wave-uniform
         m = mnew;
-        const floatx4 nm = floatx4{mnew, mnew, mnew, mnew};
-        floatx4 pv[4];
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-            const floatx4 x = sc[t] - nm;  // packed subtracts
-#pragma unroll
-            for (int e = 0; e < 4; ++e) pv[t][e] = __builtin_amdgcn_exp2f(x[e]);
-        }
-        const floatx4 ps4 = (pv[0] + pv[1]) + (pv[2] + pv[3]);  // packed adds, a tree
-        lsum += (ps4[0] + ps4[1]) + (ps4[2] + ps4[3]);
+        float ps = 0.0f;
         half8 pb[2];
 #pragma unroll
         for (int t = 0; t < 4; ++t)
 #pragma unroll
-            for (int e = 0; e < 4; ++e) pb[t >> 1][(t & 1) * 4 + e] = (_Float16) pv[t][e];
+            for (int e = 0; e < 4; ++e) {
+                const float p = __builtin_amdgcn_exp2f(sc[t][e] - mnew);
+                ps += p;
+                pb[t >> 1][(t & 1) * 4 + e] = (_Float16) p;
+            }
+        lsum = lsum * alpha + ps;
+        // the accumulator rescale only when some query's max moved (alpha = 1 everywhere otherwise: o * 1
+        // is o, bit for bit)
+        if (moved)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) o[i] *= alpha;
 
         // O^T[dim][q] += V^T[dim][key] . P^T[key][q]; k-step ks covers keys 32*ks..+32 with
         // element j<4 -> key 32ks + 4g + j, j>=4 -> key 32ks + 16 + 4g + (j-4)
@@ -185,8 +180,13 @@ __global__ __launch_bounds__(256, 2) void k_attn_encoder(const _Float16 * __rest
             const int sw = (row >> 1) & 7;
 #pragma unroll
             for (int ks = 0; ks < 2; ++ks) {
-                // keys 32ks + 4g .. +3 and 32ks + 16 + 4g .. +3: one 16-byte run of the vt_pos image
-                const half8 a = *(const half8 *) (vr + (((4 * ks + g) ^ sw) << 4));
+                const int b0 = ks * 64 + 8 * g;        // byte offset of key 32ks + 4g
+                const int b1 = ks * 64 + 32 + 8 * g;   // byte offset of key 32ks + 16 + 4g
+                const half4 lo = *(const half4 *) (vr + ((((b0 >> 4) ^ sw) << 4) | (b0 & 15)));
+                const half4 hi = *(const half4 *) (vr + ((((b1 >> 4) ^ sw) << 4) | (b1 & 15)));
+                half8 a;
+                a[0] = lo[0]; a[1] = lo[1]; a[2] = lo[2]; a[3] = lo[3];
+                a[4] = hi[0]; a[5] = hi[1]; a[6] = hi[2]; a[7] = hi[3];
                 o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, pb[ks], o[dt], 0, 0, 0);
             }
         }
@@ -348,8 +348,13 @@ __global__ __launch_bounds__(256, 2) void k_attn_encoder_sm(const _Float16 * __r
             const int sw = (row >> 1) & 7;
 #pragma unroll
             for (int ks = 0; ks < 2; ++ks) {
-                // keys 32ks + 4g .. +3 and 32ks + 16 + 4g .. +3: one 16-byte run of the vt_pos image
-                const half8 a = *(const half8 *) (vr + (((4 * ks + g) ^ sw) << 4));
+                const int b0 = ks * 64 + 8 * g;
+                const int b1 = ks * 64 + 32 + 8 * g;
+                const half4 lo = *(const half4 *) (vr + ((((b0 >> 4) ^ sw) << 4) | (b0 & 15)));
+                const half4 hi = *(const half4 *) (vr + ((((b1 >> 4) ^ sw) << 4) | (b1 & 15)));
+                half8 a;
+                a[0] = lo[0]; a[1] = lo[1]; a[2] = lo[2]; a[3] = lo[3];
+                a[4] = hi[0]; a[5] = hi[1]; a[6] = hi[2]; a[7] = hi[3];
                 o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, pb[ks], o[dt], 0, 0, 0);
             }
         }

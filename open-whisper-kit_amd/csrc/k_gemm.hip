@@ -242,8 +242,7 @@ __global__ __launch_bounds__(256, 2) void k_gemm_big(int M, int N, int K, const 
             const int r0 = m0 + wm * 64 + i * 16 + 4 * (lane >> 4);
             if constexpr (MODE == EPI_QKV_ENC) {
                 // V columns go to the transposed [clip][head][dim][Tpad] image: a lane's 4 rows
-                // are 4 consecutive t of one clip (T % 4 == 0, r0 % 4 == 0): one 8-byte store (vt_pos
-                // keeps a 4-aligned key group contiguous)
+                // are 4 consecutive t of one clip (T % 4 == 0, r0 % 4 == 0): one 8-byte store
                 const int d = ep.d;
                 if (c >= 2 * d && c < N && r0 + 3 < M && ep.T % 4 == 0) {
                     const int cc = c - 2 * d;
@@ -252,7 +251,7 @@ __global__ __launch_bounds__(256, 2) void k_gemm_big(int M, int N, int K, const 
                     half4 hv;
 #pragma unroll
                     for (int e = 0; e < 4; ++e) hv[e] = (_Float16) (acc[i][j][e] + bv);
-                    *(half4 *) (ep.out16c + (((size_t) clip * (d >> 6) + (cc >> 6)) * 64 + (cc & 63)) * ep.Tpad + vt_pos(t)) = hv;
+                    *(half4 *) (ep.out16c + (((size_t) clip * (d >> 6) + (cc >> 6)) * 64 + (cc & 63)) * ep.Tpad + t) = hv;
                     continue;
                 }
             }
@@ -637,7 +636,7 @@ __global__ __launch_bounds__(512, 1) void k_gemm_8p(int M, int N, int K, const _
                     half4 hv;
 #pragma unroll
                     for (int e = 0; e < 4; ++e) hv[e] = (_Float16) (acc[i][j][e] + bv);
-                    *(half4 *) (ep.out16c + (((size_t) clip * (d >> 6) + (cc >> 6)) * 64 + (cc & 63)) * ep.Tpad + vt_pos(t)) = hv;
+                    *(half4 *) (ep.out16c + (((size_t) clip * (d >> 6) + (cc >> 6)) * 64 + (cc & 63)) * ep.Tpad + t) = hv;
                     continue;
                 }
             }

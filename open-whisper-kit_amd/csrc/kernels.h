@@ -60,15 +60,6 @@ struct EpiParams {
     float * q8d = nullptr;
 };
 
-// Key position in the encoder's transposed V image ([clip][head][dim][Tpad], EPI_QKV_ENC): within each
-// 32-key block the 8 keys one P.V MFMA lane group g reads (4g .. 4g + 3 and 16 + 4g .. 16 + 4g + 3, the
-// S^T = K.Q^T output layout of k_attn_encoder) sit in one 16-byte run, so the attention kernels read each
-// MFMA operand with one ds_read_b128. 4-aligned key groups stay contiguous (the epilogues' 8-byte stores).
-__host__ __device__ inline int vt_pos(int t) {
-    const int k = t & 31;
-    return (t & ~31) | (((k & 15) >> 2) << 3) | ((k >> 4) << 2) | (k & 3);
-}
-
 // large tiles (encoder / conv / cross-KV / long prefill): A [M,lda] f16, W [N,ldw] f16
 void gemm_f16(hipStream_t s, int mode, int M, int N, int K, const _Float16 * A, int lda,
               const _Float16 * W, int ldw, const EpiParams & ep);
