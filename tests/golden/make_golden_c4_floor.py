@@ -36,18 +36,23 @@ from make_golden_large import SEED  # noqa: E402
 
 MINUTES = int(sys.argv[sys.argv.index("--minutes") + 1]) if "--minutes" in sys.argv else 1
 FORCED = "--forced" in sys.argv
+# --lib v3|v1: the reference built for another x86 SIMD level (oracle/ref/Makefile variants), its input
+# unperturbed -- another summation order of the same ggml path (recorded with seed "v3" / "v1")
+LIB = sys.argv[sys.argv.index("--lib") + 1] if "--lib" in sys.argv else None
 
 
 def perturbed_run(seed, name):
     cache = os.environ.get("OWK_MODEL_CACHE", "/tmp/owk_models")
     path = S.ensure_model("large-v3", SEED, cache)
     keep = os.path.join(cache, f"{name}_floor{'_tf' if FORCED else ''}_seed{seed}-{S.file_sha256(path)[:16]}.json")
+    if LIB:
+        keep = os.path.join(cache, f"{name}_floor{'_tf' if FORCED else ''}_{LIB}-{S.file_sha256(path)[:16]}.json")
     if os.path.exists(keep):
         return json.load(open(keep))["segments"]
     pcm, _ = workload(MINUTES)
     rng = np.random.default_rng(seed)
-    pp = (pcm * (1 + 1e-7 * rng.standard_normal(len(pcm)))).astype(np.float32)
-    ref = R.Ref(path, flash_attn=False, dtw_preset=AHEADS_LARGE_V3)
+    pp = pcm if LIB else (pcm * (1 + 1e-7 * rng.standard_normal(len(pcm)))).astype(np.float32)
+    ref = R.Ref(path, lib_path=R.VARIANTS[LIB] if LIB else None, flash_attn=False, dtw_preset=AHEADS_LARGE_V3)
     if FORCED:
         res = json.load(open(os.path.join(OUT, name + ".json")))["results"]
         ref.tf_set(res["windows"], force=True, open_end=res["windows_open"])
@@ -71,7 +76,7 @@ def run(seed):
         n += 1
     diffs = [(i, int(got[i][8]), int(want[i][8])) for i in range(n) if got[i][8] != want[i][8]]
     shift = max((abs(a - b) for _, a, b in diffs), default=0)
-    rec = {"seed": seed, "compared": n, "n_tokens": len(want), "n_diff": len(diffs), "max_shift": shift,
+    rec = {"seed": LIB or seed, "compared": n, "n_tokens": len(want), "n_diff": len(diffs), "max_shift": shift,
            "diffs": diffs[:2000]}
     print(f"seed {seed}: identical tokens {n} of {len(want)}; t_dtw differs on {len(diffs)} (max shift {shift} cs)",
           flush=True)
@@ -80,10 +85,13 @@ def run(seed):
 
 def main():
     args = [a for a in sys.argv[1:] if a != "--forced"]
-    if "--minutes" in args:
-        i = args.index("--minutes")
-        args = args[:i] + args[i + 2:]
+    for opt in ("--minutes", "--lib"):
+        if opt in args:
+            i = args.index(opt)
+            args = args[:i] + args[i + 2:]
     seeds = [int(a) for a in args] or [0]
+    if LIB:
+        seeds = seeds[:1]
     recs = [run(sd) for sd in seeds]
     path_json = os.path.join(OUT, workload(MINUTES)[1] + ".json")
     meta = json.load(open(path_json))  # re-read: several of these may run side by side
@@ -92,7 +100,7 @@ def main():
         if rec["seed"] == 0 and not FORCED:
             meta["results"]["tdtw_floor"] = {k: v for k, v in rec.items() if k != "seed"}
         seeds_l = [x for x in meta["results"].get(key, []) if x["seed"] != rec["seed"]]
-        meta["results"][key] = sorted(seeds_l + [rec], key=lambda x: x["seed"])
+        meta["results"][key] = sorted(seeds_l + [rec], key=lambda x: str(x["seed"]))
     with open(path_json, "w") as f:
         json.dump(meta, f, indent=0)
 
