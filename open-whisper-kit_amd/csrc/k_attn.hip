@@ -1173,7 +1173,8 @@ __global__ __launch_bounds__(256) void k_sm_split_pv(const _Float16 * __restrict
     if (!s_last || tid >= 64) return;
     // the last arriver: the 128 group partials in group order (agent-scope, L1-bypassing loads), as
     // k_attn_softmax's wave 0 adds them; then the ticket is reset for the next launch
-    // two batches of 64 loads in flight (the vmcnt limit), then the adds: two memory round trips
+    // two batches of 64 loads in flight (the vmcnt limit), then the adds: two memory round trips (all
+    // four waves loading once and adding through LDS measured 0.5 us slower, profiles/r06v_smpv_reduce_ab.txt)
     float r = 0.0f;
 #pragma unroll
     for (int g0 = 0; g0 < SM_PV_GROUPS; g0 += 64) {
