@@ -10,5 +10,5 @@ export DEBUG_CLR_GRAPH_PACKET_CAPTURE=0  # rocprofiler-sdk walks captured graph 
 timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/seqtr -o run -- \
     python tools/pipeline_bench.py --minutes $MIN --no-cpu --mode sequential --serial > gpurun_out/$TAG/seq.json 2> gpurun_out/$TAG/seq.err \
     || { echo "trace failed"; tail -5 gpurun_out/$TAG/seq.err; exit 1; }
-python tools/trace_gaps.py /tmp/seqtr --skip 20 | tee gpurun_out/$TAG/gaps.txt
+python tools/trace_gaps.py /tmp/seqtr ${GAPS_ARGS:---skip 20} | tee gpurun_out/$TAG/gaps.txt || exit 1
 python tools/prof_summary.py /tmp/seqtr > gpurun_out/$TAG/kernel_stats.txt && head -30 gpurun_out/$TAG/kernel_stats.txt
