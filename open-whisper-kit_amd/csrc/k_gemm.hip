@@ -2013,11 +2013,12 @@ __global__ __launch_bounds__(512) void k_gemm_q5_skinny(int M, int N, int K, con
 
 // decode rows (M <= 32): one 16-column tile per block, wave w takes J consecutive K blocks
 // and issues ALL its weight (packed Q5_0) and activation (int8) loads before the first
-// MFMA -- like k_gemm_rows, a launch is one memory round trip. The activation scales of the
-// whole A (M x K/32 floats) are staged in LDS (round 6 measured the alternative -- each lane loading its
-// own scales directly, no LDS stage or barrier: this kernel 7.64 -> 7.45 us and cross-Q 7.86 -> 6.76 us,
-// but the cross attention launched after the cross-Q GEMM 48.0 -> 56.4 us in every layer on the same
-// box and GFX clock, Q5_0 RTF 844 -> 824; reverted, profiles/r06i_q5_direct_scales_ab.txt); every K block's exact integer dot
+// MFMA -- like k_gemm_rows, a launch is one memory round trip. The activation scales: in the QKV, MLP0
+// and logits launches each lane loads its own outputs' scales directly (QKV 8.67 -> 7.67 us, MLP0 11.12 ->
+// 9.61, logits 61.8 -> 50.1); the other launches stage the whole A's (M x K/32 floats) in LDS behind a
+// barrier, because direct loads in the split-K partial launches made every later layer's cross attention
+// 48 -> 56 us on identical outputs (round 6, per-mode A/B: profiles/r06x_q5_direct_scales_by_mode.txt; the
+// first all-launch trial profiles/r06i_q5_direct_scales_ab.txt). Every K block's exact integer dot
 // (v_mfma_i32_16x16x32_i8) is scaled by d_a * d_w into the f32 accumulator; wave partial
 // tiles are summed in fixed wave order. K up to GQ_MAXW * J * 32 (5120 at J = 10).
 constexpr int GQ_MAXW = 16;
@@ -2035,8 +2036,11 @@ __global__ __launch_bounds__(GQ_MAXW * 64) void k_gemm_q5_rows(int M, int N, int
     constexpr int GQ_DA_PER_THREAD = 32 * GQ_J / 64 + 1;
     constexpr bool HAS_M = qf_has_m(FMT), HAS_QH = qf_has_qh(FMT);
     constexpr int TB = qf_tile_bytes(FMT), QSB = qf_qs_bytes(FMT);
+    // DIRECT: each lane loads its own activation scales with the operands (no LDS stage, no barrier before
+    // the first MFMA) -- in the QKV, MLP0 and logits launches only (see above)
+    constexpr bool DIRECT = MODE == EPI_QKV_DEC || MODE == EPI_GELU_F16 || MODE == EPI_F32;
     __shared__ floatx4 red[GQ_MAXW][NT][MT][64];
-    __shared__ float sda[GQ_MAX_SCALES];
+    __shared__ float sda[DIRECT ? 32 * 32 : GQ_MAX_SCALES];  // staged scales, or the GELU epilogue's f16 rows
     const int tid = threadIdx.x, lane = tid & 63, nw = blockDim.x >> 6;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: branch-free k range
     const int ntiles = (N + 15) >> 4, t0 = blockIdx.x * NT;
@@ -2081,7 +2085,7 @@ __global__ __launch_bounds__(GQ_MAXW * 64) void k_gemm_q5_rows(int M, int N, int
     // activation scales of this block's K range (raw f32 d; at most GQ_DA_PER_THREAD per thread:
     // M <= 32, nbl <= nw * J) to LDS as [row][kb - kblo]; every load of the launch is issued before
     // the first wait (one round trip)
-    {
+    if constexpr (!DIRECT) {
         float dv[GQ_DA_PER_THREAD];
 #pragma unroll
         for (int u = 0; u < GQ_DA_PER_THREAD; ++u) {
@@ -2095,8 +2099,8 @@ __global__ __launch_bounds__(GQ_MAXW * 64) void k_gemm_q5_rows(int M, int N, int
             const int i = tid + u * blockDim.x;
             if (i < M * nbl) sda[i] = dv[u];
         }
+        __syncthreads();
     }
-    __syncthreads();
     floatx4 acc[NT][MT], accm[NT][MT];
 #pragma unroll
     for (int t = 0; t < NT; ++t)
@@ -2115,7 +2119,7 @@ __global__ __launch_bounds__(GQ_MAXW * 64) void k_gemm_q5_rows(int M, int N, int
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
                 const int r = min(i * 16 + 4 * g + e, M - 1);
-                drs[j][i][e] = sda[min(r * nbl + (kb - kblo), GQ_MAX_SCALES - 1)];
+                drs[j][i][e] = DIRECT ? da[(size_t) r * nb + kb] : sda[min(r * nbl + (kb - kblo), GQ_MAX_SCALES - 1)];
             }
     }
 #pragma unroll
