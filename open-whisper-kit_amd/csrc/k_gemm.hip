@@ -2013,12 +2013,12 @@ __global__ __launch_bounds__(512) void k_gemm_q5_skinny(int M, int N, int K, con
 
 // decode rows (M <= 32): one 16-column tile per block, wave w takes J consecutive K blocks
 // and issues ALL its weight (packed Q5_0) and activation (int8) loads before the first
-// MFMA -- like k_gemm_rows, a launch is one memory round trip. The activation scales: in the QKV, MLP0
-// and logits launches each lane loads its own outputs' scales directly (QKV 8.67 -> 7.67 us, MLP0 11.12 ->
-// 9.61, logits 61.8 -> 50.1); the other launches stage the whole A's (M x K/32 floats) in LDS behind a
-// barrier, because direct loads in the split-K partial launches made every later layer's cross attention
-// 48 -> 56 us on identical outputs (round 6, per-mode A/B: profiles/r06x_q5_direct_scales_by_mode.txt; the
-// first all-launch trial profiles/r06i_q5_direct_scales_ab.txt). Every K block's exact integer dot
+// MFMA -- like k_gemm_rows, a launch is one memory round trip. The activation scales: in the QKV, MLP0,
+// cross-Q and logits launches each lane loads its own outputs' scales directly (QKV 8.67 -> 7.67 us, MLP0
+// 11.12 -> 9.61, cross-Q 7.83 -> 6.79, logits 61.8 -> 50.1); the split-K partial launches stage the whole
+// A's (M x K/32 floats) in LDS behind a barrier, because direct loads there made every later layer's cross
+// attention 48 -> 56 us on identical outputs (round 6, per-mode A/B: profiles/r06x_q5_direct_scales_by_mode.txt;
+// the first all-launch trial profiles/r06i_q5_direct_scales_ab.txt). Every K block's exact integer dot
 // (v_mfma_i32_16x16x32_i8) is scaled by d_a * d_w into the f32 accumulator; wave partial
 // tiles are summed in fixed wave order. K up to GQ_MAXW * J * 32 (5120 at J = 10).
 constexpr int GQ_MAXW = 16;
@@ -2037,8 +2037,8 @@ __global__ __launch_bounds__(GQ_MAXW * 64) void k_gemm_q5_rows(int M, int N, int
     constexpr bool HAS_M = qf_has_m(FMT), HAS_QH = qf_has_qh(FMT);
     constexpr int TB = qf_tile_bytes(FMT), QSB = qf_qs_bytes(FMT);
     // DIRECT: each lane loads its own activation scales with the operands (no LDS stage, no barrier before
-    // the first MFMA) -- in the QKV, MLP0 and logits launches only (see above)
-    constexpr bool DIRECT = MODE == EPI_QKV_DEC || MODE == EPI_GELU_F16 || MODE == EPI_F32;
+    // the first MFMA) -- in the QKV, MLP0, cross-Q and logits launches (see above)
+    constexpr bool DIRECT = MODE == EPI_QKV_DEC || MODE == EPI_GELU_F16 || MODE == EPI_F32 || MODE == EPI_F16;
     __shared__ floatx4 red[GQ_MAXW][NT][MT][64];
     __shared__ float sda[DIRECT ? 32 * 32 : GQ_MAX_SCALES];  // staged scales, or the GELU epilogue's f16 rows
     const int tid = threadIdx.x, lane = tid & 63, nw = blockDim.x >> 6;
